@@ -1,0 +1,225 @@
+"""Benchmark: query frames/sec of the OnePose GATsSPG hot path on MI355X.
+
+One step = one batch of synthetic query frames (config 2: 1024 keypoints x 4096 3D points,
+L = 8 leaves, batch 1 per GPU) pushed through the whole per-frame path of inference.py:
+GATsSPG matcher (12 layers, dual softmax, mutual NN; conf_matrix materialised) ->
+correspondence selection -> RANSAC-EPnP -> cm/deg error vs GT.  Inputs are resident in HBM
+before the timed region; nothing is cached across steps.
+
+    python bench.py [--gpus N --steps K --warmup W]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N  (one rank/GPU)
+
+Multi-GPU: frames are independent given the object, so each rank runs its own frames
+(weak scaling) and the only exchange is one all-gather of per-frame poses and cm/deg flags
+at the end of the timed region.  Rank 0 prints ONE JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+METRIC = "query frames/sec (1k kpts × 4k 3D pts) + cm/deg pose err, 1/2/4/8 GPU"
+FP32_MFMA_PEAK_TFLOPS = 157.3     # MI355X_MICROARCH.md: f32-input MFMA dense peak
+HBM_PEAK_GBS = 8000.0             # MI355X_MICROARCH.md: HBM3E spec
+
+
+def kernel_work(kind, B, n1, n3, L):
+    """Algorithmic work of ONE launch of each matcher kernel kind: (amount, unit, bound).
+    GEMM-shaped kernels: FLOPs; byte-moving kernels: bytes that must cross HBM."""
+    T = B * (n1 + n3)
+    C = 256
+    table = {
+        "qkv_gemm": (2 * 3 * C * C * T, "flop", "mfma"),
+        "kv_partial": (4 * 2 * 64 * 64 * T, "flop", "mfma"),
+        "attn_apply": (4 * 2 * 64 * 64 * T, "flop", "mfma"),
+        "merge_gemm": (2 * C * C * T, "flop", "mfma"),
+        "mlp1_gemm": (2 * 2 * C * 2 * C * T, "flop", "mfma"),
+        "mlp2_gemm": (2 * 2 * C * C * T, "flop", "mfma"),
+        "final_gemm": (2 * C * C * T, "flop", "mfma"),
+        "score_gemm": (2 * C * n1 * n3 * B, "flop", "mfma"),
+        # GAT: leaves once + the 3D descriptors in and out (fp32)
+        "gat": (4 * C * n3 * B * (L + 2), "byte", "hbm"),
+        # conf: read S, write conf (fp32)
+        "conf": (8 * n1 * n3 * B, "byte", "hbm"),
+    }
+    return table.get(kind)
+
+
+def profile_kinds(lib):
+    names = []
+    k = 0
+    while True:
+        n = lib.onepose_profile_kind_name(k)
+        if n is None:
+            break
+        names.append(n.decode())
+        k += 1
+    return names
+
+
+def run_profiled(lib, pipe, steps, mask, cap):
+    from onepose_amd import _lib
+    _lib.check(lib.onepose_profile_begin(mask, cap), "profile_begin")
+    for _ in range(steps):
+        pipe.enqueue()
+    kinds = np.zeros(cap, np.int32)
+    ms = np.zeros(cap, np.float32)
+    cnt = np.zeros(1, np.int32)
+    _lib.check(lib.onepose_profile_end(kinds.ctypes.data, ms.ctypes.data, cap, cnt.ctypes.data),
+               "profile_end")
+    n = int(cnt[0])
+    return kinds[:n], ms[:n]
+
+
+def cpu_baseline(sd, data, frames, obj, seconds=15.0):
+    """The oracle (numpy matcher + C RANSAC-EPnP) on the host, bounded to ~`seconds`."""
+    from oracle import matcher_np as M
+    from oracle import pnp_oracle as O
+    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    one = {k: v[:1] for k, v in data.items()}
+    n = 0
+    t0 = time.perf_counter()
+    while True:
+        pred, _ = M.forward(sd, one)
+        p2, p3 = O.select_correspondences(pred["matches0"], one["keypoints2d"][0],
+                                          one["keypoints3d"][0], 1000.0)
+        O.pnp_ransac(p2, p3, frames[0].K, scale=1000.0)
+        n += 1
+        if time.perf_counter() - t0 > seconds or n >= 8:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": n / dt, "unit": "frames/s", "cores": threads, "kind": "port",
+            "sample": f"{n} frame(s) of the timed workload (matcher + RANSAC-EPnP) on the "
+                      f"oracle (numpy float32 GATsSPG restatement + C EPnP), {dt:.1f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=1, help="frames per GPU per step")
+    ap.add_argument("--n1", type=int, default=1024)
+    ap.add_argument("--n3", type=int, default=4096)
+    ap.add_argument("--leaf", type=int, default=8)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    pg = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+        pg = dist
+
+    from onepose_amd import _lib, matcher, synthetic
+    from onepose_amd.pipeline import FramePipeline
+    lib = _lib.load()
+
+    B, n1, n3, L = args.batch, args.n1, args.n3, args.leaf
+    sd = synthetic.make_state_dict(0)
+    data, obj, frames = synthetic.make_matcher_inputs(n1, n3, L, seed=rank * 7919, batch=B)
+    m = matcher.from_state_dict(sd)
+    pipe = FramePipeline(m, data["keypoints3d"][0], data["descriptors3d_db"][0],
+                         data["descriptors2d_db"][0], B, n1, dev, scale=1000.0)
+    pipe.set_frames(data["descriptors2d_query"], data["keypoints2d"],
+                    np.stack([f.K for f in frames]), np.stack([f.pose_gt for f in frames]))
+
+    for _ in range(args.warmup):
+        pipe.enqueue()
+    torch.cuda.synchronize()
+
+    # per-kernel profile pass (all kinds) to find the dominant kernel
+    names = profile_kinds(lib)
+    kinds, ms = run_profiled(lib, pipe, 3, (1 << len(names)) - 1, 4096)
+    per_kind = {}
+    for k, t in zip(kinds, ms):
+        per_kind.setdefault(names[k], []).append(float(t))
+    total = {k: sum(v) / 3.0 for k, v in per_kind.items()}
+    dominant = max((k for k in total if kernel_work(k, B, n1, n3, L)), key=lambda k: total[k])
+    dom_id = names.index(dominant)
+
+    # timed region: K steps, events bracketing every launch of the dominant kernel
+    if pg:
+        pg.barrier()
+    torch.cuda.synchronize()
+    _lib.check(lib.onepose_profile_begin(1 << dom_id, 64 * args.steps + 64), "profile_begin")
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        pipe.enqueue()
+    result = torch.cat([pipe.pose.reshape(B, 12), pipe.R_err[:, None], pipe.t_err[:, None],
+                        pipe.cmd.double(), pipe.n_inliers[:, None].double(),
+                        pipe.status[:, None].double()], 1)
+    if pg:
+        gathered = torch.empty(world * B, result.shape[1], dtype=result.dtype, device=dev)
+        pg.all_gather_into_tensor(gathered, result)
+        result = gathered
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    cap = 64 * args.steps + 64
+    dk, dms = np.zeros(cap, np.int32), np.zeros(cap, np.float32)
+    cnt = np.zeros(1, np.int32)
+    _lib.check(lib.onepose_profile_end(dk.ctypes.data, dms.ctypes.data, cap, cnt.ctypes.data),
+               "profile_end")
+    dom_ms = float(np.mean(dms[:int(cnt[0])]))
+    if pg:
+        t = torch.tensor([elapsed], device=dev)
+        pg.all_reduce(t, op=pg.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    res = result.cpu().numpy()
+    frames_total = world * B * args.steps
+    value = frames_total / elapsed
+    work, unit, bound = kernel_work(dominant, B, n1, n3, L)
+    if unit == "flop":
+        achieved = work / (dom_ms * 1e-3) / 1e12
+        roof = {"bound": "mfma", "achieved": round(achieved, 2), "peak": FP32_MFMA_PEAK_TFLOPS,
+                "unit": "TFLOP/s", "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4),
+                "traffic": None, "kernel": dominant, "avg_launch_us": round(dom_ms * 1e3, 2)}
+    else:
+        achieved = work / (dom_ms * 1e-3) / 1e9
+        roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                "kernel": dominant, "avg_launch_us": round(dom_ms * 1e3, 2)}
+
+    if rank == 0:
+        out = {
+            "metric": METRIC, "value": round(value, 2), "unit": "frames/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "fp32", "data": "synthetic",
+            "config": {"workload": f"config 2: {n1} kpts x {n3} 3D pts, L={L}, {B} frame(s) per "
+                                   f"GPU per step; matcher + RANSAC-EPnP + cm/deg",
+                       "n1": n1, "n3": n3, "num_leaf": L, "batch_per_gpu": B,
+                       "parallelism": f"frame-dp{world}"},
+            "pose": {"cmd1": float(res[:, 14].mean()), "cmd3": float(res[:, 15].mean()),
+                     "cmd5": float(res[:, 16].mean()), "R_err_deg_mean": float(res[:, 12].mean()),
+                     "t_err_cm_mean": float(res[:, 13].mean()),
+                     "n_inliers_mean": float(res[:, 17].mean()),
+                     "status_ok": float((res[:, 18] == 0).mean())},
+            "roofline": roof,
+            "kernel_ms_per_step": {k: round(v, 4) for k, v in sorted(total.items(),
+                                                                     key=lambda kv: -kv[1])},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(sd, data, frames, obj)
+        print(json.dumps(out))
+    if pg:
+        pg.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

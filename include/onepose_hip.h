@@ -1,0 +1,163 @@
+/*
+ * onepose_hip.h -- C-ABI of libonepose_hip.so, the MI355X (gfx950) engine for OnePose's
+ * GATsSPG 2D-3D matching + RANSAC-EPnP hot path.
+ *
+ * Plain pointers and sizes only.  Conventions:
+ *   - every buffer belongs to the caller; the library never allocates or frees device
+ *     memory and never synchronises, so every entry point is hipGraph-capturable;
+ *   - "device" pointers are HIP device memory (e.g. torch tensors' data_ptr()),
+ *     "host" pointers are ordinary CPU memory;
+ *   - `stream` is a hipStream_t passed as void* (NULL = the default stream);
+ *   - every function returns ONEPOSE_OK (0) or an error code, with a thread-local message
+ *     in onepose_last_error(); no C++ exception crosses the ABI.
+ *
+ * The reference (huanghaoran111/OnePose @ /root/reference) has no FFI of its own: its hot
+ * path is PyTorch + OpenCV called from Python.  Each entry point below names the
+ * reference interface it replaces; INTEGRATION.md shows the ctypes binding
+ * (onepose_amd/_lib.py) that a maintainer would drop in.
+ */
+#ifndef ONEPOSE_HIP_H
+#define ONEPOSE_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum {
+  ONEPOSE_OK = 0,
+  ONEPOSE_ERR_INVALID = 1,      /* bad argument / shape                                  */
+  ONEPOSE_ERR_HIP = 2,          /* a HIP runtime call failed                            */
+  ONEPOSE_ERR_UNSUPPORTED = 3,  /* valid in the reference, not supported by this build  */
+  ONEPOSE_ERR_WORKSPACE = 4     /* workspace too small                                  */
+};
+
+/* Thread-local description of the last error ("" when none). */
+const char* onepose_last_error(void);
+/* ABI version, bumped on any signature change. */
+int onepose_abi_version(void);
+
+/* ------------------------------------------------------------------------------------ *
+ * GATsSPG matcher  --  replaces GATsSuperGlue.forward
+ *   (src/models/GATsSPG_architectures/GATs_SuperGlue.py:203-278, reached from
+ *    LitModelGATsSPG.forward, src/models/GATsSPG_lightning_model.py:36-37, and
+ *    inference.py:146)
+ * ------------------------------------------------------------------------------------ */
+
+/* Number of weight tensors the packer consumes, and the reference state-dict key of
+ * tensor i (e.g. "gnn.layers.1.attn.proj.0.weight").  The unused kenc_2d / kenc_3d /
+ * bin_score entries (never read by forward, GATs_SuperGlue.py:172-201) are not listed. */
+int onepose_matcher_num_tensors(void);
+const char* onepose_matcher_tensor_name(int i);
+/* Element count tensor i must have. */
+int64_t onepose_matcher_tensor_numel(int i);
+
+/* Bytes of the packed weight panel. */
+size_t onepose_matcher_packed_bytes(void);
+
+/* Pack the float32 host tensors (in onepose_matcher_tensor_name order) into the
+ * device-ready panel `packed_host` (onepose_matcher_packed_bytes() bytes, host memory).
+ * Packing permutes the q/k/v projections to head-major channel order, folds the GAT
+ * attention vectors through W (h.(W a) == (h W).a, GATs.py:68-69,113-115) and lays the
+ * matrices out as [out][in].  Upload the panel to the device once; it is read-only. */
+int onepose_matcher_pack(const float* const* tensors, int n_tensors, void* packed_host);
+
+/* Workspace bytes onepose_match needs for this shape.  with_conf=0 adds room for the
+ * score matrix that would otherwise live in `conf`. */
+size_t onepose_match_workspace_bytes(int batch, int n1, int n3, int num_leaf, int with_conf);
+
+/* One matcher forward over `batch` frames.
+ *   desc2d  [batch, 256, n1]        descriptors2d_query  (device, fp32)
+ *   desc3d  [batch, 256, n3]        descriptors3d_db     (device; bstride may be 0)
+ *   leaves  [batch, 256, n3*L]      descriptors2d_db     (device; bstride may be 0)
+ *   outputs matches0 [batch, n1] int64, matches1 [batch, n3] int64,
+ *           mscores0 [batch, n1] fp32, mscores1 [batch, n3] fp32,
+ *           conf [batch, n1, n3] fp32 or NULL (conf_matrix).
+ * Batch strides are in elements.  n1, n3 >= 1 (the empty-input branch of
+ * GATs_SuperGlue.py:223-231 is handled by the caller).  1 <= num_leaf <= 16. */
+int onepose_match(const void* packed_weights,
+                  const float* desc2d, int64_t desc2d_bstride,
+                  const float* desc3d, int64_t desc3d_bstride,
+                  const float* leaves, int64_t leaves_bstride,
+                  int batch, int n1, int n3, int num_leaf,
+                  float scale_factor, float match_threshold,
+                  int64_t* matches0, int64_t* matches1,
+                  float* mscores0, float* mscores1, float* conf,
+                  void* workspace, size_t workspace_bytes, void* stream);
+
+/* ------------------------------------------------------------------------------------ *
+ * SuperPoint descriptor sampling  --  replaces sample_descriptors
+ *   (src/models/extractors/SuperPoint/superpoint.py:95-113)
+ * keypoints [batch, n, 2] (x, y) pixels, dense [batch, c, h, w] -> out [batch, c, n],
+ * bilinear, zero padding, L2-normalised over c.  align_corners mirrors the reference's
+ * torch-version switch (superpoint.py:108).  All device pointers.
+ * ------------------------------------------------------------------------------------ */
+int onepose_sample_descriptors(const float* keypoints, const float* dense,
+                               int batch, int n, int c, int h, int w, int s,
+                               int align_corners, float* out, void* stream);
+
+/* ------------------------------------------------------------------------------------ *
+ * Correspondence selection  --  replaces the host-side masking of inference.py:147-152
+ *   (valid = matches > -1; mkpts2d = kpts2d[valid]; mkpts3d = kpts3d[matches[valid]])
+ * plus the float64 scaling + float32 conversion solvePnPRansac applies to its inputs
+ *   (eval_utils.py:22-26).
+ * matches0 [batch, n1] int64, kpts2d [batch, n1, 2] fp32, kpts3d [batch, n3, 3] fp32
+ * (kpts3d bstride may be 0) -> pts2d [batch, n1, 2], pts3d [batch, n1, 3] fp32 compacted
+ * in ascending 2D index order, counts [batch] int32.  All device pointers.
+ * ------------------------------------------------------------------------------------ */
+int onepose_select_correspondences(const int64_t* matches0, const float* kpts2d,
+                                   int64_t kpts2d_bstride, const float* kpts3d,
+                                   int64_t kpts3d_bstride, int batch, int n1, int n3,
+                                   double scale3d, float* pts2d, float* pts3d, int* counts,
+                                   void* stream);
+
+/* ------------------------------------------------------------------------------------ *
+ * Batched RANSAC-EPnP  --  replaces ransac_PnP (src/utils/eval_utils.py:18-42), i.e.
+ *   cv2.solvePnPRansac(pts3d*scale, pts2d, K, 0, reprojectionError, iterationsCount,
+ *                      flags=SOLVEPNP_EPNP) + Rodrigues + tvec/scale,
+ * restated after OpenCV 4.4's solvePnPRansac / RANSACPointSetRegistrator / epnp
+ * (same cv::RNG stream, same subset rule, same adaptive iteration count, final EPnP refit
+ * on the inliers).  One frame per batch entry; frames are independent.
+ *   pts2d [batch, max_points, 2], pts3d [batch, max_points, 3] fp32 (already scaled),
+ *   counts [batch] int32, K [batch, 9] fp64 row-major (K_bstride may be 0).
+ * Outputs: pose34 [batch, 12] fp64 row-major [R | t/scale], inlier_mask
+ * [batch, max_points] uint8, n_inliers [batch] int32, status [batch] int32:
+ *   0 = solved; 1 = fewer than 4 points (reference: cv2.error -> identity pose, no inliers);
+ *   2 = RANSAC found no model (identity pose, no inliers);
+ *   3 = exactly 4 points (P3P branch of solvePnPRansac; identity pose, no inliers).
+ * All device pointers.
+ * ------------------------------------------------------------------------------------ */
+size_t onepose_pnp_workspace_bytes(int batch, int max_points, int max_iters);
+int onepose_pnp_ransac(const float* pts2d, const float* pts3d, const int* counts,
+                       int max_points, const double* K, int64_t K_bstride, int batch,
+                       double scale, float reproj_error, int max_iters, double confidence,
+                       double* pose34, uint8_t* inlier_mask, int* n_inliers, int* status,
+                       void* workspace, size_t workspace_bytes, void* stream);
+
+/* ------------------------------------------------------------------------------------ *
+ * cm/deg pose error  --  replaces query_pose_error (src/utils/eval_utils.py:45-63) and
+ * Evaluator.cm_degree_*_metric (src/evaluators/cmd_evaluator.py:11-31).
+ * pose_pred [batch, 12], pose_gt [batch, 12] fp64 row-major 3x4 (gt bstride may be 0)
+ * -> R_err_deg [batch], t_err_cm [batch] fp64, cmd [batch, 3] uint8 for 1/3/5 cm-deg.
+ * ------------------------------------------------------------------------------------ */
+int onepose_pose_errors(const double* pose_pred, const double* pose_gt, int64_t gt_bstride,
+                        int batch, double* R_err_deg, double* t_err_cm, uint8_t* cmd,
+                        void* stream);
+
+/* ------------------------------------------------------------------------------------ *
+ * Measurement hook (bench.py's roofline).  While enabled, every launch whose kernel kind
+ * is in `kind_mask` (bit k = kind k, names from onepose_profile_kind_name) is bracketed by
+ * two HIP events recorded on the launch's own stream.  Host-side state, not for use during
+ * graph capture.  _end synchronises and returns, per bracketed launch, its kind and the
+ * elapsed milliseconds between its two events.
+ * ------------------------------------------------------------------------------------ */
+int onepose_profile_begin(uint64_t kind_mask, int capacity);
+int onepose_profile_end(int* kinds, float* ms, int capacity, int* count);
+const char* onepose_profile_kind_name(int kind);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ONEPOSE_HIP_H */

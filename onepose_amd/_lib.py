@@ -1,0 +1,86 @@
+"""ctypes binding of libonepose_hip.so (the C-ABI in include/onepose_hip.h).
+
+This is the binding a maintainer of the reference would drop in: plain
+pointers from ``torch.Tensor.data_ptr()``, the current HIP stream, and an int status mapped
+to exceptions.  The library is loaded from the package directory (built in-tree by
+``onepose_amd.build``); there is no fallback -- if it is missing, every call raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libonepose_hip.so")
+
+c_int, c_int64, c_size_t, c_float, c_double = (ctypes.c_int, ctypes.c_int64, ctypes.c_size_t,
+                                               ctypes.c_float, ctypes.c_double)
+c_void_p, c_char_p = ctypes.c_void_p, ctypes.c_char_p
+
+# name -> (restype, argtypes); mirrors include/onepose_hip.h
+PROTOTYPES = {
+    "onepose_last_error": (c_char_p, []),
+    "onepose_abi_version": (c_int, []),
+    "onepose_matcher_num_tensors": (c_int, []),
+    "onepose_matcher_tensor_name": (c_char_p, [c_int]),
+    "onepose_matcher_tensor_numel": (c_int64, [c_int]),
+    "onepose_matcher_packed_bytes": (c_size_t, []),
+    "onepose_matcher_pack": (c_int, [ctypes.POINTER(c_void_p), c_int, c_void_p]),
+    "onepose_match_workspace_bytes": (c_size_t, [c_int, c_int, c_int, c_int, c_int]),
+    "onepose_match": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64,
+                              c_int, c_int, c_int, c_int, c_float, c_float,
+                              c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                              c_void_p, c_size_t, c_void_p]),
+    "onepose_sample_descriptors": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int,
+                                           c_int, c_int, c_void_p, c_void_p]),
+    "onepose_select_correspondences": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_int64,
+                                               c_int, c_int, c_int, c_double, c_void_p, c_void_p,
+                                               c_void_p, c_void_p]),
+    "onepose_pnp_workspace_bytes": (c_size_t, [c_int, c_int, c_int]),
+    "onepose_pnp_ransac": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int64, c_int,
+                                   c_double, c_float, c_int, c_double, c_void_p, c_void_p,
+                                   c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
+    "onepose_pose_errors": (c_int, [c_void_p, c_void_p, c_int64, c_int, c_void_p, c_void_p,
+                                    c_void_p, c_void_p]),
+    "onepose_profile_begin": (c_int, [ctypes.c_uint64, c_int]),
+    "onepose_profile_end": (c_int, [c_void_p, c_void_p, c_int, c_void_p]),
+    "onepose_profile_kind_name": (c_char_p, [c_int]),
+}
+
+_lib = None
+
+
+class OnePoseError(RuntimeError):
+    pass
+
+
+def load():
+    """Load the shared library (raises if it has not been built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise OnePoseError(
+                f"{LIB_PATH} is missing: build it with `python -m onepose_amd.build` "
+                "(onepose_amd has no CPU fallback)")
+        lib = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in PROTOTYPES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = lib
+    return _lib
+
+
+def check(rc: int, what: str = "") -> None:
+    if rc != 0:
+        msg = load().onepose_last_error().decode(errors="replace")
+        raise OnePoseError(f"{what or 'onepose_hip'} failed (status {rc}): {msg}")
+
+
+def stream_ptr(device=None) -> int:
+    import torch
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def ptr(t) -> int:
+    return 0 if t is None else t.data_ptr()

@@ -1,0 +1,66 @@
+// Grouped token-GEMM on gfx950 f32-input MFMA (v_mfma_f32_32x32x2_f32: exact f32 products,
+// f32 accumulation, 157 TF/s dense peak).
+//
+//   Y[b][m][o] = epilogue( sum_k prologue(A)[b][m][k] * W[o][k] + bias[o] )
+//
+// Activations are token-major ([tokens][channels], a token's channels contiguous), so a
+// 1x1 Conv1d of the reference (x [C,N] -> W x + b) is this GEMM with the reference weight
+// [O][C] used as is.  One launch runs up to two problems (the 2D-query side and the 3D
+// side of a layer) and every batch sample of each; tiles never straddle samples, so
+// per-sample reductions (InstanceNorm statistics, softmax partials) stay per sample.
+#pragma once
+
+#include "common.h"
+
+namespace onepose {
+
+enum GemmEpi {
+  EPI_BIAS = 0,    // y = acc + bias
+  EPI_QKV = 1,     // y = acc + bias; col < phi_cols ? elu(y)+1 : y / vdiv   (q,k: phi; v: /Ns)
+  EPI_STATS = 2,   // y = acc + bias, plus per-tile (mean, M2) of every column  (InstanceNorm)
+  EPI_RESID = 3,   // y = R + (acc + bias)                                     (desc += delta)
+  EPI_SCORE = 4,   // y = acc / scale, plus per-tile row/col (max, sum exp)     (dual softmax)
+};
+enum GemmPro {
+  PRO_PLAIN = 0,
+  PRO_NORM_RELU = 1,  // a = max((a - mean[k]) * rstd[k], 0)                    (norm + ReLU)
+};
+
+struct GemmProb {
+  const float* A0;     // [batch][M][lda0]; columns [0, ksplit)
+  const float* A1;     // [batch][M][lda1]; columns [ksplit, K) (concat), may be null
+  int64_t a0_bs, a1_bs;
+  int lda0, lda1, ksplit;
+  const float* W;      // [N][ldw] (out-major); w_bs per sample (0 = shared weights)
+  int64_t w_bs;
+  int ldw;
+  const float* bias;   // [N] or null
+  float* Y;            // [batch][M][ldy]
+  int64_t y_bs;
+  int ldy;
+  const float* R;      // residual, [batch][M][ldr]
+  int64_t r_bs;
+  int ldr;
+  const float* pro_mean;   // [batch][K] (PRO_NORM_RELU)
+  const float* pro_rstd;
+  int64_t pro_bs;
+  float* stats;        // EPI_STATS: [batch][mtiles][2][N]
+  float* rowstat;      // EPI_SCORE: [batch][M][ntiles][2]
+  float* colstat;      // EPI_SCORE: [batch][N][mtiles][2]
+  float scale;         // EPI_SCORE divisor (scale_factor)
+  float vdiv;          // EPI_QKV divisor for columns >= phi_cols
+  int phi_cols;
+  int M, N, K, batch;
+  int mtiles, ntiles, tiles;   // filled by gemm_launch
+};
+
+struct GemmArgs {
+  GemmProb p[2];
+  int nprob;
+};
+
+constexpr int kGemmBM = 64, kGemmBN = 64, kGemmBK = 32;
+
+int gemm_launch(int epi, int pro, GemmArgs& args, hipStream_t stream, int kind);
+
+}  // namespace onepose

@@ -1,0 +1,1064 @@
+// Batched RANSAC-EPnP on gfx950: cv2.solvePnPRansac(..., SOLVEPNP_EPNP) as OpenCV 4.4 runs
+// it (see include/onepose_hip.h and oracle/epnp_ransac.c for the algorithm statement),
+// one workgroup per frame.
+//
+// Per RANSAC round the workgroup takes the next 64 iterations of OpenCV's loop:
+//   1. lane 0 draws the 64 subsets from the cv::RNG stream (sequential by definition:
+//      duplicate indices are redrawn);
+//   2. wave 0 solves one 5-point EPnP per lane (rvec, tvec);
+//   3. all 256 threads count inliers of the 64 models over the frame's points (float32
+//      squared reprojection error <= thr^2, as PnPRansacCallback::computeError);
+//   4. lane 0 replays OpenCV's acceptance rule in iteration order (goodCount >
+//      max(best, 4) -> new best, niters = RANSACUpdateNumIters(...)) and stops the loop
+//      exactly where OpenCV would.
+// Iterations evaluated beyond the stopping point are discarded, so the chosen model, the
+// inlier mask and the iteration count are those of the sequential algorithm.  The final
+// pose is a workgroup-parallel EPnP over the inliers.
+#include "common.h"
+
+namespace onepose {
+namespace {
+
+constexpr int kModelPoints = 5;
+constexpr int kRound = 64;
+constexpr int kThreads = 256;
+
+// ---------------------------------------------------------------------------------------
+// small dense linear algebra, double
+// ---------------------------------------------------------------------------------------
+template <int N>
+__device__ void jacobi_eigen(double* a, double* w, double* vt) {
+  double v[N * N];
+#pragma unroll
+  for (int i = 0; i < N * N; ++i) v[i] = (i % (N + 1) == 0) ? 1.0 : 0.0;
+  for (int sweep = 0; sweep < 60; ++sweep) {
+    double off = 0.0, diag = 0.0;
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      diag += a[i * N + i] * a[i * N + i];
+#pragma unroll
+      for (int j = i + 1; j < N; ++j) off += a[i * N + j] * a[i * N + j];
+    }
+    if (off <= 1e-30 * diag || off == 0.0) break;
+#pragma unroll
+    for (int p = 0; p < N - 1; ++p) {
+#pragma unroll
+      for (int q = p + 1; q < N; ++q) {
+        const double apq = a[p * N + q];
+        if (apq != 0.0) {
+          const double app = a[p * N + p], aqq = a[q * N + q];
+          const double theta = (aqq - app) / (2.0 * apq);
+          const double t = (theta >= 0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
+          const double c = 1.0 / sqrt(t * t + 1.0), s = t * c;
+#pragma unroll
+          for (int k = 0; k < N; ++k) {
+            const double akp = a[k * N + p], akq = a[k * N + q];
+            a[k * N + p] = c * akp - s * akq;
+            a[k * N + q] = s * akp + c * akq;
+          }
+#pragma unroll
+          for (int k = 0; k < N; ++k) {
+            const double apk = a[p * N + k], aqk = a[q * N + k];
+            a[p * N + k] = c * apk - s * aqk;
+            a[q * N + k] = s * apk + c * aqk;
+          }
+#pragma unroll
+          for (int k = 0; k < N; ++k) {
+            const double vkp = v[k * N + p], vkq = v[k * N + q];
+            v[k * N + p] = c * vkp - s * vkq;
+            v[k * N + q] = s * vkp + c * vkq;
+          }
+        }
+      }
+    }
+  }
+  // selection sort of eigenvalues, descending; eigenvectors to rows of vt
+  int order[N];
+#pragma unroll
+  for (int i = 0; i < N; ++i) order[i] = i;
+  for (int i = 0; i < N; ++i)
+    for (int j = i + 1; j < N; ++j)
+      if (a[order[j] * N + order[j]] > a[order[i] * N + order[i]]) {
+        const int t = order[i];
+        order[i] = order[j];
+        order[j] = t;
+      }
+  for (int i = 0; i < N; ++i) {
+    w[i] = a[order[i] * N + order[i]];
+    for (int k = 0; k < N; ++k) vt[i * N + k] = v[k * N + order[i]];
+  }
+}
+
+// least squares by Householder QR, m x n, m <= 6, full column rank
+template <int M, int N>
+__device__ void lstsq(const double* A_, const double* b_, double* x) {
+  double A[M * N], b[M];
+#pragma unroll
+  for (int i = 0; i < M * N; ++i) A[i] = A_[i];
+#pragma unroll
+  for (int i = 0; i < M; ++i) b[i] = b_[i];
+#pragma unroll
+  for (int k = 0; k < N; ++k) {
+    double norm = 0.0;
+#pragma unroll
+    for (int i = k; i < M; ++i) norm += A[i * N + k] * A[i * N + k];
+    norm = sqrt(norm);
+    if (norm == 0.0) continue;
+    const double alpha = A[k * N + k] > 0 ? -norm : norm;
+    double v[M];
+#pragma unroll
+    for (int i = 0; i < M; ++i) v[i] = (i >= k) ? A[i * N + k] : 0.0;
+    v[k] -= alpha;
+    double vv = 0.0;
+#pragma unroll
+    for (int i = k; i < M; ++i) vv += v[i] * v[i];
+    if (vv == 0.0) continue;
+#pragma unroll
+    for (int j = k; j < N; ++j) {
+      double s = 0.0;
+#pragma unroll
+      for (int i = k; i < M; ++i) s += v[i] * A[i * N + j];
+      s = 2.0 * s / vv;
+#pragma unroll
+      for (int i = k; i < M; ++i) A[i * N + j] -= s * v[i];
+    }
+    double s = 0.0;
+#pragma unroll
+    for (int i = k; i < M; ++i) s += v[i] * b[i];
+    s = 2.0 * s / vv;
+#pragma unroll
+    for (int i = k; i < M; ++i) b[i] -= s * v[i];
+  }
+#pragma unroll
+  for (int i = N - 1; i >= 0; --i) {
+    double s = b[i];
+#pragma unroll
+    for (int j = i + 1; j < N; ++j) s -= A[i * N + j] * x[j];
+    x[i] = (A[i * N + i] != 0.0) ? s / A[i * N + i] : 0.0;
+  }
+}
+
+__device__ void inv3(const double* m, double* r) {
+  const double c00 = m[4] * m[8] - m[5] * m[7];
+  const double c01 = m[5] * m[6] - m[3] * m[8];
+  const double c02 = m[3] * m[7] - m[4] * m[6];
+  const double id = 1.0 / (m[0] * c00 + m[1] * c01 + m[2] * c02);
+  r[0] = c00 * id;
+  r[1] = (m[2] * m[7] - m[1] * m[8]) * id;
+  r[2] = (m[1] * m[5] - m[2] * m[4]) * id;
+  r[3] = c01 * id;
+  r[4] = (m[0] * m[8] - m[2] * m[6]) * id;
+  r[5] = (m[2] * m[3] - m[0] * m[5]) * id;
+  r[6] = c02 * id;
+  r[7] = (m[1] * m[6] - m[0] * m[7]) * id;
+  r[8] = (m[0] * m[4] - m[1] * m[3]) * id;
+}
+
+// orthogonal polar factor of a 3x3 matrix (U V^T of its SVD)
+__device__ void polar3(const double* A, double* R) {
+  double ata[9], w[3], vt[9];
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+      ata[i * 3 + j] = A[i] * A[j] + A[3 + i] * A[3 + j] + A[6 + i] * A[6 + j];
+  jacobi_eigen<3>(ata, w, vt);
+  double u[3][3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const double sig = sqrt(w[i] > 0 ? w[i] : 0.0);
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+      const double s = A[r * 3] * vt[i * 3] + A[r * 3 + 1] * vt[i * 3 + 1] + A[r * 3 + 2] * vt[i * 3 + 2];
+      u[i][r] = sig > 1e-300 ? s / sig : 0.0;
+    }
+  }
+  if (!(w[2] > 1e-24 * w[0])) {
+    u[2][0] = u[0][1] * u[1][2] - u[0][2] * u[1][1];
+    u[2][1] = u[0][2] * u[1][0] - u[0][0] * u[1][2];
+    u[2][2] = u[0][0] * u[1][1] - u[0][1] * u[1][0];
+    const double vc0 = vt[1] * vt[5] - vt[2] * vt[4], vc1 = vt[2] * vt[3] - vt[0] * vt[5],
+                 vc2 = vt[0] * vt[4] - vt[1] * vt[3];
+    const double sgn = (vc0 * vt[6] + vc1 * vt[7] + vc2 * vt[8]) >= 0 ? 1.0 : -1.0;
+#pragma unroll
+    for (int r = 0; r < 3; ++r) u[2][r] *= sgn;
+  }
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) R[i * 3 + j] = u[0][i] * vt[j] + u[1][i] * vt[3 + j] + u[2][i] * vt[6 + j];
+}
+
+__device__ __forceinline__ double dot3(const double* a, const double* b) {
+  return a[0] * b[0] + a[1] * b[1] + a[2] * b[2];
+}
+
+// ---------------------------------------------------------------------------------------
+// EPnP pieces that do not depend on the point count (epnp.cpp)
+// ---------------------------------------------------------------------------------------
+__device__ void compute_L_6x10(const double* ut, double* l) {
+  const double* v[4] = {ut + 12 * 11, ut + 12 * 10, ut + 12 * 9, ut + 12 * 8};
+  double dv[4][6][3];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    int a = 0, b = 1;
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+#pragma unroll
+      for (int k = 0; k < 3; ++k) dv[i][j][k] = v[i][3 * a + k] - v[i][3 * b + k];
+      b++;
+      if (b > 3) {
+        a++;
+        b = a + 1;
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    double* row = l + 10 * i;
+    row[0] = dot3(dv[0][i], dv[0][i]);
+    row[1] = 2.0 * dot3(dv[0][i], dv[1][i]);
+    row[2] = dot3(dv[1][i], dv[1][i]);
+    row[3] = 2.0 * dot3(dv[0][i], dv[2][i]);
+    row[4] = 2.0 * dot3(dv[1][i], dv[2][i]);
+    row[5] = dot3(dv[2][i], dv[2][i]);
+    row[6] = 2.0 * dot3(dv[0][i], dv[3][i]);
+    row[7] = 2.0 * dot3(dv[1][i], dv[3][i]);
+    row[8] = 2.0 * dot3(dv[2][i], dv[3][i]);
+    row[9] = dot3(dv[3][i], dv[3][i]);
+  }
+}
+
+__device__ void compute_rho(const double (*cws)[3], double* rho) {
+  auto d2 = [](const double* a, const double* b) {
+    return (a[0] - b[0]) * (a[0] - b[0]) + (a[1] - b[1]) * (a[1] - b[1]) + (a[2] - b[2]) * (a[2] - b[2]);
+  };
+  rho[0] = d2(cws[0], cws[1]);
+  rho[1] = d2(cws[0], cws[2]);
+  rho[2] = d2(cws[0], cws[3]);
+  rho[3] = d2(cws[1], cws[2]);
+  rho[4] = d2(cws[1], cws[3]);
+  rho[5] = d2(cws[2], cws[3]);
+}
+
+__device__ void betas_approx(int which, const double* L, const double* rho, double* betas) {
+  if (which == 1) {
+    double l[24], b4[4];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+      l[i * 4 + 0] = L[i * 10 + 0];
+      l[i * 4 + 1] = L[i * 10 + 1];
+      l[i * 4 + 2] = L[i * 10 + 3];
+      l[i * 4 + 3] = L[i * 10 + 6];
+    }
+    lstsq<6, 4>(l, rho, b4);
+    const double sg = b4[0] < 0 ? -1.0 : 1.0;
+    betas[0] = sqrt(sg * b4[0]);
+    betas[1] = sg * b4[1] / betas[0];
+    betas[2] = sg * b4[2] / betas[0];
+    betas[3] = sg * b4[3] / betas[0];
+  } else if (which == 2) {
+    double l[18], b3[3];
+#pragma unroll
+    for (int i = 0; i < 6; ++i)
+#pragma unroll
+      for (int k = 0; k < 3; ++k) l[i * 3 + k] = L[i * 10 + k];
+    lstsq<6, 3>(l, rho, b3);
+    if (b3[0] < 0) {
+      betas[0] = sqrt(-b3[0]);
+      betas[1] = (b3[2] < 0) ? sqrt(-b3[2]) : 0.0;
+    } else {
+      betas[0] = sqrt(b3[0]);
+      betas[1] = (b3[2] > 0) ? sqrt(b3[2]) : 0.0;
+    }
+    if (b3[1] < 0) betas[0] = -betas[0];
+    betas[2] = 0.0;
+    betas[3] = 0.0;
+  } else {
+    double l[30], b5[5];
+#pragma unroll
+    for (int i = 0; i < 6; ++i)
+#pragma unroll
+      for (int k = 0; k < 5; ++k) l[i * 5 + k] = L[i * 10 + k];
+    lstsq<6, 5>(l, rho, b5);
+    if (b5[0] < 0) {
+      betas[0] = sqrt(-b5[0]);
+      betas[1] = (b5[2] < 0) ? sqrt(-b5[2]) : 0.0;
+    } else {
+      betas[0] = sqrt(b5[0]);
+      betas[1] = (b5[2] > 0) ? sqrt(b5[2]) : 0.0;
+    }
+    if (b5[1] < 0) betas[0] = -betas[0];
+    betas[2] = b5[3] / betas[0];
+    betas[3] = 0.0;
+  }
+}
+
+// epnp::qr_solve for the 6x4 Gauss-Newton system
+__device__ void qr_solve_6x4(double* A, double* b, double* X) {
+  constexpr int nr = 6, nc = 4;
+  double A1[nc], A2[nc];
+#pragma unroll
+  for (int k = 0; k < nc; k++) {
+    double eta = fabs(A[k * nc + k]);
+#pragma unroll
+    // epnp.cpp reads the pivot column before advancing, so rows k..nr-2 are scanned
+    for (int i = k + 1; i < nr; i++) eta = fmax(eta, fabs(A[(i - 1) * nc + k]));
+    if (eta == 0) return;   // X keeps its previous value, as in epnp.cpp
+    double sum2 = 0.0;
+    const double inv_eta = 1. / eta;
+#pragma unroll
+    for (int i = k; i < nr; i++) {
+      A[i * nc + k] *= inv_eta;
+      sum2 += A[i * nc + k] * A[i * nc + k];
+    }
+    double sigma = sqrt(sum2);
+    if (A[k * nc + k] < 0) sigma = -sigma;
+    A[k * nc + k] += sigma;
+    A1[k] = sigma * A[k * nc + k];
+    A2[k] = -eta * sigma;
+#pragma unroll
+    for (int j = k + 1; j < nc; j++) {
+      double sum = 0;
+#pragma unroll
+      for (int i = k; i < nr; i++) sum += A[i * nc + k] * A[i * nc + j];
+      const double tau = sum / A1[k];
+#pragma unroll
+      for (int i = k; i < nr; i++) A[i * nc + j] -= tau * A[i * nc + k];
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < nc; j++) {
+    double tau = 0;
+#pragma unroll
+    for (int i = j; i < nr; i++) tau += A[i * nc + j] * b[i];
+    tau /= A1[j];
+#pragma unroll
+    for (int i = j; i < nr; i++) b[i] -= tau * A[i * nc + j];
+  }
+  X[nc - 1] = b[nc - 1] / A2[nc - 1];
+#pragma unroll
+  for (int i = nc - 2; i >= 0; i--) {
+    double sum = 0;
+#pragma unroll
+    for (int j = i + 1; j < nc; j++) sum += A[i * nc + j] * X[j];
+    X[i] = (b[i] - sum) / A2[i];
+  }
+}
+
+__device__ void gauss_newton(const double* L, const double* rho, double* betas) {
+  double x[4] = {0.0, 0.0, 0.0, 0.0};
+  for (int it = 0; it < 5; ++it) {
+    double A[24], b[6];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+      const double* r = L + i * 10;
+      A[i * 4 + 0] = 2 * r[0] * betas[0] + r[1] * betas[1] + r[3] * betas[2] + r[6] * betas[3];
+      A[i * 4 + 1] = r[1] * betas[0] + 2 * r[2] * betas[1] + r[4] * betas[2] + r[7] * betas[3];
+      A[i * 4 + 2] = r[3] * betas[0] + r[4] * betas[1] + 2 * r[5] * betas[2] + r[8] * betas[3];
+      A[i * 4 + 3] = r[6] * betas[0] + r[7] * betas[1] + r[8] * betas[2] + 2 * r[9] * betas[3];
+      b[i] = rho[i] - (r[0] * betas[0] * betas[0] + r[1] * betas[0] * betas[1] +
+                       r[2] * betas[1] * betas[1] + r[3] * betas[0] * betas[2] +
+                       r[4] * betas[1] * betas[2] + r[5] * betas[2] * betas[2] +
+                       r[6] * betas[0] * betas[3] + r[7] * betas[1] * betas[3] +
+                       r[8] * betas[2] * betas[3] + r[9] * betas[3] * betas[3]);
+    }
+    qr_solve_6x4(A, b, x);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) betas[i] += x[i];
+  }
+}
+
+__device__ void ccs_from_betas(const double* ut, const double* betas, double (*ccs)[3]) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) ccs[j][0] = ccs[j][1] = ccs[j][2] = 0.0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const double* v = ut + 12 * (11 - i);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int k = 0; k < 3; ++k) ccs[j][k] += betas[i] * v[3 * j + k];
+  }
+}
+
+__device__ void finish_R(const double* abt, double* R) {
+  polar3(abt, R);
+  const double det = R[0] * R[4] * R[8] + R[1] * R[5] * R[6] + R[2] * R[3] * R[7] -
+                     R[2] * R[4] * R[6] - R[1] * R[3] * R[8] - R[0] * R[5] * R[7];
+  if (det < 0) {
+    R[6] = -R[6];
+    R[7] = -R[7];
+    R[8] = -R[8];
+  }
+}
+
+__device__ void rodrigues_m2v(const double* R, double* r) {
+  double rx = R[7] - R[5], ry = R[2] - R[6], rz = R[3] - R[1];
+  const double s = sqrt((rx * rx + ry * ry + rz * rz) * 0.25);
+  double c = (R[0] + R[4] + R[8] - 1) * 0.5;
+  c = c > 1. ? 1. : c < -1. ? -1. : c;
+  double theta = acos(c);
+  if (s < 1e-5) {
+    if (c > 0) {
+      rx = ry = rz = 0;
+    } else {
+      double t = (R[0] + 1) * 0.5;
+      rx = sqrt(t > 0 ? t : 0.);
+      t = (R[4] + 1) * 0.5;
+      ry = sqrt(t > 0 ? t : 0.) * (R[1] < 0 ? -1. : 1.);
+      t = (R[8] + 1) * 0.5;
+      rz = sqrt(t > 0 ? t : 0.) * (R[2] < 0 ? -1. : 1.);
+      if (fabs(rx) < fabs(ry) && fabs(rx) < fabs(rz) && (R[5] > 0) != (ry * rz > 0)) rz = -rz;
+      theta /= sqrt(rx * rx + ry * ry + rz * rz);
+      rx *= theta;
+      ry *= theta;
+      rz *= theta;
+    }
+  } else {
+    const double vth = theta * (1 / (2 * s));
+    rx *= vth;
+    ry *= vth;
+    rz *= vth;
+  }
+  r[0] = rx;
+  r[1] = ry;
+  r[2] = rz;
+}
+
+__device__ void rodrigues_v2m(const double* r, double* R) {
+  const double theta = sqrt(r[0] * r[0] + r[1] * r[1] + r[2] * r[2]);
+  if (theta < 2.220446049250313e-16) {
+#pragma unroll
+    for (int i = 0; i < 9; ++i) R[i] = (i % 4 == 0) ? 1.0 : 0.0;
+    return;
+  }
+  const double c = cos(theta), s = sin(theta), c1 = 1. - c;
+  const double it = 1. / theta;
+  const double x = r[0] * it, y = r[1] * it, z = r[2] * it;
+  const double rrt[9] = {x * x, x * y, x * z, x * y, y * y, y * z, x * z, y * z, z * z};
+  const double rx[9] = {0, -z, y, z, 0, -x, -y, x, 0};
+#pragma unroll
+  for (int i = 0; i < 9; ++i) R[i] = c * ((i % 4 == 0) ? 1.0 : 0.0) + c1 * rrt[i] + s * rx[i];
+}
+
+// ---------------------------------------------------------------------------------------
+// 5-point EPnP, one lane (RANSAC kernel): epnp::compute_pose with n = 5
+// ---------------------------------------------------------------------------------------
+__device__ void epnp5(const double* pws, const double* us, const double* K4, double* rvec,
+                      double* tvec) {
+  constexpr int n = kModelPoints;
+  const double fu = K4[0], fv = K4[1], uc = K4[2], vc = K4[3];
+  double cws[4][3];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    double s = 0.0;
+#pragma unroll
+    for (int i = 0; i < n; ++i) s += pws[3 * i + j];
+    cws[0][j] = s / n;
+  }
+  {
+    double m[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, dc[3], uct[9];
+#pragma unroll
+    for (int i = 0; i < n; ++i) {
+      double p[3];
+#pragma unroll
+      for (int j = 0; j < 3; ++j) p[j] = pws[3 * i + j] - cws[0][j];
+#pragma unroll
+      for (int r = 0; r < 3; ++r)
+#pragma unroll
+        for (int c = 0; c < 3; ++c) m[r * 3 + c] += p[r] * p[c];
+    }
+    jacobi_eigen<3>(m, dc, uct);
+#pragma unroll
+    for (int i = 1; i < 4; ++i) {
+      const double k = sqrt(dc[i - 1] / n);
+#pragma unroll
+      for (int j = 0; j < 3; ++j) cws[i][j] = cws[0][j] + k * uct[3 * (i - 1) + j];
+    }
+  }
+  double alphas[n * 4];
+  {
+    double cc[9], ci[9];
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+      for (int j = 1; j < 4; ++j) cc[3 * i + j - 1] = cws[j][i] - cws[0][i];
+    inv3(cc, ci);
+#pragma unroll
+    for (int i = 0; i < n; ++i) {
+      const double* pi = pws + 3 * i;
+      double* a = alphas + 4 * i;
+#pragma unroll
+      for (int j = 0; j < 3; ++j)
+        a[1 + j] = ci[3 * j] * (pi[0] - cws[0][0]) + ci[3 * j + 1] * (pi[1] - cws[0][1]) +
+                   ci[3 * j + 2] * (pi[2] - cws[0][2]);
+      a[0] = 1.0 - a[1] - a[2] - a[3];
+    }
+  }
+  double mtm[144];
+#pragma unroll
+  for (int i = 0; i < 144; ++i) mtm[i] = 0.0;
+#pragma unroll
+  for (int i = 0; i < n; ++i) {
+    const double* as = alphas + 4 * i;
+    const double u = us[2 * i], v = us[2 * i + 1];
+    double r1[12], r2[12];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      r1[3 * k] = as[k] * fu;
+      r1[3 * k + 1] = 0.0;
+      r1[3 * k + 2] = as[k] * (uc - u);
+      r2[3 * k] = 0.0;
+      r2[3 * k + 1] = as[k] * fv;
+      r2[3 * k + 2] = as[k] * (vc - v);
+    }
+#pragma unroll
+    for (int a = 0; a < 12; ++a)
+#pragma unroll
+      for (int b = 0; b < 12; ++b) mtm[a * 12 + b] += r1[a] * r1[b] + r2[a] * r2[b];
+  }
+  double d[12], ut[144];
+  jacobi_eigen<12>(mtm, d, ut);
+  double L[60], rho[6];
+  compute_L_6x10(ut, L);
+  compute_rho(cws, rho);
+  double bestR[9], bestT[3], bestErr = 0.0;
+  for (int which = 1; which <= 3; ++which) {
+    double betas[4], ccs[4][3], pcs[n * 3];
+    betas_approx(which, L, rho, betas);
+    gauss_newton(L, rho, betas);
+    ccs_from_betas(ut, betas, ccs);
+#pragma unroll
+    for (int i = 0; i < n; ++i) {
+      const double* a = alphas + 4 * i;
+#pragma unroll
+      for (int j = 0; j < 3; ++j)
+        pcs[3 * i + j] = a[0] * ccs[0][j] + a[1] * ccs[1][j] + a[2] * ccs[2][j] + a[3] * ccs[3][j];
+    }
+    if (pcs[2] < 0.0) {
+#pragma unroll
+      for (int i = 0; i < 3 * n; ++i) pcs[i] = -pcs[i];
+    }
+    double pc0[3] = {0, 0, 0}, pw0[3] = {0, 0, 0};
+#pragma unroll
+    for (int i = 0; i < n; ++i)
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        pc0[j] += pcs[3 * i + j];
+        pw0[j] += pws[3 * i + j];
+      }
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      pc0[j] /= n;
+      pw0[j] /= n;
+    }
+    double abt[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int i = 0; i < n; ++i)
+#pragma unroll
+      for (int j = 0; j < 3; ++j)
+#pragma unroll
+        for (int k = 0; k < 3; ++k)
+          abt[3 * j + k] += (pcs[3 * i + j] - pc0[j]) * (pws[3 * i + k] - pw0[k]);
+    double R[9], t[3];
+    finish_R(abt, R);
+#pragma unroll
+    for (int j = 0; j < 3; ++j) t[j] = pc0[j] - dot3(R + 3 * j, pw0);
+    double err = 0.0;
+#pragma unroll
+    for (int i = 0; i < n; ++i) {
+      const double* pw = pws + 3 * i;
+      const double Xc = dot3(R, pw) + t[0], Yc = dot3(R + 3, pw) + t[1];
+      const double iz = 1.0 / (dot3(R + 6, pw) + t[2]);
+      const double ue = uc + fu * Xc * iz, ve = vc + fv * Yc * iz;
+      const double du = us[2 * i] - ue, dv = us[2 * i + 1] - ve;
+      err += sqrt(du * du + dv * dv);
+    }
+    err /= n;
+    if (which == 1 || err < bestErr) {
+      bestErr = err;
+#pragma unroll
+      for (int i = 0; i < 9; ++i) bestR[i] = R[i];
+#pragma unroll
+      for (int i = 0; i < 3; ++i) bestT[i] = t[i];
+    }
+  }
+  rodrigues_m2v(bestR, rvec);
+#pragma unroll
+  for (int i = 0; i < 3; ++i) tvec[i] = bestT[i];
+}
+
+// RANSACUpdateNumIters (ptsetreg.cpp)
+__device__ int update_num_iters(double p, double ep, int model_points, int max_iters) {
+  p = fmin(fmax(p, 0.0), 1.0);
+  ep = fmin(fmax(ep, 0.0), 1.0);
+  double num = fmax(1. - p, 2.2250738585072014e-308);
+  double denom = 1. - pow(1. - ep, (double)model_points);
+  if (denom < 2.2250738585072014e-308) return 0;
+  num = log(num);
+  denom = log(denom);
+  return (denom >= 0 || -num >= max_iters * (-denom)) ? max_iters : __double2int_rn(num / denom);
+}
+
+// squared float reprojection error of one point (computeError; no fp contraction)
+__device__ __forceinline__ float reproj_err2(const double* R, const double* t, const double* K4,
+                                             float X, float Y, float Z, float u, float v) {
+#pragma clang fp contract(off)
+  const double x = R[0] * X + R[1] * Y + R[2] * Z + t[0];
+  const double y = R[3] * X + R[4] * Y + R[5] * Z + t[1];
+  double z = R[6] * X + R[7] * Y + R[8] * Z + t[2];
+  z = z != 0.0 ? 1. / z : 1.0;
+  const float pu = (float)(x * z * K4[0] + K4[2]);
+  const float pv = (float)(y * z * K4[1] + K4[3]);
+  const float du = u - pu, dv = v - pv;
+  return du * du + dv * dv;
+}
+
+// ---------------------------------------------------------------------------------------
+// workgroup reductions (double)
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// sum `cnt` per-thread values across the workgroup; every thread gets the totals
+template <int CNT>
+__device__ void block_sum(double* vals, double* scratch /* [4][CNT] */) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int i = 0; i < CNT; ++i) {
+    const double s = wave_sum_d(vals[i]);
+    if (lane == 0) scratch[wave * CNT + i] = s;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < CNT; ++i)
+    vals[i] = scratch[i] + scratch[CNT + i] + scratch[2 * CNT + i] + scratch[3 * CNT + i];
+  __syncthreads();
+}
+
+struct Shared {
+  // RANSAC round
+  int subset[kRound][kModelPoints];
+  double hypR[kRound][9];
+  double hypT[kRound][3];
+  double hypRvec[kRound][3];
+  int count[kRound];
+  // control
+  int iter, niters, max_good, done;
+  double bestRvec[3], bestT[3];
+  unsigned long long rng;
+  // refit
+  double red[4 * 78];
+  double cws[4][3];
+  double ci[9];
+  double ut[144];
+  double L[60], rho[6];
+  double betas[4];
+  double ccs[4][3];
+  double sol_R[4][9], sol_t[4][3], sol_err[4];
+  double flip;
+  int wave_cnt[4];
+  int n_inl;
+};
+
+// Workgroup-parallel EPnP over the points listed in idx[0..n) (epnp::compute_pose).
+__device__ void epnp_refit(Shared& sh, const float* p2, const float* p3, const int* idx, int n,
+                           const double* K4, double* R_out, double* t_out) {
+  const int t = threadIdx.x;
+  const double fu = K4[0], fv = K4[1], uc = K4[2], vc = K4[3];
+  // centroid
+  double v3[3] = {0, 0, 0};
+  for (int i = t; i < n; i += kThreads) {
+    const int j = idx[i];
+    v3[0] += (double)p3[3 * j];
+    v3[1] += (double)p3[3 * j + 1];
+    v3[2] += (double)p3[3 * j + 2];
+  }
+  block_sum<3>(v3, sh.red);
+  const double c0[3] = {v3[0] / n, v3[1] / n, v3[2] / n};
+  // PCA
+  double m6[6] = {0, 0, 0, 0, 0, 0};
+  for (int i = t; i < n; i += kThreads) {
+    const int j = idx[i];
+    const double p0 = (double)p3[3 * j] - c0[0], p1 = (double)p3[3 * j + 1] - c0[1],
+                 p2_ = (double)p3[3 * j + 2] - c0[2];
+    m6[0] += p0 * p0;
+    m6[1] += p0 * p1;
+    m6[2] += p0 * p2_;
+    m6[3] += p1 * p1;
+    m6[4] += p1 * p2_;
+    m6[5] += p2_ * p2_;
+  }
+  block_sum<6>(m6, sh.red);
+  if (t == 0) {
+    double m[9] = {m6[0], m6[1], m6[2], m6[1], m6[3], m6[4], m6[2], m6[4], m6[5]}, dc[3], uct[9];
+    jacobi_eigen<3>(m, dc, uct);
+    for (int j = 0; j < 3; ++j) sh.cws[0][j] = c0[j];
+    for (int i = 1; i < 4; ++i) {
+      const double k = sqrt(dc[i - 1] / n);
+      for (int j = 0; j < 3; ++j) sh.cws[i][j] = c0[j] + k * uct[3 * (i - 1) + j];
+    }
+    double cc[9];
+    for (int i = 0; i < 3; ++i)
+      for (int j = 1; j < 4; ++j) cc[3 * i + j - 1] = sh.cws[j][i] - sh.cws[0][i];
+    inv3(cc, sh.ci);
+  }
+  __syncthreads();
+  auto alphas = [&](int j, double* a) {
+    const double d0 = (double)p3[3 * j] - sh.cws[0][0], d1 = (double)p3[3 * j + 1] - sh.cws[0][1],
+                 d2 = (double)p3[3 * j + 2] - sh.cws[0][2];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) a[1 + k] = sh.ci[3 * k] * d0 + sh.ci[3 * k + 1] * d1 + sh.ci[3 * k + 2] * d2;
+    a[0] = 1.0 - a[1] - a[2] - a[3];
+  };
+  // M^T M (upper triangle, 78 entries)
+  double acc[78];
+#pragma unroll
+  for (int i = 0; i < 78; ++i) acc[i] = 0.0;
+  for (int i = t; i < n; i += kThreads) {
+    const int j = idx[i];
+    double as[4];
+    alphas(j, as);
+    const double u = (double)p2[2 * j], v = (double)p2[2 * j + 1];
+    double r1[12], r2[12];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      r1[3 * k] = as[k] * fu;
+      r1[3 * k + 1] = 0.0;
+      r1[3 * k + 2] = as[k] * (uc - u);
+      r2[3 * k] = 0.0;
+      r2[3 * k + 1] = as[k] * fv;
+      r2[3 * k + 2] = as[k] * (vc - v);
+    }
+    int e = 0;
+#pragma unroll
+    for (int a = 0; a < 12; ++a)
+#pragma unroll
+      for (int b = a; b < 12; ++b) acc[e++] += r1[a] * r1[b] + r2[a] * r2[b];
+  }
+  block_sum<78>(acc, sh.red);
+  if (t == 0) {
+    double mtm[144], d[12];
+    int e = 0;
+    for (int a = 0; a < 12; ++a)
+      for (int b = a; b < 12; ++b) {
+        mtm[a * 12 + b] = acc[e];
+        mtm[b * 12 + a] = acc[e];
+        ++e;
+      }
+    jacobi_eigen<12>(mtm, d, sh.ut);
+    compute_L_6x10(sh.ut, sh.L);
+    compute_rho(sh.cws, sh.rho);
+  }
+  __syncthreads();
+  for (int which = 1; which <= 3; ++which) {
+    if (t == 0) {
+      double betas[4];
+      betas_approx(which, sh.L, sh.rho, betas);
+      gauss_newton(sh.L, sh.rho, betas);
+      ccs_from_betas(sh.ut, betas, sh.ccs);
+      // solve_for_sign looks at the first point's camera-frame depth
+      double a[4];
+      alphas(idx[0], a);
+      const double z0 = a[0] * sh.ccs[0][2] + a[1] * sh.ccs[1][2] + a[2] * sh.ccs[2][2] + a[3] * sh.ccs[3][2];
+      sh.flip = z0 < 0.0 ? -1.0 : 1.0;
+    }
+    __syncthreads();
+    const double fl = sh.flip;
+    auto pc_of = [&](int j, double* pc) {
+      double a[4];
+      alphas(j, a);
+#pragma unroll
+      for (int k = 0; k < 3; ++k)
+        pc[k] = fl * (a[0] * sh.ccs[0][k] + a[1] * sh.ccs[1][k] + a[2] * sh.ccs[2][k] + a[3] * sh.ccs[3][k]);
+    };
+    double s6[6] = {0, 0, 0, 0, 0, 0};
+    for (int i = t; i < n; i += kThreads) {
+      const int j = idx[i];
+      double pc[3];
+      pc_of(j, pc);
+      s6[0] += pc[0];
+      s6[1] += pc[1];
+      s6[2] += pc[2];
+      s6[3] += (double)p3[3 * j];
+      s6[4] += (double)p3[3 * j + 1];
+      s6[5] += (double)p3[3 * j + 2];
+    }
+    block_sum<6>(s6, sh.red);
+    const double pc0[3] = {s6[0] / n, s6[1] / n, s6[2] / n}, pw0[3] = {s6[3] / n, s6[4] / n, s6[5] / n};
+    double abt[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    for (int i = t; i < n; i += kThreads) {
+      const int j = idx[i];
+      double pc[3];
+      pc_of(j, pc);
+      const double pw[3] = {(double)p3[3 * j] - pw0[0], (double)p3[3 * j + 1] - pw0[1],
+                            (double)p3[3 * j + 2] - pw0[2]};
+#pragma unroll
+      for (int a = 0; a < 3; ++a)
+#pragma unroll
+        for (int b = 0; b < 3; ++b) abt[3 * a + b] += (pc[a] - pc0[a]) * pw[b];
+    }
+    block_sum<9>(abt, sh.red);
+    if (t == 0) {
+      double* R = sh.sol_R[which];
+      finish_R(abt, R);
+      for (int j = 0; j < 3; ++j) sh.sol_t[which][j] = pc0[j] - dot3(R + 3 * j, pw0);
+    }
+    __syncthreads();
+    double err[1] = {0.0};
+    {
+      const double* R = sh.sol_R[which];
+      const double* tt = sh.sol_t[which];
+      for (int i = t; i < n; i += kThreads) {
+        const int j = idx[i];
+        const double pw[3] = {(double)p3[3 * j], (double)p3[3 * j + 1], (double)p3[3 * j + 2]};
+        const double Xc = dot3(R, pw) + tt[0], Yc = dot3(R + 3, pw) + tt[1];
+        const double iz = 1.0 / (dot3(R + 6, pw) + tt[2]);
+        const double ue = uc + fu * Xc * iz, ve = vc + fv * Yc * iz;
+        const double du = (double)p2[2 * j] - ue, dv = (double)p2[2 * j + 1] - ve;
+        err[0] += sqrt(du * du + dv * dv);
+      }
+    }
+    block_sum<1>(err, sh.red);
+    if (t == 0) sh.sol_err[which] = err[0] / n;
+    __syncthreads();
+  }
+  int N = 1;
+  if (sh.sol_err[2] < sh.sol_err[1]) N = 2;
+  if (sh.sol_err[3] < sh.sol_err[N]) N = 3;
+  for (int i = 0; i < 9; ++i) R_out[i] = sh.sol_R[N][i];
+  for (int i = 0; i < 3; ++i) t_out[i] = sh.sol_t[N][i];
+}
+
+__device__ __forceinline__ unsigned rng_next(unsigned long long& s) {
+  s = (unsigned long long)(unsigned)s * 4164903690ull + (unsigned)(s >> 32);
+  return (unsigned)s;
+}
+
+__global__ __launch_bounds__(kThreads) void pnp_ransac_kernel(
+    const float* __restrict__ pts2d, const float* __restrict__ pts3d, const int* __restrict__ counts,
+    int max_points, const double* __restrict__ Kmat, int64_t K_bs, double scale, float reproj,
+    int max_iters, double confidence, double* __restrict__ pose34, uint8_t* __restrict__ mask_out,
+    int* __restrict__ n_inliers, int* __restrict__ status, int* __restrict__ idx_ws) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char dyn[];
+  Shared& sh = *reinterpret_cast<Shared*>(dyn);
+  float* p2 = reinterpret_cast<float*>(dyn + ((sizeof(Shared) + 15) / 16) * 16);
+  float* p3 = p2 + 2 * max_points;
+  const int b = blockIdx.x;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int n = min(counts[b], max_points);
+  const double* K = Kmat + b * K_bs;
+  const double K4[4] = {K[0], K[4], K[2], K[5]};
+  uint8_t* mask = mask_out + (int64_t)b * max_points;
+  int* idx = idx_ws + (int64_t)b * max_points;
+  double* pose = pose34 + (int64_t)b * 12;
+
+  for (int i = t; i < max_points; i += kThreads) mask[i] = 0;
+  auto identity = [&](int st) {
+    if (t < 12) pose[t] = (t % 5 == 0) ? 1.0 : 0.0;
+    if (t == 0) {
+      n_inliers[b] = 0;
+      status[b] = st;
+    }
+  };
+  if (n < 4) {
+    identity(1);
+    return;
+  }
+  if (n == 4) {
+    identity(3);
+    return;
+  }
+  for (int i = t; i < n; i += kThreads) {
+    p2[2 * i] = pts2d[((int64_t)b * max_points + i) * 2];
+    p2[2 * i + 1] = pts2d[((int64_t)b * max_points + i) * 2 + 1];
+    p3[3 * i] = pts3d[((int64_t)b * max_points + i) * 3];
+    p3[3 * i + 1] = pts3d[((int64_t)b * max_points + i) * 3 + 1];
+    p3[3 * i + 2] = pts3d[((int64_t)b * max_points + i) * 3 + 2];
+  }
+  const float thr = (float)((double)reproj * (double)reproj);
+  if (t == 0) {
+    sh.iter = 0;
+    sh.niters = max(max_iters, 1);
+    sh.max_good = 0;
+    sh.done = (n == kModelPoints) ? 1 : 0;
+    sh.rng = 0xFFFFFFFFFFFFFFFFull;
+  }
+  __syncthreads();
+
+  while (!sh.done) {
+    if (t == 0) {  // getSubset x 64, in iteration order
+      unsigned long long s = sh.rng;
+      for (int h = 0; h < kRound; ++h) {
+        for (int i = 0; i < kModelPoints;) {
+          int ii, j;
+          for (;;) {
+            ii = (int)(rng_next(s) % (unsigned)n);
+            for (j = 0; j < i; ++j)
+              if (ii == sh.subset[h][j]) break;
+            if (j == i) break;
+          }
+          sh.subset[h][i] = ii;
+          ++i;
+        }
+      }
+      sh.rng = s;
+    }
+    __syncthreads();
+    if (wave == 0) {  // one EPnP model per lane
+      double pws[15], us[10], rvec[3], tvec[3];
+#pragma unroll
+      for (int i = 0; i < kModelPoints; ++i) {
+        const int j = sh.subset[lane][i];
+        pws[3 * i] = p3[3 * j];
+        pws[3 * i + 1] = p3[3 * j + 1];
+        pws[3 * i + 2] = p3[3 * j + 2];
+        us[2 * i] = p2[2 * j];
+        us[2 * i + 1] = p2[2 * j + 1];
+      }
+      epnp5(pws, us, K4, rvec, tvec);
+      double R[9];
+      rodrigues_v2m(rvec, R);
+      for (int i = 0; i < 9; ++i) sh.hypR[lane][i] = R[i];
+      for (int i = 0; i < 3; ++i) {
+        sh.hypT[lane][i] = tvec[i];
+        sh.hypRvec[lane][i] = rvec[i];
+      }
+      sh.count[lane] = 0;
+    }
+    __syncthreads();
+    // inlier counts: wave w takes hypotheses w, w+4, ...; lanes sweep the points
+    for (int h = wave; h < kRound; h += 4) {
+      int c = 0;
+      for (int i = lane; i < n; i += 64)
+        c += reproj_err2(sh.hypR[h], sh.hypT[h], K4, p3[3 * i], p3[3 * i + 1], p3[3 * i + 2],
+                         p2[2 * i], p2[2 * i + 1]) <= thr;
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) c += __shfl_xor(c, o, 64);
+      if (lane == 0) sh.count[h] = c;
+    }
+    __syncthreads();
+    if (t == 0) {  // OpenCV's acceptance rule, in iteration order
+      int iter = sh.iter, niters = sh.niters, best = sh.max_good;
+      for (int h = 0; h < kRound && iter < niters; ++h, ++iter) {
+        const int good = sh.count[h];
+        if (good > max(best, kModelPoints - 1)) {
+          best = good;
+          for (int i = 0; i < 3; ++i) {
+            sh.bestRvec[i] = sh.hypRvec[h][i];
+            sh.bestT[i] = sh.hypT[h][i];
+          }
+          niters = update_num_iters(confidence, (double)(n - good) / n, kModelPoints, niters);
+        }
+      }
+      sh.iter = iter;
+      sh.niters = niters;
+      sh.max_good = best;
+      sh.done = iter >= niters;
+    }
+    __syncthreads();
+  }
+
+  int nin;
+  if (n == kModelPoints) {
+    for (int i = t; i < n; i += kThreads) idx[i] = i;
+    nin = n;
+  } else {
+    if (sh.max_good <= 0) {
+      identity(2);
+      return;
+    }
+    // inlier mask of the best model, compacted in point order
+    double R[9];
+    rodrigues_v2m(sh.bestRvec, R);
+    if (t == 0) sh.n_inl = 0;
+    __syncthreads();
+    for (int base = 0; base < n; base += kThreads) {
+      const int i = base + t;
+      bool in = false;
+      if (i < n)
+        in = reproj_err2(R, sh.bestT, K4, p3[3 * i], p3[3 * i + 1], p3[3 * i + 2], p2[2 * i],
+                         p2[2 * i + 1]) <= thr;
+      const unsigned long long bal = __ballot(in);
+      if (lane == 0) sh.wave_cnt[wave] = __popcll(bal);
+      __syncthreads();
+      int off = sh.n_inl;
+      for (int w = 0; w < wave; ++w) off += sh.wave_cnt[w];
+      if (in) {
+        idx[off + __popcll(bal & ((1ull << lane) - 1ull))] = i;
+        mask[i] = 1;
+      }
+      __syncthreads();
+      if (t == 0) sh.n_inl += sh.wave_cnt[0] + sh.wave_cnt[1] + sh.wave_cnt[2] + sh.wave_cnt[3];
+      __syncthreads();
+    }
+    nin = sh.n_inl;
+  }
+  __threadfence_block();
+  __syncthreads();
+  if (n == kModelPoints)
+    for (int i = t; i < n; i += kThreads) mask[i] = 1;
+  double Rf[9], tf[3], rv[3], Rr[9];
+  epnp_refit(sh, p2, p3, idx, nin, K4, Rf, tf);
+  rodrigues_m2v(Rf, rv);       // solvePnP returns rvec ...
+  rodrigues_v2m(rv, Rr);       // ... and eval_utils.py:31 turns it back into R
+  if (t == 0) {
+    for (int i = 0; i < 3; ++i) {
+      for (int j = 0; j < 3; ++j) pose[i * 4 + j] = Rr[i * 3 + j];
+      pose[i * 4 + 3] = tf[i] / scale;
+    }
+    n_inliers[b] = nin;
+    status[b] = 0;
+  }
+}
+
+}  // namespace
+}  // namespace onepose
+
+using namespace onepose;
+
+extern "C" {
+
+size_t onepose_pnp_workspace_bytes(int batch, int max_points, int max_iters) {
+  (void)max_iters;
+  if (batch <= 0 || max_points <= 0) return 0;
+  return align_up((size_t)batch * max_points * sizeof(int), 256);
+}
+
+int onepose_pnp_ransac(const float* pts2d, const float* pts3d, const int* counts, int max_points,
+                       const double* K, int64_t K_bstride, int batch, double scale,
+                       float reproj_error, int max_iters, double confidence, double* pose34,
+                       uint8_t* inlier_mask, int* n_inliers, int* status, void* workspace,
+                       size_t workspace_bytes, void* stream) {
+  clear_error();
+  OP_REQUIRE(pts2d && pts3d && counts && K && pose34 && inlier_mask && n_inliers && status,
+             "pnp: null pointer");
+  OP_REQUIRE(batch >= 1 && max_points >= 1 && max_points <= 8192, "pnp: batch=%d max_points=%d",
+             batch, max_points);
+  OP_REQUIRE(confidence > 0 && confidence < 1, "pnp: confidence %f not in (0,1)", confidence);
+  OP_REQUIRE(scale != 0.0, "pnp: scale 0");
+  const size_t need = onepose_pnp_workspace_bytes(batch, max_points, max_iters);
+  if (!workspace || workspace_bytes < need) {
+    set_error("pnp: workspace %zu < %zu bytes", workspace_bytes, need);
+    return ONEPOSE_ERR_WORKSPACE;
+  }
+  const size_t lds = ((sizeof(Shared) + 15) / 16) * 16 + (size_t)max_points * 5 * sizeof(float);
+  OP_REQUIRE(lds <= 160 * 1024, "pnp: max_points=%d needs %zu B of LDS", max_points, lds);
+  static bool attr_set = false;
+  if (!attr_set) {
+    OP_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(pnp_ransac_kernel),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    attr_set = true;
+  }
+  OP_LAUNCH(K_PNP, static_cast<hipStream_t>(stream), pnp_ransac_kernel, dim3(batch), dim3(kThreads), lds,
+                     static_cast<hipStream_t>(stream), pts2d, pts3d, counts, max_points, K,
+                     K_bstride, scale, reproj_error, max_iters, confidence, pose34, inlier_mask,
+                     n_inliers, status, static_cast<int*>(workspace));
+  return ONEPOSE_OK;
+}
+
+}  // extern "C"

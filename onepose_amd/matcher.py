@@ -1,0 +1,218 @@
+"""Drop-in ``GATsSuperGlue`` whose forward runs on libonepose_hip (MI355X).
+
+Same constructor (``hparams`` dict / AttributeDict), same parameter names and shapes (so a
+reference state dict or a Lightning checkpoint's ``matcher.*`` entries load unchanged) and
+the same ``forward(data) -> (pred, conf_matrix)`` contract as
+``src/models/GATsSPG_architectures/GATs_SuperGlue.py:162-278``:
+
+* inputs ``keypoints2d [B,N1,2]``, ``keypoints3d [B,N3,3]``, ``descriptors2d_query
+  [B,256,N1]``, ``descriptors3d_db [B,256,N3]``, ``descriptors2d_db [B,256,N3*L]``
+  (extra keys ignored; everything upcast to float32 as :219-221 does);
+* ``pred`` holds batch element 0 only: ``matches0/1`` int64 (-1 = unmatched),
+  ``matching_scores0/1`` float32; ``conf_matrix`` keeps the whole batch (:269-278);
+* no keypoints on either side returns the reference's bare dict with int32 indices and
+  ``skip_train`` (:223-231);
+* a ``match_type`` other than ``'softmax'`` raises ``NotImplementedError`` (:275-276).
+
+The parameters are ordinary ``nn.Parameter``s (PyTorch is the weight store); the first
+forward after they change packs them (head-major q/k/v, folded GAT vectors) into one
+device-resident panel.  The module has no CPU path: tensors must live on a ROCm device
+and ``libonepose_hip.so`` must be built, otherwise forward raises.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+from . import _lib
+
+SUPPORTED = {"include_self": True, "additional": False, "with_linear_transform": False}
+
+
+def _hp(hparams, key, default=None):
+    if isinstance(hparams, dict):
+        return hparams.get(key, default)
+    return getattr(hparams, key, default)
+
+
+def _mlp(channels):
+    """Conv1d / InstanceNorm1d / ReLU stack with the reference's module indices (:135-147)."""
+    layers = []
+    for i in range(1, len(channels)):
+        layers.append(nn.Conv1d(channels[i - 1], channels[i], kernel_size=1, bias=True))
+        if i < len(channels) - 1:
+            layers.append(nn.InstanceNorm1d(channels[i]))
+            layers.append(nn.ReLU())
+    return nn.Sequential(*layers)
+
+
+class KeypointEncoder(nn.Module):
+    """Parameter holder for ``kenc_2d`` / ``kenc_3d`` (present in checkpoints, never used by
+    the reference forward, :172-182)."""
+
+    def __init__(self, inp_dim, feature_dim, layers):
+        super().__init__()
+        self.encoder = _mlp([inp_dim, *layers, feature_dim])
+        nn.init.constant_(self.encoder[-1].bias, 0.0)
+
+
+class GraphAttentionLayer(nn.Module):
+    """Parameters of ``GATs.py:9-57`` (W [in,out], a [2*out,1])."""
+
+    def __init__(self, in_features=256, out_features=256, dropout=0.6, alpha=0.2, concat=True,
+                 include_self=True, additional=False, with_linear_transform=False):
+        super().__init__()
+        self.dropout, self.alpha, self.concat = dropout, alpha, concat
+        self.include_self, self.additional = include_self, additional
+        self.with_linear_transform = with_linear_transform
+        self.W = nn.Parameter(torch.empty(in_features, out_features))
+        nn.init.xavier_normal_(self.W.data, gain=1.414)
+        self.a = nn.Parameter(torch.empty(2 * out_features, 1))
+        nn.init.xavier_normal_(self.a.data, gain=1.414)
+
+
+class MultiHeadedAttention(nn.Module):
+    def __init__(self, num_heads: int, d_model: int):
+        super().__init__()
+        self.dim, self.num_heads = d_model // num_heads, num_heads
+        self.merge = nn.Conv1d(d_model, d_model, kernel_size=1)
+        self.proj = nn.ModuleList([nn.Conv1d(d_model, d_model, kernel_size=1) for _ in range(3)])
+
+
+class AttentionPropagation(nn.Module):
+    def __init__(self, feature_dim: int, num_heads: int):
+        super().__init__()
+        self.attn = MultiHeadedAttention(num_heads, feature_dim)
+        self.mlp = _mlp([feature_dim * 2, feature_dim * 2, feature_dim])
+        nn.init.constant_(self.mlp[-1].bias, 0.0)
+
+
+class AttentionalGNN(nn.Module):
+    """['GATs', 'self', 'cross'] * 4 (:52-65)."""
+
+    def __init__(self, feature_dim, layer_names, include_self, additional, with_linear_transform):
+        super().__init__()
+        self.layers = nn.ModuleList([
+            GraphAttentionLayer(256, 256, 0.6, 0.2, True, include_self, additional,
+                                with_linear_transform)
+            if i % 3 == 0 else AttentionPropagation(feature_dim, 4)
+            for i in range(len(layer_names))])
+        self.names = list(layer_names)
+
+
+class GATsSuperGlue(nn.Module):
+    def __init__(self, hparams):
+        super().__init__()
+        self.hparams = hparams
+        self.match_type = _hp(hparams, "match_type")
+        dim = _hp(hparams, "descriptor_dim", 256)
+        if dim != 256:
+            raise NotImplementedError("onepose_amd kernels are built for descriptor_dim=256")
+        for k, v in SUPPORTED.items():
+            if bool(_hp(hparams, k, v)) != v:
+                raise NotImplementedError(f"onepose_amd supports {k}={v} only (GATsSPG config)")
+        enc = list(_hp(hparams, "keypoints_encoder", [32, 64, 128]))
+        self.kenc_2d = KeypointEncoder(3, dim, enc)
+        self.kenc_3d = KeypointEncoder(4, dim, enc)
+        self.gnn = AttentionalGNN(dim, ["GATs", "self", "cross"] * 4, True, False, False)
+        self.final_proj = nn.Conv1d(dim, dim, kernel_size=1, bias=True)
+        self.register_parameter("bin_score", nn.Parameter(torch.tensor(1.0)))
+        self._packed = None
+        self._packed_key = None
+
+    # ---------------------------------------------------------------- weight packing
+    def _weight_tensors(self):
+        lib = _lib.load()
+        sd = dict(self.named_parameters())
+        out = []
+        for i in range(lib.onepose_matcher_num_tensors()):
+            name = lib.onepose_matcher_tensor_name(i).decode()
+            t = sd[name]
+            if t.numel() != lib.onepose_matcher_tensor_numel(i):
+                raise ValueError(f"{name}: {t.numel()} elements, expected "
+                                 f"{lib.onepose_matcher_tensor_numel(i)}")
+            out.append(t)
+        return out
+
+    def packed_weights(self, device):
+        tensors = self._weight_tensors()
+        key = (str(device),) + tuple((t.data_ptr(), t._version) for t in tensors)
+        if self._packed is not None and self._packed_key == key:
+            return self._packed
+        lib = _lib.load()
+        host = [t.detach().to("cpu", torch.float32).contiguous() for t in tensors]
+        arr = (_lib.c_void_p * len(host))(*[h.data_ptr() for h in host])
+        buf = np.empty(lib.onepose_matcher_packed_bytes() // 4, dtype=np.float32)
+        _lib.check(lib.onepose_matcher_pack(arr, len(host), buf.ctypes.data), "matcher_pack")
+        self._packed = torch.from_numpy(buf).to(device)
+        self._packed_key = key
+        return self._packed
+
+    # ---------------------------------------------------------------- forward
+    @staticmethod
+    def _operand(x):
+        """[B, C, N] float32 with contiguous (C, N); batch stride may be 0 (expanded)."""
+        x = x.float()
+        if x.stride(2) != 1 or x.stride(1) != x.shape[2]:
+            x = x.contiguous()
+        bstride = x.stride(0) if x.shape[0] > 1 else x.shape[1] * x.shape[2]
+        return x, bstride
+
+    def forward(self, data):
+        kpts2d, kpts3d = data["keypoints2d"].float(), data["keypoints3d"].float()
+        if kpts2d.shape[1] == 0 or kpts3d.shape[1] == 0:
+            shape0, shape1 = kpts2d.shape[:-1], kpts3d.shape[:-1]
+            return {
+                "matches0": kpts2d.new_full(shape0, -1, dtype=torch.int)[0],
+                "matches1": kpts3d.new_full(shape1, -1, dtype=torch.int)[0],
+                "matching_scores0": kpts2d.new_zeros(shape0)[0],
+                "matching_scores1": kpts3d.new_zeros(shape1)[0],
+                "skip_train": True,
+            }
+        if self.match_type != "softmax":
+            raise NotImplementedError
+        d2, s2 = self._operand(data["descriptors2d_query"])
+        d3, s3 = self._operand(data["descriptors3d_db"])
+        db, sl = self._operand(data["descriptors2d_db"])
+        if d2.device.type != "cuda":
+            raise RuntimeError("onepose_amd.GATsSuperGlue runs on a ROCm GPU only; "
+                               "move the inputs with .cuda()")
+        B, C, n1 = d2.shape
+        n3 = d3.shape[2]
+        nleaf = int(db.shape[2] / n3)
+        if nleaf * n3 != db.shape[2] or C != 256 or d3.shape[0] != B or db.shape[0] != B:
+            raise ValueError(f"bad matcher input shapes {tuple(d2.shape)} {tuple(d3.shape)} "
+                             f"{tuple(db.shape)}")
+        dev = d2.device
+        return self._run(d2, s2, d3, s3, db, sl, B, n1, n3, nleaf, dev)
+
+    def _run(self, d2, s2, d3, s3, db, sl, B, n1, n3, nleaf, dev):
+        lib = _lib.load()
+        with torch.cuda.device(dev):
+            w = self.packed_weights(dev)
+            m0 = torch.empty(B, n1, dtype=torch.int64, device=dev)
+            m1 = torch.empty(B, n3, dtype=torch.int64, device=dev)
+            ms0 = torch.empty(B, n1, dtype=torch.float32, device=dev)
+            ms1 = torch.empty(B, n3, dtype=torch.float32, device=dev)
+            conf = torch.empty(B, n1, n3, dtype=torch.float32, device=dev)
+            ws_bytes = lib.onepose_match_workspace_bytes(B, n1, n3, nleaf, 1)
+            ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
+            rc = lib.onepose_match(
+                w.data_ptr(), d2.data_ptr(), s2, d3.data_ptr(), s3, db.data_ptr(), sl,
+                B, n1, n3, nleaf, float(_hp(self.hparams, "scale_factor")),
+                float(_hp(self.hparams, "match_threshold")),
+                m0.data_ptr(), m1.data_ptr(), ms0.data_ptr(), ms1.data_ptr(), conf.data_ptr(),
+                ws.data_ptr(), ws_bytes, _lib.stream_ptr(dev))
+            _lib.check(rc, "onepose_match")
+        pred = {"matches0": m0[0], "matches1": m1[0],
+                "matching_scores0": ms0[0], "matching_scores1": ms1[0]}
+        return pred, conf
+
+
+def from_state_dict(state_dict, hparams=None) -> GATsSuperGlue:
+    """Build the matcher from a reference-format state dict (numpy arrays or tensors)."""
+    from .synthetic import DEFAULT_HPARAMS
+    m = GATsSuperGlue(dict(hparams or DEFAULT_HPARAMS))
+    m.load_state_dict({k: torch.as_tensor(np.asarray(v)) for k, v in state_dict.items()})
+    return m.eval()

@@ -1,0 +1,105 @@
+"""Per-object frame pipeline: the whole per-frame hot path of ``inference.py:132-160`` on the
+device, with no host round trip and no per-frame re-upload of the object's 3D tensors.
+
+    matcher (onepose_match) -> correspondence selection -> RANSAC-EPnP -> cm/deg error
+
+The object's descriptors / leaves / 3D points are uploaded once (``inference.py:89-90``
+re-uploads them every frame).  All buffers are allocated at construction, so ``enqueue()``
+only launches kernels on the current stream and can be captured in a HIP graph
+(``torch.cuda.CUDAGraph``) and replayed.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from . import _lib
+from .matcher import GATsSuperGlue
+
+
+class FramePipeline:
+    def __init__(self, matcher: GATsSuperGlue, keypoints3d, desc3d, leaves, batch: int, n1: int,
+                 device, scale: float = 1000.0, reprojection_error: float = 5.0,
+                 iterations_count: int = 10000, confidence: float = 0.99, with_conf=True):
+        self.lib = _lib.load()
+        self.device = torch.device(device)
+        self.B, self.n1 = int(batch), int(n1)
+        self.scale, self.reproj = float(scale), float(reprojection_error)
+        self.iters, self.conf_level = int(iterations_count), float(confidence)
+        hp = matcher.hparams
+        self.scale_factor = float(hp["scale_factor"] if isinstance(hp, dict) else hp.scale_factor)
+        self.threshold = float(hp["match_threshold"] if isinstance(hp, dict) else hp.match_threshold)
+        dev = self.device
+        f32 = dict(dtype=torch.float32, device=dev)
+        self.weights = matcher.packed_weights(dev)
+        self.kp3 = torch.as_tensor(np.asarray(keypoints3d), **f32).reshape(-1, 3).contiguous()
+        self.desc3d = torch.as_tensor(np.asarray(desc3d), **f32).reshape(256, -1).contiguous()
+        self.n3 = self.desc3d.shape[1]
+        self.leaves = torch.as_tensor(np.asarray(leaves), **f32).reshape(256, -1).contiguous()
+        self.L = self.leaves.shape[1] // self.n3
+        assert self.L * self.n3 == self.leaves.shape[1] and self.kp3.shape[0] == self.n3
+        B = self.B
+        # per-frame inputs (filled by the caller)
+        self.desc2d = torch.zeros(B, 256, n1, **f32)
+        self.kpts2d = torch.zeros(B, n1, 2, **f32)
+        self.K = torch.zeros(B, 3, 3, dtype=torch.float64, device=dev)
+        self.pose_gt = torch.zeros(B, 3, 4, dtype=torch.float64, device=dev)
+        # outputs
+        self.matches0 = torch.empty(B, n1, dtype=torch.int64, device=dev)
+        self.matches1 = torch.empty(B, self.n3, dtype=torch.int64, device=dev)
+        self.mscores0 = torch.empty(B, n1, **f32)
+        self.mscores1 = torch.empty(B, self.n3, **f32)
+        self.conf = torch.empty(B, n1, self.n3, **f32) if with_conf else None
+        self.pts2d = torch.empty(B, n1, 2, **f32)
+        self.pts3d = torch.empty(B, n1, 3, **f32)
+        self.counts = torch.empty(B, dtype=torch.int32, device=dev)
+        self.pose = torch.empty(B, 3, 4, dtype=torch.float64, device=dev)
+        self.inlier_mask = torch.empty(B, n1, dtype=torch.uint8, device=dev)
+        self.n_inliers = torch.empty(B, dtype=torch.int32, device=dev)
+        self.status = torch.empty(B, dtype=torch.int32, device=dev)
+        self.R_err = torch.empty(B, dtype=torch.float64, device=dev)
+        self.t_err = torch.empty(B, dtype=torch.float64, device=dev)
+        self.cmd = torch.empty(B, 3, dtype=torch.uint8, device=dev)
+        self.ws_match_bytes = self.lib.onepose_match_workspace_bytes(B, n1, self.n3, self.L,
+                                                                     int(with_conf))
+        self.ws_match = torch.empty(self.ws_match_bytes, dtype=torch.uint8, device=dev)
+        self.ws_pnp_bytes = self.lib.onepose_pnp_workspace_bytes(B, n1, self.iters)
+        self.ws_pnp = torch.empty(self.ws_pnp_bytes, dtype=torch.uint8, device=dev)
+
+    def set_frames(self, desc2d, kpts2d, K, pose_gt):
+        """Copy B frames' inputs into the static buffers (host or device arrays)."""
+        self.desc2d.copy_(torch.as_tensor(np.asarray(desc2d), dtype=torch.float32))
+        self.kpts2d.copy_(torch.as_tensor(np.asarray(kpts2d), dtype=torch.float32))
+        self.K.copy_(torch.as_tensor(np.asarray(K), dtype=torch.float64).expand_as(self.K))
+        self.pose_gt.copy_(torch.as_tensor(np.asarray(pose_gt), dtype=torch.float64)[..., :3, :]
+                           .expand_as(self.pose_gt))
+
+    def enqueue_match(self):
+        s = _lib.stream_ptr(self.device)
+        _lib.check(self.lib.onepose_match(
+            self.weights.data_ptr(), self.desc2d.data_ptr(), 256 * self.n1,
+            self.desc3d.data_ptr(), 0, self.leaves.data_ptr(), 0,
+            self.B, self.n1, self.n3, self.L, self.scale_factor, self.threshold,
+            self.matches0.data_ptr(), self.matches1.data_ptr(), self.mscores0.data_ptr(),
+            self.mscores1.data_ptr(), _lib.ptr(self.conf), self.ws_match.data_ptr(),
+            self.ws_match_bytes, s), "onepose_match")
+
+    def enqueue_pose(self):
+        s = _lib.stream_ptr(self.device)
+        lib = self.lib
+        _lib.check(lib.onepose_select_correspondences(
+            self.matches0.data_ptr(), self.kpts2d.data_ptr(), self.n1 * 2, self.kp3.data_ptr(), 0,
+            self.B, self.n1, self.n3, self.scale, self.pts2d.data_ptr(), self.pts3d.data_ptr(),
+            self.counts.data_ptr(), s), "select_correspondences")
+        _lib.check(lib.onepose_pnp_ransac(
+            self.pts2d.data_ptr(), self.pts3d.data_ptr(), self.counts.data_ptr(), self.n1,
+            self.K.data_ptr(), 9, self.B, self.scale, self.reproj, self.iters, self.conf_level,
+            self.pose.data_ptr(), self.inlier_mask.data_ptr(), self.n_inliers.data_ptr(),
+            self.status.data_ptr(), self.ws_pnp.data_ptr(), self.ws_pnp_bytes, s), "pnp_ransac")
+        _lib.check(lib.onepose_pose_errors(
+            self.pose.data_ptr(), self.pose_gt.data_ptr(), 12, self.B, self.R_err.data_ptr(),
+            self.t_err.data_ptr(), self.cmd.data_ptr(), s), "pose_errors")
+
+    def enqueue(self):
+        self.enqueue_match()
+        self.enqueue_pose()

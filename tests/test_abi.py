@@ -1,0 +1,151 @@
+"""CPU tests of the C-ABI boundary: the library loads, exports every symbol the header
+declares, and its host-side weight packer lays the reference weights out as documented."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+from conftest import REPO
+
+
+def header_symbols():
+    src = open(os.path.join(REPO, "include", "onepose_hip.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(onepose_\w+)\s*\(", src)))
+
+
+def test_header_declares_the_boundary():
+    syms = header_symbols()
+    for s in ["onepose_match", "onepose_matcher_pack", "onepose_pnp_ransac",
+              "onepose_sample_descriptors", "onepose_select_correspondences",
+              "onepose_pose_errors", "onepose_last_error"]:
+        assert s in syms
+
+
+def test_library_exports_every_header_symbol():
+    from onepose_amd import _lib
+    lib = _lib.load()
+    missing = [s for s in header_symbols() if not hasattr(lib, s)]
+    assert not missing, missing
+    assert set(header_symbols()) == set(_lib.PROTOTYPES), "ctypes prototypes out of sync"
+    assert lib.onepose_abi_version() == 1
+
+
+def test_tensor_list_matches_reference_state_dict():
+    from onepose_amd import _lib, synthetic
+    lib = _lib.load()
+    sd = synthetic.make_state_dict(0)
+    names = [lib.onepose_matcher_tensor_name(i).decode() for i in range(lib.onepose_matcher_num_tensors())]
+    assert len(names) == 106
+    for i, n in enumerate(names):
+        assert n in sd, n
+        assert sd[n].size == lib.onepose_matcher_tensor_numel(i)
+    unused = set(sd) - set(names)
+    assert all(k.startswith(("kenc_", "bin_score")) for k in unused)
+    # the used parameter count quoted in SURVEY.md §8b
+    assert sum(sd[n].size for n in names) == 5_587_200
+
+
+def _pack(sd):
+    from onepose_amd import _lib
+    lib = _lib.load()
+    names = [lib.onepose_matcher_tensor_name(i).decode() for i in range(lib.onepose_matcher_num_tensors())]
+    host = [np.ascontiguousarray(sd[n], np.float32) for n in names]
+    arr = (ctypes.c_void_p * len(host))(*[h.ctypes.data for h in host])
+    buf = np.empty(lib.onepose_matcher_packed_bytes() // 4, np.float32)
+    assert lib.onepose_matcher_pack(arr, len(host), buf.ctypes.data) == 0
+    return buf
+
+
+def test_pack_layout():
+    from onepose_amd import synthetic
+    sd = synthetic.make_state_dict(3)
+    buf = _pack(sd)
+    ap_floats = 768 * 256 + 768 + 256 * 256 + 256 + 512 * 512 + 512 + 256 * 512 + 256
+    # first attention layer is gnn.layers.1
+    p = buf[:ap_floats]
+    wqkv = p[:768 * 256].reshape(768, 256)
+    bqkv = p[768 * 256:768 * 257]
+    for j in range(3):
+        w = sd[f"gnn.layers.1.attn.proj.{j}.weight"][:, :, 0]
+        b = sd[f"gnn.layers.1.attn.proj.{j}.bias"]
+        for h in range(4):
+            for d in (0, 17, 63):
+                np.testing.assert_array_equal(wqkv[j * 256 + h * 64 + d], w[d * 4 + h])
+                assert bqkv[j * 256 + h * 64 + d] == b[d * 4 + h]
+    wm = p[768 * 257:768 * 257 + 65536].reshape(256, 256)
+    merge = sd["gnn.layers.1.attn.merge.weight"][:, :, 0]
+    for h in range(4):
+        for q in (0, 5, 63):
+            np.testing.assert_array_equal(wm[:, h * 64 + q], merge[:, q * 4 + h])
+    # GAT fold: wa = W @ a (layer 0)
+    gat0 = buf[8 * ap_floats:8 * ap_floats + 512]
+    W, a = sd["gnn.layers.0.W"].astype(np.float64), sd["gnn.layers.0.a"][:, 0].astype(np.float64)
+    np.testing.assert_allclose(gat0[:256], W @ a[:256], rtol=1e-6, atol=1e-7)
+    np.testing.assert_allclose(gat0[256:], W @ a[256:], rtol=1e-6, atol=1e-7)
+    fin = buf[8 * ap_floats + 4 * 512:]
+    np.testing.assert_array_equal(fin[:65536], sd["final_proj.weight"].reshape(-1))
+
+
+def test_pack_rejects_wrong_count():
+    from onepose_amd import _lib
+    lib = _lib.load()
+    arr = (ctypes.c_void_p * 3)()
+    assert lib.onepose_matcher_pack(arr, 3, None) != 0
+    assert b"null" in lib.onepose_last_error() or b"expected" in lib.onepose_last_error()
+
+
+def test_workspace_sizes():
+    from onepose_amd import _lib
+    lib = _lib.load()
+    a = lib.onepose_match_workspace_bytes(1, 1024, 4096, 8, 1)
+    b = lib.onepose_match_workspace_bytes(1, 1024, 4096, 8, 0)
+    assert a > 0 and b - a >= 1024 * 4096 * 4
+    assert lib.onepose_match_workspace_bytes(0, 1, 1, 8, 1) == 0
+    assert lib.onepose_pnp_workspace_bytes(2, 1024, 10000) >= 2 * 1024 * 4
+
+
+def test_module_state_dict_keys_match_reference():
+    """The drop-in module accepts the reference's full state dict (strict)."""
+    from onepose_amd import matcher, synthetic
+    sd = synthetic.make_state_dict(0)
+    m = matcher.from_state_dict(sd)
+    assert set(m.state_dict().keys()) == set(sd.keys())
+    assert sum(p.numel() for p in m.parameters()) == 5_674_401
+
+
+def test_empty_input_path_matches_reference():
+    """GATs_SuperGlue.py:223-231 -- a bare dict with int32 indices (golden from the reference)."""
+    import torch
+    from conftest import golden
+    from onepose_amd import matcher, synthetic
+    g = golden("matcher_empty")
+    m = matcher.from_state_dict(synthetic.make_state_dict(0))
+    out = m({"keypoints2d": torch.zeros(1, 0, 2), "keypoints3d": torch.zeros(1, 5, 3),
+             "descriptors2d_query": torch.zeros(1, 256, 0), "descriptors3d_db": torch.zeros(1, 256, 5),
+             "descriptors2d_db": torch.zeros(1, 256, 40)})
+    assert isinstance(out, dict) and out["skip_train"] is True
+    for k in ("matches0", "matches1", "matching_scores0", "matching_scores1"):
+        assert out[k].numpy().dtype == g[k].dtype
+        np.testing.assert_array_equal(out[k].numpy(), g[k])
+
+
+def test_cpu_forward_fails_loudly():
+    import torch
+    from onepose_amd import matcher, synthetic
+    m = matcher.from_state_dict(synthetic.make_state_dict(0))
+    data, _, _ = synthetic.make_matcher_inputs(16, 8, 2, seed=0)
+    with pytest.raises(RuntimeError, match="GPU"):
+        m({k: torch.from_numpy(v) for k, v in data.items()})
+
+
+def test_unsupported_match_type():
+    import torch
+    from onepose_amd import matcher, synthetic
+    hp = dict(synthetic.DEFAULT_HPARAMS, match_type="sinkhorn")
+    m = matcher.from_state_dict(synthetic.make_state_dict(0), hp)
+    data, _, _ = synthetic.make_matcher_inputs(16, 8, 2, seed=0)
+    with pytest.raises(NotImplementedError):
+        m({k: torch.from_numpy(v) for k, v in data.items()})

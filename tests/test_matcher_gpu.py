@@ -1,0 +1,113 @@
+"""HIP matcher (libonepose_hip.so through the drop-in module) vs the reference's fixtures and
+the numpy oracle.
+
+Tolerances: correspondence indices are compared exactly except on rows/columns whose
+reference margin (top-1 minus top-2 conf, or |mscore - match_threshold|) is below
+MARGIN -- there fp32 summation order may legitimately flip a decision; the tests count
+those and require them to be rare.  conf_matrix / matching scores: |diff| <= 2e-5
+(values lie in [0, 1]; fp32 MFMA products are exact, only the summation order differs
+from the CPU reference)."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden
+from onepose_amd import matcher, synthetic
+
+pytestmark = pytest.mark.gpu
+
+MARGIN = 1e-4
+ATOL = 2e-5
+
+
+def run_matcher(sd, data, device, expand=False):
+    m = matcher.from_state_dict(sd).to(device)
+    t = {k: torch.from_numpy(v).to(device) for k, v in data.items()}
+    if expand:   # the per-object tensors shared across the batch (stride 0)
+        for k in ("descriptors3d_db", "descriptors2d_db", "keypoints3d"):
+            t[k] = t[k][:1].expand_as(t[k])
+    with torch.no_grad():
+        pred, conf = m(t)
+    torch.cuda.synchronize()
+    return {k: v.cpu().numpy() for k, v in pred.items()}, conf.cpu().numpy()
+
+
+def check_indices(got, ref, margin, what):
+    bad = got != ref
+    unexplained = bad & (margin > MARGIN)
+    assert not unexplained.any(), f"{what}: {int(unexplained.sum())} index mismatches " \
+                                  f"at rows {np.nonzero(unexplained)[0][:10]}"
+    assert bad.sum() <= max(1, 0.002 * bad.size), f"{what}: {int(bad.sum())} low-margin flips"
+
+
+def margins(g):
+    top = g["row_top2"][0]
+    row_margin = np.minimum(top[:, 0] - top[:, 1], np.abs(g["matching_scores0"] - 0.2))
+    ctop = g["col_top2"][0]
+    col_margin = np.minimum(ctop[0] - ctop[1], np.abs(g["matching_scores1"] - 0.2))
+    return row_margin, col_margin
+
+
+@pytest.mark.parametrize("name", ["matcher_c1_wc", "matcher_c1_rand", "matcher_b2",
+                                  "matcher_ragged", "matcher_c2_idx"])
+def test_matcher_matches_reference_fixture(name, device):
+    g = golden(name)
+    n1, n3, L, B, seed, wc = [int(g[k]) for k in ("n1", "n3", "num_leaf", "batch", "seed",
+                                                   "well_conditioned")]
+    sd = synthetic.make_state_dict(seed, well_conditioned=bool(wc))
+    data, _, _ = synthetic.make_matcher_inputs(n1, n3, L, seed=seed, batch=B)
+    pred, conf = run_matcher(sd, data, device)
+    rm, cm = margins(g)
+    check_indices(pred["matches0"], g["matches0"], rm, "matches0")
+    check_indices(pred["matches1"], g["matches1"], cm, "matches1")
+    np.testing.assert_allclose(pred["matching_scores0"], g["matching_scores0"], atol=ATOL)
+    np.testing.assert_allclose(pred["matching_scores1"], g["matching_scores1"], atol=ATOL)
+    if "conf" in g:
+        np.testing.assert_allclose(conf, g["conf"], atol=ATOL)
+    np.testing.assert_allclose(conf.sum(axis=2), g["conf_row_sum"], rtol=1e-4, atol=1e-4)
+    np.testing.assert_allclose(conf.sum(axis=1), g["conf_col_sum"], rtol=1e-4, atol=1e-4)
+    assert pred["matches0"].dtype == np.int64 and pred["matches1"].dtype == np.int64
+
+
+def test_matcher_vs_oracle_batch_shared_object(device):
+    """Batch of 3 frames against one object passed as stride-0 (expanded) tensors."""
+    from oracle import matcher_np as M
+    sd = synthetic.make_state_dict(5)
+    data, _, _ = synthetic.make_matcher_inputs(200, 330, 6, seed=5, batch=3)
+    pred, conf = run_matcher(sd, data, device, expand=True)
+    opred, oconf = M.forward(sd, data)
+    np.testing.assert_allclose(conf, oconf, atol=ATOL)
+    top = -np.sort(-oconf[0], axis=1)[:, :2]
+    check_indices(pred["matches0"], opred["matches0"],
+                  np.minimum(top[:, 0] - top[:, 1], np.abs(opred["matching_scores0"] - 0.2)),
+                  "matches0")
+    assert (pred["matches0"] > -1).sum() > 20
+
+
+def test_matcher_deterministic(device):
+    sd = synthetic.make_state_dict(6)
+    data, _, _ = synthetic.make_matcher_inputs(256, 512, 8, seed=6)
+    a = run_matcher(sd, data, device)
+    b = run_matcher(sd, data, device)
+    np.testing.assert_array_equal(a[1], b[1])
+    np.testing.assert_array_equal(a[0]["matches0"], b[0]["matches0"])
+
+
+def test_matcher_full_size_properties(device):
+    """Config 3 shape (1024 x 16384, L=8) at batch 2: size-independent properties --
+    conf rows/cols are products of softmaxes (sum <= 1), matches are mutual and mutually
+    consistent, and most synthetic inliers are matched correctly."""
+    sd = synthetic.make_state_dict(7)
+    data, obj, frames = synthetic.make_matcher_inputs(1024, 16384, 8, seed=7, batch=2)
+    pred, conf = run_matcher(sd, data, device, expand=True)
+    assert np.all(conf >= 0) and np.all(conf.sum(axis=2) <= 1 + 1e-4)
+    m0, m1 = pred["matches0"], pred["matches1"]
+    for i in np.nonzero(m0 > -1)[0]:
+        assert m1[m0[i]] == i
+    assert ((m1 > -1).sum()) == ((m0 > -1).sum())
+    truth = frames[0].true_match
+    good = (m0 > -1) & (m0 == truth)
+    assert good.sum() >= 0.8 * (m0 > -1).sum()
+    # argmax consistency with the returned conf
+    valid = m0 > -1
+    np.testing.assert_array_equal(conf[0].argmax(axis=1)[valid], m0[valid])
