@@ -112,6 +112,8 @@ def main():
     ap.add_argument("--n3", type=int, default=4096)
     ap.add_argument("--leaf", type=int, default=8)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--stream", action="store_true",
+                    help="overlap step k's pose stage with step k+1's matcher (2 streams)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -158,11 +160,16 @@ def main():
     torch.cuda.synchronize()
     _lib.check(lib.onepose_profile_begin(1 << dom_id, 64 * args.steps + 64), "profile_begin")
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        pipe.enqueue()
-    result = torch.cat([pipe.pose.reshape(B, 12), pipe.R_err[:, None], pipe.t_err[:, None],
-                        pipe.cmd.double(), pipe.n_inliers[:, None].double(),
-                        pipe.status[:, None].double()], 1)
+    if not args.stream:
+        for _ in range(args.steps):
+            pipe.enqueue()
+        last = pipe.slots[0]
+    else:   # frame k's pose stage overlaps frame k+1's matcher (two streams, two slots)
+        pipe.run_stream(args.steps)
+        last = pipe.slots[(args.steps - 1) % len(pipe.slots)]
+    result = torch.cat([last.pose.reshape(B, 12), last.R_err[:, None], last.t_err[:, None],
+                        last.cmd.double(), last.n_inliers[:, None].double(),
+                        last.status[:, None].double()], 1)
     if pg:
         gathered = torch.empty(world * B, result.shape[1], dtype=result.dtype, device=dev)
         pg.all_gather_into_tensor(gathered, result)
@@ -202,7 +209,9 @@ def main():
             "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "fp32", "data": "synthetic",
             "config": {"workload": f"config 2: {n1} kpts x {n3} 3D pts, L={L}, {B} frame(s) per "
-                                   f"GPU per step; matcher + RANSAC-EPnP + cm/deg",
+                                   f"GPU per step; matcher + RANSAC-EPnP + cm/deg"
+                                   + ("; pose stage of step k overlaps the matcher of step "
+                                      "k+1 (2 streams)" if args.stream else ""),
                        "n1": n1, "n3": n3, "num_leaf": L, "batch_per_gpu": B,
                        "parallelism": f"frame-dp{world}"},
             "pose": {"cmd1": float(res[:, 14].mean()), "cmd3": float(res[:, 15].mean()),

@@ -52,7 +52,8 @@ Prof g_prof;
 const char* kKindNames[K_NUM_KINDS] = {
     "transpose_in", "gat", "qkv_gemm", "kv_partial", "kv_reduce", "attn_apply", "merge_gemm",
     "mlp1_gemm", "stats_finalize", "mlp2_gemm", "final_gemm", "l2norm", "score_gemm",
-    "softmax_reduce", "conf", "mutual", "select", "pnp_ransac", "pose_error", "sample_desc"};
+    "softmax_reduce", "conf", "mutual", "select", "pnp_ransac", "pose_error", "sample_desc",
+    "pnp_refit"};
 }  // namespace
 
 void prof_pre(int kind, hipStream_t s) {
@@ -168,9 +169,9 @@ __global__ __launch_bounds__(256) void transpose_in_kernel(const float* __restri
 // Linear-attention source reduction, one 64-token chunk per workgroup, one head per wave:
 //   KVpart[h][d][q] = sum_m phi(k)[m][h,d] * v[m][h,q]      (einsum 'bdhm,bqhm->bqdh', :96)
 //   kspart[h*64+d]  = sum_m phi(k)[m][h,d]                 (key.sum(3), :97)
-// on v_mfma_f32_32x32x2_f32 with the token as the K dimension: for a fixed token, 32
-// consecutive lanes read 32 consecutive channels (coalesced 128 B) straight into the A and
-// B operand registers.
+// The chunk's phi(k)|v rows (2 KB contiguous per token) are staged into LDS 32 tokens at a
+// time with 16-byte loads; v_mfma_f32_32x32x2_f32 then runs with the token as the K
+// dimension straight out of LDS (32 consecutive lanes read 32 consecutive channels).
 struct KvProb {
   const float* qkv;   // [B][N][768]
   float* part;        // [B][chunks][4][64][64]
@@ -183,39 +184,48 @@ struct KvArgs {
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 
+constexpr int kKvStage = 32;   // tokens per LDS stage
+
 __global__ __launch_bounds__(256) void kv_partial_kernel(KvArgs args) {
+  __shared__ __attribute__((aligned(16))) float stage[kKvStage * 512];
   int bid = blockIdx.x;
   const bool second = bid >= args.p[0].blocks;
   const KvProb& P = second ? args.p[1] : args.p[0];
   if (second) bid -= args.p[0].blocks;
   const int b = bid / P.chunks, chunk = bid - b * P.chunks;
-  const int lane = threadIdx.x & 63, h = threadIdx.x >> 6;
+  const int t = threadIdx.x, lane = t & 63, h = t >> 6;
   const int half = lane >> 5, l32 = lane & 31;
   const float* base = P.qkv + (int64_t)b * P.n * 768;
-  const int m_begin = chunk * 64, m_end = min(P.n, m_begin + 64);
+  const int m_begin = chunk * 64;
 
   floatx16 acc00, acc01, acc10, acc11;
 #pragma unroll
   for (int i = 0; i < 16; ++i) acc00[i] = acc01[i] = acc10[i] = acc11[i] = 0.f;
   float ks0 = 0.f, ks1 = 0.f;
-  const int kcol = 256 + h * 64 + l32, vcol = 512 + h * 64 + l32;
-#pragma unroll 4
-  for (int m = m_begin; m < m_begin + 64; m += 2) {
-    const int tok = m + half;
-    float a0 = 0.f, a1 = 0.f, v0 = 0.f, v1 = 0.f;
-    if (tok < m_end) {
-      const float* row = base + (int64_t)tok * 768;
-      a0 = row[kcol];
-      a1 = row[kcol + 32];
-      v0 = row[vcol];
-      v1 = row[vcol + 32];
+  for (int s0 = 0; s0 < 64; s0 += kKvStage) {
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < kKvStage * 128 / 256; ++i) {   // 32 rows x 128 float4
+      const int e = t + 256 * i, r = e >> 7, c4 = e & 127;
+      const int tok = m_begin + s0 + r;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (tok < P.n) v = *reinterpret_cast<const float4*>(base + (int64_t)tok * 768 + 256 + c4 * 4);
+      *reinterpret_cast<float4*>(stage + r * 512 + c4 * 4) = v;
     }
-    ks0 += a0;
-    ks1 += a1;
-    acc00 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, v0, acc00, 0, 0, 0);
-    acc01 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, v1, acc01, 0, 0, 0);
-    acc10 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, v0, acc10, 0, 0, 0);
-    acc11 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, v1, acc11, 0, 0, 0);
+    __syncthreads();
+    const float* ka = stage + h * 64 + l32;
+    const float* va = stage + 256 + h * 64 + l32;
+#pragma unroll 4
+    for (int k = 0; k < kKvStage; k += 2) {
+      const int r = (k + half) * 512;
+      const float a0 = ka[r], a1 = ka[r + 32], v0 = va[r], v1 = va[r + 32];
+      ks0 += a0;
+      ks1 += a1;
+      acc00 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, v0, acc00, 0, 0, 0);
+      acc01 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, v1, acc01, 0, 0, 0);
+      acc10 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, v0, acc10, 0, 0, 0);
+      acc11 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, v1, acc11, 0, 0, 0);
+    }
   }
   float* out = P.part + ((int64_t)b * P.chunks + chunk) * 16384 + h * 4096;
 #pragma unroll
@@ -235,40 +245,61 @@ __global__ __launch_bounds__(256) void kv_partial_kernel(KvArgs args) {
   }
 }
 
-// Sum the chunk partials in chunk order (deterministic) -> KVt[h][q][d], ksum[256].
-__global__ __launch_bounds__(256) void kv_reduce_kernel(KvArgs args, float* kvt, float* ksum,
+// Sum the chunk partials -> KV[h][d][q], ksum[256], one float4 of outputs per thread with
+// eight chunk loads in flight; the summation order is fixed (deterministic).
+__global__ __launch_bounds__(256) void kv_reduce_kernel(KvArgs args, float* kv, float* ksum,
                                                         int batch) {
-  const int64_t per = 16384 + 256;
-  int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  const int64_t total = 2 * (int64_t)batch * per;
-  if (idx >= total) return;
-  const int src = (int)(idx / (batch * per));
-  const int64_t r = idx - (int64_t)src * batch * per;
-  const int b = (int)(r / per);
-  const int e = (int)(r - (int64_t)b * per);
+  constexpr int per = (16384 + 256) / 4;   // float4 outputs per (source, sample)
+  const int idx = blockIdx.x * 256 + threadIdx.x;
+  if (idx >= 2 * batch * per) return;
+  const int src = idx / (batch * per);
+  const int r = idx - src * batch * per;
+  const int b = r / per, e4 = r - b * per;
   const KvProb& P = src ? args.p[1] : args.p[0];
-  if (e < 16384) {
-    const int h = e >> 12, d = (e >> 6) & 63, q = e & 63;
-    const float* p = P.part + (int64_t)b * P.chunks * 16384 + e;
-    float s = 0.f;
-    for (int c = 0; c < P.chunks; ++c) s += p[(int64_t)c * 16384];
-    kvt[((int64_t)src * batch + b) * 16384 + h * 4096 + q * 64 + d] = s;
+  const float4* p;
+  int64_t stride;
+  float4* out;
+  if (e4 < 4096) {
+    p = reinterpret_cast<const float4*>(P.part + (int64_t)b * P.chunks * 16384) + e4;
+    stride = 4096;
+    out = reinterpret_cast<float4*>(kv + ((int64_t)src * batch + b) * 16384) + e4;
   } else {
-    const int c0 = e - 16384;
-    const float* p = P.kspart + (int64_t)b * P.chunks * 256 + c0;
-    float s = 0.f;
-    for (int c = 0; c < P.chunks; ++c) s += p[(int64_t)c * 256];
-    ksum[((int64_t)src * batch + b) * 256 + c0] = s;
+    p = reinterpret_cast<const float4*>(P.kspart + (int64_t)b * P.chunks * 256) + (e4 - 4096);
+    stride = 64;
+    out = reinterpret_cast<float4*>(ksum + ((int64_t)src * batch + b) * 256) + (e4 - 4096);
   }
+  float4 acc[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) acc[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+  int c = 0;
+  for (; c + 8 <= P.chunks; c += 8) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float4 v = p[(int64_t)(c + j) * stride];
+      acc[j].x += v.x; acc[j].y += v.y; acc[j].z += v.z; acc[j].w += v.w;
+    }
+  }
+  float4 tail = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (; c < P.chunks; ++c) {
+    const float4 v = p[(int64_t)c * stride];
+    tail.x += v.x; tail.y += v.y; tail.z += v.z; tail.w += v.w;
+  }
+  float4 s = acc[0];
+#pragma unroll
+  for (int j = 1; j < 8; ++j) { s.x += acc[j].x; s.y += acc[j].y; s.z += acc[j].z; s.w += acc[j].w; }
+  s.x += tail.x; s.y += tail.y; s.z += tail.z; s.w += tail.w;
+  *out = s;
 }
 
 // Linear-attention apply (GATs_SuperGlue.py:97-98):
 //   Z[n,h]   = 1 / (sum_d phi(q)[n][h,d] * ksum[h,d] + 1e-6)
 //   O[n][h*64+q] = (sum_d phi(q)[n][h,d] * KV[h][d][q]) * Z[n,h] * Ns
-// One 64-token tile per workgroup, one head per wave, 2x2 32x32 MFMA accumulators.
+// One 64-token tile per workgroup, one head per wave.  phi(q) tile [64][256] and the four
+// 64x64 KV blocks (transposed to [h][q][d]) are staged in LDS (pitches 260 / 68 floats:
+// conflict-free ds_read_b128), then 2x2 32x32 MFMA accumulators per wave.
 struct ApplyProb {
   const float* qkv;    // query side [B][Nq][768] (phi(q) in columns 0..255)
-  const float* kvt;    // source [B][4][64 q][64 d]
+  const float* kv;     // source [B][4][64 d][64 q]
   const float* ksum;   // source [B][256]
   float* out;          // [B][Nq][256]
   int nq;
@@ -278,49 +309,66 @@ struct ApplyProb {
 struct ApplyArgs {
   ApplyProb p[2];
 };
+constexpr int kQPitch = 260, kKvPitch = 68;
+constexpr size_t kApplyLds = (64 * kQPitch + 4 * 64 * kKvPitch + 4 * 64) * sizeof(float);
 
 __global__ __launch_bounds__(256) void attn_apply_kernel(ApplyArgs args) {
-  __shared__ float zs[4][64];
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  float* qs = sm;                          // [64][260]
+  float* kvs = qs + 64 * kQPitch;          // [4][64 q][68]
+  float* zs = kvs + 4 * 64 * kKvPitch;     // [4][64]
   int bid = blockIdx.x;
   const bool second = bid >= args.p[0].blocks;
   const ApplyProb& P = second ? args.p[1] : args.p[0];
   if (second) bid -= args.p[0].blocks;
   const int b = bid / P.mtiles, mt = bid - b * P.mtiles;
   const int m0 = mt * 64;
-  const int lane = threadIdx.x & 63, h = threadIdx.x >> 6;
+  const int t = threadIdx.x, lane = t & 63, h = t >> 6;
   const int half = lane >> 5, l32 = lane & 31;
   const float* q = P.qkv + (int64_t)b * P.nq * 768;
-  const float* kv = P.kvt + (int64_t)b * 16384 + h * 4096;
-  const float* ks = P.ksum + (int64_t)b * 256 + h * 64;
-
-  {  // Z for token m0 + lane, head h
-    const int tok = m0 + lane;
-    float z = 0.f;
-    if (tok < P.nq) {
-      const float* row = q + (int64_t)tok * 768 + h * 64;
-      float s = 0.f;
-#pragma unroll 4
-      for (int d = 0; d < 64; d += 4) {
-        const float4 a = *reinterpret_cast<const float4*>(row + d);
-        const float4 k = *reinterpret_cast<const float4*>(ks + d);
-        s += a.x * k.x;
-        s += a.y * k.y;
-        s += a.z * k.z;
-        s += a.w * k.w;
-      }
-      z = 1.0f / (s + 1e-6f);
-    }
-    zs[h][lane] = z;
+  const float* kvg = P.kv + (int64_t)b * 16384;
+  const float* ks = P.ksum + (int64_t)b * 256;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {   // phi(q) tile: 64 rows x 64 float4
+    const int e = t + 256 * i, r = e >> 6, c4 = e & 63;
+    const int tok = m0 + r;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (tok < P.nq) v = *reinterpret_cast<const float4*>(q + (int64_t)tok * 768 + c4 * 4);
+    *reinterpret_cast<float4*>(qs + r * kQPitch + c4 * 4) = v;
   }
-
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {   // KV[h][d][q] -> kvs[h][q][d]
+    const int e = t + 256 * i;     // float4 index over [4][64][16]
+    const int hh = e >> 10, d = (e >> 4) & 63, q4 = e & 15;
+    const float4 v = *reinterpret_cast<const float4*>(kvg + hh * 4096 + d * 64 + q4 * 4);
+    float* o = kvs + hh * 64 * kKvPitch + (q4 * 4) * kKvPitch + d;
+    o[0] = v.x;
+    o[kKvPitch] = v.y;
+    o[2 * kKvPitch] = v.z;
+    o[3 * kKvPitch] = v.w;
+  }
+  __syncthreads();
+  {  // Z for token `lane`, head h
+    const float* row = qs + lane * kQPitch + h * 64;
+    float s = 0.f;
+#pragma unroll 4
+    for (int d = 0; d < 64; d += 4) {
+      const float4 a = *reinterpret_cast<const float4*>(row + d);
+      const float4 k = *reinterpret_cast<const float4*>(ks + h * 64 + d);
+      s += a.x * k.x;
+      s += a.y * k.y;
+      s += a.z * k.z;
+      s += a.w * k.w;
+    }
+    zs[h * 64 + lane] = 1.0f / (s + 1e-6f);
+  }
   floatx16 acc[2][2];
 #pragma unroll
   for (int i = 0; i < 16; ++i) acc[0][0][i] = acc[0][1][i] = acc[1][0][i] = acc[1][1][i] = 0.f;
-  const int t0 = min(m0 + l32, P.nq - 1), t1 = min(m0 + 32 + l32, P.nq - 1);
-  const float* qa0 = q + (int64_t)t0 * 768 + h * 64 + half * 4;
-  const float* qa1 = q + (int64_t)t1 * 768 + h * 64 + half * 4;
-  const float* kb0 = kv + l32 * 64 + half * 4;
-  const float* kb1 = kv + (32 + l32) * 64 + half * 4;
+  const float* qa0 = qs + l32 * kQPitch + h * 64 + half * 4;
+  const float* qa1 = qa0 + 32 * kQPitch;
+  const float* kb0 = kvs + h * 64 * kKvPitch + l32 * kKvPitch + half * 4;
+  const float* kb1 = kb0 + 32 * kKvPitch;
 #pragma unroll
   for (int kk = 0; kk < 8; ++kk) {
     const float4 a0 = *reinterpret_cast<const float4*>(qa0 + kk * 8);
@@ -343,7 +391,7 @@ __global__ __launch_bounds__(256) void attn_apply_kernel(ApplyArgs args) {
       const int row = tb * 32 + (i & 3) + 8 * (i >> 2) + 4 * half;
       const int tok = m0 + row;
       if (tok < P.nq) {
-        const float z = zs[h][row];
+        const float z = zs[h * 64 + row];
         o[(int64_t)tok * 256 + l32] = acc[tb][0][i] * z * P.ns;
         o[(int64_t)tok * 256 + 32 + l32] = acc[tb][1][i] * z * P.ns;
       }
@@ -352,7 +400,9 @@ __global__ __launch_bounds__(256) void attn_apply_kernel(ApplyArgs args) {
 }
 
 // InstanceNorm1d statistics (GATs_SuperGlue.py:145; biased variance, eps 1e-5): combine the
-// per-64-row-tile (mean, M2) partials in tile order (Chan et al.), -> mean, rstd per channel.
+// per-64-row-tile (mean, M2) partials (Chan et al., double).  One workgroup per (side,
+// sample, 64-channel group); four tile-interleaved partial combines per channel, merged in
+// a fixed order.
 struct StatsProb {
   const float* part;  // [B][mtiles][2][512]
   float* mean;        // [B][512]
@@ -362,36 +412,43 @@ struct StatsProb {
 struct StatsArgs {
   StatsProb p[2];
 };
+__device__ __forceinline__ void chan_merge(double& n, double& mean, double& m2, double nb,
+                                           double mb, double m2b) {
+  if (nb == 0.0) return;
+  const double nn = n + nb;
+  const double delta = mb - mean;
+  mean += delta * (nb / nn);
+  m2 += m2b + delta * delta * (n * nb / nn);
+  n = nn;
+}
 __global__ __launch_bounds__(256) void stats_finalize_kernel(StatsArgs args, int batch) {
-  const int idx = blockIdx.x * 256 + threadIdx.x;
-  const int total = 2 * batch * 512;
-  if (idx >= total) return;
-  const int side = idx / (batch * 512);
-  const int r = idx - side * batch * 512;
-  const int b = r / 512, c = r - b * 512;
+  __shared__ double red[3][4][64];
+  const int g = blockIdx.x & 7, b = (blockIdx.x >> 3) % batch, side = (blockIdx.x >> 3) / batch;
   const StatsProb& P = side ? args.p[1] : args.p[0];
+  const int t = threadIdx.x, tg = t >> 6, c = g * 64 + (t & 63);
   const float* part = P.part + (int64_t)b * P.mtiles * 1024;
   double n = 0.0, mean = 0.0, m2 = 0.0;
-  for (int t = 0; t < P.mtiles; ++t) {
-    const double nb = (double)min(64, P.m - t * 64);
-    const double mb = part[t * 1024 + c], m2b = part[t * 1024 + 512 + c];
-    const double nn = n + nb;
-    const double delta = mb - mean;
-    mean += delta * (nb / nn);
-    m2 += m2b + delta * delta * (n * nb / nn);
-    n = nn;
+  for (int ti = tg; ti < P.mtiles; ti += 4) {
+    const double nb = (double)min(64, P.m - ti * 64);
+    chan_merge(n, mean, m2, nb, part[ti * 1024 + c], part[ti * 1024 + 512 + c]);
   }
-  const double var = m2 / n;
-  P.mean[b * 512 + c] = (float)mean;
-  P.rstd[b * 512 + c] = (float)(1.0 / sqrt(var + 1e-5));
+  red[0][tg][t & 63] = n;
+  red[1][tg][t & 63] = mean;
+  red[2][tg][t & 63] = m2;
+  __syncthreads();
+  if (tg == 0) {
+    for (int k = 1; k < 4; ++k) chan_merge(n, mean, m2, red[0][k][t], red[1][k][t], red[2][k][t]);
+    P.mean[b * 512 + c] = (float)mean;
+    P.rstd[b * 512 + c] = (float)(1.0 / sqrt(m2 / n + 1e-5));
+  }
 }
 
 // GraphAttentionLayer (GATs.py:62-123) with include_self=True, with_linear_transform=False,
 // additional=False, concat=True, W a folded (h.(W a) == (h W) a):
 //   s3 = h3.wa_hi, s2_j = leaf_j.wa_lo, e = LeakyReLU_0.2(s3 + [s3, s2_1..L])
 //   alpha = softmax(e), out = ELU(alpha_0 h3 + sum_j alpha_j leaf_j)
-// P = 32/L 3D points per workgroup; the workgroup's P*L leaf columns are staged in LDS once
-// and read twice (logits, weighted sum) -- leaves cross HBM exactly once per layer.
+// P = 64/L 3D points per workgroup; the workgroup's P*L leaf columns are staged in LDS once
+// (16-byte loads) and read twice (logits, weighted sum) -- leaves cross HBM once per layer.
 __global__ __launch_bounds__(256) void gat_kernel(const float* __restrict__ x3,
                                                   const float* __restrict__ leaves,
                                                   int64_t leaves_bs, const float* __restrict__ wa,
@@ -407,10 +464,22 @@ __global__ __launch_bounds__(256) void gat_kernel(const float* __restrict__ x3,
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int64_t ncol = (int64_t)n3 * L;
   const float* lv = leaves + b * leaves_bs + (int64_t)p0 * L;
-  const int total = 256 * cols;
-  for (int e = t; e < total; e += 256) {
-    const int c = e / cols, j = e - c * cols;
-    lt[c * pitch + j] = ((int64_t)p0 * L + j < ncol) ? lv[(int64_t)c * ncol + j] : 0.f;
+  if ((ncol & 3) == 0 && (cols & 3) == 0 && (int64_t)(p0 + P) * L <= ncol) {
+    const int c4s = cols >> 2;   // 16-byte loads; rows are 16-byte aligned
+    for (int e = t; e < 256 * c4s; e += 256) {
+      const int c = e / c4s, j4 = e - c * c4s;
+      const float4 v = *reinterpret_cast<const float4*>(lv + (int64_t)c * ncol + j4 * 4);
+      float* d = lt + c * pitch + j4 * 4;
+      d[0] = v.x;
+      d[1] = v.y;
+      d[2] = v.z;
+      d[3] = v.w;
+    }
+  } else {
+    for (int e = t; e < 256 * cols; e += 256) {
+      const int c = e / cols, j = e - c * cols;
+      lt[c * pitch + j] = ((int64_t)p0 * L + j < ncol) ? lv[(int64_t)c * ncol + j] : 0.f;
+    }
   }
   const float* xb = x3 + (int64_t)b * n3 * kDim;
   for (int e = t; e < P * 256; e += 256) {
@@ -835,6 +904,28 @@ size_t onepose_match_workspace_bytes(int batch, int n1, int n3, int num_leaf, in
   return make_plan(nullptr, batch, n1, n3, with_conf != 0).bytes;
 }
 
+}  // extern "C"
+
+namespace onepose {
+namespace {
+int init_kernel_attributes() {
+  static int rc = -1;
+  if (rc == -1) {
+    rc = ONEPOSE_OK;
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(attn_apply_kernel),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)kApplyLds) !=
+            hipSuccess ||
+        hipFuncSetAttribute(reinterpret_cast<const void*>(gat_kernel),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
+      rc = ONEPOSE_ERR_HIP;
+  }
+  return rc;
+}
+}  // namespace
+}  // namespace onepose
+
+extern "C" {
+
 int onepose_match(const void* packed_weights, const float* desc2d, int64_t desc2d_bstride,
                   const float* desc3d, int64_t desc3d_bstride, const float* leaves,
                   int64_t leaves_bstride, int batch, int n1, int n3, int num_leaf,
@@ -855,6 +946,10 @@ int onepose_match(const void* packed_weights, const float* desc2d, int64_t desc2
     return ONEPOSE_ERR_WORKSPACE;
   }
   hipStream_t st = static_cast<hipStream_t>(stream_);
+  if (init_kernel_attributes() != ONEPOSE_OK) {
+    set_error("match: hipFuncSetAttribute failed");
+    return ONEPOSE_ERR_HIP;
+  }
   Plan p = make_plan(workspace, batch, n1, n3, with_conf);
   const float* wbase = static_cast<const float*>(packed_weights);
   const int B = batch;
@@ -867,7 +962,7 @@ int onepose_match(const void* packed_weights, const float* desc2d, int64_t desc2
 
   int c2 = 0, c3 = 0, ap = 0, gat = 0;
   const int ch2 = ceil_div(n1, 64), ch3 = ceil_div(n3, 64);
-  const int gat_p = num_leaf >= 32 ? 1 : 32 / num_leaf;
+  const int gat_p = max(1, 64 / num_leaf);
   const size_t gat_lds =
       (size_t)(256 * (gat_p * num_leaf + 1) + gat_p * 256 + gat_p * (1 + num_leaf)) * 4;
   for (int layer = 0; layer < kLayers; ++layer) {
@@ -898,9 +993,9 @@ int onepose_match(const void* packed_weights, const float* desc2d, int64_t desc2
     kva.p[1] = {p.qkv3, p.kvpart3, p.kspart3, n3, ch3, B * ch3};
     OP_LAUNCH(K_KV_PARTIAL, st, kv_partial_kernel, dim3(B * (ch2 + ch3)), dim3(256), 0, st, kva);
     {
-      const int64_t total = 2 * (int64_t)B * (16384 + 256);
-      OP_LAUNCH(K_KV_REDUCE, st, kv_reduce_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
-                         st, kva, p.kvt, p.ksum, B);
+      const int total = 2 * B * (16384 + 256) / 4;
+      OP_LAUNCH(K_KV_REDUCE, st, kv_reduce_kernel, dim3(ceil_div(total, 256)), dim3(256), 0, st,
+                kva, p.kvt, p.ksum, B);
     }
     {  // self: side s attends to itself; cross: 2D attends to 3D and vice versa
       const int src2 = (kind == 1) ? 0 : 1, src3 = (kind == 1) ? 1 : 0;
@@ -910,7 +1005,7 @@ int onepose_match(const void* packed_weights, const float* desc2d, int64_t desc2
                  p.o2, n1, ns2, ch2, B * ch2};
       aa.p[1] = {p.qkv3, p.kvt + (size_t)src3 * B * 16384, p.ksum + (size_t)src3 * B * 256,
                  p.o3, n3, ns3, ch3, B * ch3};
-      OP_LAUNCH(K_APPLY, st, attn_apply_kernel, dim3(B * (ch2 + ch3)), dim3(256), 0, st, aa);
+      OP_LAUNCH(K_APPLY, st, attn_apply_kernel, dim3(B * (ch2 + ch3)), dim3(256), kApplyLds, st, aa);
     }
     {  // merge
       GemmArgs a;
@@ -940,7 +1035,7 @@ int onepose_match(const void* packed_weights, const float* desc2d, int64_t desc2
       StatsArgs sa;
       sa.p[0] = {p.stats2, p.mean, p.rstd, n1, ch2};
       sa.p[1] = {p.stats3, p.mean + (size_t)B * 512, p.rstd + (size_t)B * 512, n3, ch3};
-      OP_LAUNCH(K_STATS, st, stats_finalize_kernel, dim3(ceil_div(2 * B * 512, 256)), dim3(256), 0,
+      OP_LAUNCH(K_STATS, st, stats_finalize_kernel, dim3(2 * B * 8), dim3(256), 0,
                          st, sa, B);
     }
     {  // MLP conv 2 on ReLU(InstanceNorm(.)) + residual: desc + delta

@@ -26,72 +26,305 @@ constexpr int kThreads = 256;
 // ---------------------------------------------------------------------------------------
 // small dense linear algebra, double
 // ---------------------------------------------------------------------------------------
-template <int N>
-__device__ void jacobi_eigen(double* a, double* w, double* vt) {
-  double v[N * N];
-#pragma unroll
-  for (int i = 0; i < N * N; ++i) v[i] = (i % (N + 1) == 0) ? 1.0 : 0.0;
-  for (int sweep = 0; sweep < 60; ++sweep) {
-    double off = 0.0, diag = 0.0;
-#pragma unroll
-    for (int i = 0; i < N; ++i) {
-      diag += a[i * N + i] * a[i * N + i];
-#pragma unroll
-      for (int j = i + 1; j < N; ++j) off += a[i * N + j] * a[i * N + j];
-    }
+// Cyclic Jacobi for the 3x3 symmetric matrices (PCA of the control points, polar factor):
+// eigenvalues descending in w, eigenvectors as rows of vt.  Static indices only.
+__device__ __forceinline__ void jacobi3(double* a, double* w, double* vt) {
+  double v[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
+  for (int sweep = 0; sweep < 30; ++sweep) {
+    const double off = a[1] * a[1] + a[2] * a[2] + a[5] * a[5];
+    const double diag = a[0] * a[0] + a[4] * a[4] + a[8] * a[8];
     if (off <= 1e-30 * diag || off == 0.0) break;
 #pragma unroll
-    for (int p = 0; p < N - 1; ++p) {
+    for (int p = 0; p < 2; ++p) {
 #pragma unroll
-      for (int q = p + 1; q < N; ++q) {
-        const double apq = a[p * N + q];
+      for (int q = p + 1; q < 3; ++q) {
+        const double apq = a[p * 3 + q];
         if (apq != 0.0) {
-          const double app = a[p * N + p], aqq = a[q * N + q];
-          const double theta = (aqq - app) / (2.0 * apq);
+          const double theta = (a[q * 3 + q] - a[p * 3 + p]) / (2.0 * apq);
           const double t = (theta >= 0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
           const double c = 1.0 / sqrt(t * t + 1.0), s = t * c;
 #pragma unroll
-          for (int k = 0; k < N; ++k) {
-            const double akp = a[k * N + p], akq = a[k * N + q];
-            a[k * N + p] = c * akp - s * akq;
-            a[k * N + q] = s * akp + c * akq;
+          for (int k = 0; k < 3; ++k) {
+            const double akp = a[k * 3 + p], akq = a[k * 3 + q];
+            a[k * 3 + p] = c * akp - s * akq;
+            a[k * 3 + q] = s * akp + c * akq;
           }
 #pragma unroll
-          for (int k = 0; k < N; ++k) {
-            const double apk = a[p * N + k], aqk = a[q * N + k];
-            a[p * N + k] = c * apk - s * aqk;
-            a[q * N + k] = s * apk + c * aqk;
+          for (int k = 0; k < 3; ++k) {
+            const double apk = a[p * 3 + k], aqk = a[q * 3 + k];
+            a[p * 3 + k] = c * apk - s * aqk;
+            a[q * 3 + k] = s * apk + c * aqk;
           }
 #pragma unroll
-          for (int k = 0; k < N; ++k) {
-            const double vkp = v[k * N + p], vkq = v[k * N + q];
-            v[k * N + p] = c * vkp - s * vkq;
-            v[k * N + q] = s * vkp + c * vkq;
+          for (int k = 0; k < 3; ++k) {
+            const double vkp = v[k * 3 + p], vkq = v[k * 3 + q];
+            v[k * 3 + p] = c * vkp - s * vkq;
+            v[k * 3 + q] = s * vkp + c * vkq;
           }
         }
       }
     }
   }
-  // selection sort of eigenvalues, descending; eigenvectors to rows of vt
-  int order[N];
+  double e[3] = {a[0], a[4], a[8]};
+  double c0[3] = {v[0], v[3], v[6]}, c1[3] = {v[1], v[4], v[7]}, c2[3] = {v[2], v[5], v[8]};
+  auto cswap = [](double& x, double& y, double* u, double* z) {
+    if (y > x) {
+      double t = x; x = y; y = t;
 #pragma unroll
-  for (int i = 0; i < N; ++i) order[i] = i;
-  for (int i = 0; i < N; ++i)
-    for (int j = i + 1; j < N; ++j)
-      if (a[order[j] * N + order[j]] > a[order[i] * N + order[i]]) {
-        const int t = order[i];
-        order[i] = order[j];
-        order[j] = t;
+      for (int k = 0; k < 3; ++k) { t = u[k]; u[k] = z[k]; z[k] = t; }
+    }
+  };
+  cswap(e[0], e[1], c0, c1);
+  cswap(e[1], e[2], c1, c2);
+  cswap(e[0], e[1], c0, c1);
+  w[0] = e[0]; w[1] = e[1]; w[2] = e[2];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) { vt[k] = c0[k]; vt[3 + k] = c1[k]; vt[6 + k] = c2[k]; }
+}
+
+// The four eigenvectors of the symmetric 12x12 matrix M^T M with the smallest eigenvalues,
+// ascending (vec[0] = smallest) -- the rows 11, 10, 9, 8 of the U^T that epnp.cpp takes
+// from cvSVD(MtM).  Register-resident (static indices only):
+//   1. Householder tridiagonalisation T = Q^T A Q (reflectors kept in A's lower part);
+//   2. block inverse iteration with 4 vectors on T + sigma I (LDL^T, sigma = 1e-9 |T|),
+//      until the 4-dimensional subspace stops moving;
+//   3. Rayleigh-Ritz on the 4x4 projection (Jacobi), then back-transform through Q.
+// The invariant subspace is the same one any exact eigen-solver returns; inside a
+// (numerically) degenerate cluster the basis is arbitrary, as it is for cvSVD.
+#define LI(i, j) ((i) * ((i) + 1) / 2 + (j))
+// hh: 55 doubles of per-lane scratch (LDS), element q at hh[q * hs], where the reflectors
+// wait for the back-transform instead of occupying registers during the iteration.
+template <int ITERS>
+__device__ __forceinline__ void eig12_small4(double (&a)[78], double (&vec)[4][12], double* hh, int hs) {
+  constexpr int n = 12;
+  double tau[n - 2], e[n - 1], d[n];
+#pragma unroll
+  for (int k = 0; k < n - 2; ++k) {
+    const double alpha = a[LI(k + 1, k)];
+    double xn = 0.0;
+#pragma unroll
+    for (int i = k + 2; i < n; ++i) xn += a[LI(i, k)] * a[LI(i, k)];
+    double beta = alpha, tk = 0.0;
+    if (xn != 0.0) {
+      beta = -copysign(sqrt(alpha * alpha + xn), alpha);
+      tk = (beta - alpha) / beta;
+      const double sc = 1.0 / (alpha - beta);
+#pragma unroll
+      for (int i = k + 2; i < n; ++i) a[LI(i, k)] *= sc;
+    }
+    tau[k] = tk;
+    e[k] = beta;
+    if (tk != 0.0) {
+      // v = [1, a[k+2..][k]] on rows k+1..n-1;  p = tk * A22 v
+      double pv[n];
+#pragma unroll
+      for (int i = k + 1; i < n; ++i) {
+        double s = 0.0;
+#pragma unroll
+        for (int j = k + 1; j < n; ++j) {
+          const double vj = (j == k + 1) ? 1.0 : a[LI(j, k)];
+          const double aij = (i >= j) ? a[LI(i, j)] : a[LI(j, i)];
+          s += aij * vj;
+        }
+        pv[i] = tk * s;
       }
-  for (int i = 0; i < N; ++i) {
-    w[i] = a[order[i] * N + order[i]];
-    for (int k = 0; k < N; ++k) vt[i * N + k] = v[k * N + order[i]];
+      double pvv = 0.0;
+#pragma unroll
+      for (int i = k + 1; i < n; ++i) pvv += pv[i] * ((i == k + 1) ? 1.0 : a[LI(i, k)]);
+      const double half = 0.5 * tk * pvv;
+#pragma unroll
+      for (int i = k + 1; i < n; ++i) pv[i] -= half * ((i == k + 1) ? 1.0 : a[LI(i, k)]);
+#pragma unroll
+      for (int i = k + 1; i < n; ++i) {
+        const double vi = (i == k + 1) ? 1.0 : a[LI(i, k)];
+#pragma unroll
+        for (int j = k + 1; j <= i; ++j) {
+          const double vj = (j == k + 1) ? 1.0 : a[LI(j, k)];
+          a[LI(i, j)] -= vi * pv[j] + pv[i] * vj;
+        }
+      }
+    }
+  }
+  e[n - 2] = a[LI(n - 1, n - 2)];
+#pragma unroll
+  for (int i = 0; i < n; ++i) d[i] = a[LI(i, i)];
+  {
+    int q = 0;
+#pragma unroll
+    for (int k = 0; k < n - 2; ++k) {
+      hh[q++ * hs] = tau[k];
+#pragma unroll
+      for (int i = k + 2; i < n; ++i) hh[q++ * hs] = a[LI(i, k)];
+    }
+  }
+
+  // LDL^T of T + sigma I
+  double tn = 0.0;
+#pragma unroll
+  for (int i = 0; i < n; ++i) tn = fmax(tn, fabs(d[i]) + (i > 0 ? fabs(e[i - 1]) : 0.0) + (i < n - 1 ? fabs(e[i]) : 0.0));
+  const double sigma = 1e-9 * tn + 1e-300;
+  double ipiv[n], lo[n - 1];
+  {
+    double piv = d[0] + sigma;
+#pragma unroll
+    for (int i = 0; i < n - 1; ++i) {
+      ipiv[i] = 1.0 / piv;
+      lo[i] = e[i] * ipiv[i];
+      piv = d[i + 1] + sigma - lo[i] * e[i];
+    }
+    ipiv[n - 1] = 1.0 / piv;
+  }
+
+  double x[4][n];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int i = 0; i < n; ++i) x[j][i] = 1.0 + 0.37 * (double)(((i + 3) * (j + 5) * 7) % 11) - 0.13 * j;
+
+  auto orthonormalize = [&](double (&y)[4][n]) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+#pragma unroll
+      for (int r = 0; r < 2; ++r) {   // MGS, twice for stability
+#pragma unroll
+        for (int q = 0; q < j; ++q) {
+          double dp = 0.0;
+#pragma unroll
+          for (int i = 0; i < n; ++i) dp += y[q][i] * y[j][i];
+#pragma unroll
+          for (int i = 0; i < n; ++i) y[j][i] -= dp * y[q][i];
+        }
+      }
+      double nn = 0.0;
+#pragma unroll
+      for (int i = 0; i < n; ++i) nn += y[j][i] * y[j][i];
+      const double inv = 1.0 / sqrt(nn);
+#pragma unroll
+      for (int i = 0; i < n; ++i) y[j][i] *= inv;
+    }
+  };
+  orthonormalize(x);
+  // fixed iteration count: the subspace error shrinks like ((l4+s)/(l5+s))^ITERS
+  for (int it = 0; it < ITERS; ++it) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {   // x <- (T + sigma I)^-1 x, in place
+      double z = x[j][0];
+#pragma unroll
+      for (int i = 1; i < n; ++i) {
+        z = x[j][i] - lo[i - 1] * z;
+        x[j][i] = z;
+      }
+#pragma unroll
+      for (int i = 0; i < n; ++i) x[j][i] *= ipiv[i];
+#pragma unroll
+      for (int i = n - 2; i >= 0; --i) x[j][i] -= lo[i] * x[j][i + 1];
+    }
+    orthonormalize(x);
+  }
+  // Rayleigh-Ritz: H = X T X^T
+  double h[16], hv[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
+#pragma unroll
+  for (int p = 0; p < 4; ++p)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      double dp = 0.0;
+#pragma unroll
+      for (int i = 0; i < n; ++i) {
+        const double txq = d[i] * x[q][i] + (i > 0 ? e[i - 1] * x[q][i - 1] : 0.0) +
+                           (i < n - 1 ? e[i] * x[q][i + 1] : 0.0);
+        dp += x[p][i] * txq;
+      }
+      h[p * 4 + q] = dp;
+    }
+#pragma unroll
+  for (int p = 0; p < 4; ++p)
+#pragma unroll
+    for (int q = p + 1; q < 4; ++q) h[p * 4 + q] = h[q * 4 + p] = 0.5 * (h[p * 4 + q] + h[q * 4 + p]);
+  for (int sweep = 0; sweep < 30; ++sweep) {
+    double off = 0.0, dg = 0.0;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      dg += h[p * 5] * h[p * 5];
+#pragma unroll
+      for (int q = p + 1; q < 4; ++q) off += h[p * 4 + q] * h[p * 4 + q];
+    }
+    if (off <= 1e-32 * dg || off == 0.0) break;
+#pragma unroll
+    for (int p = 0; p < 3; ++p)
+#pragma unroll
+      for (int q = p + 1; q < 4; ++q) {
+        const double apq = h[p * 4 + q];
+        if (apq != 0.0) {
+          const double theta = (h[q * 5] - h[p * 5]) / (2.0 * apq);
+          const double t = (theta >= 0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
+          const double c = 1.0 / sqrt(t * t + 1.0), s = t * c;
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const double akp = h[k * 4 + p], akq = h[k * 4 + q];
+            h[k * 4 + p] = c * akp - s * akq;
+            h[k * 4 + q] = s * akp + c * akq;
+          }
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const double apk = h[p * 4 + k], aqk = h[q * 4 + k];
+            h[p * 4 + k] = c * apk - s * aqk;
+            h[q * 4 + k] = s * apk + c * aqk;
+          }
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const double vkp = hv[k * 4 + p], vkq = hv[k * 4 + q];
+            hv[k * 4 + p] = c * vkp - s * vkq;
+            hv[k * 4 + q] = s * vkp + c * vkq;
+          }
+        }
+      }
+  }
+  // ascending order of the Ritz values (static sorting network on 4 slots)
+  double ev[4] = {h[0], h[5], h[10], h[15]};
+  int ord[4] = {0, 1, 2, 3};
+  auto cs = [&](int i, int j) {
+    if (ev[j] < ev[i]) {
+      double t = ev[i]; ev[i] = ev[j]; ev[j] = t;
+      int u = ord[i]; ord[i] = ord[j]; ord[j] = u;
+    }
+  };
+  cs(0, 1); cs(2, 3); cs(0, 2); cs(1, 3); cs(1, 2);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    double c4[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {   // column ord[r] of hv, selected statically
+      c4[q] = hv[q * 4 + 0];
+      c4[q] = (ord[r] == 1) ? hv[q * 4 + 1] : c4[q];
+      c4[q] = (ord[r] == 2) ? hv[q * 4 + 2] : c4[q];
+      c4[q] = (ord[r] == 3) ? hv[q * 4 + 3] : c4[q];
+    }
+    double y[n];
+#pragma unroll
+    for (int i = 0; i < n; ++i) y[i] = c4[0] * x[0][i] + c4[1] * x[1][i] + c4[2] * x[2][i] + c4[3] * x[3][i];
+    // back-transform: y <- H_0 H_1 ... H_{n-3} y
+#pragma unroll
+    for (int k = n - 3; k >= 0; --k) {
+      const int q0 = k * (2 * n - k - 1) / 2;   // start of reflector k in hh
+      const double tk = hh[q0 * hs];
+      if (tk != 0.0) {
+        double s = y[k + 1];
+#pragma unroll
+        for (int i = k + 2; i < n; ++i) s += hh[(q0 + i - k - 1) * hs] * y[i];
+        s *= tk;
+        y[k + 1] -= s;
+#pragma unroll
+        for (int i = k + 2; i < n; ++i) y[i] -= s * hh[(q0 + i - k - 1) * hs];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < n; ++i) vec[r][i] = y[i];
   }
 }
 
 // least squares by Householder QR, m x n, m <= 6, full column rank
 template <int M, int N>
-__device__ void lstsq(const double* A_, const double* b_, double* x) {
+__device__ __forceinline__ void lstsq(const double* A_, const double* b_, double* x) {
   double A[M * N], b[M];
 #pragma unroll
   for (int i = 0; i < M * N; ++i) A[i] = A_[i];
@@ -138,7 +371,7 @@ __device__ void lstsq(const double* A_, const double* b_, double* x) {
   }
 }
 
-__device__ void inv3(const double* m, double* r) {
+__device__ __forceinline__ void inv3(const double* m, double* r) {
   const double c00 = m[4] * m[8] - m[5] * m[7];
   const double c01 = m[5] * m[6] - m[3] * m[8];
   const double c02 = m[3] * m[7] - m[4] * m[6];
@@ -155,14 +388,14 @@ __device__ void inv3(const double* m, double* r) {
 }
 
 // orthogonal polar factor of a 3x3 matrix (U V^T of its SVD)
-__device__ void polar3(const double* A, double* R) {
+__device__ __forceinline__ void polar3(const double* A, double* R) {
   double ata[9], w[3], vt[9];
 #pragma unroll
   for (int i = 0; i < 3; ++i)
 #pragma unroll
     for (int j = 0; j < 3; ++j)
       ata[i * 3 + j] = A[i] * A[j] + A[3 + i] * A[3 + j] + A[6 + i] * A[6 + j];
-  jacobi_eigen<3>(ata, w, vt);
+  jacobi3(ata, w, vt);
   double u[3][3];
 #pragma unroll
   for (int i = 0; i < 3; ++i) {
@@ -196,8 +429,9 @@ __device__ __forceinline__ double dot3(const double* a, const double* b) {
 // ---------------------------------------------------------------------------------------
 // EPnP pieces that do not depend on the point count (epnp.cpp)
 // ---------------------------------------------------------------------------------------
-__device__ void compute_L_6x10(const double* ut, double* l) {
-  const double* v[4] = {ut + 12 * 11, ut + 12 * 10, ut + 12 * 9, ut + 12 * 8};
+// vs: the four eigenvectors, vs + 12*i = i-th smallest (epnp.cpp's ut + 12*(11-i))
+__device__ __forceinline__ void compute_L_6x10(const double* vs, double* l) {
+  const double* v[4] = {vs, vs + 12, vs + 24, vs + 36};
   double dv[4][6][3];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
@@ -229,7 +463,7 @@ __device__ void compute_L_6x10(const double* ut, double* l) {
   }
 }
 
-__device__ void compute_rho(const double (*cws)[3], double* rho) {
+__device__ __forceinline__ void compute_rho(const double (*cws)[3], double* rho) {
   auto d2 = [](const double* a, const double* b) {
     return (a[0] - b[0]) * (a[0] - b[0]) + (a[1] - b[1]) * (a[1] - b[1]) + (a[2] - b[2]) * (a[2] - b[2]);
   };
@@ -241,7 +475,7 @@ __device__ void compute_rho(const double (*cws)[3], double* rho) {
   rho[5] = d2(cws[2], cws[3]);
 }
 
-__device__ void betas_approx(int which, const double* L, const double* rho, double* betas) {
+__device__ __forceinline__ void betas_approx(int which, const double* L, const double* rho, double* betas) {
   if (which == 1) {
     double l[24], b4[4];
 #pragma unroll
@@ -295,7 +529,7 @@ __device__ void betas_approx(int which, const double* L, const double* rho, doub
 }
 
 // epnp::qr_solve for the 6x4 Gauss-Newton system
-__device__ void qr_solve_6x4(double* A, double* b, double* X) {
+__device__ __forceinline__ void qr_solve_6x4(double* A, double* b, double* X) {
   constexpr int nr = 6, nc = 4;
   double A1[nc], A2[nc];
 #pragma unroll
@@ -346,7 +580,7 @@ __device__ void qr_solve_6x4(double* A, double* b, double* X) {
   }
 }
 
-__device__ void gauss_newton(const double* L, const double* rho, double* betas) {
+__device__ __forceinline__ void gauss_newton(const double* L, const double* rho, double* betas) {
   double x[4] = {0.0, 0.0, 0.0, 0.0};
   for (int it = 0; it < 5; ++it) {
     double A[24], b[6];
@@ -369,12 +603,12 @@ __device__ void gauss_newton(const double* L, const double* rho, double* betas) 
   }
 }
 
-__device__ void ccs_from_betas(const double* ut, const double* betas, double (*ccs)[3]) {
+__device__ __forceinline__ void ccs_from_betas(const double* vs, const double* betas, double (*ccs)[3]) {
 #pragma unroll
   for (int j = 0; j < 4; ++j) ccs[j][0] = ccs[j][1] = ccs[j][2] = 0.0;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    const double* v = ut + 12 * (11 - i);
+    const double* v = vs + 12 * i;
 #pragma unroll
     for (int j = 0; j < 4; ++j)
 #pragma unroll
@@ -382,7 +616,7 @@ __device__ void ccs_from_betas(const double* ut, const double* betas, double (*c
   }
 }
 
-__device__ void finish_R(const double* abt, double* R) {
+__device__ __forceinline__ void finish_R(const double* abt, double* R) {
   polar3(abt, R);
   const double det = R[0] * R[4] * R[8] + R[1] * R[5] * R[6] + R[2] * R[3] * R[7] -
                      R[2] * R[4] * R[6] - R[1] * R[3] * R[8] - R[0] * R[5] * R[7];
@@ -393,7 +627,7 @@ __device__ void finish_R(const double* abt, double* R) {
   }
 }
 
-__device__ void rodrigues_m2v(const double* R, double* r) {
+__device__ __forceinline__ void rodrigues_m2v(const double* R, double* r) {
   double rx = R[7] - R[5], ry = R[2] - R[6], rz = R[3] - R[1];
   const double s = sqrt((rx * rx + ry * ry + rz * rz) * 0.25);
   double c = (R[0] + R[4] + R[8] - 1) * 0.5;
@@ -426,7 +660,7 @@ __device__ void rodrigues_m2v(const double* R, double* r) {
   r[2] = rz;
 }
 
-__device__ void rodrigues_v2m(const double* r, double* R) {
+__device__ __forceinline__ void rodrigues_v2m(const double* r, double* R) {
   const double theta = sqrt(r[0] * r[0] + r[1] * r[1] + r[2] * r[2]);
   if (theta < 2.220446049250313e-16) {
 #pragma unroll
@@ -443,86 +677,86 @@ __device__ void rodrigues_v2m(const double* r, double* R) {
 }
 
 // ---------------------------------------------------------------------------------------
-// 5-point EPnP, one lane (RANSAC kernel): epnp::compute_pose with n = 5
+// 5-point EPnP, one lane (RANSAC kernel): epnp::compute_pose with n = 5.  The points are
+// read from the workgroup's LDS copy through `sub` whenever needed (volatile reads), so they
+// do not occupy registers across the eigen-solve.
 // ---------------------------------------------------------------------------------------
-__device__ void epnp5(const double* pws, const double* us, const double* K4, double* rvec,
-                      double* tvec) {
+__device__ __forceinline__ void epnp5(const volatile int* sub, const volatile float* p2, const volatile float* p3,
+                      const double* K4, double* rvec, double* tvec, double* hh, int hs) {
   constexpr int n = kModelPoints;
   const double fu = K4[0], fv = K4[1], uc = K4[2], vc = K4[3];
-  double cws[4][3];
-#pragma unroll
-  for (int j = 0; j < 3; ++j) {
-    double s = 0.0;
-#pragma unroll
-    for (int i = 0; i < n; ++i) s += pws[3 * i + j];
-    cws[0][j] = s / n;
-  }
+  auto PW = [&](int i, int j) { return (double)p3[3 * sub[i] + j]; };
+  auto US = [&](int i, int j) { return (double)p2[2 * sub[i] + j]; };
+  double cw0[3], ci[9], rho[6];
+  double mtm[78];
   {
+    double cws[4][3];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      double s = 0.0;
+#pragma unroll
+      for (int i = 0; i < n; ++i) s += PW(i, j);
+      cws[0][j] = s / n;
+    }
     double m[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, dc[3], uct[9];
 #pragma unroll
     for (int i = 0; i < n; ++i) {
       double p[3];
 #pragma unroll
-      for (int j = 0; j < 3; ++j) p[j] = pws[3 * i + j] - cws[0][j];
+      for (int j = 0; j < 3; ++j) p[j] = PW(i, j) - cws[0][j];
 #pragma unroll
       for (int r = 0; r < 3; ++r)
 #pragma unroll
         for (int c = 0; c < 3; ++c) m[r * 3 + c] += p[r] * p[c];
     }
-    jacobi_eigen<3>(m, dc, uct);
+    jacobi3(m, dc, uct);
 #pragma unroll
     for (int i = 1; i < 4; ++i) {
       const double k = sqrt(dc[i - 1] / n);
 #pragma unroll
       for (int j = 0; j < 3; ++j) cws[i][j] = cws[0][j] + k * uct[3 * (i - 1) + j];
     }
-  }
-  double alphas[n * 4];
-  {
-    double cc[9], ci[9];
+    double cc[9];
 #pragma unroll
     for (int i = 0; i < 3; ++i)
 #pragma unroll
       for (int j = 1; j < 4; ++j) cc[3 * i + j - 1] = cws[j][i] - cws[0][i];
     inv3(cc, ci);
 #pragma unroll
+    for (int j = 0; j < 3; ++j) cw0[j] = cws[0][j];
+    compute_rho(cws, rho);
+#pragma unroll
+    for (int i = 0; i < 78; ++i) mtm[i] = 0.0;
+#pragma unroll
     for (int i = 0; i < n; ++i) {
-      const double* pi = pws + 3 * i;
-      double* a = alphas + 4 * i;
+      double as[4];
 #pragma unroll
       for (int j = 0; j < 3; ++j)
-        a[1 + j] = ci[3 * j] * (pi[0] - cws[0][0]) + ci[3 * j + 1] * (pi[1] - cws[0][1]) +
-                   ci[3 * j + 2] * (pi[2] - cws[0][2]);
-      a[0] = 1.0 - a[1] - a[2] - a[3];
+        as[1 + j] = ci[3 * j] * (PW(i, 0) - cw0[0]) + ci[3 * j + 1] * (PW(i, 1) - cw0[1]) +
+                    ci[3 * j + 2] * (PW(i, 2) - cw0[2]);
+      as[0] = 1.0 - as[1] - as[2] - as[3];
+      const double u = US(i, 0), v = US(i, 1);
+      double r1[12], r2[12];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        r1[3 * k] = as[k] * fu;
+        r1[3 * k + 1] = 0.0;
+        r1[3 * k + 2] = as[k] * (uc - u);
+        r2[3 * k] = 0.0;
+        r2[3 * k + 1] = as[k] * fv;
+        r2[3 * k + 2] = as[k] * (vc - v);
+      }
+#pragma unroll
+      for (int a = 0; a < 12; ++a)
+#pragma unroll
+        for (int b = 0; b <= a; ++b) mtm[LI(a, b)] += r1[a] * r1[b] + r2[a] * r2[b];
     }
   }
-  double mtm[144];
-#pragma unroll
-  for (int i = 0; i < 144; ++i) mtm[i] = 0.0;
-#pragma unroll
-  for (int i = 0; i < n; ++i) {
-    const double* as = alphas + 4 * i;
-    const double u = us[2 * i], v = us[2 * i + 1];
-    double r1[12], r2[12];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      r1[3 * k] = as[k] * fu;
-      r1[3 * k + 1] = 0.0;
-      r1[3 * k + 2] = as[k] * (uc - u);
-      r2[3 * k] = 0.0;
-      r2[3 * k + 1] = as[k] * fv;
-      r2[3 * k + 2] = as[k] * (vc - v);
-    }
-#pragma unroll
-    for (int a = 0; a < 12; ++a)
-#pragma unroll
-      for (int b = 0; b < 12; ++b) mtm[a * 12 + b] += r1[a] * r1[b] + r2[a] * r2[b];
-  }
-  double d[12], ut[144];
-  jacobi_eigen<12>(mtm, d, ut);
-  double L[60], rho[6];
+  double ev4[4][12];
+  eig12_small4<28>(mtm, ev4, hh, hs);
+  const double* ut = &ev4[0][0];
+  double L[60];
   compute_L_6x10(ut, L);
-  compute_rho(cws, rho);
   double bestR[9], bestT[3], bestErr = 0.0;
   for (int which = 1; which <= 3; ++which) {
     double betas[4], ccs[4][3], pcs[n * 3];
@@ -531,7 +765,12 @@ __device__ void epnp5(const double* pws, const double* us, const double* K4, dou
     ccs_from_betas(ut, betas, ccs);
 #pragma unroll
     for (int i = 0; i < n; ++i) {
-      const double* a = alphas + 4 * i;
+      double a[4];
+#pragma unroll
+      for (int j = 0; j < 3; ++j)
+        a[1 + j] = ci[3 * j] * (PW(i, 0) - cw0[0]) + ci[3 * j + 1] * (PW(i, 1) - cw0[1]) +
+                   ci[3 * j + 2] * (PW(i, 2) - cw0[2]);
+      a[0] = 1.0 - a[1] - a[2] - a[3];
 #pragma unroll
       for (int j = 0; j < 3; ++j)
         pcs[3 * i + j] = a[0] * ccs[0][j] + a[1] * ccs[1][j] + a[2] * ccs[2][j] + a[3] * ccs[3][j];
@@ -546,7 +785,7 @@ __device__ void epnp5(const double* pws, const double* us, const double* K4, dou
 #pragma unroll
       for (int j = 0; j < 3; ++j) {
         pc0[j] += pcs[3 * i + j];
-        pw0[j] += pws[3 * i + j];
+        pw0[j] += PW(i, j);
       }
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
@@ -559,8 +798,7 @@ __device__ void epnp5(const double* pws, const double* us, const double* K4, dou
 #pragma unroll
       for (int j = 0; j < 3; ++j)
 #pragma unroll
-        for (int k = 0; k < 3; ++k)
-          abt[3 * j + k] += (pcs[3 * i + j] - pc0[j]) * (pws[3 * i + k] - pw0[k]);
+        for (int k = 0; k < 3; ++k) abt[3 * j + k] += (pcs[3 * i + j] - pc0[j]) * (PW(i, k) - pw0[k]);
     double R[9], t[3];
     finish_R(abt, R);
 #pragma unroll
@@ -568,11 +806,11 @@ __device__ void epnp5(const double* pws, const double* us, const double* K4, dou
     double err = 0.0;
 #pragma unroll
     for (int i = 0; i < n; ++i) {
-      const double* pw = pws + 3 * i;
+      const double pw[3] = {PW(i, 0), PW(i, 1), PW(i, 2)};
       const double Xc = dot3(R, pw) + t[0], Yc = dot3(R + 3, pw) + t[1];
       const double iz = 1.0 / (dot3(R + 6, pw) + t[2]);
       const double ue = uc + fu * Xc * iz, ve = vc + fv * Yc * iz;
-      const double du = us[2 * i] - ue, dv = us[2 * i + 1] - ve;
+      const double du = US(i, 0) - ue, dv = US(i, 1) - ve;
       err += sqrt(du * du + dv * dv);
     }
     err /= n;
@@ -590,7 +828,7 @@ __device__ void epnp5(const double* pws, const double* us, const double* K4, dou
 }
 
 // RANSACUpdateNumIters (ptsetreg.cpp)
-__device__ int update_num_iters(double p, double ep, int model_points, int max_iters) {
+__device__ __forceinline__ int update_num_iters(double p, double ep, int model_points, int max_iters) {
   p = fmin(fmax(p, 0.0), 1.0);
   ep = fmin(fmax(ep, 0.0), 1.0);
   double num = fmax(1. - p, 2.2250738585072014e-308);
@@ -626,7 +864,7 @@ __device__ __forceinline__ double wave_sum_d(double v) {
 
 // sum `cnt` per-thread values across the workgroup; every thread gets the totals
 template <int CNT>
-__device__ void block_sum(double* vals, double* scratch /* [4][CNT] */) {
+__device__ __forceinline__ void block_sum(double* vals, double* scratch /* [4][CNT] */) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #pragma unroll
   for (int i = 0; i < CNT; ++i) {
@@ -641,6 +879,7 @@ __device__ void block_sum(double* vals, double* scratch /* [4][CNT] */) {
 }
 
 struct Shared {
+  double hh[65 * kRound];   // per-lane Householder scratch of eig12_small4
   // RANSAC round
   int subset[kRound][kModelPoints];
   double hypR[kRound][9];
@@ -655,7 +894,7 @@ struct Shared {
   double red[4 * 78];
   double cws[4][3];
   double ci[9];
-  double ut[144];
+  double vs[48];
   double L[60], rho[6];
   double betas[4];
   double ccs[4][3];
@@ -666,7 +905,7 @@ struct Shared {
 };
 
 // Workgroup-parallel EPnP over the points listed in idx[0..n) (epnp::compute_pose).
-__device__ void epnp_refit(Shared& sh, const float* p2, const float* p3, const int* idx, int n,
+__device__ __forceinline__ void epnp_refit(Shared& sh, const float* p2, const float* p3, const int* idx, int n,
                            const double* K4, double* R_out, double* t_out) {
   const int t = threadIdx.x;
   const double fu = K4[0], fv = K4[1], uc = K4[2], vc = K4[3];
@@ -696,7 +935,7 @@ __device__ void epnp_refit(Shared& sh, const float* p2, const float* p3, const i
   block_sum<6>(m6, sh.red);
   if (t == 0) {
     double m[9] = {m6[0], m6[1], m6[2], m6[1], m6[3], m6[4], m6[2], m6[4], m6[5]}, dc[3], uct[9];
-    jacobi_eigen<3>(m, dc, uct);
+    jacobi3(m, dc, uct);
     for (int j = 0; j < 3; ++j) sh.cws[0][j] = c0[j];
     for (int i = 1; i < 4; ++i) {
       const double k = sqrt(dc[i - 1] / n);
@@ -734,24 +973,17 @@ __device__ void epnp_refit(Shared& sh, const float* p2, const float* p3, const i
       r2[3 * k + 1] = as[k] * fv;
       r2[3 * k + 2] = as[k] * (vc - v);
     }
-    int e = 0;
 #pragma unroll
     for (int a = 0; a < 12; ++a)
 #pragma unroll
-      for (int b = a; b < 12; ++b) acc[e++] += r1[a] * r1[b] + r2[a] * r2[b];
+      for (int b = 0; b <= a; ++b) acc[LI(a, b)] += r1[a] * r1[b] + r2[a] * r2[b];
   }
   block_sum<78>(acc, sh.red);
   if (t == 0) {
-    double mtm[144], d[12];
-    int e = 0;
-    for (int a = 0; a < 12; ++a)
-      for (int b = a; b < 12; ++b) {
-        mtm[a * 12 + b] = acc[e];
-        mtm[b * 12 + a] = acc[e];
-        ++e;
-      }
-    jacobi_eigen<12>(mtm, d, sh.ut);
-    compute_L_6x10(sh.ut, sh.L);
+    double ev4[4][12];
+    eig12_small4<100>(acc, ev4, sh.hh, 1);
+    for (int i = 0; i < 48; ++i) sh.vs[i] = (&ev4[0][0])[i];
+    compute_L_6x10(sh.vs, sh.L);
     compute_rho(sh.cws, sh.rho);
   }
   __syncthreads();
@@ -760,7 +992,7 @@ __device__ void epnp_refit(Shared& sh, const float* p2, const float* p3, const i
       double betas[4];
       betas_approx(which, sh.L, sh.rho, betas);
       gauss_newton(sh.L, sh.rho, betas);
-      ccs_from_betas(sh.ut, betas, sh.ccs);
+      ccs_from_betas(sh.vs, betas, sh.ccs);
       // solve_for_sign looks at the first point's camera-frame depth
       double a[4];
       alphas(idx[0], a);
@@ -910,17 +1142,8 @@ __global__ __launch_bounds__(kThreads) void pnp_ransac_kernel(
     }
     __syncthreads();
     if (wave == 0) {  // one EPnP model per lane
-      double pws[15], us[10], rvec[3], tvec[3];
-#pragma unroll
-      for (int i = 0; i < kModelPoints; ++i) {
-        const int j = sh.subset[lane][i];
-        pws[3 * i] = p3[3 * j];
-        pws[3 * i + 1] = p3[3 * j + 1];
-        pws[3 * i + 2] = p3[3 * j + 2];
-        us[2 * i] = p2[2 * j];
-        us[2 * i + 1] = p2[2 * j + 1];
-      }
-      epnp5(pws, us, K4, rvec, tvec);
+      double rvec[3], tvec[3];
+      epnp5(sh.subset[lane], p2, p3, K4, rvec, tvec, sh.hh + lane, kRound);
       double R[9];
       rodrigues_v2m(rvec, R);
       for (int i = 0; i < 9; ++i) sh.hypR[lane][i] = R[i];
@@ -998,21 +1221,40 @@ __global__ __launch_bounds__(kThreads) void pnp_ransac_kernel(
     }
     nin = sh.n_inl;
   }
-  __threadfence_block();
-  __syncthreads();
   if (n == kModelPoints)
     for (int i = t; i < n; i += kThreads) mask[i] = 1;
+  if (t == 0) {   // the refit kernel reads these
+    n_inliers[b] = nin;
+    status[b] = 0;
+  }
+}
+
+// EPnP on the RANSAC inliers (solvePnPRansac's final solvePnP call), then
+// Rodrigues(R) -> rvec -> Rodrigues(rvec) as eval_utils.py:31 rebuilds R, t / scale.
+__global__ __launch_bounds__(kThreads) void pnp_refit_kernel(
+    const float* __restrict__ pts2d, const float* __restrict__ pts3d, int max_points,
+    const double* __restrict__ Kmat, int64_t K_bs, double scale, double* __restrict__ pose34,
+    const int* __restrict__ n_inliers, const int* __restrict__ status,
+    const int* __restrict__ idx_ws) {
+  __shared__ Shared sh;
+  const int b = blockIdx.x;
+  if (status[b] != 0) return;
+  const int t = threadIdx.x;
+  const int nin = n_inliers[b];
+  const double* K = Kmat + b * K_bs;
+  const double K4[4] = {K[0], K[4], K[2], K[5]};
+  const float* p2 = pts2d + (int64_t)b * max_points * 2;
+  const float* p3 = pts3d + (int64_t)b * max_points * 3;
   double Rf[9], tf[3], rv[3], Rr[9];
-  epnp_refit(sh, p2, p3, idx, nin, K4, Rf, tf);
-  rodrigues_m2v(Rf, rv);       // solvePnP returns rvec ...
-  rodrigues_v2m(rv, Rr);       // ... and eval_utils.py:31 turns it back into R
+  epnp_refit(sh, p2, p3, idx_ws + (int64_t)b * max_points, nin, K4, Rf, tf);
+  rodrigues_m2v(Rf, rv);
+  rodrigues_v2m(rv, Rr);
   if (t == 0) {
+    double* pose = pose34 + (int64_t)b * 12;
     for (int i = 0; i < 3; ++i) {
       for (int j = 0; j < 3; ++j) pose[i * 4 + j] = Rr[i * 3 + j];
       pose[i * 4 + 3] = tf[i] / scale;
     }
-    n_inliers[b] = nin;
-    status[b] = 0;
   }
 }
 
@@ -1054,10 +1296,13 @@ int onepose_pnp_ransac(const float* pts2d, const float* pts3d, const int* counts
                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     attr_set = true;
   }
-  OP_LAUNCH(K_PNP, static_cast<hipStream_t>(stream), pnp_ransac_kernel, dim3(batch), dim3(kThreads), lds,
-                     static_cast<hipStream_t>(stream), pts2d, pts3d, counts, max_points, K,
-                     K_bstride, scale, reproj_error, max_iters, confidence, pose34, inlier_mask,
-                     n_inliers, status, static_cast<int*>(workspace));
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  OP_LAUNCH(K_PNP, st, pnp_ransac_kernel, dim3(batch), dim3(kThreads), lds, st, pts2d, pts3d,
+            counts, max_points, K, K_bstride, scale, reproj_error, max_iters, confidence, pose34,
+            inlier_mask, n_inliers, status, static_cast<int*>(workspace));
+  OP_LAUNCH(K_PNP_REFIT, st, pnp_refit_kernel, dim3(batch), dim3(kThreads), 0, st, pts2d, pts3d,
+            max_points, K, K_bstride, scale, pose34, n_inliers, status,
+            static_cast<const int*>(workspace));
   return ONEPOSE_OK;
 }
 

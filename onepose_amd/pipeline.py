@@ -4,9 +4,13 @@ device, with no host round trip and no per-frame re-upload of the object's 3D te
     matcher (onepose_match) -> correspondence selection -> RANSAC-EPnP -> cm/deg error
 
 The object's descriptors / leaves / 3D points are uploaded once (``inference.py:89-90``
-re-uploads them every frame).  All buffers are allocated at construction, so ``enqueue()``
-only launches kernels on the current stream and can be captured in a HIP graph
-(``torch.cuda.CUDAGraph``) and replayed.
+re-uploads them every frame).  All buffers are allocated at construction, so the enqueue
+methods only launch kernels on the current stream and can be captured in a HIP graph.
+
+Streaming (``run_stream``): the pose stage of frame k needs one CU (one workgroup per
+frame) while the matcher of frame k+1 needs the whole chip, so the two run on separate HIP
+streams with two buffer slots; events order matcher(k) -> pose(k) and pose(k) -> the
+matcher that next overwrites slot k % 2.  Every frame still runs every kernel.
 """
 from __future__ import annotations
 
@@ -17,10 +21,35 @@ from . import _lib
 from .matcher import GATsSuperGlue
 
 
+class _Slot:
+    def __init__(self, B, n1, n3, dev, with_conf, lib, L, iters):
+        f32 = dict(dtype=torch.float32, device=dev)
+        self.matches0 = torch.empty(B, n1, dtype=torch.int64, device=dev)
+        self.matches1 = torch.empty(B, n3, dtype=torch.int64, device=dev)
+        self.mscores0 = torch.empty(B, n1, **f32)
+        self.mscores1 = torch.empty(B, n3, **f32)
+        self.conf = torch.empty(B, n1, n3, **f32) if with_conf else None
+        self.pts2d = torch.empty(B, n1, 2, **f32)
+        self.pts3d = torch.empty(B, n1, 3, **f32)
+        self.counts = torch.empty(B, dtype=torch.int32, device=dev)
+        self.pose = torch.empty(B, 3, 4, dtype=torch.float64, device=dev)
+        self.inlier_mask = torch.empty(B, n1, dtype=torch.uint8, device=dev)
+        self.n_inliers = torch.empty(B, dtype=torch.int32, device=dev)
+        self.status = torch.empty(B, dtype=torch.int32, device=dev)
+        self.R_err = torch.empty(B, dtype=torch.float64, device=dev)
+        self.t_err = torch.empty(B, dtype=torch.float64, device=dev)
+        self.cmd = torch.empty(B, 3, dtype=torch.uint8, device=dev)
+        self.ws_match_bytes = lib.onepose_match_workspace_bytes(B, n1, n3, L, int(with_conf))
+        self.ws_match = torch.empty(self.ws_match_bytes, dtype=torch.uint8, device=dev)
+        self.ws_pnp_bytes = lib.onepose_pnp_workspace_bytes(B, n1, iters)
+        self.ws_pnp = torch.empty(self.ws_pnp_bytes, dtype=torch.uint8, device=dev)
+
+
 class FramePipeline:
     def __init__(self, matcher: GATsSuperGlue, keypoints3d, desc3d, leaves, batch: int, n1: int,
                  device, scale: float = 1000.0, reprojection_error: float = 5.0,
-                 iterations_count: int = 10000, confidence: float = 0.99, with_conf=True):
+                 iterations_count: int = 10000, confidence: float = 0.99, with_conf=True,
+                 slots: int = 2):
         self.lib = _lib.load()
         self.device = torch.device(device)
         self.B, self.n1 = int(batch), int(n1)
@@ -44,27 +73,15 @@ class FramePipeline:
         self.kpts2d = torch.zeros(B, n1, 2, **f32)
         self.K = torch.zeros(B, 3, 3, dtype=torch.float64, device=dev)
         self.pose_gt = torch.zeros(B, 3, 4, dtype=torch.float64, device=dev)
-        # outputs
-        self.matches0 = torch.empty(B, n1, dtype=torch.int64, device=dev)
-        self.matches1 = torch.empty(B, self.n3, dtype=torch.int64, device=dev)
-        self.mscores0 = torch.empty(B, n1, **f32)
-        self.mscores1 = torch.empty(B, self.n3, **f32)
-        self.conf = torch.empty(B, n1, self.n3, **f32) if with_conf else None
-        self.pts2d = torch.empty(B, n1, 2, **f32)
-        self.pts3d = torch.empty(B, n1, 3, **f32)
-        self.counts = torch.empty(B, dtype=torch.int32, device=dev)
-        self.pose = torch.empty(B, 3, 4, dtype=torch.float64, device=dev)
-        self.inlier_mask = torch.empty(B, n1, dtype=torch.uint8, device=dev)
-        self.n_inliers = torch.empty(B, dtype=torch.int32, device=dev)
-        self.status = torch.empty(B, dtype=torch.int32, device=dev)
-        self.R_err = torch.empty(B, dtype=torch.float64, device=dev)
-        self.t_err = torch.empty(B, dtype=torch.float64, device=dev)
-        self.cmd = torch.empty(B, 3, dtype=torch.uint8, device=dev)
-        self.ws_match_bytes = self.lib.onepose_match_workspace_bytes(B, n1, self.n3, self.L,
-                                                                     int(with_conf))
-        self.ws_match = torch.empty(self.ws_match_bytes, dtype=torch.uint8, device=dev)
-        self.ws_pnp_bytes = self.lib.onepose_pnp_workspace_bytes(B, n1, self.iters)
-        self.ws_pnp = torch.empty(self.ws_pnp_bytes, dtype=torch.uint8, device=dev)
+        self.slots = [_Slot(B, n1, self.n3, dev, with_conf, self.lib, self.L, self.iters)
+                      for _ in range(max(1, slots))]
+
+    def __getattr__(self, name):
+        # slot-0 outputs as attributes (pipe.pose, pipe.matches0, ...) for the common case
+        slots = self.__dict__.get("slots")
+        if slots is not None and hasattr(slots[0], name):
+            return getattr(slots[0], name)
+        raise AttributeError(name)
 
     def set_frames(self, desc2d, kpts2d, K, pose_gt):
         """Copy B frames' inputs into the static buffers (host or device arrays)."""
@@ -74,32 +91,58 @@ class FramePipeline:
         self.pose_gt.copy_(torch.as_tensor(np.asarray(pose_gt), dtype=torch.float64)[..., :3, :]
                            .expand_as(self.pose_gt))
 
-    def enqueue_match(self):
+    def enqueue_match(self, slot: int = 0):
+        o = self.slots[slot]
         s = _lib.stream_ptr(self.device)
         _lib.check(self.lib.onepose_match(
             self.weights.data_ptr(), self.desc2d.data_ptr(), 256 * self.n1,
             self.desc3d.data_ptr(), 0, self.leaves.data_ptr(), 0,
             self.B, self.n1, self.n3, self.L, self.scale_factor, self.threshold,
-            self.matches0.data_ptr(), self.matches1.data_ptr(), self.mscores0.data_ptr(),
-            self.mscores1.data_ptr(), _lib.ptr(self.conf), self.ws_match.data_ptr(),
-            self.ws_match_bytes, s), "onepose_match")
+            o.matches0.data_ptr(), o.matches1.data_ptr(), o.mscores0.data_ptr(),
+            o.mscores1.data_ptr(), _lib.ptr(o.conf), o.ws_match.data_ptr(),
+            o.ws_match_bytes, s), "onepose_match")
 
-    def enqueue_pose(self):
+    def enqueue_pose(self, slot: int = 0):
+        o = self.slots[slot]
         s = _lib.stream_ptr(self.device)
         lib = self.lib
         _lib.check(lib.onepose_select_correspondences(
-            self.matches0.data_ptr(), self.kpts2d.data_ptr(), self.n1 * 2, self.kp3.data_ptr(), 0,
-            self.B, self.n1, self.n3, self.scale, self.pts2d.data_ptr(), self.pts3d.data_ptr(),
-            self.counts.data_ptr(), s), "select_correspondences")
+            o.matches0.data_ptr(), self.kpts2d.data_ptr(), self.n1 * 2, self.kp3.data_ptr(), 0,
+            self.B, self.n1, self.n3, self.scale, o.pts2d.data_ptr(), o.pts3d.data_ptr(),
+            o.counts.data_ptr(), s), "select_correspondences")
         _lib.check(lib.onepose_pnp_ransac(
-            self.pts2d.data_ptr(), self.pts3d.data_ptr(), self.counts.data_ptr(), self.n1,
+            o.pts2d.data_ptr(), o.pts3d.data_ptr(), o.counts.data_ptr(), self.n1,
             self.K.data_ptr(), 9, self.B, self.scale, self.reproj, self.iters, self.conf_level,
-            self.pose.data_ptr(), self.inlier_mask.data_ptr(), self.n_inliers.data_ptr(),
-            self.status.data_ptr(), self.ws_pnp.data_ptr(), self.ws_pnp_bytes, s), "pnp_ransac")
+            o.pose.data_ptr(), o.inlier_mask.data_ptr(), o.n_inliers.data_ptr(),
+            o.status.data_ptr(), o.ws_pnp.data_ptr(), o.ws_pnp_bytes, s), "pnp_ransac")
         _lib.check(lib.onepose_pose_errors(
-            self.pose.data_ptr(), self.pose_gt.data_ptr(), 12, self.B, self.R_err.data_ptr(),
-            self.t_err.data_ptr(), self.cmd.data_ptr(), s), "pose_errors")
+            o.pose.data_ptr(), self.pose_gt.data_ptr(), 12, self.B, o.R_err.data_ptr(),
+            o.t_err.data_ptr(), o.cmd.data_ptr(), s), "pose_errors")
 
-    def enqueue(self):
-        self.enqueue_match()
-        self.enqueue_pose()
+    def enqueue(self, slot: int = 0):
+        self.enqueue_match(slot)
+        self.enqueue_pose(slot)
+
+    def run_stream(self, steps: int, match_stream=None, pose_stream=None):
+        """Enqueue `steps` frames (batches) with matcher(k+1) overlapping pose(k).
+        Returns the pose stream; the caller synchronises."""
+        ms = match_stream or torch.cuda.current_stream(self.device)
+        ps = pose_stream or torch.cuda.Stream(self.device)
+        n = len(self.slots)
+        matched = [torch.cuda.Event() for _ in range(n)]
+        posed = [None] * n
+        for k in range(steps):
+            sl = k % n
+            with torch.cuda.stream(ms):
+                if posed[sl] is not None:
+                    ms.wait_event(posed[sl])
+                self.enqueue_match(sl)
+                matched[sl].record(ms)
+            with torch.cuda.stream(ps):
+                ps.wait_event(matched[sl])
+                self.enqueue_pose(sl)
+                ev = torch.cuda.Event()
+                ev.record(ps)
+                posed[sl] = ev
+        ms.wait_stream(ps)
+        return ps
