@@ -38,11 +38,9 @@ def kernel_work(kind, B, n1, n3, L):
     T = B * (n1 + n3)
     C = 256
     table = {
-        "qkv_gemm": (2 * 3 * C * C * T, "flop", "mfma"),
-        "kv_partial": (4 * 2 * 64 * 64 * T, "flop", "mfma"),
-        "attn_apply": (4 * 2 * 64 * 64 * T, "flop", "mfma"),
-        "merge_gemm": (2 * C * C * T, "flop", "mfma"),
-        "mlp1_gemm": (2 * 2 * C * 2 * C * T, "flop", "mfma"),
+        "kv_gemm": (2 * 2 * C * C * T, "flop", "mfma"),
+        "q_gemm": (2 * C * C * T, "flop", "mfma"),
+        "mlp1_gemm": (2 * 2 * C * 2 * C * T, "flop", "mfma"),   # [W1a | Mf] [x ; QZ]
         "mlp2_gemm": (2 * 2 * C * C * T, "flop", "mfma"),
         "final_gemm": (2 * C * C * T, "flop", "mfma"),
         "score_gemm": (2 * C * n1 * n3 * B, "flop", "mfma"),

@@ -5,9 +5,10 @@
 //
 // Activations are token-major ([tokens][channels], a token's channels contiguous), so a
 // 1x1 Conv1d of the reference (x [C,N] -> W x + b) is this GEMM with the reference weight
-// [O][C] used as is.  One launch runs up to two problems (the 2D-query side and the 3D
-// side of a layer) and every batch sample of each; tiles never straddle samples, so
-// per-sample reductions (InstanceNorm statistics, softmax partials) stay per sample.
+// [O][C] used as is.  A and W may each be split along K at `ksplit` into two sources (the
+// MLP's cat[x, message] input and its folded weights).  One launch runs up to two problems
+// (the 2D-query side and the 3D side of a layer) and every batch sample of each; tiles never
+// straddle samples, so per-sample reductions stay per sample.
 #pragma once
 
 #include "common.h"
@@ -16,10 +17,12 @@ namespace onepose {
 
 enum GemmEpi {
   EPI_BIAS = 0,    // y = acc + bias
-  EPI_QKV = 1,     // y = acc + bias; col < phi_cols ? elu(y)+1 : y / vdiv   (q,k: phi; v: /Ns)
+  EPI_KVPART = 1,  // 128-col tile = [k_h | v_h]: phi(k), v/vdiv -> per-tile KV_h = phi(k)^T v
+                   //   and sum phi(k) partials (linear-attention source reduction)
   EPI_STATS = 2,   // y = acc + bias, plus per-tile (mean, M2) of every column  (InstanceNorm)
   EPI_RESID = 3,   // y = R + (acc + bias)                                     (desc += delta)
   EPI_SCORE = 4,   // y = acc / scale, plus per-tile row/col (max, sum exp)     (dual softmax)
+  EPI_QZ = 5,      // 64-col tile = q_h: phi(q) * Z * Ns, Z = 1/(phi(q).ksum_h + 1e-6)
 };
 enum GemmPro {
   PRO_PLAIN = 0,
@@ -31,9 +34,12 @@ struct GemmProb {
   const float* A1;     // [batch][M][lda1]; columns [ksplit, K) (concat), may be null
   int64_t a0_bs, a1_bs;
   int lda0, lda1, ksplit;
-  const float* W;      // [N][ldw] (out-major); w_bs per sample (0 = shared weights)
+  const float* W;      // [N][ldw] (out-major) for k < ksplit; w_bs per sample (0 = shared)
   int64_t w_bs;
   int ldw;
+  const float* W1;     // [N][ldw1] for k >= ksplit (null: W continues)
+  int64_t w1_bs;
+  int ldw1;
   const float* bias;   // [N] or null
   float* Y;            // [batch][M][ldy]
   int64_t y_bs;
@@ -47,9 +53,13 @@ struct GemmProb {
   float* stats;        // EPI_STATS: [batch][mtiles][2][N]
   float* rowstat;      // EPI_SCORE: [batch][M][ntiles][2]
   float* colstat;      // EPI_SCORE: [batch][N][mtiles][2]
+  float* kvpart;       // EPI_KVPART: [batch][mtiles][4][64][64]
+  float* kspart;       // EPI_KVPART: [batch][mtiles][256]
+  const float* ksum;   // EPI_QZ: [batch][256] of the attention source
+  int64_t ksum_bs;
   float scale;         // EPI_SCORE divisor (scale_factor)
-  float vdiv;          // EPI_QKV divisor for columns >= phi_cols
-  int phi_cols;
+  float vdiv;          // EPI_KVPART: v divisor (source length)
+  float ns;            // EPI_QZ: source length (v_length)
   int M, N, K, batch;
   int mtiles, ntiles, tiles;   // filled by gemm_launch
 };
@@ -59,8 +69,13 @@ struct GemmArgs {
   int nprob;
 };
 
-constexpr int kGemmBM = 64, kGemmBN = 64, kGemmBK = 32;
+constexpr int kGemmBM = 64, kGemmBK = 32;
 
-int gemm_launch(int epi, int pro, GemmArgs& args, hipStream_t stream, int kind);
+// bn = 64 or 128 (column tile); EPI_KVPART needs 128, EPI_QZ 64.
+int gemm_launch(int epi, int pro, int bn, GemmArgs& args, hipStream_t stream, int kind);
+
+// Zero-initialised problem with the common fields set.
+GemmProb gemm_prob(const float* A, int lda, const float* W, int ldw, const float* bias,
+                   float* Y, int ldy, int M, int N, int K, int batch);
 
 }  // namespace onepose

@@ -2,9 +2,11 @@
 //
 // Data layout in HBM (per batch sample, fp32):
 //   X2 [N1][256], X3 [N3][256]       token-major descriptors (ping-pong buffers)
-//   QKV [N][768]                     phi(q) | phi(k) | v/Ns, channels head-major (h*64+d)
-//   KVt [h][q][d], ksum [h*64+d]     linear-attention state of one source tensor
-//   O, MSG [N][256], Y1 [N][512]     attention output, merged message, MLP hidden
+//   KVpart [chunk][h][d][q]          per-64-token linear-attention partials (kv GEMM epilogue)
+//   KV [h][d][q], ksum [h*64+d]      linear-attention state of one source tensor
+//   QZ [N][256]                      phi(q) * Z * Ns, channels head-major (h*64+d)
+//   Mf [512][256]                    per-frame folded weights  (W1b Wm) KV_h^T  per head
+//   Y1 [N][512]                      MLP hidden
 //   S/conf [N1][N3]                  score matrix, overwritten in place by conf_matrix
 // The reference's [B, C, N] inputs are transposed once on entry; the leaf descriptors
 // ([B, 256, N3*L], per-object constants, 33.5 MB at N3=4096) are read in place by the
@@ -13,7 +15,17 @@
 // Layer schedule (AttentionalGNN.forward, GATs_SuperGlue.py:67-85): for each of the 12
 // layers, GAT layers update X3 only; self/cross layers run both sides in the same
 // launches (two problems per grid) because delta0 and delta1 both read the pre-update
-// descriptors (:77-78, :82-83).
+// descriptors (:77-78, :82-83).  One attention layer (AttentionPropagation, :123-132):
+//   1. kv GEMM  [phi(k)_h | v_h/Ns] per 128-column tile, epilogue: KV_h / sum phi(k) partials
+//   2. kv_reduce: KV[src], ksum[src]
+//   3. m_fold: Mf = C_h KV_h^T with C = W1b Wm  (merge conv folded into MLP conv 1)
+//   4. q GEMM, epilogue phi(q) * Z * Ns
+//   5. MLP conv 1 = [W1a | Mf] [x ; QZ] + (b1 + W1b bm), epilogue InstanceNorm partials
+//   6. InstanceNorm statistics
+//   7. MLP conv 2 on ReLU(norm(.)) + residual
+// Steps 3-5 are an exact re-association of message = merge(attention), MLP(cat[x, msg])
+// (the linear attention output and the merge conv are linear in the message): the fp32
+// result differs from the reference's evaluation order only in rounding.
 #include <cmath>
 #include <cstdarg>
 #include <cstring>
@@ -50,10 +62,9 @@ struct Prof {
 };
 Prof g_prof;
 const char* kKindNames[K_NUM_KINDS] = {
-    "transpose_in", "gat", "qkv_gemm", "kv_partial", "kv_reduce", "attn_apply", "merge_gemm",
-    "mlp1_gemm", "stats_finalize", "mlp2_gemm", "final_gemm", "l2norm", "score_gemm",
-    "softmax_reduce", "conf", "mutual", "select", "pnp_ransac", "pose_error", "sample_desc",
-    "pnp_refit"};
+    "transpose_in", "gat", "kv_gemm", "q_gemm", "kv_reduce", "m_fold", "mlp1_gemm",
+    "stats_finalize", "mlp2_gemm", "final_gemm", "l2norm", "score_gemm", "softmax_reduce",
+    "conf", "mutual", "select", "pnp_ransac", "pnp_refit", "pose_error", "sample_desc"};
 }  // namespace
 
 void prof_pre(int kind, hipStream_t s) {
@@ -76,25 +87,33 @@ constexpr int kLayers = 12;
 constexpr int kApLayers = 8;
 constexpr int kGatLayers = 4;
 
-// packed panel, floats
-constexpr int64_t kApWqkv = 768 * 256, kApBqkv = 768, kApWm = 256 * 256, kApBm = 256;
-constexpr int64_t kApW1 = 512 * 512, kApB1 = 512, kApW2 = 256 * 512, kApB2 = 256;
-constexpr int64_t kApFloats = kApWqkv + kApBqkv + kApWm + kApBm + kApW1 + kApB1 + kApW2 + kApB2;
+// packed panel, floats (per attention layer):
+//   Wkv [512][256]: per head h: 64 rows of k_h then 64 rows of v_h (ref rows d*4+h)
+//   bkv [512], Wq [256][256] head-major rows, bq [256]
+//   W1a [512][256] = mlp.0.weight[:, :256]
+//   C   [512][256] = mlp.0.weight[:, 256:] @ merge.weight, columns head-major (h*64+q)
+//   b1f [512]      = mlp.0.bias + mlp.0.weight[:, 256:] @ merge.bias
+//   W2 [256][512], b2 [256]
+constexpr int64_t kApWkv = 512 * 256, kApBkv = 512, kApWq = 256 * 256, kApBq = 256;
+constexpr int64_t kApW1a = 512 * 256, kApC = 512 * 256, kApB1 = 512, kApW2 = 256 * 512,
+                  kApB2 = 256;
+constexpr int64_t kApFloats = kApWkv + kApBkv + kApWq + kApBq + kApW1a + kApC + kApB1 + kApW2 + kApB2;
 constexpr int64_t kGatFloats = 512;
 constexpr int64_t kFinalFloats = 256 * 256 + 256;
 constexpr int64_t kPackedFloats = kApLayers * kApFloats + kGatLayers * kGatFloats + kFinalFloats;
 
 struct ApW {
-  const float *wqkv, *bqkv, *wm, *bm, *w1, *b1, *w2, *b2;
+  const float *wkv, *bkv, *wq, *bq, *w1a, *c, *b1, *w2, *b2;
 };
 ApW ap_weights(const float* base, int ap) {
   const float* p = base + (int64_t)ap * kApFloats;
   ApW w;
-  w.wqkv = p; p += kApWqkv;
-  w.bqkv = p; p += kApBqkv;
-  w.wm = p; p += kApWm;
-  w.bm = p; p += kApBm;
-  w.w1 = p; p += kApW1;
+  w.wkv = p; p += kApWkv;
+  w.bkv = p; p += kApBkv;
+  w.wq = p; p += kApWq;
+  w.bq = p; p += kApBq;
+  w.w1a = p; p += kApW1a;
+  w.c = p; p += kApC;
   w.b1 = p; p += kApB1;
   w.w2 = p; p += kApW2;
   w.b2 = p;
@@ -166,17 +185,13 @@ __global__ __launch_bounds__(256) void transpose_in_kernel(const float* __restri
   }
 }
 
-// Linear-attention source reduction, one 64-token chunk per workgroup, one head per wave:
-//   KVpart[h][d][q] = sum_m phi(k)[m][h,d] * v[m][h,q]      (einsum 'bdhm,bqhm->bqdh', :96)
-//   kspart[h*64+d]  = sum_m phi(k)[m][h,d]                 (key.sum(3), :97)
-// The chunk's phi(k)|v rows (2 KB contiguous per token) are staged into LDS 32 tokens at a
-// time with 16-byte loads; v_mfma_f32_32x32x2_f32 then runs with the token as the K
-// dimension straight out of LDS (32 consecutive lanes read 32 consecutive channels).
+// Linear-attention source state.  The kv GEMM's epilogue (EPI_KVPART) leaves, per 64-token
+// chunk, KVpart[h][d][q] = sum_m phi(k)[m][h,d] v[m][h,q]/Ns  (einsum 'bdhm,bqhm->bqdh', :96)
+// and kspart[h*64+d] = sum_m phi(k)[m][h,d]  (key.sum(3), :97); kv_reduce sums the chunks.
 struct KvProb {
-  const float* qkv;   // [B][N][768]
-  float* part;        // [B][chunks][4][64][64]
-  float* kspart;      // [B][chunks][256]
-  int n, chunks, blocks;
+  const float* part;  // [B][chunks][4][64][64]
+  const float* kspart;  // [B][chunks][256]
+  int chunks;
 };
 struct KvArgs {
   KvProb p[2];
@@ -184,78 +199,19 @@ struct KvArgs {
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 
-constexpr int kKvStage = 32;   // tokens per LDS stage
-
-__global__ __launch_bounds__(256) void kv_partial_kernel(KvArgs args) {
-  __shared__ __attribute__((aligned(16))) float stage[kKvStage * 512];
-  int bid = blockIdx.x;
-  const bool second = bid >= args.p[0].blocks;
-  const KvProb& P = second ? args.p[1] : args.p[0];
-  if (second) bid -= args.p[0].blocks;
-  const int b = bid / P.chunks, chunk = bid - b * P.chunks;
-  const int t = threadIdx.x, lane = t & 63, h = t >> 6;
-  const int half = lane >> 5, l32 = lane & 31;
-  const float* base = P.qkv + (int64_t)b * P.n * 768;
-  const int m_begin = chunk * 64;
-
-  floatx16 acc00, acc01, acc10, acc11;
-#pragma unroll
-  for (int i = 0; i < 16; ++i) acc00[i] = acc01[i] = acc10[i] = acc11[i] = 0.f;
-  float ks0 = 0.f, ks1 = 0.f;
-  for (int s0 = 0; s0 < 64; s0 += kKvStage) {
-    __syncthreads();
-#pragma unroll
-    for (int i = 0; i < kKvStage * 128 / 256; ++i) {   // 32 rows x 128 float4
-      const int e = t + 256 * i, r = e >> 7, c4 = e & 127;
-      const int tok = m_begin + s0 + r;
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (tok < P.n) v = *reinterpret_cast<const float4*>(base + (int64_t)tok * 768 + 256 + c4 * 4);
-      *reinterpret_cast<float4*>(stage + r * 512 + c4 * 4) = v;
-    }
-    __syncthreads();
-    const float* ka = stage + h * 64 + l32;
-    const float* va = stage + 256 + h * 64 + l32;
-#pragma unroll 4
-    for (int k = 0; k < kKvStage; k += 2) {
-      const int r = (k + half) * 512;
-      const float a0 = ka[r], a1 = ka[r + 32], v0 = va[r], v1 = va[r + 32];
-      ks0 += a0;
-      ks1 += a1;
-      acc00 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, v0, acc00, 0, 0, 0);
-      acc01 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, v1, acc01, 0, 0, 0);
-      acc10 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, v0, acc10, 0, 0, 0);
-      acc11 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, v1, acc11, 0, 0, 0);
-    }
-  }
-  float* out = P.part + ((int64_t)b * P.chunks + chunk) * 16384 + h * 4096;
-#pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    const int d = (i & 3) + 8 * (i >> 2) + 4 * half;
-    out[d * 64 + l32] = acc00[i];
-    out[d * 64 + 32 + l32] = acc01[i];
-    out[(d + 32) * 64 + l32] = acc10[i];
-    out[(d + 32) * 64 + 32 + l32] = acc11[i];
-  }
-  ks0 += __shfl_xor(ks0, 32, 64);
-  ks1 += __shfl_xor(ks1, 32, 64);
-  if (half == 0) {
-    float* ko = P.kspart + ((int64_t)b * P.chunks + chunk) * 256 + h * 64;
-    ko[l32] = ks0;
-    ko[32 + l32] = ks1;
-  }
-}
-
-// Sum the chunk partials -> KV[h][d][q], ksum[256], one float4 of outputs per thread with
-// eight chunk loads in flight; the summation order is fixed (deterministic).
+// Sum the chunk partials -> KV[h][d][q], ksum[256].  Each workgroup owns 64 float4 outputs
+// of one (source, sample); its four waves sum interleaved quarters of the chunks (eight
+// loads in flight each) and the quarters are added in a fixed order (deterministic).
 __global__ __launch_bounds__(256) void kv_reduce_kernel(KvArgs args, float* kv, float* ksum,
                                                         int batch) {
-  constexpr int per = (16384 + 256) / 4;   // float4 outputs per (source, sample)
-  const int idx = blockIdx.x * 256 + threadIdx.x;
-  if (idx >= 2 * batch * per) return;
-  const int src = idx / (batch * per);
-  const int r = idx - src * batch * per;
-  const int b = r / per, e4 = r - b * per;
+  constexpr int per = (16384 + 256) / 4;   // float4 outputs per (source, sample) = 4160
+  constexpr int groups = per / 64;         // 65 workgroups per (source, sample)
+  __shared__ float4 red[4][64];
+  const int g = blockIdx.x % groups, bs = blockIdx.x / groups;
+  const int b = bs % batch, src = bs / batch;
   const KvProb& P = src ? args.p[1] : args.p[0];
+  const int lane = threadIdx.x & 63, q4 = threadIdx.x >> 6;
+  const int e4 = g * 64 + lane;
   const float4* p;
   int64_t stride;
   float4* out;
@@ -268,135 +224,65 @@ __global__ __launch_bounds__(256) void kv_reduce_kernel(KvArgs args, float* kv, 
     stride = 64;
     out = reinterpret_cast<float4*>(ksum + ((int64_t)src * batch + b) * 256) + (e4 - 4096);
   }
-  float4 acc[8];
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  int c = q4;
+  for (; c + 28 < P.chunks; c += 32) {
+    float4 v[8];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) acc[j] = make_float4(0.f, 0.f, 0.f, 0.f);
-  int c = 0;
-  for (; c + 8 <= P.chunks; c += 8) {
+    for (int j = 0; j < 8; ++j) v[j] = p[(int64_t)(c + 4 * j) * stride];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const float4 v = p[(int64_t)(c + j) * stride];
-      acc[j].x += v.x; acc[j].y += v.y; acc[j].z += v.z; acc[j].w += v.w;
-    }
+    for (int j = 0; j < 8; ++j) { acc.x += v[j].x; acc.y += v[j].y; acc.z += v[j].z; acc.w += v[j].w; }
   }
-  float4 tail = make_float4(0.f, 0.f, 0.f, 0.f);
-  for (; c < P.chunks; ++c) {
+  for (; c < P.chunks; c += 4) {
     const float4 v = p[(int64_t)c * stride];
-    tail.x += v.x; tail.y += v.y; tail.z += v.z; tail.w += v.w;
+    acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
   }
-  float4 s = acc[0];
+  red[q4][lane] = acc;
+  __syncthreads();
+  if (q4 == 0) {
+    float4 s = red[0][lane];
 #pragma unroll
-  for (int j = 1; j < 8; ++j) { s.x += acc[j].x; s.y += acc[j].y; s.z += acc[j].z; s.w += acc[j].w; }
-  s.x += tail.x; s.y += tail.y; s.z += tail.z; s.w += tail.w;
-  *out = s;
+    for (int j = 1; j < 4; ++j) { s.x += red[j][lane].x; s.y += red[j][lane].y; s.z += red[j][lane].z; s.w += red[j][lane].w; }
+    *out = s;
+  }
 }
 
-// Linear-attention apply (GATs_SuperGlue.py:97-98):
-//   Z[n,h]   = 1 / (sum_d phi(q)[n][h,d] * ksum[h,d] + 1e-6)
-//   O[n][h*64+q] = (sum_d phi(q)[n][h,d] * KV[h][d][q]) * Z[n,h] * Ns
-// One 64-token tile per workgroup, one head per wave.  phi(q) tile [64][256] and the four
-// 64x64 KV blocks (transposed to [h][q][d]) are staged in LDS (pitches 260 / 68 floats:
-// conflict-free ds_read_b128), then 2x2 32x32 MFMA accumulators per wave.
-struct ApplyProb {
-  const float* qkv;    // query side [B][Nq][768] (phi(q) in columns 0..255)
-  const float* kv;     // source [B][4][64 d][64 q]
-  const float* ksum;   // source [B][256]
-  float* out;          // [B][Nq][256]
-  int nq;
-  float ns;            // source length (v_length)
-  int mtiles, blocks;
+// Folded message weights, per (side, sample, head h, 64-row block of o):
+//   Mf[o][h*64+d] = sum_q C[o][h*64+q] * KV_src[h][d][q]
+// so that  W1b merge(attention(x, src)) = Mf (phi(q) * Z * Ns)  (GATs_SuperGlue.py:96-98,
+// :119-120, then mlp[0]).  64x64 output, K = 64, 2x2 waves of 32x32 MFMA tiles; operands
+// are L2-resident (C: 512 KB per layer, KV: 64 KB per source).
+struct FoldProb {
+  const float* kv;    // [B][4][64][64] of the source
+  float* mf;          // [B][512][256]
 };
-struct ApplyArgs {
-  ApplyProb p[2];
+struct FoldArgs {
+  FoldProb p[2];
+  const float* c;     // [512][256]
 };
-constexpr int kQPitch = 260, kKvPitch = 68;
-constexpr size_t kApplyLds = (64 * kQPitch + 4 * 64 * kKvPitch + 4 * 64) * sizeof(float);
-
-__global__ __launch_bounds__(256) void attn_apply_kernel(ApplyArgs args) {
-  extern __shared__ __attribute__((aligned(16))) float sm[];
-  float* qs = sm;                          // [64][260]
-  float* kvs = qs + 64 * kQPitch;          // [4][64 q][68]
-  float* zs = kvs + 4 * 64 * kKvPitch;     // [4][64]
-  int bid = blockIdx.x;
-  const bool second = bid >= args.p[0].blocks;
-  const ApplyProb& P = second ? args.p[1] : args.p[0];
-  if (second) bid -= args.p[0].blocks;
-  const int b = bid / P.mtiles, mt = bid - b * P.mtiles;
-  const int m0 = mt * 64;
-  const int t = threadIdx.x, lane = t & 63, h = t >> 6;
-  const int half = lane >> 5, l32 = lane & 31;
-  const float* q = P.qkv + (int64_t)b * P.nq * 768;
-  const float* kvg = P.kv + (int64_t)b * 16384;
-  const float* ks = P.ksum + (int64_t)b * 256;
+__global__ __launch_bounds__(256) void m_fold_kernel(FoldArgs args, int batch) {
+  const int ot = blockIdx.x & 7, h = (blockIdx.x >> 3) & 3;
+  const int bs = blockIdx.x >> 5, b = bs % batch, side = bs / batch;
+  const FoldProb& P = side ? args.p[1] : args.p[0];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wm = wave >> 1, wn = wave & 1, half = lane >> 5, l32 = lane & 31;
+  const float* a = args.c + (int64_t)(ot * 64 + wm * 32 + l32) * 256 + h * 64 + half * 4;
+  const float* w = P.kv + (int64_t)b * 16384 + h * 4096 + (wn * 32 + l32) * 64 + half * 4;
+  floatx16 acc;
 #pragma unroll
-  for (int i = 0; i < 16; ++i) {   // phi(q) tile: 64 rows x 64 float4
-    const int e = t + 256 * i, r = e >> 6, c4 = e & 63;
-    const int tok = m0 + r;
-    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (tok < P.nq) v = *reinterpret_cast<const float4*>(q + (int64_t)tok * 768 + c4 * 4);
-    *reinterpret_cast<float4*>(qs + r * kQPitch + c4 * 4) = v;
-  }
-#pragma unroll
-  for (int i = 0; i < 16; ++i) {   // KV[h][d][q] -> kvs[h][q][d]
-    const int e = t + 256 * i;     // float4 index over [4][64][16]
-    const int hh = e >> 10, d = (e >> 4) & 63, q4 = e & 15;
-    const float4 v = *reinterpret_cast<const float4*>(kvg + hh * 4096 + d * 64 + q4 * 4);
-    float* o = kvs + hh * 64 * kKvPitch + (q4 * 4) * kKvPitch + d;
-    o[0] = v.x;
-    o[kKvPitch] = v.y;
-    o[2 * kKvPitch] = v.z;
-    o[3 * kKvPitch] = v.w;
-  }
-  __syncthreads();
-  {  // Z for token `lane`, head h
-    const float* row = qs + lane * kQPitch + h * 64;
-    float s = 0.f;
-#pragma unroll 4
-    for (int d = 0; d < 64; d += 4) {
-      const float4 a = *reinterpret_cast<const float4*>(row + d);
-      const float4 k = *reinterpret_cast<const float4*>(ks + h * 64 + d);
-      s += a.x * k.x;
-      s += a.y * k.y;
-      s += a.z * k.z;
-      s += a.w * k.w;
-    }
-    zs[h * 64 + lane] = 1.0f / (s + 1e-6f);
-  }
-  floatx16 acc[2][2];
-#pragma unroll
-  for (int i = 0; i < 16; ++i) acc[0][0][i] = acc[0][1][i] = acc[1][0][i] = acc[1][1][i] = 0.f;
-  const float* qa0 = qs + l32 * kQPitch + h * 64 + half * 4;
-  const float* qa1 = qa0 + 32 * kQPitch;
-  const float* kb0 = kvs + h * 64 * kKvPitch + l32 * kKvPitch + half * 4;
-  const float* kb1 = kb0 + 32 * kKvPitch;
+  for (int i = 0; i < 16; ++i) acc[i] = 0.f;
 #pragma unroll
   for (int kk = 0; kk < 8; ++kk) {
-    const float4 a0 = *reinterpret_cast<const float4*>(qa0 + kk * 8);
-    const float4 a1 = *reinterpret_cast<const float4*>(qa1 + kk * 8);
-    const float4 b0 = *reinterpret_cast<const float4*>(kb0 + kk * 8);
-    const float4 b1 = *reinterpret_cast<const float4*>(kb1 + kk * 8);
-#define MF(ACC, A, B) ACC = __builtin_amdgcn_mfma_f32_32x32x2f32(A, B, ACC, 0, 0, 0)
-    MF(acc[0][0], a0.x, b0.x); MF(acc[0][0], a0.y, b0.y); MF(acc[0][0], a0.z, b0.z); MF(acc[0][0], a0.w, b0.w);
-    MF(acc[0][1], a0.x, b1.x); MF(acc[0][1], a0.y, b1.y); MF(acc[0][1], a0.z, b1.z); MF(acc[0][1], a0.w, b1.w);
-    MF(acc[1][0], a1.x, b0.x); MF(acc[1][0], a1.y, b0.y); MF(acc[1][0], a1.z, b0.z); MF(acc[1][0], a1.w, b0.w);
-    MF(acc[1][1], a1.x, b1.x); MF(acc[1][1], a1.y, b1.y); MF(acc[1][1], a1.z, b1.z); MF(acc[1][1], a1.w, b1.w);
-#undef MF
+    const float4 av = *reinterpret_cast<const float4*>(a + kk * 8);
+    const float4 wv = *reinterpret_cast<const float4*>(w + kk * 8);
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av.x, wv.x, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av.y, wv.y, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av.z, wv.z, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av.w, wv.w, acc, 0, 0, 0);
   }
-  __syncthreads();
-  float* o = P.out + (int64_t)b * P.nq * 256 + h * 64;
+  float* out = P.mf + (int64_t)b * 512 * 256 + (ot * 64 + wm * 32) * 256 + h * 64 + wn * 32 + l32;
 #pragma unroll
-  for (int tb = 0; tb < 2; ++tb) {
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int row = tb * 32 + (i & 3) + 8 * (i >> 2) + 4 * half;
-      const int tok = m0 + row;
-      if (tok < P.nq) {
-        const float z = zs[h * 64 + row];
-        o[(int64_t)tok * 256 + l32] = acc[tb][0][i] * z * P.ns;
-        o[(int64_t)tok * 256 + 32 + l32] = acc[tb][1][i] * z * P.ns;
-      }
-    }
-  }
+  for (int i = 0; i < 16; ++i) out[((i & 3) + 8 * (i >> 2) + 4 * half) * 256] = acc[i];
 }
 
 // InstanceNorm1d statistics (GATs_SuperGlue.py:145; biased variance, eps 1e-5): combine the
@@ -691,10 +577,9 @@ namespace {
 
 struct Plan {
   float *x2[2], *x3[2];
-  float *qkv2, *qkv3;
   float *kvpart2, *kvpart3, *kspart2, *kspart3;
-  float *kvt, *ksum;
-  float *o2, *o3, *msg2, *msg3, *y12, *y13;
+  float *kv, *ksum, *mf;
+  float *qz2, *qz3, *y12, *y13;
   float *stats2, *stats3, *mean, *rstd;
   float *f2, *f3, *s;
   float *rowpart, *colpart, *rowmax, *rowsum, *colmax, *colsum;
@@ -710,19 +595,16 @@ Plan make_plan(void* ws, int B, int n1, int n3, bool with_conf) {
     p.x2[i] = c.take<float>(t2 * 256);
     p.x3[i] = c.take<float>(t3 * 256);
   }
-  p.qkv2 = c.take<float>(t2 * 768);
-  p.qkv3 = c.take<float>(t3 * 768);
   const int ch2 = ceil_div(n1, 64), ch3 = ceil_div(n3, 64);
   p.kvpart2 = c.take<float>((size_t)B * ch2 * 16384);
   p.kvpart3 = c.take<float>((size_t)B * ch3 * 16384);
   p.kspart2 = c.take<float>((size_t)B * ch2 * 256);
   p.kspart3 = c.take<float>((size_t)B * ch3 * 256);
-  p.kvt = c.take<float>((size_t)2 * B * 16384);
+  p.kv = c.take<float>((size_t)2 * B * 16384);
   p.ksum = c.take<float>((size_t)2 * B * 256);
-  p.o2 = c.take<float>(t2 * 256);
-  p.o3 = c.take<float>(t3 * 256);
-  p.msg2 = c.take<float>(t2 * 256);
-  p.msg3 = c.take<float>(t3 * 256);
+  p.mf = c.take<float>((size_t)2 * B * 512 * 256);
+  p.qz2 = c.take<float>(t2 * 256);
+  p.qz3 = c.take<float>(t3 * 256);
   p.y12 = c.take<float>(t2 * 512);
   p.y13 = c.take<float>(t3 * 512);
   p.stats2 = c.take<float>((size_t)B * ch2 * 1024);
@@ -742,29 +624,6 @@ Plan make_plan(void* ws, int B, int n1, int n3, bool with_conf) {
   p.colbest = c.take<unsigned long long>(t3);
   p.bytes = align_up(c.off, 256);
   return p;
-}
-
-GemmProb gemm_prob(const float* A, int lda, const float* W, int ldw, const float* bias,
-                   float* Y, int ldy, int M, int N, int K, int batch) {
-  GemmProb g;
-  memset(&g, 0, sizeof(g));
-  g.A0 = A;
-  g.lda0 = lda;
-  g.a0_bs = (int64_t)M * lda;
-  g.ksplit = K;
-  g.W = W;
-  g.ldw = ldw;
-  g.bias = bias;
-  g.Y = Y;
-  g.ldy = ldy;
-  g.y_bs = (int64_t)M * ldy;
-  g.M = M;
-  g.N = N;
-  g.K = K;
-  g.batch = batch;
-  g.scale = 1.f;
-  g.vdiv = 1.f;
-  return g;
 }
 
 }  // namespace
@@ -858,38 +717,59 @@ int onepose_matcher_pack(const float* const* tensors, int n_tensors, void* packe
       continue;
     }
     float* p = out + (int64_t)ap * kApFloats;
-    float* wqkv = p;
-    float* bqkv = wqkv + kApWqkv;
-    float* wm = bqkv + kApBqkv;
-    float* bm = wm + kApWm;
-    float* w1 = bm + kApBm;
-    float* b1 = w1 + kApW1;
+    float* wkv = p;
+    float* bkv = wkv + kApWkv;
+    float* wq = bkv + kApBkv;
+    float* bq = wq + kApWq;
+    float* w1a = bq + kApBq;
+    float* cw = w1a + kApW1a;
+    float* b1 = cw + kApC;
     float* w2 = b1 + kApB1;
     float* b2 = w2 + kApW2;
-    // q/k/v: packed row h*64+d <- reference row d*4+h (view(B, 64, 4, N), :116)
+    const float* pw[3];
+    const float* pb[3];
     for (int j = 0; j < 3; ++j) {
-      const float* w = tensors[ti++];
-      const float* bias = tensors[ti++];
-      for (int cp = 0; cp < 256; ++cp) {
-        const int h = cp / 64, d = cp % 64, cr = d * 4 + h;
-        memcpy(wqkv + (int64_t)(j * 256 + cp) * 256, w + (int64_t)cr * 256, 256 * sizeof(float));
-        bqkv[j * 256 + cp] = bias[cr];
+      pw[j] = tensors[ti++];
+      pb[j] = tensors[ti++];
+    }
+    const float* mw = tensors[ti++];   // merge [256][256]
+    const float* mb = tensors[ti++];
+    const float* m0w = tensors[ti++];  // mlp.0 [512][512]
+    const float* m0b = tensors[ti++];
+    const float* m3w = tensors[ti++];  // mlp.3 [256][512]
+    const float* m3b = tensors[ti++];
+    // q: packed row h*64+d <- reference row d*4+h (view(B, 64, 4, N), :116)
+    for (int cp = 0; cp < 256; ++cp) {
+      const int h = cp / 64, d = cp % 64, cr = d * 4 + h;
+      memcpy(wq + (int64_t)cp * 256, pw[0] + (int64_t)cr * 256, 256 * sizeof(float));
+      bq[cp] = pb[0][cr];
+    }
+    // k / v interleaved per head: rows [128h, 128h+64) = k_h, [128h+64, 128h+128) = v_h
+    for (int h = 0; h < 4; ++h)
+      for (int d = 0; d < 64; ++d) {
+        const int cr = d * 4 + h;
+        memcpy(wkv + (int64_t)(128 * h + d) * 256, pw[1] + (int64_t)cr * 256, 256 * sizeof(float));
+        memcpy(wkv + (int64_t)(128 * h + 64 + d) * 256, pw[2] + (int64_t)cr * 256,
+               256 * sizeof(float));
+        bkv[128 * h + d] = pb[1][cr];
+        bkv[128 * h + 64 + d] = pb[2][cr];
+      }
+    // MLP conv 1 split: x part as is; message part folded with the merge conv
+    for (int o = 0; o < 512; ++o) {
+      memcpy(w1a + (int64_t)o * 256, m0w + (int64_t)o * 512, 256 * sizeof(float));
+      double bacc = (double)m0b[o];
+      for (int j = 0; j < 256; ++j) bacc += (double)m0w[(int64_t)o * 512 + 256 + j] * mb[j];
+      b1[o] = (float)bacc;
+      for (int cp = 0; cp < 256; ++cp) {   // merge input channel q*4+h -> packed h*64+q
+        const int h = cp / 64, q = cp % 64, cr = q * 4 + h;
+        double acc = 0.0;
+        for (int j = 0; j < 256; ++j)
+          acc += (double)m0w[(int64_t)o * 512 + 256 + j] * (double)mw[(int64_t)j * 256 + cr];
+        cw[(int64_t)o * 256 + cp] = (float)acc;
       }
     }
-    {  // merge: packed column h*64+q <- reference column q*4+h
-      const float* w = tensors[ti++];
-      const float* bias = tensors[ti++];
-      for (int o = 0; o < 256; ++o)
-        for (int cp = 0; cp < 256; ++cp) {
-          const int h = cp / 64, q = cp % 64;
-          wm[o * 256 + cp] = w[o * 256 + q * 4 + h];
-        }
-      memcpy(bm, bias, 256 * sizeof(float));
-    }
-    memcpy(w1, tensors[ti++], kApW1 * sizeof(float));
-    memcpy(b1, tensors[ti++], kApB1 * sizeof(float));
-    memcpy(w2, tensors[ti++], kApW2 * sizeof(float));
-    memcpy(b2, tensors[ti++], kApB2 * sizeof(float));
+    memcpy(w2, m3w, kApW2 * sizeof(float));
+    memcpy(b2, m3b, kApB2 * sizeof(float));
     ++ap;
   }
   float* fin = out + kApLayers * kApFloats + kGatLayers * kGatFloats;
@@ -912,10 +792,7 @@ int init_kernel_attributes() {
   static int rc = -1;
   if (rc == -1) {
     rc = ONEPOSE_OK;
-    if (hipFuncSetAttribute(reinterpret_cast<const void*>(attn_apply_kernel),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)kApplyLds) !=
-            hipSuccess ||
-        hipFuncSetAttribute(reinterpret_cast<const void*>(gat_kernel),
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(gat_kernel),
                             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
       rc = ONEPOSE_ERR_HIP;
   }
@@ -977,68 +854,80 @@ int onepose_match(const void* packed_weights, const float* desc2d, int64_t desc2
     }
     const ApW w = ap_weights(wbase, ap++);
     int rc;
-    {  // q | k | v projections of both tensors
+    // self: each side attends to itself; cross: 2D <-> 3D.  Source of side s: src(s).
+    const int src2 = (kind == 1) ? 0 : 1, src3 = (kind == 1) ? 1 : 0;
+    const int ns2 = src2 == 0 ? n1 : n3, ns3 = src3 == 0 ? n1 : n3;
+    {  // 1. [phi(k)_h | v_h / Ns] of both tensors -> per-chunk KV / ksum partials
       GemmArgs a;
       a.nprob = 2;
-      a.p[0] = gemm_prob(p.x2[c2], 256, w.wqkv, 256, w.bqkv, p.qkv2, 768, n1, 768, 256, B);
-      a.p[0].phi_cols = 512;
+      a.p[0] = gemm_prob(p.x2[c2], 256, w.wkv, 256, w.bkv, nullptr, 0, n1, 512, 256, B);
       a.p[0].vdiv = (float)n1;
-      a.p[1] = gemm_prob(p.x3[c3], 256, w.wqkv, 256, w.bqkv, p.qkv3, 768, n3, 768, 256, B);
-      a.p[1].phi_cols = 512;
+      a.p[0].kvpart = p.kvpart2;
+      a.p[0].kspart = p.kspart2;
+      a.p[1] = gemm_prob(p.x3[c3], 256, w.wkv, 256, w.bkv, nullptr, 0, n3, 512, 256, B);
       a.p[1].vdiv = (float)n3;
-      if ((rc = gemm_launch(EPI_QKV, PRO_PLAIN, a, st, K_QKV)) != ONEPOSE_OK) return rc;
+      a.p[1].kvpart = p.kvpart3;
+      a.p[1].kspart = p.kspart3;
+      if ((rc = gemm_launch(EPI_KVPART, PRO_PLAIN, 128, a, st, K_KV_GEMM)) != ONEPOSE_OK)
+        return rc;
     }
-    KvArgs kva;
-    kva.p[0] = {p.qkv2, p.kvpart2, p.kspart2, n1, ch2, B * ch2};
-    kva.p[1] = {p.qkv3, p.kvpart3, p.kspart3, n3, ch3, B * ch3};
-    OP_LAUNCH(K_KV_PARTIAL, st, kv_partial_kernel, dim3(B * (ch2 + ch3)), dim3(256), 0, st, kva);
-    {
-      const int total = 2 * B * (16384 + 256) / 4;
-      OP_LAUNCH(K_KV_REDUCE, st, kv_reduce_kernel, dim3(ceil_div(total, 256)), dim3(256), 0, st,
-                kva, p.kvt, p.ksum, B);
+    {  // 2. KV[src], ksum[src]
+      KvArgs kva;
+      kva.p[0] = {p.kvpart2, p.kspart2, ch2};
+      kva.p[1] = {p.kvpart3, p.kspart3, ch3};
+      OP_LAUNCH(K_KV_REDUCE, st, kv_reduce_kernel, dim3(2 * B * 65), dim3(256), 0, st, kva, p.kv,
+                p.ksum, B);
     }
-    {  // self: side s attends to itself; cross: 2D attends to 3D and vice versa
-      const int src2 = (kind == 1) ? 0 : 1, src3 = (kind == 1) ? 1 : 0;
-      const float ns2 = (float)(src2 == 0 ? n1 : n3), ns3 = (float)(src3 == 0 ? n1 : n3);
-      ApplyArgs aa;
-      aa.p[0] = {p.qkv2, p.kvt + (size_t)src2 * B * 16384, p.ksum + (size_t)src2 * B * 256,
-                 p.o2, n1, ns2, ch2, B * ch2};
-      aa.p[1] = {p.qkv3, p.kvt + (size_t)src3 * B * 16384, p.ksum + (size_t)src3 * B * 256,
-                 p.o3, n3, ns3, ch3, B * ch3};
-      OP_LAUNCH(K_APPLY, st, attn_apply_kernel, dim3(B * (ch2 + ch3)), dim3(256), kApplyLds, st, aa);
+    {  // 3. folded message weights per side
+      FoldArgs fa;
+      fa.c = w.c;
+      fa.p[0] = {p.kv + (size_t)src2 * B * 16384, p.mf};
+      fa.p[1] = {p.kv + (size_t)src3 * B * 16384, p.mf + (size_t)B * 512 * 256};
+      OP_LAUNCH(K_MFOLD, st, m_fold_kernel, dim3(2 * B * 32), dim3(256), 0, st, fa, B);
     }
-    {  // merge
+    {  // 4. phi(q) * Z * Ns
       GemmArgs a;
       a.nprob = 2;
-      a.p[0] = gemm_prob(p.o2, 256, w.wm, 256, w.bm, p.msg2, 256, n1, 256, 256, B);
-      a.p[1] = gemm_prob(p.o3, 256, w.wm, 256, w.bm, p.msg3, 256, n3, 256, 256, B);
-      if ((rc = gemm_launch(EPI_BIAS, PRO_PLAIN, a, st, K_MERGE)) != ONEPOSE_OK) return rc;
+      a.p[0] = gemm_prob(p.x2[c2], 256, w.wq, 256, w.bq, p.qz2, 256, n1, 256, 256, B);
+      a.p[0].ksum = p.ksum + (size_t)src2 * B * 256;
+      a.p[0].ksum_bs = 256;
+      a.p[0].ns = (float)ns2;
+      a.p[1] = gemm_prob(p.x3[c3], 256, w.wq, 256, w.bq, p.qz3, 256, n3, 256, 256, B);
+      a.p[1].ksum = p.ksum + (size_t)src3 * B * 256;
+      a.p[1].ksum_bs = 256;
+      a.p[1].ns = (float)ns3;
+      if ((rc = gemm_launch(EPI_QZ, PRO_PLAIN, 64, a, st, K_Q_GEMM)) != ONEPOSE_OK) return rc;
     }
-    {  // MLP conv 1 on cat[x, message] + InstanceNorm partials
+    {  // 5. MLP conv 1 on [x ; QZ] with [W1a | Mf] + InstanceNorm partials
       GemmArgs a;
       a.nprob = 2;
-      a.p[0] = gemm_prob(p.x2[c2], 256, w.w1, 512, w.b1, p.y12, 512, n1, 512, 512, B);
-      a.p[0].A1 = p.msg2;
+      a.p[0] = gemm_prob(p.x2[c2], 256, w.w1a, 256, w.b1, p.y12, 512, n1, 512, 512, B);
+      a.p[0].A1 = p.qz2;
       a.p[0].lda1 = 256;
       a.p[0].a1_bs = (int64_t)n1 * 256;
       a.p[0].ksplit = 256;
+      a.p[0].W1 = p.mf;
+      a.p[0].ldw1 = 256;
+      a.p[0].w1_bs = 512 * 256;
       a.p[0].stats = p.stats2;
-      a.p[1] = gemm_prob(p.x3[c3], 256, w.w1, 512, w.b1, p.y13, 512, n3, 512, 512, B);
-      a.p[1].A1 = p.msg3;
+      a.p[1] = gemm_prob(p.x3[c3], 256, w.w1a, 256, w.b1, p.y13, 512, n3, 512, 512, B);
+      a.p[1].A1 = p.qz3;
       a.p[1].lda1 = 256;
       a.p[1].a1_bs = (int64_t)n3 * 256;
       a.p[1].ksplit = 256;
+      a.p[1].W1 = p.mf + (size_t)B * 512 * 256;
+      a.p[1].ldw1 = 256;
+      a.p[1].w1_bs = 512 * 256;
       a.p[1].stats = p.stats3;
-      if ((rc = gemm_launch(EPI_STATS, PRO_PLAIN, a, st, K_MLP1)) != ONEPOSE_OK) return rc;
+      if ((rc = gemm_launch(EPI_STATS, PRO_PLAIN, 64, a, st, K_MLP1)) != ONEPOSE_OK) return rc;
     }
-    {
+    {  // 6. InstanceNorm statistics
       StatsArgs sa;
       sa.p[0] = {p.stats2, p.mean, p.rstd, n1, ch2};
       sa.p[1] = {p.stats3, p.mean + (size_t)B * 512, p.rstd + (size_t)B * 512, n3, ch3};
-      OP_LAUNCH(K_STATS, st, stats_finalize_kernel, dim3(2 * B * 8), dim3(256), 0,
-                         st, sa, B);
+      OP_LAUNCH(K_STATS, st, stats_finalize_kernel, dim3(2 * B * 8), dim3(256), 0, st, sa, B);
     }
-    {  // MLP conv 2 on ReLU(InstanceNorm(.)) + residual: desc + delta
+    {  // 7. MLP conv 2 on ReLU(InstanceNorm(.)) + residual: desc + delta
       GemmArgs a;
       a.nprob = 2;
       a.p[0] = gemm_prob(p.y12, 512, w.w2, 512, w.b2, p.x2[c2 ^ 1], 256, n1, 256, 512, B);
@@ -1055,7 +944,8 @@ int onepose_match(const void* packed_weights, const float* desc2d, int64_t desc2
       a.p[1].pro_mean = p.mean + (size_t)B * 512;
       a.p[1].pro_rstd = p.rstd + (size_t)B * 512;
       a.p[1].pro_bs = 512;
-      if ((rc = gemm_launch(EPI_RESID, PRO_NORM_RELU, a, st, K_MLP2)) != ONEPOSE_OK) return rc;
+      if ((rc = gemm_launch(EPI_RESID, PRO_NORM_RELU, 64, a, st, K_MLP2)) != ONEPOSE_OK)
+        return rc;
     }
     c2 ^= 1;
     c3 ^= 1;
@@ -1068,7 +958,7 @@ int onepose_match(const void* packed_weights, const float* desc2d, int64_t desc2
     a.nprob = 2;
     a.p[0] = gemm_prob(p.x2[c2], 256, fw, 256, fw + 65536, p.f2, 256, n1, 256, 256, B);
     a.p[1] = gemm_prob(p.x3[c3], 256, fw, 256, fw + 65536, p.f3, 256, n3, 256, 256, B);
-    if ((rc = gemm_launch(EPI_BIAS, PRO_PLAIN, a, st, K_FINAL)) != ONEPOSE_OK) return rc;
+    if ((rc = gemm_launch(EPI_BIAS, PRO_PLAIN, 64, a, st, K_FINAL)) != ONEPOSE_OK) return rc;
     const int rows = B * (n1 + n3);
     OP_LAUNCH(K_L2NORM, st, l2norm_kernel, dim3(ceil_div(rows, 4)), dim3(256), 0, st, p.f2, B * n1,
                        p.f3, B * n3);
@@ -1081,7 +971,7 @@ int onepose_match(const void* packed_weights, const float* desc2d, int64_t desc2
     a.p[0].scale = scale_factor;
     a.p[0].rowstat = p.rowpart;
     a.p[0].colstat = p.colpart;
-    if ((rc = gemm_launch(EPI_SCORE, PRO_PLAIN, a, st, K_SCORE)) != ONEPOSE_OK) return rc;
+    if ((rc = gemm_launch(EPI_SCORE, PRO_PLAIN, 64, a, st, K_SCORE)) != ONEPOSE_OK) return rc;
   }
   {
     const int64_t total = (int64_t)B * (n1 + n3);

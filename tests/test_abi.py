@@ -59,33 +59,55 @@ def _pack(sd):
     return buf
 
 
+AP_FLOATS = 512 * 256 + 512 + 256 * 256 + 256 + 512 * 256 + 512 * 256 + 512 + 256 * 512 + 256
+
+
 def test_pack_layout():
+    """Packed panel of the first attention layer (gnn.layers.1), GAT fold, final proj."""
     from onepose_amd import synthetic
     sd = synthetic.make_state_dict(3)
     buf = _pack(sd)
-    ap_floats = 768 * 256 + 768 + 256 * 256 + 256 + 512 * 512 + 512 + 256 * 512 + 256
-    # first attention layer is gnn.layers.1
-    p = buf[:ap_floats]
-    wqkv = p[:768 * 256].reshape(768, 256)
-    bqkv = p[768 * 256:768 * 257]
-    for j in range(3):
-        w = sd[f"gnn.layers.1.attn.proj.{j}.weight"][:, :, 0]
-        b = sd[f"gnn.layers.1.attn.proj.{j}.bias"]
-        for h in range(4):
-            for d in (0, 17, 63):
-                np.testing.assert_array_equal(wqkv[j * 256 + h * 64 + d], w[d * 4 + h])
-                assert bqkv[j * 256 + h * 64 + d] == b[d * 4 + h]
-    wm = p[768 * 257:768 * 257 + 65536].reshape(256, 256)
-    merge = sd["gnn.layers.1.attn.merge.weight"][:, :, 0]
+    p = buf[:AP_FLOATS].astype(np.float64)
+    off = 0
+
+    def take(n):
+        nonlocal off
+        out = p[off:off + n]
+        off += n
+        return out
+    wkv = take(512 * 256).reshape(512, 256)
+    bkv = take(512)
+    wq = take(256 * 256).reshape(256, 256)
+    bq = take(256)
+    w1a = take(512 * 256).reshape(512, 256)
+    cw = take(512 * 256).reshape(512, 256)
+    b1 = take(512)
+    w2 = take(256 * 512).reshape(256, 512)
+    q_w = sd["gnn.layers.1.attn.proj.0.weight"][:, :, 0]
+    k_w = sd["gnn.layers.1.attn.proj.1.weight"][:, :, 0]
+    v_w = sd["gnn.layers.1.attn.proj.2.weight"][:, :, 0]
     for h in range(4):
-        for q in (0, 5, 63):
-            np.testing.assert_array_equal(wm[:, h * 64 + q], merge[:, q * 4 + h])
+        for d in (0, 17, 63):
+            np.testing.assert_array_equal(wq[h * 64 + d], q_w[d * 4 + h])
+            np.testing.assert_array_equal(wkv[128 * h + d], k_w[d * 4 + h])
+            np.testing.assert_array_equal(wkv[128 * h + 64 + d], v_w[d * 4 + h])
+            assert bkv[128 * h + 64 + d] == sd["gnn.layers.1.attn.proj.2.bias"][d * 4 + h]
+            assert bq[h * 64 + d] == sd["gnn.layers.1.attn.proj.0.bias"][d * 4 + h]
+    m0 = sd["gnn.layers.1.mlp.0.weight"][:, :, 0].astype(np.float64)
+    merge = sd["gnn.layers.1.attn.merge.weight"][:, :, 0].astype(np.float64)
+    np.testing.assert_array_equal(w1a, m0[:, :256])
+    fold = m0[:, 256:] @ merge                       # columns in reference order q*4+h
+    perm = np.array([(c % 64) * 4 + c // 64 for c in range(256)])
+    np.testing.assert_allclose(cw, fold[:, perm], rtol=1e-5, atol=1e-6)
+    b1f = sd["gnn.layers.1.mlp.0.bias"] + m0[:, 256:] @ sd["gnn.layers.1.attn.merge.bias"]
+    np.testing.assert_allclose(b1, b1f, rtol=1e-5, atol=1e-6)
+    np.testing.assert_array_equal(w2, sd["gnn.layers.1.mlp.3.weight"][:, :, 0])
     # GAT fold: wa = W @ a (layer 0)
-    gat0 = buf[8 * ap_floats:8 * ap_floats + 512]
+    gat0 = buf[8 * AP_FLOATS:8 * AP_FLOATS + 512]
     W, a = sd["gnn.layers.0.W"].astype(np.float64), sd["gnn.layers.0.a"][:, 0].astype(np.float64)
     np.testing.assert_allclose(gat0[:256], W @ a[:256], rtol=1e-6, atol=1e-7)
     np.testing.assert_allclose(gat0[256:], W @ a[256:], rtol=1e-6, atol=1e-7)
-    fin = buf[8 * ap_floats + 4 * 512:]
+    fin = buf[8 * AP_FLOATS + 4 * 512:]
     np.testing.assert_array_equal(fin[:65536], sd["final_proj.weight"].reshape(-1))
 
 
