@@ -30,6 +30,8 @@ sys.path.insert(0, REPO)
 METRIC = "query frames/sec (1k kpts × 4k 3D pts) + cm/deg pose err, 1/2/4/8 GPU"
 FP32_MFMA_PEAK_TFLOPS = 157.3     # MI355X_MICROARCH.md: f32-input MFMA dense peak
 HBM_PEAK_GBS = 8000.0             # MI355X_MICROARCH.md: HBM3E spec
+# kernels that record device stamps (onepose_profile_begin_device): timeable inside graphs
+STAMPED = {"kv_gemm", "q_gemm", "mlp1_gemm", "mlp2_gemm", "final_gemm", "score_gemm"}
 
 
 def kernel_work(kind, B, n1, n3, L):
@@ -110,8 +112,18 @@ def main():
     ap.add_argument("--n3", type=int, default=4096)
     ap.add_argument("--leaf", type=int, default=8)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--stream", action="store_true",
-                    help="overlap step k's pose stage with step k+1's matcher (2 streams)")
+    ap.add_argument("--serial", action="store_true",
+                    help="one stream: step k+1 starts after step k's pose stage (default: the "
+                         "pose stage of step k overlaps the matcher of step k+1 on 2 streams)")
+    ap.add_argument("--diag-steps", action="store_true",
+                    help="diagnostic: record an event after every timed step and report the "
+                         "per-step GPU times")
+    ap.add_argument("--eager", action="store_true",
+                    help="launch every kernel from the host each step instead of replaying "
+                         "captured HIP graphs")
+    ap.add_argument("--diag-repeats", type=int, default=0,
+                    help="diagnostic: after the timed region, time it again this many times "
+                         "and report those ms/step too (value always comes from the first)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -142,29 +154,61 @@ def main():
         pipe.enqueue()
     torch.cuda.synchronize()
 
-    # per-kernel profile pass (all kinds) to find the dominant kernel
+    # per-kernel profile pass (all kinds, HIP events, eager) to find the dominant kernel
     names = profile_kinds(lib)
     kinds, ms = run_profiled(lib, pipe, 3, (1 << len(names)) - 1, 4096)
     per_kind = {}
     for k, t in zip(kinds, ms):
         per_kind.setdefault(names[k], []).append(float(t))
     total = {k: sum(v) / 3.0 for k, v in per_kind.items()}
-    dominant = max((k for k in total if kernel_work(k, B, n1, n3, L)), key=lambda k: total[k])
+    # the dominant kernel is timed by device stamps, which the token GEMMs record
+    dominant = max((k for k in total if kernel_work(k, B, n1, n3, L) and k in STAMPED),
+                   key=lambda k: total[k])
     dom_id = names.index(dominant)
 
-    # timed region: K steps, events bracketing every launch of the dominant kernel
+    # Timed region: K steps; every step runs every kernel of the frame path.  With graphs
+    # (default) the matcher stage and the pose stage are each one HIP-graph replay (captured
+    # once per buffer slot before the timed region).  Default schedule: the pose stage of
+    # step k (one workgroup per frame) overlaps the matcher of step k+1 on a second stream.
+    overlap, graphs_on = not args.serial, not args.eager
+    # stamping must be on while the graphs are captured (the accumulator address is a kernel
+    # argument); begin_device again below re-zeroes the same accumulators
+    _lib.check(lib.onepose_profile_begin_device(1 << dom_id), "profile_begin_device")
+    stage_graphs = pipe.capture_stages(torch.cuda.graph_pool_handle()) if graphs_on else None
+    step_graph = pipe.capture(0) if graphs_on and not overlap else None
+
+    step_events = []
+
+    def run_steps(k):
+        if args.diag_steps and k == args.steps:
+            out = None
+            for _ in range(k):
+                out = run_steps(1)
+                ev = torch.cuda.Event(enable_timing=True)
+                ev.record()
+                step_events.append(ev)
+            return out
+        if overlap:
+            pipe.run_stream(k, graphs=stage_graphs)
+            return pipe.slots[(k - 1) % len(pipe.slots)]
+        for _ in range(k):
+            if step_graph is not None:
+                step_graph.replay()
+            else:
+                pipe.enqueue()
+        return pipe.slots[0]
+
+    run_steps(2)    # first replay of each graph (upload) stays out of the timed region
+    torch.cuda.synchronize()
+    # the dominant kernel's launches are timed on the device (first workgroup start -> last
+    # workgroup end), accumulated over every launch inside the timed region
+    _lib.check(lib.onepose_profile_begin_device(1 << dom_id), "profile_begin_device")
     if pg:
         pg.barrier()
     torch.cuda.synchronize()
-    _lib.check(lib.onepose_profile_begin(1 << dom_id, 64 * args.steps + 64), "profile_begin")
     t0 = time.perf_counter()
-    if not args.stream:
-        for _ in range(args.steps):
-            pipe.enqueue()
-        last = pipe.slots[0]
-    else:   # frame k's pose stage overlaps frame k+1's matcher (two streams, two slots)
-        pipe.run_stream(args.steps)
-        last = pipe.slots[(args.steps - 1) % len(pipe.slots)]
+    last = run_steps(args.steps)
+    host_enqueue = time.perf_counter() - t0   # host time to issue the K steps
     result = torch.cat([last.pose.reshape(B, 12), last.R_err[:, None], last.t_err[:, None],
                         last.cmd.double(), last.n_inliers[:, None].double(),
                         last.status[:, None].double()], 1)
@@ -174,42 +218,50 @@ def main():
         result = gathered
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    cap = 64 * args.steps + 64
-    dk, dms = np.zeros(cap, np.int32), np.zeros(cap, np.float32)
-    cnt = np.zeros(1, np.int32)
-    _lib.check(lib.onepose_profile_end(dk.ctypes.data, dms.ctypes.data, cap, cnt.ctypes.data),
-               "profile_end")
-    dom_ms = float(np.mean(dms[:int(cnt[0])]))
+    nk = len(names)
+    launches, tot_ms = np.zeros(nk, np.int64), np.zeros(nk, np.float64)
+    _lib.check(lib.onepose_profile_end_device(launches.ctypes.data, tot_ms.ctypes.data, nk),
+               "profile_end_device")
+    n_dom = int(launches[dom_id])
+    assert n_dom > 0 and tot_ms[dom_id] > 0, "dominant-kernel timing missing"
+    dom_ms = float(tot_ms[dom_id] / n_dom)
     if pg:
         t = torch.tensor([elapsed], device=dev)
         pg.all_reduce(t, op=pg.ReduceOp.MAX)
         elapsed = float(t.item())
 
+    diag = []
+    if step_events:
+        diag.append([round(a.elapsed_time(b), 3) for a, b in zip(step_events, step_events[1:])])
+    for _ in range(args.diag_repeats):
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        run_steps(args.steps)
+        torch.cuda.synchronize()
+        diag.append(round((time.perf_counter() - t1) / args.steps * 1e3, 4))
+
     res = result.cpu().numpy()
     frames_total = world * B * args.steps
     value = frames_total / elapsed
     work, unit, bound = kernel_work(dominant, B, n1, n3, L)
-    if unit == "flop":
-        achieved = work / (dom_ms * 1e-3) / 1e12
-        roof = {"bound": "mfma", "achieved": round(achieved, 2), "peak": FP32_MFMA_PEAK_TFLOPS,
-                "unit": "TFLOP/s", "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4),
-                "traffic": None, "kernel": dominant, "avg_launch_us": round(dom_ms * 1e3, 2)}
-    else:
-        achieved = work / (dom_ms * 1e-3) / 1e9
-        roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                "kernel": dominant, "avg_launch_us": round(dom_ms * 1e3, 2)}
+    achieved = work / (dom_ms * 1e-3) / 1e12
+    roof = {"bound": "mfma", "achieved": round(achieved, 2), "peak": FP32_MFMA_PEAK_TFLOPS,
+            "unit": "TFLOP/s", "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4),
+            "traffic": None, "kernel": dominant, "avg_launch_us": round(dom_ms * 1e3, 2),
+            "launches_timed": n_dom, "flop_per_launch": work,
+            "timing": "device clock, first workgroup start to last workgroup end"}
 
     if rank == 0:
+        sched = ("pose stage of step k overlaps the matcher of step k+1 (2 streams)" if overlap
+                 else "serial steps")
+        sched += "; stages replayed as HIP graphs" if graphs_on else "; host-launched kernels"
         out = {
             "metric": METRIC, "value": round(value, 2), "unit": "frames/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "fp32", "data": "synthetic",
             "config": {"workload": f"config 2: {n1} kpts x {n3} 3D pts, L={L}, {B} frame(s) per "
-                                   f"GPU per step; matcher + RANSAC-EPnP + cm/deg"
-                                   + ("; pose stage of step k overlaps the matcher of step "
-                                      "k+1 (2 streams)" if args.stream else ""),
+                                   f"GPU per step; matcher + RANSAC-EPnP + cm/deg; {sched}",
                        "n1": n1, "n3": n3, "num_leaf": L, "batch_per_gpu": B,
                        "parallelism": f"frame-dp{world}"},
             "pose": {"cmd1": float(res[:, 14].mean()), "cmd3": float(res[:, 15].mean()),
@@ -218,8 +270,10 @@ def main():
                      "n_inliers_mean": float(res[:, 17].mean()),
                      "status_ok": float((res[:, 18] == 0).mean())},
             "roofline": roof,
+            "host_enqueue_ms_per_step": round(host_enqueue / args.steps * 1e3, 4),
             "kernel_ms_per_step": {k: round(v, 4) for k, v in sorted(total.items(),
                                                                      key=lambda kv: -kv[1])},
+            **({"diag_ms_per_step": diag} if diag else {}),
         }
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(sd, data, frames, obj)

@@ -154,6 +154,18 @@ int onepose_pose_errors(const double* pose_pred, const double* pose_gt, int64_t 
  * elapsed milliseconds between its two events.
  * ------------------------------------------------------------------------------------ */
 int onepose_profile_begin(uint64_t kind_mask, int capacity);
+/* Device-stamp variant, usable inside captured HIP graphs (event brackets are not).  While
+ * enabled, each launch of a masked kind that supports stamps (the token GEMMs: kv/q/mlp1/
+ * mlp2/final/score) is timed by its own workgroups on the device's constant-rate clock
+ * (s_memrealtime): first workgroup start to last workgroup end; the last workgroup adds the
+ * duration to a per-kind total and re-arms the slot, so graph replays and repeated launches
+ * all accumulate.  Launches of one kind must not run concurrently while enabled.  A graph
+ * captured while enabled carries the accumulator address and keeps timing when replayed;
+ * calling _begin_device again re-zeroes the accumulators (same addresses).
+ * _end_device synchronises the device and returns, per kind k < n_kinds, the number of
+ * launches timed and their total milliseconds. */
+int onepose_profile_begin_device(uint64_t kind_mask);
+int onepose_profile_end_device(int64_t* launches, double* total_ms, int n_kinds);
 int onepose_profile_end(int* kinds, float* ms, int capacity, int* count);
 const char* onepose_profile_kind_name(int kind);
 

@@ -43,6 +43,8 @@ PROTOTYPES = {
     "onepose_pose_errors": (c_int, [c_void_p, c_void_p, c_int64, c_int, c_void_p, c_void_p,
                                     c_void_p, c_void_p]),
     "onepose_profile_begin": (c_int, [ctypes.c_uint64, c_int]),
+    "onepose_profile_begin_device": (c_int, [ctypes.c_uint64]),
+    "onepose_profile_end_device": (c_int, [c_void_p, c_void_p, c_int]),
     "onepose_profile_end": (c_int, [c_void_p, c_void_p, c_int, c_void_p]),
     "onepose_profile_kind_name": (c_char_p, [c_int]),
 }

@@ -49,6 +49,37 @@ enum KernelKind {
 };
 void prof_pre(int kind, hipStream_t s);
 void prof_post(int kind, hipStream_t s);
+// Device-stamp accumulator of one kernel kind (onepose_profile_begin_device).
+struct StampAcc {
+  unsigned long long start;      // min over the running launch's workgroups (~0 when armed)
+  unsigned long long total;      // sum of finished launches' durations, clock ticks
+  unsigned long long launches;   // finished launches
+  unsigned int arrived;          // workgroups of the running launch that have finished
+  unsigned int pad;
+};
+// Accumulator for the next launch of `kind`, or null when stamping is off for it.
+StampAcc* prof_stamp_slot(int kind);
+
+__device__ __forceinline__ void stamp_begin(StampAcc* s) {
+  if (s != nullptr && threadIdx.x == 0) atomicMin(&s->start, (unsigned long long)wall_clock64());
+}
+// Every thread of the workgroup calls this at the kernel's end (s is launch-uniform).  The
+// workgroup that arrives last reads the clock after its arrival, so no earlier workgroup
+// ended later; it books the launch and re-arms the slot.  No fence: an agent-scope release
+// would write back the XCD's L2 (microseconds) and the timing needs no data hand-off.
+__device__ __forceinline__ void stamp_end(StampAcc* s) {
+  if (s == nullptr) return;
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  const unsigned int blocks = gridDim.x * gridDim.y * gridDim.z;
+  if (atomicAdd(&s->arrived, 1u) == blocks - 1) {
+    const unsigned long long e = (unsigned long long)wall_clock64();
+    const unsigned long long b = atomicExch(&s->start, ~0ull);
+    atomicAdd(&s->total, e - b);
+    atomicAdd(&s->launches, 1ull);
+    atomicExch(&s->arrived, 0u);
+  }
+}
 
 // hipLaunchKernelGGL bracketed by the profiling hook, then a launch-error check
 #define OP_LAUNCH(kind, stream, ...)            \
@@ -90,5 +121,13 @@ __device__ __forceinline__ float wave_max(float v) {
 
 // F.elu as ATen computes it (x > 0 ? x : exp(x) - 1), GATs.py:102 / GATs_SuperGlue.py:90-91
 __device__ __forceinline__ float elu1(float x) { return x > 0.f ? x : (expf(x) - 1.0f); }
+
+// Bijection hardware block id -> logical id giving each XCD (hardware blocks b, b+8, ...)
+// a contiguous range of logical ids.  Placement is a speed hint only, never correctness.
+__device__ __forceinline__ int xcd_contiguous(int bid, int grid) {
+  const int xcd = bid & 7, idx = bid >> 3;
+  const int per = grid >> 3, rem = grid & 7;
+  return xcd < rem ? xcd * (per + 1) + idx : rem * (per + 1) + (xcd - rem) * per + idx;
+}
 
 }  // namespace onepose

@@ -67,6 +67,7 @@ struct GemmProb {
 struct GemmArgs {
   GemmProb p[2];
   int nprob;
+  StampAcc* stamp;   // device-stamp profiling accumulator (set by gemm_launch) or null
 };
 
 constexpr int kGemmBM = 64, kGemmBK = 32;

@@ -92,14 +92,17 @@ __device__ __forceinline__ void store_stage(float* lds_a, float* lds_w, Stage<BN
 }
 
 template <int EPI, int PRO, int BN>
-__global__ __launch_bounds__(256) void gemm_f32_kernel(GemmArgs args) {
+__device__ __forceinline__ void gemm_body(const GemmArgs& args) {
   constexpr int FN = BN / 64;           // accumulators per wave
   constexpr int STAGE = (BM + BN) * PITCH;
   __shared__ __attribute__((aligned(16))) float lds[2 * STAGE];
   __shared__ float zrow[BM];
   __shared__ float zrow_stats[(EPI == EPI_STATS) ? 512 : 1];
 
-  int bid = blockIdx.x;
+  // XCD-aware tile order: blocks are dealt round-robin over the 8 XCDs, so hand each XCD a
+  // contiguous run of logical tiles -- the N-tiles of one M-tile then share that XCD's L2
+  // (A is fetched once per XCD instead of once per N-tile).
+  int bid = xcd_contiguous(blockIdx.x, gridDim.x);
   const bool second = bid >= args.p[0].tiles;
 #define F(x) (second ? args.p[1].x : args.p[0].x)
   if (second) bid -= args.p[0].tiles;
@@ -138,16 +141,21 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmArgs args) {
 #pragma unroll
     for (int i = 0; i < 16; ++i) acc[j][i] = 0.f;
 
+  // Prefetch distance 2: while the MFMAs consume K step kt from LDS, step kt+1 sits in
+  // registers (loaded one step earlier) and step kt+2's loads are in flight, so each global
+  // load has two MFMA phases to land (a lone 64x64 tile per CU has no other waves to hide
+  // the latency behind).
   const int nk = c.K / BK;
-  Stage<BN> st;
-  load_stage<PRO, BN>(c, m0, n0, 0, st);
-  store_stage<PRO, BN>(lds, lds + BM * PITCH, st, m0, c.M);
+  Stage<BN> s0, s1;
+  load_stage<PRO, BN>(c, m0, n0, 0, s0);
+  if (nk > 1) load_stage<PRO, BN>(c, m0, n0, BK, s1);
+  store_stage<PRO, BN>(lds, lds + BM * PITCH, s0, m0, c.M);
   __syncthreads();
 
-  for (int kt = 0; kt < nk; ++kt) {
+  auto step = [&](int kt, Stage<BN>& next, Stage<BN>& spare) __attribute__((always_inline)) {
     const float* la = lds + (kt & 1) * STAGE;
     const float* lw = la + BM * PITCH;
-    if (kt + 1 < nk) load_stage<PRO, BN>(c, m0, n0, (kt + 1) * BK, st);
+    if (kt + 2 < nk) load_stage<PRO, BN>(c, m0, n0, (kt + 2) * BK, spare);
     const float* pa = la + (wm * 32 + (lane & 31)) * PITCH + (lane >> 5) * 4;
     const float* pw = lw + (wn * (BN / 2) + (lane & 31)) * PITCH + (lane >> 5) * 4;
 #pragma unroll
@@ -164,9 +172,13 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmArgs args) {
     }
     if (kt + 1 < nk) {
       float* na = lds + ((kt + 1) & 1) * STAGE;
-      store_stage<PRO, BN>(na, na + BM * PITCH, st, m0, c.M);
+      store_stage<PRO, BN>(na, na + BM * PITCH, next, m0, c.M);
     }
     __syncthreads();
+  };
+  for (int kt = 0; kt < nk; kt += 2) {
+    step(kt, s1, s0);
+    if (kt + 1 < nk) step(kt + 1, s0, s1);
   }
 
   // ---- epilogue ----
@@ -335,6 +347,13 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmArgs args) {
 }
 
 template <int EPI, int PRO, int BN>
+__global__ __launch_bounds__(256) void gemm_f32_kernel(GemmArgs args) {
+  stamp_begin(args.stamp);
+  gemm_body<EPI, PRO, BN>(args);
+  stamp_end(args.stamp);
+}
+
+template <int EPI, int PRO, int BN>
 void launch_one(GemmArgs& args, int grid, hipStream_t stream) {
   hipLaunchKernelGGL((gemm_f32_kernel<EPI, PRO, BN>), dim3(grid), dim3(256), 0, stream, args);
 }
@@ -384,9 +403,11 @@ int gemm_launch(int epi, int pro, int bn, GemmArgs& args, hipStream_t stream, in
     grid += P.tiles;
   }
   if (grid == 0) return ONEPOSE_OK;
+  args.stamp = nullptr;
 #define CASE(E, PR, BN_)                          \
   if (epi == E && pro == PR && bn == BN_) {       \
     prof_pre(kind, stream);                       \
+    args.stamp = prof_stamp_slot(kind);           \
     launch_one<E, PR, BN_>(args, grid, stream);   \
     prof_post(kind, stream);                      \
     OP_LAUNCHED();                                \

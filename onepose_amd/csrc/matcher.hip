@@ -56,9 +56,11 @@ void clear_error() { g_last_error.clear(); }
 namespace {
 struct Prof {
   uint64_t mask = 0;
+  bool device = false;   // device-stamp mode
   std::vector<hipEvent_t> ev;
   std::vector<int> kinds;
   int n = 0;
+  StampAcc* acc = nullptr;   // device, one per kind
 };
 Prof g_prof;
 const char* kKindNames[K_NUM_KINDS] = {
@@ -67,11 +69,18 @@ const char* kKindNames[K_NUM_KINDS] = {
     "conf", "mutual", "select", "pnp_ransac", "pnp_refit", "pose_error", "sample_desc"};
 }  // namespace
 
+StampAcc* prof_stamp_slot(int kind) {
+  if (!g_prof.device || !((g_prof.mask >> kind) & 1ull)) return nullptr;
+  return g_prof.acc + kind;
+}
+
 void prof_pre(int kind, hipStream_t s) {
+  if (g_prof.device) return;
   if (!((g_prof.mask >> kind) & 1ull) || 2 * g_prof.n + 1 >= (int)g_prof.ev.size()) return;
   hipEventRecord(g_prof.ev[2 * g_prof.n], s);
 }
 void prof_post(int kind, hipStream_t s) {
+  if (g_prof.device) return;
   if (!((g_prof.mask >> kind) & 1ull) || 2 * g_prof.n + 1 >= (int)g_prof.ev.size()) return;
   hipEventRecord(g_prof.ev[2 * g_prof.n + 1], s);
   g_prof.kinds[g_prof.n] = kind;
@@ -651,6 +660,40 @@ int onepose_profile_begin(uint64_t kind_mask, int capacity) {
   g_prof.kinds.assign(capacity + 1, -1);
   g_prof.n = 0;
   g_prof.mask = kind_mask;
+  g_prof.device = false;
+  return ONEPOSE_OK;
+}
+
+int onepose_profile_begin_device(uint64_t kind_mask) {
+  clear_error();
+  if (g_prof.acc == nullptr) OP_HIP(hipMalloc(&g_prof.acc, sizeof(StampAcc) * K_NUM_KINDS));
+  std::vector<StampAcc> init(K_NUM_KINDS);
+  for (auto& a : init) a = StampAcc{~0ull, 0ull, 0ull, 0u, 0u};
+  OP_HIP(hipMemcpy(g_prof.acc, init.data(), sizeof(StampAcc) * K_NUM_KINDS,
+                   hipMemcpyHostToDevice));
+  g_prof.n = 0;
+  g_prof.mask = kind_mask;
+  g_prof.device = true;
+  return ONEPOSE_OK;
+}
+
+int onepose_profile_end_device(int64_t* launches, double* total_ms, int n_kinds) {
+  clear_error();
+  OP_REQUIRE(g_prof.device, "profile_end_device: device stamping not active");
+  g_prof.device = false;
+  g_prof.mask = 0;
+  OP_HIP(hipDeviceSynchronize());
+  std::vector<StampAcc> a(K_NUM_KINDS);
+  OP_HIP(hipMemcpy(a.data(), g_prof.acc, sizeof(StampAcc) * K_NUM_KINDS, hipMemcpyDeviceToHost));
+  int dev = 0, khz = 0;
+  OP_HIP(hipGetDevice(&dev));
+  OP_HIP(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev));
+  OP_REQUIRE(khz > 0, "profile: wall clock rate unavailable");
+  for (int k = 0; k < n_kinds; ++k) {
+    const bool ok = k < K_NUM_KINDS;
+    if (launches) launches[k] = ok ? (int64_t)a[k].launches : 0;
+    if (total_ms) total_ms[k] = ok ? (double)a[k].total / khz : 0.0;
+  }
   return ONEPOSE_OK;
 }
 

@@ -123,26 +123,60 @@ class FramePipeline:
         self.enqueue_match(slot)
         self.enqueue_pose(slot)
 
-    def run_stream(self, steps: int, match_stream=None, pose_stream=None):
-        """Enqueue `steps` frames (batches) with matcher(k+1) overlapping pose(k).
-        Returns the pose stream; the caller synchronises."""
+    def capture(self, slot: int = 0, pool=None) -> "torch.cuda.CUDAGraph":
+        """Capture one whole step (``enqueue(slot)``: ~60 launches) as a HIP graph.
+
+        Every launch reads and writes this pipeline's static buffers, so replaying the graph
+        after ``set_frames`` (or after writing new frames into ``desc2d``/``kpts2d``/``K``/
+        ``pose_gt`` in place) runs the full hot path for the new inputs; the graph removes the
+        per-launch host overhead, not any work."""
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, pool=pool):
+            self.enqueue(slot)
+        return g
+
+    def capture_stages(self, pool=None):
+        """Capture, per buffer slot, the matcher stage and the pose stage as two HIP graphs
+        (for ``run_stream(graphs=...)``)."""
+        out = []
+        for sl in range(len(self.slots)):
+            gm, gp = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+            with torch.cuda.graph(gm, pool=pool):
+                self.enqueue_match(sl)
+            with torch.cuda.graph(gp, pool=pool):
+                self.enqueue_pose(sl)
+            out.append((gm, gp))
+        return out
+
+    def run_stream(self, steps: int, match_stream=None, pose_stream=None, graphs=None):
+        """Enqueue `steps` frames (batches) with matcher(k+1) overlapping pose(k); with
+        `graphs` (from ``capture_stages``) each stage is one graph replay.  The match stream
+        waits for the pose stream at the end; the caller synchronises."""
         ms = match_stream or torch.cuda.current_stream(self.device)
-        ps = pose_stream or torch.cuda.Stream(self.device)
+        ps = pose_stream or getattr(self, "_pose_stream", None)
+        if ps is None:
+            ps = self._pose_stream = torch.cuda.Stream(self.device)
         n = len(self.slots)
         matched = [torch.cuda.Event() for _ in range(n)]
-        posed = [None] * n
+        posed = [torch.cuda.Event() for _ in range(n)]
+        used = [False] * n
         for k in range(steps):
             sl = k % n
             with torch.cuda.stream(ms):
-                if posed[sl] is not None:
+                if used[sl]:                      # slot's previous pose stage has read it
                     ms.wait_event(posed[sl])
-                self.enqueue_match(sl)
+                if graphs:
+                    graphs[sl][0].replay()
+                else:
+                    self.enqueue_match(sl)
                 matched[sl].record(ms)
             with torch.cuda.stream(ps):
                 ps.wait_event(matched[sl])
-                self.enqueue_pose(sl)
-                ev = torch.cuda.Event()
-                ev.record(ps)
-                posed[sl] = ev
+                if graphs:
+                    graphs[sl][1].replay()
+                else:
+                    self.enqueue_pose(sl)
+                posed[sl].record(ps)
+            used[sl] = True
         ms.wait_stream(ps)
         return ps

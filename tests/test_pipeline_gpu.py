@@ -1,0 +1,87 @@
+"""The per-frame pipeline (matcher -> selection -> RANSAC-EPnP -> cm/deg) gives bit-identical
+results whether its launches come from the host, from a replayed HIP graph, or from the
+two-stream overlapped schedule -- and a captured graph picks up new frames written into the
+pipeline's static input buffers."""
+import numpy as np
+import pytest
+import torch
+
+from onepose_amd import matcher, synthetic
+from onepose_amd.pipeline import FramePipeline
+
+N1, N3, L, B = 256, 1024, 8, 2
+
+
+def _outputs(slot):
+    return {k: getattr(slot, k).cpu().numpy().copy()
+            for k in ("matches0", "matches1", "mscores0", "pose", "inlier_mask", "n_inliers",
+                      "status", "R_err", "t_err", "cmd")}
+
+
+def _assert_same(a, b):
+    for k in a:
+        np.testing.assert_array_equal(a[k], b[k], err_msg=k)
+
+
+@pytest.fixture(scope="module")
+def setup():
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    dev = torch.device("cuda", 0)
+    sd = synthetic.make_state_dict(0)
+    data, obj, frames = synthetic.make_matcher_inputs(N1, N3, L, seed=5, batch=2 * B)
+    m = matcher.from_state_dict(sd)
+    pipe = FramePipeline(m, data["keypoints3d"][0], data["descriptors3d_db"][0],
+                         data["descriptors2d_db"][0], B, N1, dev, scale=1000.0)
+    Ks = np.stack([f.K for f in frames])
+    gts = np.stack([f.pose_gt for f in frames])
+    batches = [(data["descriptors2d_query"][i:i + B], data["keypoints2d"][i:i + B],
+                Ks[i:i + B], gts[i:i + B]) for i in (0, B)]
+    return pipe, batches
+
+
+@pytest.mark.gpu
+def test_graph_replay_matches_eager(setup):
+    pipe, batches = setup
+    eager = []
+    for bt in batches:
+        pipe.set_frames(*bt)
+        pipe.enqueue(0)
+        torch.cuda.synchronize()
+        eager.append(_outputs(pipe.slots[0]))
+    assert eager[0]["status"].tolist() == [0] * B
+
+    pipe.set_frames(*batches[0])
+    g = pipe.capture(0)
+    for i, bt in enumerate(batches + batches):
+        pipe.set_frames(*bt)          # new frame data into the captured buffers
+        g.replay()
+        torch.cuda.synchronize()
+        _assert_same(eager[i % 2], _outputs(pipe.slots[0]))
+
+
+@pytest.mark.gpu
+def test_stream_schedule_matches_eager(setup):
+    pipe, batches = setup
+    pipe.set_frames(*batches[1])
+    pipe.enqueue(0)
+    torch.cuda.synchronize()
+    ref = _outputs(pipe.slots[0])
+    pipe.run_stream(5)
+    torch.cuda.synchronize()
+    for s in pipe.slots:
+        _assert_same(ref, _outputs(s))
+
+
+@pytest.mark.gpu
+def test_stream_schedule_with_stage_graphs_matches_eager(setup):
+    pipe, batches = setup
+    pipe.set_frames(*batches[0])
+    pipe.enqueue(0)
+    torch.cuda.synchronize()
+    ref = _outputs(pipe.slots[0])
+    graphs = pipe.capture_stages()
+    pipe.run_stream(7, graphs=graphs)
+    torch.cuda.synchronize()
+    for s in pipe.slots:
+        _assert_same(ref, _outputs(s))
