@@ -50,7 +50,7 @@ struct GemmProb {
   const float* pro_mean;   // [batch][K] (PRO_NORM_RELU)
   const float* pro_rstd;
   int64_t pro_bs;
-  float* stats;        // EPI_STATS: [batch][mtiles][2][N]
+  float* stats;        // EPI_STATS: [batch][mtiles][2][N]  (mtiles = ceil(M / tile rows))
   float* rowstat;      // EPI_SCORE: [batch][M][ntiles][2]
   float* colstat;      // EPI_SCORE: [batch][N][mtiles][2]
   float* kvpart;       // EPI_KVPART: [batch][mtiles][4][64][64]
@@ -70,10 +70,19 @@ struct GemmArgs {
   StampAcc* stamp;   // device-stamp profiling accumulator (set by gemm_launch) or null
 };
 
-constexpr int kGemmBM = 64, kGemmBK = 32;
+// Tile configurations: BM x BN output tile, K split into KS slices inside the workgroup.
+enum GemmTile {
+  TILE_64x64 = 0,      // score, mlp1 (STATS), mlp2 (RESID+NORM), final
+  TILE_32x64_K2 = 1,   // q (QZ: one head per tile), K split in two inside the workgroup
+  TILE_32x128 = 2,     // kv (KVPART: [k_h | v_h] per tile)
+};
 
-// bn = 64 or 128 (column tile); EPI_KVPART needs 128, EPI_QZ 64.
-int gemm_launch(int epi, int pro, int bn, GemmArgs& args, hipStream_t stream, int kind);
+// Supported (epilogue, prologue, tile) combinations: KVPART/32x128, QZ/32x64_K2, STATS/64x64,
+// RESID+NORM/64x64, SCORE/64x64, BIAS/64x64.  K must be a multiple of twice the tile's stage
+// depth (32 * KS).
+int gemm_launch(int epi, int pro, int tile, GemmArgs& args, hipStream_t stream, int kind);
+// Rows per M-tile of a configuration (the chunk size of the STATS / KVPART partials).
+int gemm_tile_rows(int tile);
 
 // Zero-initialised problem with the common fields set.
 GemmProb gemm_prob(const float* A, int lda, const float* W, int ldw, const float* bias,

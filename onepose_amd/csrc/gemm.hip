@@ -1,15 +1,21 @@
 // fp32 MFMA grouped token-GEMM (see gemm.h).
 //
-// Tile: 64 tokens x BN outputs x 32-deep K step, 256 threads = 4 waves in a 2x2 grid; each
-// wave owns 32 x BN/2 outputs = BN/64 accumulators of v_mfma_f32_32x32x2_f32.  Operands are
-// staged through double-buffered LDS images [row][k] with a 36-float row pitch: a
-// ds_read_b128 lane group (16 lanes, 16 distinct rows, same k) covers 16 distinct 16-byte
-// slots of the 64-bank row -- conflict free (9*i mod 16 is a permutation).  Each b128 read
-// feeds four MFMAs: within one group of 8 k-values, lane half h carries k = 8*kk + 4*h + j
-// into MFMA j, identically for A and W, so the k-sum is unchanged (a re-ordering of it).
-// The next K step's global loads are issued before the MFMAs and are only consumed (prologue
-// transform + LDS store) after them, so the loads overlap the matrix work; one barrier per
-// K step.
+// A workgroup (4 or 8 waves) owns a BM x BN output tile.  Its waves form a
+// WM x WN x KS grid: each wave owns a 32 x (FN*32) block of v_mfma_f32_32x32x2_f32
+// accumulators and one of the KS k-slices of every stage (KS > 1 splits the K loop inside
+// the workgroup; the slices are added through LDS in a fixed order at the end).  The tile
+// shape trades per-workgroup efficiency (64 x 64: least LDS / L2 traffic per FLOP) against
+// filling 256 CUs: the narrow 256-wide q output and the 128-wide [k_h | v_h] KV tiles use
+// 32-row tiles (q also splits K in two) to get more workgroups.
+//
+// Operands are staged through double-buffered LDS images [row][k] of BKS = 32*KS columns
+// with a (BKS+4)-float pitch: a ds_read_b128 lane group (16 lanes, 16 distinct rows, same k)
+// hits 16 distinct 16-byte bank slots (pitch = 4 mod 64 floats, or 36), so reads are
+// conflict free.  Each b128 read feeds four MFMAs: within one group of 8 k-values, lane half
+// h carries k = 8*kk + 4*h + j into MFMA j, identically for A and W, so the k-sum is a
+// re-ordering of the plain sum.  Global loads run two stages ahead of the MFMAs (register
+// stage + LDS stage); loads are branch- and select-free so the compiler waits on exactly the
+// older stage.  One barrier per stage.
 #include "gemm.h"
 
 #include <cstring>
@@ -20,13 +26,27 @@ typedef float floatx16 __attribute__((ext_vector_type(16)));
 
 namespace {
 
-constexpr int BM = kGemmBM, BK = kGemmBK;
-constexpr int PITCH = BK + 4;   // 36 floats
+template <int BM_, int BN_, int KS_, int NW_, int BKS_>
+struct Tile {
+  static constexpr int BM = BM_, BN = BN_, KS = KS_, NW = NW_, BKS = BKS_;
+  static constexpr int NT = 64 * NW;            // threads
+  static constexpr int WM = BM / 32;            // waves along M
+  static constexpr int WN = NW / (WM * KS);     // waves along N
+  static constexpr int FN = BN / (32 * WN);     // accumulators per wave
+  static constexpr int KKW = BKS / KS / 8;      // 8-deep MFMA groups per wave per stage
+  static constexpr int PITCH = BKS + 4;
+  static constexpr int KQ = BKS / 4;            // float4 per row per stage
+  static constexpr int A4 = BM * KQ / NT;       // float4 of A per thread per stage
+  static constexpr int W4 = BN * KQ / NT;
+  static constexpr int STAGE = (BM + BN) * PITCH;
+  static_assert(WM * WN * KS == NW && FN >= 1 && A4 >= 1 && W4 >= 1 && KKW >= 2, "tile shape");
+  static_assert(NT % KQ == 0 && BM * KQ % NT == 0 && BN * KQ % NT == 0, "one k-quad per thread");
+};
 
-template <int BN>
+template <class T>
 struct Stage {
-  float4 a[2];
-  float4 w[BN / 32];
+  float4 a[T::A4];
+  float4 w[T::W4];
   float4 mean, rstd;
 };
 
@@ -37,10 +57,14 @@ struct Ctx {
   int lda0, lda1, ldw0, ldw1, ksplit, M, N, K;
 };
 
-template <int PRO, int BN>
-__device__ __forceinline__ void load_stage(const Ctx& c, int m0, int n0, int k0, Stage<BN>& s) {
+// Rows past M (N) are loaded from the last valid row: they only feed accumulator rows
+// (columns) that are never stored, and every reducing epilogue masks them when it stages the
+// tile, so they need no zeroing -- a select right behind each load would make the wave wait
+// for the load it just issued.
+template <int PRO, class T>
+__device__ __forceinline__ void load_stage(const Ctx& c, int m0, int n0, int k0, Stage<T>& s) {
   const int t = threadIdx.x;
-  const int kq = (t & 7) * 4;
+  const int kq = (t % T::KQ) * 4;
   const bool first = k0 < c.ksplit;
   const float* A = first ? c.a0 : c.a1;
   const int lda = first ? c.lda0 : c.lda1;
@@ -52,56 +76,46 @@ __device__ __forceinline__ void load_stage(const Ctx& c, int m0, int n0, int k0,
     s.rstd = *reinterpret_cast<const float4*>(c.rstd + k0 + kq);
   }
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int m = m0 + (t >> 3) + 32 * i;
-    s.a[i] = (m < c.M) ? *reinterpret_cast<const float4*>(A + (int64_t)m * lda + kk)
-                       : make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int i = 0; i < T::A4; ++i) {
+    const int m = min(m0 + (t + T::NT * i) / T::KQ, c.M - 1);
+    s.a[i] = *reinterpret_cast<const float4*>(A + (int64_t)m * lda + kk);
   }
 #pragma unroll
-  for (int i = 0; i < BN / 32; ++i) {
-    const int o = n0 + (t >> 3) + 32 * i;
-    s.w[i] = (o < c.N) ? *reinterpret_cast<const float4*>(W + (int64_t)o * ldw + kk)
-                       : make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int i = 0; i < T::W4; ++i) {
+    const int o = min(n0 + (t + T::NT * i) / T::KQ, c.N - 1);
+    s.w[i] = *reinterpret_cast<const float4*>(W + (int64_t)o * ldw + kk);
   }
 }
 
-template <int PRO, int BN>
-__device__ __forceinline__ void store_stage(float* lds_a, float* lds_w, Stage<BN>& s, int m0,
-                                            int M) {
+template <int PRO, class T>
+__device__ __forceinline__ void store_stage(float* lds_a, float* lds_w, Stage<T>& s) {
   const int t = threadIdx.x;
-  const int kq = (t & 7) * 4;
+  const int kq = (t % T::KQ) * 4;
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int row = (t >> 3) + 32 * i;
+  for (int i = 0; i < T::A4; ++i) {
     float4 v = s.a[i];
     if (PRO == PRO_NORM_RELU) {
-      if (m0 + row < M) {
-        v.x = fmaxf((v.x - s.mean.x) * s.rstd.x, 0.f);
-        v.y = fmaxf((v.y - s.mean.y) * s.rstd.y, 0.f);
-        v.z = fmaxf((v.z - s.mean.z) * s.rstd.z, 0.f);
-        v.w = fmaxf((v.w - s.mean.w) * s.rstd.w, 0.f);
-      }
+      v.x = fmaxf((v.x - s.mean.x) * s.rstd.x, 0.f);
+      v.y = fmaxf((v.y - s.mean.y) * s.rstd.y, 0.f);
+      v.z = fmaxf((v.z - s.mean.z) * s.rstd.z, 0.f);
+      v.w = fmaxf((v.w - s.mean.w) * s.rstd.w, 0.f);
     }
-    *reinterpret_cast<float4*>(lds_a + row * PITCH + kq) = v;
+    *reinterpret_cast<float4*>(lds_a + ((t + T::NT * i) / T::KQ) * T::PITCH + kq) = v;
   }
 #pragma unroll
-  for (int i = 0; i < BN / 32; ++i) {
-    const int row = (t >> 3) + 32 * i;
-    *reinterpret_cast<float4*>(lds_w + row * PITCH + kq) = s.w[i];
-  }
+  for (int i = 0; i < T::W4; ++i)
+    *reinterpret_cast<float4*>(lds_w + ((t + T::NT * i) / T::KQ) * T::PITCH + kq) = s.w[i];
 }
 
-template <int EPI, int PRO, int BN>
+template <int EPI, int PRO, class T>
 __device__ __forceinline__ void gemm_body(const GemmArgs& args) {
-  constexpr int FN = BN / 64;           // accumulators per wave
-  constexpr int STAGE = (BM + BN) * PITCH;
+  constexpr int BM = T::BM, BN = T::BN, FN = T::FN, STAGE = T::STAGE, PITCH = T::PITCH;
   __shared__ __attribute__((aligned(16))) float lds[2 * STAGE];
   __shared__ float zrow[BM];
-  __shared__ float zrow_stats[(EPI == EPI_STATS) ? 512 : 1];
+  __shared__ float part[(EPI == EPI_STATS) ? (T::NT / 64) * BN * 2 : 1];
 
   // XCD-aware tile order: blocks are dealt round-robin over the 8 XCDs, so hand each XCD a
-  // contiguous run of logical tiles -- the N-tiles of one M-tile then share that XCD's L2
-  // (A is fetched once per XCD instead of once per N-tile).
+  // contiguous run of logical tiles -- the N-tiles of one M-tile then share that XCD's L2.
   int bid = xcd_contiguous(blockIdx.x, gridDim.x);
   const bool second = bid >= args.p[0].tiles;
 #define F(x) (second ? args.p[1].x : args.p[0].x)
@@ -131,9 +145,12 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args) {
   c.mean = F(pro_mean) + b * F(pro_bs);
   c.rstd = F(pro_rstd) + b * F(pro_bs);
 
-  const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
+  const int t = threadIdx.x;
+  const int lane = t & 63;
+  const int wave = t >> 6;
+  const int ks = wave / (T::WM * T::WN);
+  const int wm = (wave % (T::WM * T::WN)) / T::WN;
+  const int wn = wave % T::WN;
 
   floatx16 acc[FN];
 #pragma unroll
@@ -141,107 +158,158 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args) {
 #pragma unroll
     for (int i = 0; i < 16; ++i) acc[j][i] = 0.f;
 
-  // Prefetch distance 2: while the MFMAs consume K step kt from LDS, step kt+1 sits in
-  // registers (loaded one step earlier) and step kt+2's loads are in flight, so each global
-  // load has two MFMA phases to land (a lone 64x64 tile per CU has no other waves to hide
-  // the latency behind).
-  const int nk = c.K / BK;
-  Stage<BN> s0, s1;
-  load_stage<PRO, BN>(c, m0, n0, 0, s0);
-  if (nk > 1) load_stage<PRO, BN>(c, m0, n0, BK, s1);
-  store_stage<PRO, BN>(lds, lds + BM * PITCH, s0, m0, c.M);
-  __syncthreads();
-
-  auto step = [&](int kt, Stage<BN>& next, Stage<BN>& spare) __attribute__((always_inline)) {
-    const float* la = lds + (kt & 1) * STAGE;
-    const float* lw = la + BM * PITCH;
-    if (kt + 2 < nk) load_stage<PRO, BN>(c, m0, n0, (kt + 2) * BK, spare);
-    const float* pa = la + (wm * 32 + (lane & 31)) * PITCH + (lane >> 5) * 4;
-    const float* pw = lw + (wn * (BN / 2) + (lane & 31)) * PITCH + (lane >> 5) * 4;
+  // Main loop, software-pipelined across the per-stage barrier.  Step kt consumes stage kt
+  // from registers (fragments read from LDS right after the previous barrier):
+  //   issue global loads of stage kt+2 | MFMA kk0 | store stage kt+1 to the other LDS buffer
+  //   | MFMA kk1, kk2 | barrier | read stage kt+1's fragments | MFMA kk3 (hides that read)
+  // so the matrix pipe is fed through the store / barrier / LDS-read phase of every stage.
+  // Global loads run two stages ahead (register stage + LDS stage).
+  const int nk = c.K / T::BKS;
+  Stage<T> s0, s1;
+  constexpr int KKW = T::KKW;
+  struct Frag {
+    float4 a[KKW];
+    float4 w[KKW][FN];
+  };
+  Frag f0, f1;
+  const int kofs = ks * KKW * 8 + (lane >> 5) * 4;
+  const int a_off = (wm * 32 + (lane & 31)) * PITCH + kofs;
+  const int w_off = BM * PITCH + (wn * FN * 32 + (lane & 31)) * PITCH + kofs;
+  auto read_frag = [&](const float* buf, Frag& f) __attribute__((always_inline)) {
 #pragma unroll
-    for (int kk = 0; kk < BK / 8; ++kk) {
-      const float4 a = *reinterpret_cast<const float4*>(pa + kk * 8);
+    for (int kk = 0; kk < KKW; ++kk) {
+      f.a[kk] = *reinterpret_cast<const float4*>(buf + a_off + kk * 8);
 #pragma unroll
-      for (int j = 0; j < FN; ++j) {
-        const float4 w = *reinterpret_cast<const float4*>(pw + j * 32 * PITCH + kk * 8);
-        acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, w.x, acc[j], 0, 0, 0);
-        acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, w.y, acc[j], 0, 0, 0);
-        acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, w.z, acc[j], 0, 0, 0);
-        acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, w.w, acc[j], 0, 0, 0);
-      }
+      for (int j = 0; j < FN; ++j)
+        f.w[kk][j] = *reinterpret_cast<const float4*>(buf + w_off + j * 32 * PITCH + kk * 8);
     }
-    if (kt + 1 < nk) {
-      float* na = lds + ((kt + 1) & 1) * STAGE;
-      store_stage<PRO, BN>(na, na + BM * PITCH, next, m0, c.M);
+  };
+  auto mfma_kk = [&](const Frag& f, int kk) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(f.a[kk].x, f.w[kk][j].x, acc[j], 0, 0, 0);
+      acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(f.a[kk].y, f.w[kk][j].y, acc[j], 0, 0, 0);
+      acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(f.a[kk].z, f.w[kk][j].z, acc[j], 0, 0, 0);
+      acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(f.a[kk].w, f.w[kk][j].w, acc[j], 0, 0, 0);
+    }
+  };
+
+  load_stage<PRO, T>(c, m0, n0, 0, s0);
+  load_stage<PRO, T>(c, m0, n0, T::BKS, s1);
+  store_stage<PRO, T>(lds, lds + BM * PITCH, s0);
+  __syncthreads();
+  read_frag(lds, f0);
+
+  auto step = [&](int kt, Stage<T>& next, Stage<T>& spare, const Frag& cur, Frag& nxt)
+      __attribute__((always_inline)) {
+    // unconditional: past the end the last stage is re-read into the spare set and ignored
+    load_stage<PRO, T>(c, m0, n0, min(kt + 2, nk - 1) * T::BKS, spare);
+    mfma_kk(cur, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    float* na = lds + ((kt + 1) & 1) * STAGE;
+    store_stage<PRO, T>(na, na + BM * PITCH, next);   // (unused after the last step)
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int kk = 1; kk < KKW - 1; ++kk) mfma_kk(cur, kk);
+    __syncthreads();
+    read_frag(na, nxt);                               // (unused after the last step)
+    __builtin_amdgcn_sched_barrier(0);
+    mfma_kk(cur, KKW - 1);
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  for (int kt = 0; kt < nk; kt += 2) {   // nk is even (checked at launch)
+    step(kt, s1, s0, f0, f1);
+    step(kt + 1, s0, s1, f1, f0);
+  }
+  __syncthreads();   // every wave done with the LDS stages before they are reused below
+
+  // ---- k-slice reduction: slices 1..KS-1 add into slice 0 in order (deterministic) ----
+  if (T::KS > 1) {
+    float* red = lds;   // [KS-1][WM*WN][FN][16][64]
+    static_assert((T::KS - 1) * T::WM * T::WN * FN * 16 * 64 <= 2 * STAGE, "reduction fits");
+    const int blk = wave % (T::WM * T::WN);
+    if (ks > 0) {
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+          red[((((ks - 1) * T::WM * T::WN + blk) * FN + j) * 16 + i) * 64 + lane] = acc[j][i];
     }
     __syncthreads();
-  };
-  for (int kt = 0; kt < nk; kt += 2) {
-    step(kt, s1, s0);
-    if (kt + 1 < nk) step(kt + 1, s0, s1);
+    if (ks == 0) {
+      for (int s = 1; s < T::KS; ++s)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+#pragma unroll
+          for (int i = 0; i < 16; ++i)
+            acc[j][i] += red[((((s - 1) * T::WM * T::WN + blk) * FN + j) * 16 + i) * 64 + lane];
+    }
+    __syncthreads();
   }
 
-  // ---- epilogue ----
+  // ---- epilogue (waves of slice 0 own the accumulators) ----
   const int M = c.M, N = c.N;
   const float* biasp = F(bias);
   float* Y = F(Y) + b * F(y_bs);
   const int ldy = F(ldy);
-  float* tile = lds;   // [64][BN+1] staging for the reducing epilogues
+  float* tile = lds;   // [BM][BN+1] staging for the reducing epilogues
   constexpr int TP = BN + 1;
   constexpr bool kStage =
       EPI == EPI_STATS || EPI == EPI_SCORE || EPI == EPI_KVPART || EPI == EPI_QZ;
 
-  float res[FN][16];
-  if (EPI == EPI_RESID) {   // all residual loads issued before the first store
-    const float* R = F(R) + b * F(r_bs);
-    const int ldr = F(ldr);
+  if (ks == 0) {
+    float res[FN][16];
+    if (EPI == EPI_RESID) {   // all residual loads issued before the first store
+      const float* R = F(R) + b * F(r_bs);
+      const int ldr = F(ldr);
 #pragma unroll
-    for (int j = 0; j < FN; ++j) {
-      const int gn = n0 + wn * (BN / 2) + j * 32 + (lane & 31);
+      for (int j = 0; j < FN; ++j) {
+        const int gn = min(n0 + wn * FN * 32 + j * 32 + (lane & 31), N - 1);
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int gm = m0 + wm * 32 + (i & 3) + 8 * (i >> 2) + 4 * (lane >> 5);
-        res[j][i] = (gm < M && gn < N) ? R[(int64_t)gm * ldr + gn] : 0.f;
-      }
-    }
-  }
-#pragma unroll
-  for (int j = 0; j < FN; ++j) {
-    const int col = wn * (BN / 2) + j * 32 + (lane & 31);
-    const int gn = n0 + col;
-    const bool col_ok = gn < N;
-    const float bias = (EPI != EPI_SCORE && biasp != nullptr && col_ok) ? biasp[gn] : 0.f;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int row = wm * 32 + (i & 3) + 8 * (i >> 2) + 4 * (lane >> 5);
-      const int gm = m0 + row;
-      float y;
-      if (EPI == EPI_SCORE) {
-        y = acc[j][i] / F(scale);
-      } else {
-        y = acc[j][i] + bias;
-        if (EPI == EPI_QZ) y = elu1(y) + 1.0f;
-        if (EPI == EPI_KVPART) y = (col < 64) ? (elu1(y) + 1.0f) : (y / F(vdiv));
-      }
-      if (EPI == EPI_BIAS || EPI == EPI_STATS || EPI == EPI_SCORE || EPI == EPI_RESID) {
-        if (gm < M && col_ok) {
-          if (EPI == EPI_RESID) y = res[j][i] + y;
-          Y[(int64_t)gm * ldy + gn] = y;
+        for (int i = 0; i < 16; ++i) {
+          const int gm = min(m0 + wm * 32 + (i & 3) + 8 * (i >> 2) + 4 * (lane >> 5), M - 1);
+          res[j][i] = R[(int64_t)gm * ldr + gn];
         }
       }
-      if (kStage) tile[row * TP + col] = (gm < M) ? y : 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int col = wn * FN * 32 + j * 32 + (lane & 31);
+      const int gn = n0 + col;
+      const bool col_ok = gn < N;
+      const float bias = (EPI != EPI_SCORE && biasp != nullptr && col_ok) ? biasp[gn] : 0.f;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int row = wm * 32 + (i & 3) + 8 * (i >> 2) + 4 * (lane >> 5);
+        const int gm = m0 + row;
+        float y;
+        if (EPI == EPI_SCORE) {
+          y = acc[j][i] / F(scale);
+        } else {
+          y = acc[j][i] + bias;
+          if (EPI == EPI_QZ) y = elu1(y) + 1.0f;
+          if (EPI == EPI_KVPART) y = (col < 64) ? (elu1(y) + 1.0f) : (y / F(vdiv));
+        }
+        if (EPI == EPI_BIAS || EPI == EPI_STATS || EPI == EPI_SCORE || EPI == EPI_RESID) {
+          if (gm < M && col_ok) {
+            if (EPI == EPI_RESID) y = res[j][i] + y;
+            Y[(int64_t)gm * ldy + gn] = y;
+          }
+        }
+        if (kStage) tile[row * TP + col] = (gm < M) ? y : 0.f;
+      }
     }
   }
   if (!kStage) return;
   __syncthreads();
-  const int t = threadIdx.x;
   const int rows = min(BM, M - m0);
 
   if (EPI == EPI_STATS) {
-    // per column: 4 row groups of 16 -> (sum, M2 about the group mean), Chan-merged in order
-    float* part = reinterpret_cast<float*>(zrow_stats);
+    // per column: NRG row groups -> (mean, M2 about the group mean), Chan-merged in order
+    static_assert(EPI != EPI_STATS || BN == 64, "stats tile is 64 columns");
+    constexpr int NRG = T::NT / 64, RG = BM / NRG;
     const int col = t & 63, rg = t >> 6;
-    const int r0 = rg * 16, r1 = min(r0 + 16, rows);
+    const int r0 = rg * RG, r1 = min(r0 + RG, rows);
     const int cnt = max(r1 - r0, 0);
     float s = 0.f;
     for (int rr = r0; rr < r1; ++rr) s += tile[rr * TP + col];
@@ -256,8 +324,8 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args) {
     __syncthreads();
     if (t < 64 && n0 + t < N) {
       float n = 0.f, mean = 0.f, M2 = 0.f;
-      for (int g = 0; g < 4; ++g) {
-        const float nb = (float)max(min(g * 16 + 16, rows) - g * 16, 0);
+      for (int g = 0; g < NRG; ++g) {
+        const float nb = (float)max(min(g * RG + RG, rows) - g * RG, 0);
         if (nb == 0.f) continue;
         const float mb = part[(g * 64 + t) * 2], m2b = part[(g * 64 + t) * 2 + 1];
         const float nn = n + nb, delta = mb - mean;
@@ -297,28 +365,27 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args) {
   }
   if (EPI == EPI_QZ) {
     // Z[row] = 1 / (phi(q)_row . ksum_h + 1e-6), h = the head this 64-column tile holds
-    {
-      const float* ks = F(ksum) + b * F(ksum_bs) + n0;
+    static_assert(EPI != EPI_QZ || BN == 64, "QZ tile is one head");
+    if (t < 4 * BM) {
+      const float* ks_h = F(ksum) + b * F(ksum_bs) + n0;
       const int row = t >> 2, q = t & 3;   // 4 lanes per row, 16 channels each
       float s = 0.f;
 #pragma unroll
-      for (int cc = 0; cc < 16; ++cc) s += tile[row * TP + q * 16 + cc] * ks[q * 16 + cc];
+      for (int cc = 0; cc < 16; ++cc) s += tile[row * TP + q * 16 + cc] * ks_h[q * 16 + cc];
       s += __shfl_xor(s, 1, 64);
       s += __shfl_xor(s, 2, 64);
       if (q == 0) zrow[row] = 1.0f / (s + 1e-6f);
     }
     __syncthreads();
     const float ns = F(ns);
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int row = (t >> 4) + 16 * (i & 3);
-      const int cc = (t & 15) + 16 * (i >> 2);
-      const int gm = m0 + row;
-      if (gm < M) Y[(int64_t)gm * ldy + n0 + cc] = tile[row * TP + cc] * zrow[row] * ns;
+    for (int e = t; e < BM * 64; e += T::NT) {
+      const int row = e >> 6, cc = e & 63;
+      if (m0 + row < M) Y[(int64_t)(m0 + row) * ldy + n0 + cc] = tile[row * TP + cc] * zrow[row] * ns;
     }
   }
   if (EPI == EPI_KVPART) {
     // KV_h[d][q] = sum_rows phi(k)[row][d] * v[row][q]   (columns 0..63 | 64..127 of the tile)
+    static_assert(EPI != EPI_KVPART || (BN == 128 && T::NW == 4), "KVPART tile is [k_h | v_h]");
     const int h = n0 / 128;
     if (t < 64) {
       float s = 0.f;
@@ -346,19 +413,37 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args) {
 #undef F
 }
 
-template <int EPI, int PRO, int BN>
-__global__ __launch_bounds__(256) void gemm_f32_kernel(GemmArgs args) {
+template <int EPI, int PRO, class T>
+__global__ __launch_bounds__(T::NT) void gemm_f32_kernel(GemmArgs args) {
   stamp_begin(args.stamp);
-  gemm_body<EPI, PRO, BN>(args);
+  gemm_body<EPI, PRO, T>(args);
   stamp_end(args.stamp);
 }
 
-template <int EPI, int PRO, int BN>
+using T64x64 = Tile<64, 64, 1, 4, 32>;
+using T32x64k2 = Tile<32, 64, 2, 4, 64>;
+using T32x128 = Tile<32, 128, 1, 4, 32>;
+
+template <int EPI, int PRO, class T>
 void launch_one(GemmArgs& args, int grid, hipStream_t stream) {
-  hipLaunchKernelGGL((gemm_f32_kernel<EPI, PRO, BN>), dim3(grid), dim3(256), 0, stream, args);
+  hipLaunchKernelGGL((gemm_f32_kernel<EPI, PRO, T>), dim3(grid), dim3(T::NT), 0, stream, args);
+}
+
+struct TileDims {
+  int bm, bn, bks;
+};
+TileDims tile_dims(int tile) {
+  switch (tile) {
+    case TILE_64x64: return {64, 64, 32};
+    case TILE_32x64_K2: return {32, 64, 64};
+    case TILE_32x128: return {32, 128, 32};
+    default: return {0, 0, 0};
+  }
 }
 
 }  // namespace
+
+int gemm_tile_rows(int tile) { return tile_dims(tile).bm; }
 
 GemmProb gemm_prob(const float* A, int lda, const float* W, int ldw, const float* bias,
                    float* Y, int ldy, int M, int N, int K, int batch) {
@@ -384,7 +469,9 @@ GemmProb gemm_prob(const float* A, int lda, const float* W, int ldw, const float
   return g;
 }
 
-int gemm_launch(int epi, int pro, int bn, GemmArgs& args, hipStream_t stream, int kind) {
+int gemm_launch(int epi, int pro, int tile, GemmArgs& args, hipStream_t stream, int kind) {
+  const TileDims td = tile_dims(tile);
+  OP_REQUIRE(td.bm > 0, "gemm: unknown tile %d", tile);
   int grid = 0;
   for (int i = 0; i < 2; ++i) {
     GemmProb& P = args.p[i];
@@ -392,35 +479,37 @@ int gemm_launch(int epi, int pro, int bn, GemmArgs& args, hipStream_t stream, in
       P.tiles = 0;
       continue;
     }
-    OP_REQUIRE(P.K % kGemmBK == 0, "gemm: K=%d not a multiple of %d", P.K, kGemmBK);
-    OP_REQUIRE(P.ksplit % kGemmBK == 0, "gemm: ksplit=%d", P.ksplit);
+    OP_REQUIRE(P.M > 0 && P.N > 0, "gemm: empty problem");
+    OP_REQUIRE(P.K % (2 * td.bks) == 0, "gemm: K=%d not a multiple of %d", P.K, 2 * td.bks);
+    OP_REQUIRE(P.ksplit % td.bks == 0, "gemm: ksplit=%d", P.ksplit);
     OP_REQUIRE(P.lda0 % 4 == 0 && P.ldw % 4 == 0, "gemm: unaligned leading dimension");
-    OP_REQUIRE(epi != EPI_KVPART || (bn == 128 && P.N % 128 == 0), "gemm: KVPART tiling");
-    OP_REQUIRE(epi != EPI_QZ || (bn == 64 && P.N % 64 == 0), "gemm: QZ tiling");
-    P.mtiles = ceil_div(P.M, kGemmBM);
-    P.ntiles = ceil_div(P.N, bn);
+    OP_REQUIRE(epi != EPI_KVPART || (td.bn == 128 && P.N % 128 == 0), "gemm: KVPART tiling");
+    OP_REQUIRE(epi != EPI_QZ || (td.bn == 64 && P.N % 64 == 0), "gemm: QZ tiling");
+    OP_REQUIRE(epi != EPI_STATS || td.bn == 64, "gemm: STATS tiling");
+    P.mtiles = ceil_div(P.M, td.bm);
+    P.ntiles = ceil_div(P.N, td.bn);
     P.tiles = P.mtiles * P.ntiles * P.batch;
     grid += P.tiles;
   }
   if (grid == 0) return ONEPOSE_OK;
   args.stamp = nullptr;
-#define CASE(E, PR, BN_)                          \
-  if (epi == E && pro == PR && bn == BN_) {       \
+#define CASE(E, PR, TI, T)                        \
+  if (epi == E && pro == PR && tile == TI) {      \
     prof_pre(kind, stream);                       \
     args.stamp = prof_stamp_slot(kind);           \
-    launch_one<E, PR, BN_>(args, grid, stream);   \
+    launch_one<E, PR, T>(args, grid, stream);     \
     prof_post(kind, stream);                      \
     OP_LAUNCHED();                                \
     return ONEPOSE_OK;                            \
   }
-  CASE(EPI_BIAS, PRO_PLAIN, 64)
-  CASE(EPI_KVPART, PRO_PLAIN, 128)
-  CASE(EPI_QZ, PRO_PLAIN, 64)
-  CASE(EPI_STATS, PRO_PLAIN, 64)
-  CASE(EPI_RESID, PRO_NORM_RELU, 64)
-  CASE(EPI_SCORE, PRO_PLAIN, 64)
+  CASE(EPI_KVPART, PRO_PLAIN, TILE_32x128, T32x128)
+  CASE(EPI_QZ, PRO_PLAIN, TILE_32x64_K2, T32x64k2)
+  CASE(EPI_STATS, PRO_PLAIN, TILE_64x64, T64x64)
+  CASE(EPI_RESID, PRO_NORM_RELU, TILE_64x64, T64x64)
+  CASE(EPI_SCORE, PRO_PLAIN, TILE_64x64, T64x64)
+  CASE(EPI_BIAS, PRO_PLAIN, TILE_64x64, T64x64)
 #undef CASE
-  set_error("gemm: unsupported epilogue/prologue/bn %d/%d/%d", epi, pro, bn);
+  set_error("gemm: unsupported epilogue/prologue/tile %d/%d/%d", epi, pro, tile);
   return ONEPOSE_ERR_INVALID;
 }
 

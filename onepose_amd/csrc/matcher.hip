@@ -35,6 +35,10 @@
 
 namespace onepose {
 
+// GEMM tile per layer GEMM (gemm.h; measured per shape on config 2).
+constexpr int kTileKV = TILE_32x128, kTileQ = TILE_32x64_K2, kTileMLP1 = TILE_64x64,
+              kTileMLP2 = TILE_64x64, kTileFinal = TILE_64x64;
+
 // ------------------------------------------------------------------------------------
 // errors
 // ------------------------------------------------------------------------------------
@@ -302,7 +306,7 @@ struct StatsProb {
   const float* part;  // [B][mtiles][2][512]
   float* mean;        // [B][512]
   float* rstd;
-  int m, mtiles;
+  int m, mtiles, rows;   // tokens, partial tiles, rows per tile
 };
 struct StatsArgs {
   StatsProb p[2];
@@ -324,7 +328,7 @@ __global__ __launch_bounds__(256) void stats_finalize_kernel(StatsArgs args, int
   const float* part = P.part + (int64_t)b * P.mtiles * 1024;
   double n = 0.0, mean = 0.0, m2 = 0.0;
   for (int ti = tg; ti < P.mtiles; ti += 4) {
-    const double nb = (double)min(64, P.m - ti * 64);
+    const double nb = (double)min(P.rows, P.m - ti * P.rows);
     chan_merge(n, mean, m2, nb, part[ti * 1024 + c], part[ti * 1024 + 512 + c]);
   }
   red[0][tg][t & 63] = n;
@@ -604,11 +608,12 @@ Plan make_plan(void* ws, int B, int n1, int n3, bool with_conf) {
     p.x2[i] = c.take<float>(t2 * 256);
     p.x3[i] = c.take<float>(t3 * 256);
   }
-  const int ch2 = ceil_div(n1, 64), ch3 = ceil_div(n3, 64);
-  p.kvpart2 = c.take<float>((size_t)B * ch2 * 16384);
-  p.kvpart3 = c.take<float>((size_t)B * ch3 * 16384);
-  p.kspart2 = c.take<float>((size_t)B * ch2 * 256);
-  p.kspart3 = c.take<float>((size_t)B * ch3 * 256);
+  const int ch2 = ceil_div(n1, 64), ch3 = ceil_div(n3, 64);   // score tiles
+  const int kvr = gemm_tile_rows(kTileKV), str = gemm_tile_rows(kTileMLP1);
+  p.kvpart2 = c.take<float>((size_t)B * ceil_div(n1, kvr) * 16384);
+  p.kvpart3 = c.take<float>((size_t)B * ceil_div(n3, kvr) * 16384);
+  p.kspart2 = c.take<float>((size_t)B * ceil_div(n1, kvr) * 256);
+  p.kspart3 = c.take<float>((size_t)B * ceil_div(n3, kvr) * 256);
   p.kv = c.take<float>((size_t)2 * B * 16384);
   p.ksum = c.take<float>((size_t)2 * B * 256);
   p.mf = c.take<float>((size_t)2 * B * 512 * 256);
@@ -616,8 +621,8 @@ Plan make_plan(void* ws, int B, int n1, int n3, bool with_conf) {
   p.qz3 = c.take<float>(t3 * 256);
   p.y12 = c.take<float>(t2 * 512);
   p.y13 = c.take<float>(t3 * 512);
-  p.stats2 = c.take<float>((size_t)B * ch2 * 1024);
-  p.stats3 = c.take<float>((size_t)B * ch3 * 1024);
+  p.stats2 = c.take<float>((size_t)B * ceil_div(n1, str) * 1024);
+  p.stats3 = c.take<float>((size_t)B * ceil_div(n3, str) * 1024);
   p.mean = c.take<float>((size_t)2 * B * 512);
   p.rstd = c.take<float>((size_t)2 * B * 512);
   p.f2 = c.take<float>(t2 * 256);
@@ -911,13 +916,13 @@ int onepose_match(const void* packed_weights, const float* desc2d, int64_t desc2
       a.p[1].vdiv = (float)n3;
       a.p[1].kvpart = p.kvpart3;
       a.p[1].kspart = p.kspart3;
-      if ((rc = gemm_launch(EPI_KVPART, PRO_PLAIN, 128, a, st, K_KV_GEMM)) != ONEPOSE_OK)
+      if ((rc = gemm_launch(EPI_KVPART, PRO_PLAIN, kTileKV, a, st, K_KV_GEMM)) != ONEPOSE_OK)
         return rc;
     }
     {  // 2. KV[src], ksum[src]
       KvArgs kva;
-      kva.p[0] = {p.kvpart2, p.kspart2, ch2};
-      kva.p[1] = {p.kvpart3, p.kspart3, ch3};
+      kva.p[0] = {p.kvpart2, p.kspart2, ceil_div(n1, gemm_tile_rows(kTileKV))};
+      kva.p[1] = {p.kvpart3, p.kspart3, ceil_div(n3, gemm_tile_rows(kTileKV))};
       OP_LAUNCH(K_KV_REDUCE, st, kv_reduce_kernel, dim3(2 * B * 65), dim3(256), 0, st, kva, p.kv,
                 p.ksum, B);
     }
@@ -939,7 +944,7 @@ int onepose_match(const void* packed_weights, const float* desc2d, int64_t desc2
       a.p[1].ksum = p.ksum + (size_t)src3 * B * 256;
       a.p[1].ksum_bs = 256;
       a.p[1].ns = (float)ns3;
-      if ((rc = gemm_launch(EPI_QZ, PRO_PLAIN, 64, a, st, K_Q_GEMM)) != ONEPOSE_OK) return rc;
+      if ((rc = gemm_launch(EPI_QZ, PRO_PLAIN, kTileQ, a, st, K_Q_GEMM)) != ONEPOSE_OK) return rc;
     }
     {  // 5. MLP conv 1 on [x ; QZ] with [W1a | Mf] + InstanceNorm partials
       GemmArgs a;
@@ -962,12 +967,14 @@ int onepose_match(const void* packed_weights, const float* desc2d, int64_t desc2
       a.p[1].ldw1 = 256;
       a.p[1].w1_bs = 512 * 256;
       a.p[1].stats = p.stats3;
-      if ((rc = gemm_launch(EPI_STATS, PRO_PLAIN, 64, a, st, K_MLP1)) != ONEPOSE_OK) return rc;
+      if ((rc = gemm_launch(EPI_STATS, PRO_PLAIN, kTileMLP1, a, st, K_MLP1)) != ONEPOSE_OK) return rc;
     }
     {  // 6. InstanceNorm statistics
       StatsArgs sa;
-      sa.p[0] = {p.stats2, p.mean, p.rstd, n1, ch2};
-      sa.p[1] = {p.stats3, p.mean + (size_t)B * 512, p.rstd + (size_t)B * 512, n3, ch3};
+      const int str = gemm_tile_rows(kTileMLP1);
+      sa.p[0] = {p.stats2, p.mean, p.rstd, n1, ceil_div(n1, str), str};
+      sa.p[1] = {p.stats3, p.mean + (size_t)B * 512, p.rstd + (size_t)B * 512, n3,
+                 ceil_div(n3, str), str};
       OP_LAUNCH(K_STATS, st, stats_finalize_kernel, dim3(2 * B * 8), dim3(256), 0, st, sa, B);
     }
     {  // 7. MLP conv 2 on ReLU(InstanceNorm(.)) + residual: desc + delta
@@ -987,7 +994,7 @@ int onepose_match(const void* packed_weights, const float* desc2d, int64_t desc2
       a.p[1].pro_mean = p.mean + (size_t)B * 512;
       a.p[1].pro_rstd = p.rstd + (size_t)B * 512;
       a.p[1].pro_bs = 512;
-      if ((rc = gemm_launch(EPI_RESID, PRO_NORM_RELU, 64, a, st, K_MLP2)) != ONEPOSE_OK)
+      if ((rc = gemm_launch(EPI_RESID, PRO_NORM_RELU, kTileMLP2, a, st, K_MLP2)) != ONEPOSE_OK)
         return rc;
     }
     c2 ^= 1;
@@ -1001,7 +1008,7 @@ int onepose_match(const void* packed_weights, const float* desc2d, int64_t desc2
     a.nprob = 2;
     a.p[0] = gemm_prob(p.x2[c2], 256, fw, 256, fw + 65536, p.f2, 256, n1, 256, 256, B);
     a.p[1] = gemm_prob(p.x3[c3], 256, fw, 256, fw + 65536, p.f3, 256, n3, 256, 256, B);
-    if ((rc = gemm_launch(EPI_BIAS, PRO_PLAIN, 64, a, st, K_FINAL)) != ONEPOSE_OK) return rc;
+    if ((rc = gemm_launch(EPI_BIAS, PRO_PLAIN, kTileFinal, a, st, K_FINAL)) != ONEPOSE_OK) return rc;
     const int rows = B * (n1 + n3);
     OP_LAUNCH(K_L2NORM, st, l2norm_kernel, dim3(ceil_div(rows, 4)), dim3(256), 0, st, p.f2, B * n1,
                        p.f3, B * n3);
@@ -1014,7 +1021,7 @@ int onepose_match(const void* packed_weights, const float* desc2d, int64_t desc2
     a.p[0].scale = scale_factor;
     a.p[0].rowstat = p.rowpart;
     a.p[0].colstat = p.colpart;
-    if ((rc = gemm_launch(EPI_SCORE, PRO_PLAIN, 64, a, st, K_SCORE)) != ONEPOSE_OK) return rc;
+    if ((rc = gemm_launch(EPI_SCORE, PRO_PLAIN, TILE_64x64, a, st, K_SCORE)) != ONEPOSE_OK) return rc;
   }
   {
     const int64_t total = (int64_t)B * (n1 + n3);
