@@ -179,7 +179,9 @@ def main():
 
     step_events = []
 
-    def run_steps(k):
+    marks = []   # per step: events at matcher start / matcher done / pose done
+
+    def run_steps(k, record=False):
         if args.diag_steps and k == args.steps:
             out = None
             for _ in range(k):
@@ -189,7 +191,7 @@ def main():
                 step_events.append(ev)
             return out
         if overlap:
-            pipe.run_stream(k, graphs=stage_graphs)
+            pipe.run_stream(k, graphs=stage_graphs, marks=marks if record else None)
             return pipe.slots[(k - 1) % len(pipe.slots)]
         for _ in range(k):
             if step_graph is not None:
@@ -207,7 +209,7 @@ def main():
         pg.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    last = run_steps(args.steps)
+    last = run_steps(args.steps, record=True)
     host_enqueue = time.perf_counter() - t0   # host time to issue the K steps
     result = torch.cat([last.pose.reshape(B, 12), last.R_err[:, None], last.t_err[:, None],
                         last.cmd.double(), last.n_inliers[:, None].double(),
@@ -230,6 +232,14 @@ def main():
         pg.all_reduce(t, op=pg.ReduceOp.MAX)
         elapsed = float(t.item())
 
+    stage_ms = None
+    if marks:   # matcher / pose stage GPU times over the timed region (diagnostic)
+        mt = [a.elapsed_time(b) for a, b, _ in marks]
+        pt = [b.elapsed_time(c) for _, b, c in marks]
+        stage_ms = {"matcher_mean": round(float(np.mean(mt)), 4),
+                    "matcher_max": round(float(np.max(mt)), 4),
+                    "pose_mean": round(float(np.mean(pt)), 4),
+                    "pose_max": round(float(np.max(pt)), 4)}
     diag = []
     if step_events:
         diag.append([round(a.elapsed_time(b), 3) for a, b in zip(step_events, step_events[1:])])
@@ -271,6 +281,7 @@ def main():
                      "status_ok": float((res[:, 18] == 0).mean())},
             "roofline": roof,
             "host_enqueue_ms_per_step": round(host_enqueue / args.steps * 1e3, 4),
+            **({"stage_ms": stage_ms} if stage_ms else {}),
             "kernel_ms_per_step": {k: round(v, 4) for k, v in sorted(total.items(),
                                                                      key=lambda kv: -kv[1])},
             **({"diag_ms_per_step": diag} if diag else {}),

@@ -87,6 +87,27 @@ int onepose_match(const void* packed_weights,
                   float* mscores0, float* mscores1, float* conf,
                   void* workspace, size_t workspace_bytes, void* stream);
 
+/* Per-object leaf preparation.  The GAT layers read the leaves point-major
+ * ([n3][num_leaf][256]: one 3D point's leaves contiguous) -- onepose_match transposes its
+ * reference-layout input into the workspace on every call; a caller that keeps one object
+ * resident across frames (inference.py:89-90 uploads it per frame) can transpose once with
+ * onepose_prepare_leaves and call onepose_match_prepared.
+ *   leaves [batch, 256, n3*L] (bstride elements)  ->  out [batch, n3*L, 256]
+ * onepose_match_prepared takes the same arguments as onepose_match with the prepared leaves
+ * (prepared_bstride elements per sample, 0 = shared) and the same workspace size. */
+size_t onepose_leaves_prepared_bytes(int batch, int n3, int num_leaf);
+int onepose_prepare_leaves(const float* leaves, int64_t leaves_bstride, int batch, int n3,
+                           int num_leaf, float* out, void* stream);
+int onepose_match_prepared(const void* packed_weights,
+                           const float* desc2d, int64_t desc2d_bstride,
+                           const float* desc3d, int64_t desc3d_bstride,
+                           const float* leaves_prepared, int64_t prepared_bstride,
+                           int batch, int n1, int n3, int num_leaf,
+                           float scale_factor, float match_threshold,
+                           int64_t* matches0, int64_t* matches1,
+                           float* mscores0, float* mscores1, float* conf,
+                           void* workspace, size_t workspace_bytes, void* stream);
+
 /* ------------------------------------------------------------------------------------ *
  * SuperPoint descriptor sampling  --  replaces sample_descriptors
  *   (src/models/extractors/SuperPoint/superpoint.py:95-113)

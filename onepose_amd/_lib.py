@@ -31,6 +31,13 @@ PROTOTYPES = {
                               c_int, c_int, c_int, c_int, c_float, c_float,
                               c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                               c_void_p, c_size_t, c_void_p]),
+    "onepose_match_prepared": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_int64, c_void_p,
+                                       c_int64, c_int, c_int, c_int, c_int, c_float, c_float,
+                                       c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                       c_void_p, c_size_t, c_void_p]),
+    "onepose_leaves_prepared_bytes": (c_size_t, [c_int, c_int, c_int]),
+    "onepose_prepare_leaves": (c_int, [c_void_p, c_int64, c_int, c_int, c_int, c_void_p,
+                                       c_void_p]),
     "onepose_sample_descriptors": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int,
                                            c_int, c_int, c_void_p, c_void_p]),
     "onepose_select_correspondences": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_int64,

@@ -178,23 +178,53 @@ const std::vector<TensorSpec>& tensor_specs() {
 // kernels
 // ------------------------------------------------------------------------------------
 
-// [B][256][N] (batch stride `bs`, may be 0) -> [B][N][256]
-__global__ __launch_bounds__(256) void transpose_in_kernel(const float* __restrict__ src,
-                                                           int64_t bs, int n,
-                                                           float* __restrict__ dst) {
+// Reference layout [B][256][n] (channel-major, GATs_SuperGlue.py:211-217) -> token-major
+// [B][n][256], both inputs in one launch.  64 tokens x 64 channels per workgroup through a
+// padded LDS tile; 16-byte loads along tokens when n % 4 == 0, 16-byte stores along channels.
+struct TransProb {
+  const float* src;
+  int64_t bs;
+  int n, tiles;   // tokens, workgroups per sample (ceil(n/64) * 4)
+  float* dst;
+};
+struct TransArgs {
+  TransProb p[2];
+};
+__global__ __launch_bounds__(256) void transpose_in_kernel(TransArgs args, int batch) {
   __shared__ float tile[64][65];
-  const int n0 = blockIdx.x * 64, c0 = blockIdx.y * 64, b = blockIdx.z;
-  const float* s = src + b * bs;
-  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
-  for (int r = ty; r < 64; r += 4) {
-    const int nn = n0 + tx;
-    tile[r][tx] = (nn < n) ? s[(int64_t)(c0 + r) * n + nn] : 0.f;
+  int bid = blockIdx.x;
+  const bool second = bid >= args.p[0].tiles * batch;
+  const TransProb& P = second ? args.p[1] : args.p[0];
+  if (second) bid -= args.p[0].tiles * batch;
+  const int b = bid / P.tiles, r = bid - b * P.tiles;
+  const int n0 = (r >> 2) * 64, c0 = (r & 3) * 64, n = P.n;
+  const float* s = P.src + b * P.bs;
+  const int t = threadIdx.x;
+  if ((n & 3) == 0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {   // 64 channels x 16 float4 of tokens
+      const int e = t + 256 * i, ch = e >> 4, tq = (e & 15) * 4;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (n0 + tq < n) v = *reinterpret_cast<const float4*>(s + (int64_t)(c0 + ch) * n + n0 + tq);
+      tile[ch][tq] = v.x;
+      tile[ch][tq + 1] = v.y;
+      tile[ch][tq + 2] = v.z;
+      tile[ch][tq + 3] = v.w;
+    }
+  } else {
+    for (int i = 0; i < 16; ++i) {
+      const int ch = (t >> 6) + 4 * i, tk = t & 63;
+      tile[ch][tk] = (n0 + tk < n) ? s[(int64_t)(c0 + ch) * n + n0 + tk] : 0.f;
+    }
   }
   __syncthreads();
-  float* d = dst + (int64_t)b * n * kDim;
-  for (int r = ty; r < 64; r += 4) {
-    const int nn = n0 + r;
-    if (nn < n) d[(int64_t)nn * kDim + c0 + tx] = tile[tx][r];
+  float* d = P.dst + (int64_t)b * n * kDim;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {   // 64 tokens x 16 float4 of channels
+    const int e = t + 256 * i, tk = e >> 4, cq = (e & 15) * 4;
+    if (n0 + tk < n)
+      *reinterpret_cast<float4*>(d + (int64_t)(n0 + tk) * kDim + c0 + cq) =
+          make_float4(tile[cq][tk], tile[cq + 1][tk], tile[cq + 2][tk], tile[cq + 3][tk]);
   }
 }
 
@@ -321,22 +351,23 @@ __device__ __forceinline__ void chan_merge(double& n, double& mean, double& m2, 
   n = nn;
 }
 __global__ __launch_bounds__(256) void stats_finalize_kernel(StatsArgs args, int batch) {
-  __shared__ double red[3][4][64];
-  const int g = blockIdx.x & 7, b = (blockIdx.x >> 3) % batch, side = (blockIdx.x >> 3) / batch;
+  // workgroup = (side, sample, 16 channels); thread = (channel, tile group of every 16th tile)
+  __shared__ double red[3][16][17];
+  const int g = blockIdx.x & 31, b = (blockIdx.x >> 5) % batch, side = (blockIdx.x >> 5) / batch;
   const StatsProb& P = side ? args.p[1] : args.p[0];
-  const int t = threadIdx.x, tg = t >> 6, c = g * 64 + (t & 63);
+  const int t = threadIdx.x, tg = t >> 4, cl = t & 15, c = g * 16 + cl;
   const float* part = P.part + (int64_t)b * P.mtiles * 1024;
   double n = 0.0, mean = 0.0, m2 = 0.0;
-  for (int ti = tg; ti < P.mtiles; ti += 4) {
+  for (int ti = tg; ti < P.mtiles; ti += 16) {
     const double nb = (double)min(P.rows, P.m - ti * P.rows);
     chan_merge(n, mean, m2, nb, part[ti * 1024 + c], part[ti * 1024 + 512 + c]);
   }
-  red[0][tg][t & 63] = n;
-  red[1][tg][t & 63] = mean;
-  red[2][tg][t & 63] = m2;
+  red[0][tg][cl] = n;
+  red[1][tg][cl] = mean;
+  red[2][tg][cl] = m2;
   __syncthreads();
   if (tg == 0) {
-    for (int k = 1; k < 4; ++k) chan_merge(n, mean, m2, red[0][k][t], red[1][k][t], red[2][k][t]);
+    for (int k = 1; k < 16; ++k) chan_merge(n, mean, m2, red[0][k][cl], red[1][k][cl], red[2][k][cl]);
     P.mean[b * 512 + c] = (float)mean;
     P.rstd[b * 512 + c] = (float)(1.0 / sqrt(m2 / n + 1e-5));
   }
@@ -346,93 +377,67 @@ __global__ __launch_bounds__(256) void stats_finalize_kernel(StatsArgs args, int
 // additional=False, concat=True, W a folded (h.(W a) == (h W) a):
 //   s3 = h3.wa_hi, s2_j = leaf_j.wa_lo, e = LeakyReLU_0.2(s3 + [s3, s2_1..L])
 //   alpha = softmax(e), out = ELU(alpha_0 h3 + sum_j alpha_j leaf_j)
-// P = 64/L 3D points per workgroup; the workgroup's P*L leaf columns are staged in LDS once
-// (16-byte loads) and read twice (logits, weighted sum) -- leaves cross HBM once per layer.
+// One wave per 3D point over point-major leaves [n3][L][256]: each leaf row is one 1 KB
+// coalesced load (a float4 per lane), the L+1 logits are wave reductions, softmax and ELU run
+// in registers -- no LDS, every leaf byte crosses HBM once per layer.
+template <int MAXL>
 __global__ __launch_bounds__(256) void gat_kernel(const float* __restrict__ x3,
-                                                  const float* __restrict__ leaves,
+                                                  const float* __restrict__ leaves_pm,
                                                   int64_t leaves_bs, const float* __restrict__ wa,
                                                   float* __restrict__ y3, int n3, int L,
-                                                  int P) {
-  extern __shared__ float smem[];
-  const int cols = P * L;
-  const int pitch = cols + 1;
-  float* lt = smem;                      // [256][pitch]
-  float* h3 = lt + 256 * pitch;          // [8][256]
-  float* logit = h3 + P * 256;           // [P][1+L]
-  const int b = blockIdx.y, p0 = blockIdx.x * P;
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  const int64_t ncol = (int64_t)n3 * L;
-  const float* lv = leaves + b * leaves_bs + (int64_t)p0 * L;
-  if ((ncol & 3) == 0 && (cols & 3) == 0 && (int64_t)(p0 + P) * L <= ncol) {
-    const int c4s = cols >> 2;   // 16-byte loads; rows are 16-byte aligned
-    for (int e = t; e < 256 * c4s; e += 256) {
-      const int c = e / c4s, j4 = e - c * c4s;
-      const float4 v = *reinterpret_cast<const float4*>(lv + (int64_t)c * ncol + j4 * 4);
-      float* d = lt + c * pitch + j4 * 4;
-      d[0] = v.x;
-      d[1] = v.y;
-      d[2] = v.z;
-      d[3] = v.w;
-    }
-  } else {
-    for (int e = t; e < 256 * cols; e += 256) {
-      const int c = e / cols, j = e - c * cols;
-      lt[c * pitch + j] = ((int64_t)p0 * L + j < ncol) ? lv[(int64_t)c * ncol + j] : 0.f;
-    }
-  }
-  const float* xb = x3 + (int64_t)b * n3 * kDim;
-  for (int e = t; e < P * 256; e += 256) {
-    const int p = e >> 8, c = e & 255;
-    h3[e] = (p0 + p < n3) ? xb[(int64_t)(p0 + p) * kDim + c] : 0.f;
-  }
-  __syncthreads();
-  const float* wa_lo = wa;
-  const float* wa_hi = wa + 256;
-  // logits: dots 0..cols-1 are leaves, cols..cols+7 are the 3D points
-  for (int k = wave; k < cols + P; k += 4) {
-    float s = 0.f;
-    if (k < cols) {
+                                                  int batch) {
+  const int gw = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int b = gw / n3, p = gw - b * n3;
+  if (b >= batch) return;
+  const int lane = threadIdx.x & 63;
+  const float4 wl = reinterpret_cast<const float4*>(wa)[lane];
+  const float4 wh = reinterpret_cast<const float4*>(wa + 256)[lane];
+  const float4 h = reinterpret_cast<const float4*>(x3 + ((int64_t)b * n3 + p) * kDim)[lane];
+  const float* lp = leaves_pm + b * leaves_bs + (int64_t)p * L * kDim;
+  float4 lf[MAXL];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) s += lt[(lane + 64 * i) * pitch + k] * wa_lo[lane + 64 * i];
-    } else {
+  for (int j = 0; j < MAXL; ++j)
+    if (j < L) lf[j] = reinterpret_cast<const float4*>(lp + j * kDim)[lane];
+  float d[MAXL + 1];
+  d[0] = h.x * wh.x + h.y * wh.y + h.z * wh.z + h.w * wh.w;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) s += h3[(k - cols) * 256 + lane + 64 * i] * wa_hi[lane + 64 * i];
-    }
-    s = wave_sum(s);
-    if (lane == 0) {
-      if (k < cols) logit[(k / L) * (1 + L) + 1 + (k % L)] = s;
-      else logit[(k - cols) * (1 + L)] = s;
-    }
+  for (int j = 0; j < MAXL; ++j)
+    d[j + 1] = (j < L) ? lf[j].x * wl.x + lf[j].y * wl.y + lf[j].z * wl.z + lf[j].w * wl.w : 0.f;
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1)
+#pragma unroll
+    for (int j = 0; j <= MAXL; ++j) d[j] += __shfl_xor(d[j], o, 64);
+  const float s3 = d[0];
+  float e[MAXL + 1];
+  float mx = -INFINITY;
+#pragma unroll
+  for (int j = 0; j <= MAXL; ++j) {
+    if (j > L) break;
+    float v = s3 + (j == 0 ? s3 : d[j]);
+    v = v > 0.f ? v : v * 0.2f;
+    e[j] = v;
+    mx = fmaxf(mx, v);
   }
-  __syncthreads();
-  if (t < P) {
-    float* e = logit + t * (1 + L);
-    const float s3 = e[0];
-    float mx = -INFINITY;
-    for (int j = 0; j <= L; ++j) {
-      float v = s3 + (j == 0 ? s3 : e[j]);
-      v = v > 0.f ? v : v * 0.2f;
-      e[j] = v;
-      mx = fmaxf(mx, v);
-    }
-    float sum = 0.f;
-    for (int j = 0; j <= L; ++j) {
-      const float v = expf(e[j] - mx);
-      e[j] = v;
-      sum += v;
-    }
-    for (int j = 0; j <= L; ++j) e[j] = e[j] / sum;
+  float sum = 0.f;
+#pragma unroll
+  for (int j = 0; j <= MAXL; ++j) {
+    if (j > L) break;
+    e[j] = expf(e[j] - mx);
+    sum += e[j];
   }
-  __syncthreads();
-  float* yb = y3 + (int64_t)b * n3 * kDim;
-  const int c = t;
-  for (int p = 0; p < P; ++p) {
-    if (p0 + p >= n3) break;
-    const float* al = logit + p * (1 + L);
-    float acc = al[0] * h3[p * 256 + c];
-    for (int j = 0; j < L; ++j) acc += al[1 + j] * lt[c * pitch + p * L + j];
-    yb[(int64_t)(p0 + p) * kDim + c] = elu1(acc);
+  const float a0 = e[0] / sum;
+  float4 acc = make_float4(a0 * h.x, a0 * h.y, a0 * h.z, a0 * h.w);
+#pragma unroll
+  for (int j = 0; j < MAXL; ++j) {
+    if (j >= L) break;
+    const float a = e[j + 1] / sum;
+    acc.x += a * lf[j].x;
+    acc.y += a * lf[j].y;
+    acc.z += a * lf[j].z;
+    acc.w += a * lf[j].w;
   }
+  reinterpret_cast<float4*>(y3 + ((int64_t)b * n3 + p) * kDim)[lane] =
+      make_float4(elu1(acc.x), elu1(acc.y), elu1(acc.z), elu1(acc.w));
 }
 
 // F.normalize(x, p=2, dim=channels), one wave per token row (GATs_SuperGlue.py:245-246).
@@ -454,32 +459,42 @@ __global__ __launch_bounds__(256) void l2norm_kernel(float* x2, int rows2, float
 }
 
 // Combine the score GEMM's per-tile softmax partials: rows over N3 tiles (softmax dim 2),
-// columns over N1 tiles (softmax dim 1).  Also resets the packed argmax words.
+// columns over N1 tiles (softmax dim 1); one wave per row / column, partials across lanes.
+// Also resets the packed argmax words.
 __global__ __launch_bounds__(256) void softmax_reduce_kernel(
     const float* rowpart, int ntiles3, const float* colpart, int mtiles1, int batch, int n1,
     int n3, float* rowmax, float* rowsum, float* colmax, float* colsum,
     unsigned long long* rowbest, unsigned long long* colbest) {
-  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t idx = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
   const int64_t nr = (int64_t)batch * n1, nc = (int64_t)batch * n3;
+  const float* p;
+  int nt;
   if (idx < nr) {
-    const float* p = rowpart + idx * ntiles3 * 2;
-    float mx = -INFINITY;
-    for (int i = 0; i < ntiles3; ++i) mx = fmaxf(mx, p[2 * i]);
-    float s = 0.f;
-    for (int i = 0; i < ntiles3; ++i) s += p[2 * i + 1] * expf(p[2 * i] - mx);
-    rowmax[idx] = mx;
-    rowsum[idx] = s;
-    rowbest[idx] = 0ull;
+    p = rowpart + idx * ntiles3 * 2;
+    nt = ntiles3;
   } else if (idx < nr + nc) {
-    const int64_t j = idx - nr;
-    const float* p = colpart + j * mtiles1 * 2;
-    float mx = -INFINITY;
-    for (int i = 0; i < mtiles1; ++i) mx = fmaxf(mx, p[2 * i]);
-    float s = 0.f;
-    for (int i = 0; i < mtiles1; ++i) s += p[2 * i + 1] * expf(p[2 * i] - mx);
-    colmax[j] = mx;
-    colsum[j] = s;
-    colbest[j] = 0ull;
+    p = colpart + (idx - nr) * mtiles1 * 2;
+    nt = mtiles1;
+  } else {
+    return;
+  }
+  float mx = -INFINITY;
+  for (int i = lane; i < nt; i += 64) mx = fmaxf(mx, p[2 * i]);
+  mx = wave_max(mx);
+  float s = 0.f;
+  for (int i = lane; i < nt; i += 64) s += p[2 * i + 1] * expf(p[2 * i] - mx);
+  s = wave_sum(s);
+  if (lane == 0) {
+    if (idx < nr) {
+      rowmax[idx] = mx;
+      rowsum[idx] = s;
+      rowbest[idx] = 0ull;
+    } else {
+      colmax[idx - nr] = mx;
+      colsum[idx - nr] = s;
+      colbest[idx - nr] = 0ull;
+    }
   }
 }
 
@@ -501,40 +516,77 @@ __device__ __forceinline__ unsigned long long shfl_xor_u64(unsigned long long v,
 }
 
 // conf = softmax(S, dim=1) * softmax(S, dim=2) (GATs_SuperGlue.py:253) in place over S,
-// plus row/column max+argmax (:256) folded in through 64-bit atomicMax.
+// plus row/column max+argmax (:256) folded in through 64-bit atomicMax.  Workgroup = 32 rows
+// (2D) x 256 columns (3D); wave w owns rows 8w..8w+7, lane l owns 4 columns (16-byte loads
+// when n3 % 4 == 0), all loads issued before any use.  Row winners: in-wave reduction, one
+// atomic per row per workgroup; column winners: per thread over its rows, then over the four
+// waves in LDS, one atomic per column per workgroup.
+template <bool VEC>
 __global__ __launch_bounds__(256) void conf_kernel(float* S, int n1, int n3,
                                                    const float* rowmax, const float* rowsum,
                                                    const float* colmax, const float* colsum,
                                                    unsigned long long* rowbest,
                                                    unsigned long long* colbest, int write_conf) {
-  __shared__ unsigned long long cb[4][64];
-  const int nt3 = (n3 + 63) / 64;
-  const int tilen = blockIdx.x % nt3, tilem = blockIdx.x / nt3;
+  __shared__ unsigned long long cb[4][256];
+  const int ct = (n3 + 255) / 256;
+  const int tilec = blockIdx.x % ct, tiler = blockIdx.x / ct;
   const int b = blockIdx.y;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int m = tilen * 64 + lane;           // 3D column
-  const bool col_ok = m < n3;
   float* Sb = S + (int64_t)b * n1 * n3;
-  float cmx = 0.f, cinv = 0.f;
-  if (col_ok) {
-    cmx = colmax[(int64_t)b * n3 + m];
-    cinv = 1.0f / colsum[(int64_t)b * n3 + m];
+  int col[4];
+  bool cok[4];
+  float cmx[4], cinv[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    col[j] = tilec * 256 + (VEC ? lane * 4 + j : lane + 64 * j);
+    cok[j] = col[j] < n3;
+    cmx[j] = cok[j] ? colmax[(int64_t)b * n3 + col[j]] : 0.f;
+    cinv[j] = cok[j] ? 1.0f / colsum[(int64_t)b * n3 + col[j]] : 0.f;
   }
-  unsigned long long cbest = 0ull;
-  for (int i = 0; i < 16; ++i) {
-    const int n = tilem * 64 + wave + 4 * i;  // 2D row
-    if (n >= n1) break;
+  float v[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int n = min(tiler * 32 + wave * 8 + i, n1 - 1);
+    const float* ps = Sb + (int64_t)n * n3;
+    if (VEC && cok[0]) {
+      const float4 q = *reinterpret_cast<const float4*>(ps + col[0]);
+      v[i][0] = q.x;
+      v[i][1] = q.y;
+      v[i][2] = q.z;
+      v[i][3] = q.w;
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[i][j] = cok[j] ? ps[col[j]] : 0.f;
+    }
+  }
+  unsigned long long cbest[4] = {0ull, 0ull, 0ull, 0ull};
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int n = tiler * 32 + wave * 8 + i;
+    if (n >= n1) break;   // wave-uniform
     const float rmx = rowmax[(int64_t)b * n1 + n];
     const float rinv = 1.0f / rowsum[(int64_t)b * n1 + n];
     unsigned long long key = 0ull;
-    if (col_ok) {
-      float* ps = Sb + (int64_t)n * n3 + m;
-      const float s = *ps;
-      const float c = (expf(s - cmx) * cinv) * (expf(s - rmx) * rinv);
-      if (write_conf) *ps = c;
-      key = pack_best(c, m);
-      const unsigned long long ck = pack_best(c, n);
-      cbest = ck > cbest ? ck : cbest;
+    float c[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      c[j] = (expf(v[i][j] - cmx[j]) * cinv[j]) * (expf(v[i][j] - rmx) * rinv);
+      if (cok[j]) {
+        const unsigned long long rk = pack_best(c[j], col[j]);
+        key = rk > key ? rk : key;
+        const unsigned long long ck = pack_best(c[j], n);
+        cbest[j] = ck > cbest[j] ? ck : cbest[j];
+      }
+    }
+    if (write_conf) {
+      float* ps = Sb + (int64_t)n * n3;
+      if (VEC && cok[0]) {
+        *reinterpret_cast<float4*>(ps + col[0]) = make_float4(c[0], c[1], c[2], c[3]);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (cok[j]) ps[col[j]] = c[j];
+      }
     }
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) {
@@ -543,12 +595,16 @@ __global__ __launch_bounds__(256) void conf_kernel(float* S, int n1, int n3,
     }
     if (lane == 0 && key != 0ull) atomicMax(rowbest + (int64_t)b * n1 + n, key);
   }
-  cb[wave][lane] = cbest;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) cb[wave][VEC ? lane * 4 + j : lane + 64 * j] = cbest[j];
   __syncthreads();
-  if (wave == 0 && col_ok) {
-    unsigned long long k = cb[0][lane];
-    for (int w = 1; w < 4; ++w) k = cb[w][lane] > k ? cb[w][lane] : k;
-    if (k != 0ull) atomicMax(colbest + (int64_t)b * n3 + m, k);
+  {
+    const int cc = threadIdx.x, cg = tilec * 256 + cc;
+    if (cg < n3) {
+      unsigned long long k = cb[0][cc];
+      for (int w = 1; w < 4; ++w) k = cb[w][cc] > k ? cb[w][cc] : k;
+      if (k != 0ull) atomicMax(colbest + (int64_t)b * n3 + cg, k);
+    }
   }
 }
 
@@ -597,10 +653,11 @@ struct Plan {
   float *f2, *f3, *s;
   float *rowpart, *colpart, *rowmax, *rowsum, *colmax, *colsum;
   unsigned long long *rowbest, *colbest;
+  float* leaves_pm;   // point-major copy of the leaves (onepose_match only)
   size_t bytes;
 };
 
-Plan make_plan(void* ws, int B, int n1, int n3, bool with_conf) {
+Plan make_plan(void* ws, int B, int n1, int n3, int L, bool with_conf) {
   Carve c(ws);
   Plan p;
   const size_t t2 = (size_t)B * n1, t3 = (size_t)B * n3;
@@ -636,6 +693,7 @@ Plan make_plan(void* ws, int B, int n1, int n3, bool with_conf) {
   p.colsum = c.take<float>(t3);
   p.rowbest = c.take<unsigned long long>(t2);
   p.colbest = c.take<unsigned long long>(t3);
+  p.leaves_pm = c.take<float>(t3 * L * 256);
   p.bytes = align_up(c.off, 256);
   return p;
 }
@@ -827,75 +885,54 @@ int onepose_matcher_pack(const float* const* tensors, int n_tensors, void* packe
 }
 
 size_t onepose_match_workspace_bytes(int batch, int n1, int n3, int num_leaf, int with_conf) {
-  (void)num_leaf;
+  clear_error();
   if (batch <= 0 || n1 <= 0 || n3 <= 0) return 0;
-  return make_plan(nullptr, batch, n1, n3, with_conf != 0).bytes;
+  OP_REQUIRE(num_leaf >= 1 && num_leaf <= 16, "workspace: num_leaf=%d", num_leaf);
+  return make_plan(nullptr, batch, n1, n3, num_leaf, with_conf != 0).bytes;
 }
+
+}  // extern "C"
+
+extern "C" {
 
 }  // extern "C"
 
 namespace onepose {
 namespace {
-int init_kernel_attributes() {
-  static int rc = -1;
-  if (rc == -1) {
-    rc = ONEPOSE_OK;
-    if (hipFuncSetAttribute(reinterpret_cast<const void*>(gat_kernel),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
-      rc = ONEPOSE_ERR_HIP;
-  }
-  return rc;
-}
-}  // namespace
-}  // namespace onepose
 
-extern "C" {
-
-int onepose_match(const void* packed_weights, const float* desc2d, int64_t desc2d_bstride,
-                  const float* desc3d, int64_t desc3d_bstride, const float* leaves,
-                  int64_t leaves_bstride, int batch, int n1, int n3, int num_leaf,
-                  float scale_factor, float match_threshold, int64_t* matches0,
-                  int64_t* matches1, float* mscores0, float* mscores1, float* conf,
-                  void* workspace, size_t workspace_bytes, void* stream_) {
-  clear_error();
-  OP_REQUIRE(packed_weights && desc2d && desc3d && leaves, "match: null input");
-  OP_REQUIRE(matches0 && matches1 && mscores0 && mscores1, "match: null output");
-  OP_REQUIRE(batch >= 1 && n1 >= 1 && n3 >= 1, "match: batch=%d n1=%d n3=%d", batch, n1, n3);
-  OP_REQUIRE(num_leaf >= 1 && num_leaf <= 16, "match: num_leaf=%d not in [1,16]", num_leaf);
-  OP_REQUIRE(scale_factor != 0.f, "match: scale_factor 0");
+// The matcher forward on point-major leaves [*, n3*L, 256] (leaves_pm_bs elements per sample).
+int match_impl(const void* packed_weights, const float* desc2d, int64_t desc2d_bstride,
+               const float* desc3d, int64_t desc3d_bstride, const float* leaves_pm,
+               int64_t leaves_pm_bs, int batch, int n1, int n3, int num_leaf, float scale_factor,
+               float match_threshold, int64_t* matches0, int64_t* matches1, float* mscores0,
+               float* mscores1, float* conf, const Plan& p, hipStream_t st) {
   const bool with_conf = conf != nullptr;
-  const Plan need = make_plan(nullptr, batch, n1, n3, with_conf);
-  OP_REQUIRE(workspace != nullptr, "match: null workspace");
-  if (workspace_bytes < need.bytes) {
-    set_error("match: workspace %zu < %zu bytes", workspace_bytes, need.bytes);
-    return ONEPOSE_ERR_WORKSPACE;
-  }
-  hipStream_t st = static_cast<hipStream_t>(stream_);
-  if (init_kernel_attributes() != ONEPOSE_OK) {
-    set_error("match: hipFuncSetAttribute failed");
-    return ONEPOSE_ERR_HIP;
-  }
-  Plan p = make_plan(workspace, batch, n1, n3, with_conf);
   const float* wbase = static_cast<const float*>(packed_weights);
   const int B = batch;
   float* S = with_conf ? conf : p.s;
+  const float* leaves = leaves_pm;
+  const int64_t leaves_bstride = leaves_pm_bs;
 
-  OP_LAUNCH(K_TRANSPOSE, st, transpose_in_kernel, dim3(ceil_div(n1, 64), 4, B), dim3(256), 0, st,
-                     desc2d, desc2d_bstride, n1, p.x2[0]);
-  OP_LAUNCH(K_TRANSPOSE, st, transpose_in_kernel, dim3(ceil_div(n3, 64), 4, B), dim3(256), 0, st,
-                     desc3d, desc3d_bstride, n3, p.x3[0]);
+  {
+    TransArgs ta;
+    ta.p[0] = {desc2d, desc2d_bstride, n1, ceil_div(n1, 64) * 4, p.x2[0]};
+    ta.p[1] = {desc3d, desc3d_bstride, n3, ceil_div(n3, 64) * 4, p.x3[0]};
+    OP_LAUNCH(K_TRANSPOSE, st, transpose_in_kernel, dim3((ta.p[0].tiles + ta.p[1].tiles) * B),
+              dim3(256), 0, st, ta, B);
+  }
 
   int c2 = 0, c3 = 0, ap = 0, gat = 0;
   const int ch2 = ceil_div(n1, 64), ch3 = ceil_div(n3, 64);
-  const int gat_p = max(1, 64 / num_leaf);
-  const size_t gat_lds =
-      (size_t)(256 * (gat_p * num_leaf + 1) + gat_p * 256 + gat_p * (1 + num_leaf)) * 4;
   for (int layer = 0; layer < kLayers; ++layer) {
     const int kind = layer % 3;  // 0 GATs, 1 self, 2 cross
     if (kind == 0) {
-      OP_LAUNCH(K_GAT, st, gat_kernel, dim3(ceil_div(n3, gat_p), B), dim3(256), gat_lds, st,
-                         p.x3[c3], leaves, leaves_bstride, gat_weights(wbase, gat), p.x3[c3 ^ 1],
-                         n3, num_leaf, gat_p);
+      const dim3 ggrid(ceil_div(B * n3, 4));
+      if (num_leaf <= 8)
+        OP_LAUNCH(K_GAT, st, gat_kernel<8>, ggrid, dim3(256), 0, st, p.x3[c3], leaves,
+                  leaves_bstride, gat_weights(wbase, gat), p.x3[c3 ^ 1], n3, num_leaf, B);
+      else
+        OP_LAUNCH(K_GAT, st, gat_kernel<16>, ggrid, dim3(256), 0, st, p.x3[c3], leaves,
+                  leaves_bstride, gat_weights(wbase, gat), p.x3[c3 ^ 1], n3, num_leaf, B);
       c3 ^= 1;
       ++gat;
       continue;
@@ -975,7 +1012,7 @@ int onepose_match(const void* packed_weights, const float* desc2d, int64_t desc2
       sa.p[0] = {p.stats2, p.mean, p.rstd, n1, ceil_div(n1, str), str};
       sa.p[1] = {p.stats3, p.mean + (size_t)B * 512, p.rstd + (size_t)B * 512, n3,
                  ceil_div(n3, str), str};
-      OP_LAUNCH(K_STATS, st, stats_finalize_kernel, dim3(2 * B * 8), dim3(256), 0, st, sa, B);
+      OP_LAUNCH(K_STATS, st, stats_finalize_kernel, dim3(2 * B * 32), dim3(256), 0, st, sa, B);
     }
     {  // 7. MLP conv 2 on ReLU(InstanceNorm(.)) + residual: desc + delta
       GemmArgs a;
@@ -1025,16 +1062,112 @@ int onepose_match(const void* packed_weights, const float* desc2d, int64_t desc2
   }
   {
     const int64_t total = (int64_t)B * (n1 + n3);
-    OP_LAUNCH(K_SMX_REDUCE, st, softmax_reduce_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256),
+    OP_LAUNCH(K_SMX_REDUCE, st, softmax_reduce_kernel, dim3((unsigned)((total + 3) / 4)), dim3(256),
                        0, st, p.rowpart, ch3, p.colpart, ch2, B, n1, n3, p.rowmax, p.rowsum,
                        p.colmax, p.colsum, p.rowbest, p.colbest);
-    OP_LAUNCH(K_CONF, st, conf_kernel, dim3(ch2 * ch3, B), dim3(256), 0, st, S, n1, n3, p.rowmax,
-                       p.rowsum, p.colmax, p.colsum, p.rowbest, p.colbest, with_conf ? 1 : 0);
+    const dim3 cgrid(ceil_div(n1, 32) * ceil_div(n3, 256), B);
+    if (n3 % 4 == 0)
+      OP_LAUNCH(K_CONF, st, conf_kernel<true>, cgrid, dim3(256), 0, st, S, n1, n3, p.rowmax,
+                p.rowsum, p.colmax, p.colsum, p.rowbest, p.colbest, with_conf ? 1 : 0);
+    else
+      OP_LAUNCH(K_CONF, st, conf_kernel<false>, cgrid, dim3(256), 0, st, S, n1, n3, p.rowmax,
+                p.rowsum, p.colmax, p.colsum, p.rowbest, p.colbest, with_conf ? 1 : 0);
     OP_LAUNCH(K_MUTUAL, st, mutual_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st,
                        p.rowbest, p.colbest, B, n1, n3, match_threshold, matches0, matches1,
                        mscores0, mscores1);
   }
   return ONEPOSE_OK;
+}
+
+int check_match_args(const void* packed_weights, const float* desc2d, const float* desc3d,
+                     const float* leaves, int batch, int n1, int n3, int num_leaf,
+                     float scale_factor, const int64_t* matches0, const int64_t* matches1,
+                     const float* mscores0, const float* mscores1, const void* workspace) {
+  OP_REQUIRE(packed_weights && desc2d && desc3d && leaves, "match: null input");
+  OP_REQUIRE(matches0 && matches1 && mscores0 && mscores1, "match: null output");
+  OP_REQUIRE(batch >= 1 && n1 >= 1 && n3 >= 1, "match: batch=%d n1=%d n3=%d", batch, n1, n3);
+  OP_REQUIRE(num_leaf >= 1 && num_leaf <= 16, "match: num_leaf=%d not in [1,16]", num_leaf);
+  OP_REQUIRE(scale_factor != 0.f, "match: scale_factor 0");
+  OP_REQUIRE(workspace != nullptr, "match: null workspace");
+  return ONEPOSE_OK;
+}
+
+}  // namespace
+}  // namespace onepose
+
+extern "C" {
+
+size_t onepose_leaves_prepared_bytes(int batch, int n3, int num_leaf) {
+  if (batch <= 0 || n3 <= 0 || num_leaf <= 0) return 0;
+  return (size_t)batch * n3 * num_leaf * 256 * sizeof(float);
+}
+
+int onepose_prepare_leaves(const float* leaves, int64_t leaves_bstride, int batch, int n3,
+                           int num_leaf, float* out, void* stream_) {
+  clear_error();
+  OP_REQUIRE(leaves && out, "prepare_leaves: null pointer");
+  OP_REQUIRE(batch >= 1 && n3 >= 1 && num_leaf >= 1 && num_leaf <= 16,
+             "prepare_leaves: batch=%d n3=%d num_leaf=%d", batch, n3, num_leaf);
+  hipStream_t st = static_cast<hipStream_t>(stream_);
+  const int ncol = n3 * num_leaf;
+  TransArgs ta;
+  ta.p[0] = {leaves, leaves_bstride, ncol, ceil_div(ncol, 64) * 4, out};
+  ta.p[1] = {leaves, 0, 1, 0, out};
+  OP_LAUNCH(K_TRANSPOSE, st, transpose_in_kernel, dim3(ta.p[0].tiles * batch), dim3(256), 0, st,
+            ta, batch);
+  return ONEPOSE_OK;
+}
+
+int onepose_match(const void* packed_weights, const float* desc2d, int64_t desc2d_bstride,
+                  const float* desc3d, int64_t desc3d_bstride, const float* leaves,
+                  int64_t leaves_bstride, int batch, int n1, int n3, int num_leaf,
+                  float scale_factor, float match_threshold, int64_t* matches0,
+                  int64_t* matches1, float* mscores0, float* mscores1, float* conf,
+                  void* workspace, size_t workspace_bytes, void* stream_) {
+  clear_error();
+  int rc = check_match_args(packed_weights, desc2d, desc3d, leaves, batch, n1, n3, num_leaf,
+                            scale_factor, matches0, matches1, mscores0, mscores1, workspace);
+  if (rc != ONEPOSE_OK) return rc;
+  const Plan need = make_plan(nullptr, batch, n1, n3, num_leaf, conf != nullptr);
+  if (workspace_bytes < need.bytes) {
+    set_error("match: workspace %zu < %zu bytes", workspace_bytes, need.bytes);
+    return ONEPOSE_ERR_WORKSPACE;
+  }
+  hipStream_t st = static_cast<hipStream_t>(stream_);
+  const Plan p = make_plan(workspace, batch, n1, n3, num_leaf, conf != nullptr);
+  // reference layout [*, 256, n3*L] -> point-major copy in the workspace
+  const int lb = leaves_bstride == 0 ? 1 : batch;
+  if ((rc = onepose_prepare_leaves(leaves, leaves_bstride, lb, n3, num_leaf, p.leaves_pm,
+                                   stream_)) != ONEPOSE_OK)
+    return rc;
+  const int64_t pm_bs = leaves_bstride == 0 ? 0 : (int64_t)n3 * num_leaf * 256;
+  return match_impl(packed_weights, desc2d, desc2d_bstride, desc3d, desc3d_bstride, p.leaves_pm,
+                    pm_bs, batch, n1, n3, num_leaf, scale_factor, match_threshold, matches0,
+                    matches1, mscores0, mscores1, conf, p, st);
+}
+
+int onepose_match_prepared(const void* packed_weights, const float* desc2d,
+                           int64_t desc2d_bstride, const float* desc3d, int64_t desc3d_bstride,
+                           const float* leaves_prepared, int64_t prepared_bstride, int batch,
+                           int n1, int n3, int num_leaf, float scale_factor,
+                           float match_threshold, int64_t* matches0, int64_t* matches1,
+                           float* mscores0, float* mscores1, float* conf, void* workspace,
+                           size_t workspace_bytes, void* stream_) {
+  clear_error();
+  int rc = check_match_args(packed_weights, desc2d, desc3d, leaves_prepared, batch, n1, n3,
+                            num_leaf, scale_factor, matches0, matches1, mscores0, mscores1,
+                            workspace);
+  if (rc != ONEPOSE_OK) return rc;
+  const Plan need = make_plan(nullptr, batch, n1, n3, num_leaf, conf != nullptr);
+  if (workspace_bytes < need.bytes) {
+    set_error("match: workspace %zu < %zu bytes", workspace_bytes, need.bytes);
+    return ONEPOSE_ERR_WORKSPACE;
+  }
+  const Plan p = make_plan(workspace, batch, n1, n3, num_leaf, conf != nullptr);
+  return match_impl(packed_weights, desc2d, desc2d_bstride, desc3d, desc3d_bstride,
+                    leaves_prepared, prepared_bstride, batch, n1, n3, num_leaf, scale_factor,
+                    match_threshold, matches0, matches1, mscores0, mscores1, conf, p,
+                    static_cast<hipStream_t>(stream_));
 }
 
 }  // extern "C"

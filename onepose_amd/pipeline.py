@@ -67,6 +67,11 @@ class FramePipeline:
         self.leaves = torch.as_tensor(np.asarray(leaves), **f32).reshape(256, -1).contiguous()
         self.L = self.leaves.shape[1] // self.n3
         assert self.L * self.n3 == self.leaves.shape[1] and self.kp3.shape[0] == self.n3
+        # the object's leaves, transposed once to the point-major layout the GAT layers read
+        self.leaves_pm = torch.empty(self.n3 * self.L * 256, **f32)
+        _lib.check(self.lib.onepose_prepare_leaves(
+            self.leaves.data_ptr(), 0, 1, self.n3, self.L, self.leaves_pm.data_ptr(),
+            _lib.stream_ptr(dev)), "prepare_leaves")
         B = self.B
         # per-frame inputs (filled by the caller)
         self.desc2d = torch.zeros(B, 256, n1, **f32)
@@ -94,13 +99,13 @@ class FramePipeline:
     def enqueue_match(self, slot: int = 0):
         o = self.slots[slot]
         s = _lib.stream_ptr(self.device)
-        _lib.check(self.lib.onepose_match(
+        _lib.check(self.lib.onepose_match_prepared(
             self.weights.data_ptr(), self.desc2d.data_ptr(), 256 * self.n1,
-            self.desc3d.data_ptr(), 0, self.leaves.data_ptr(), 0,
+            self.desc3d.data_ptr(), 0, self.leaves_pm.data_ptr(), 0,
             self.B, self.n1, self.n3, self.L, self.scale_factor, self.threshold,
             o.matches0.data_ptr(), o.matches1.data_ptr(), o.mscores0.data_ptr(),
             o.mscores1.data_ptr(), _lib.ptr(o.conf), o.ws_match.data_ptr(),
-            o.ws_match_bytes, s), "onepose_match")
+            o.ws_match_bytes, s), "onepose_match_prepared")
 
     def enqueue_pose(self, slot: int = 0):
         o = self.slots[slot]
@@ -148,10 +153,12 @@ class FramePipeline:
             out.append((gm, gp))
         return out
 
-    def run_stream(self, steps: int, match_stream=None, pose_stream=None, graphs=None):
+    def run_stream(self, steps: int, match_stream=None, pose_stream=None, graphs=None,
+                   marks=None):
         """Enqueue `steps` frames (batches) with matcher(k+1) overlapping pose(k); with
         `graphs` (from ``capture_stages``) each stage is one graph replay.  The match stream
-        waits for the pose stream at the end; the caller synchronises."""
+        waits for the pose stream at the end; the caller synchronises.  `marks` (a list)
+        receives per step (start, matcher done, pose done) timing events."""
         ms = match_stream or torch.cuda.current_stream(self.device)
         ps = pose_stream or getattr(self, "_pose_stream", None)
         if ps is None:
@@ -162,14 +169,20 @@ class FramePipeline:
         used = [False] * n
         for k in range(steps):
             sl = k % n
+            mk = [torch.cuda.Event(enable_timing=True) for _ in range(3)] if marks is not None \
+                else None
             with torch.cuda.stream(ms):
                 if used[sl]:                      # slot's previous pose stage has read it
                     ms.wait_event(posed[sl])
+                if mk:
+                    mk[0].record(ms)
                 if graphs:
                     graphs[sl][0].replay()
                 else:
                     self.enqueue_match(sl)
                 matched[sl].record(ms)
+                if mk:
+                    mk[1].record(ms)
             with torch.cuda.stream(ps):
                 ps.wait_event(matched[sl])
                 if graphs:
@@ -177,6 +190,10 @@ class FramePipeline:
                 else:
                     self.enqueue_pose(sl)
                 posed[sl].record(ps)
+                if mk:
+                    mk[2].record(ps)
             used[sl] = True
+            if mk:
+                marks.append(mk)
         ms.wait_stream(ps)
         return ps

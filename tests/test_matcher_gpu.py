@@ -111,3 +111,43 @@ def test_matcher_full_size_properties(device):
     # argmax consistency with the returned conf
     valid = m0 > -1
     np.testing.assert_array_equal(conf[0].argmax(axis=1)[valid], m0[valid])
+
+
+@pytest.mark.parametrize("n1,n3,L", [(200, 777, 8), (96, 300, 3), (128, 256, 12)])
+def test_prepared_leaves_path_is_identical(device, n1, n3, L):
+    """onepose_match_prepared on leaves transposed once by onepose_prepare_leaves gives the
+    same bits as onepose_match on the reference layout (same kernels after the transpose);
+    L=12 runs the wider GAT instantiation, n3=777 a ragged cloud."""
+    from onepose_amd import _lib
+    lib = _lib.load()
+    sd = synthetic.make_state_dict(1)
+    data, _, _ = synthetic.make_matcher_inputs(n1, n3, L, seed=4)
+    m = matcher.from_state_dict(sd)
+    w = m.packed_weights(device)
+    t = {k: torch.from_numpy(v).to(device).contiguous() for k, v in data.items()}
+    f32 = dict(dtype=torch.float32, device=device)
+    ws_bytes = lib.onepose_match_workspace_bytes(1, n1, n3, L, 1)
+    outs = []
+    for prepared in (False, True):
+        o = dict(m0=torch.empty(1, n1, dtype=torch.int64, device=device),
+                 m1=torch.empty(1, n3, dtype=torch.int64, device=device),
+                 s0=torch.empty(1, n1, **f32), s1=torch.empty(1, n3, **f32),
+                 conf=torch.empty(1, n1, n3, **f32))
+        ws = torch.empty(ws_bytes, dtype=torch.uint8, device=device)
+        s = _lib.stream_ptr(device)
+        leaves, fn = t["descriptors2d_db"], lib.onepose_match
+        if prepared:
+            pm = torch.empty(lib.onepose_leaves_prepared_bytes(1, n3, L) // 4, **f32)
+            _lib.check(lib.onepose_prepare_leaves(leaves.data_ptr(), 0, 1, n3, L, pm.data_ptr(), s),
+                       "prepare_leaves")
+            leaves, fn = pm, lib.onepose_match_prepared
+        _lib.check(fn(w.data_ptr(), t["descriptors2d_query"].data_ptr(), 256 * n1,
+                      t["descriptors3d_db"].data_ptr(), 256 * n3, leaves.data_ptr(), 0, 1, n1, n3,
+                      L, float(m.hparams["scale_factor"]), float(m.hparams["match_threshold"]),
+                      o["m0"].data_ptr(), o["m1"].data_ptr(), o["s0"].data_ptr(),
+                      o["s1"].data_ptr(), o["conf"].data_ptr(), ws.data_ptr(), ws_bytes, s),
+                   "match")
+        torch.cuda.synchronize()
+        outs.append({k: v.cpu().numpy() for k, v in o.items()})
+    for k in outs[0]:
+        np.testing.assert_array_equal(outs[0][k], outs[1][k], err_msg=k)
