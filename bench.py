@@ -31,7 +31,7 @@ METRIC = "query frames/sec (1k kpts × 4k 3D pts) + cm/deg pose err, 1/2/4/8 GPU
 FP32_MFMA_PEAK_TFLOPS = 157.3     # MI355X_MICROARCH.md: f32-input MFMA dense peak
 HBM_PEAK_GBS = 8000.0             # MI355X_MICROARCH.md: HBM3E spec
 # kernels that record device stamps (onepose_profile_begin_device): timeable inside graphs
-STAMPED = {"kv_gemm", "q_gemm", "mlp1_gemm", "mlp2_gemm", "final_gemm", "score_gemm"}
+STAMPED = {"qkv_gemm", "mlp1_gemm", "mlp2_gemm", "final_gemm", "score_gemm"}
 
 
 def kernel_work(kind, B, n1, n3, L):
@@ -40,8 +40,7 @@ def kernel_work(kind, B, n1, n3, L):
     T = B * (n1 + n3)
     C = 256
     table = {
-        "kv_gemm": (2 * 2 * C * C * T, "flop", "mfma"),
-        "q_gemm": (2 * C * C * T, "flop", "mfma"),
+        "qkv_gemm": (2 * 3 * C * C * T, "flop", "mfma"),      # [q | k v] = Wqkv x
         "mlp1_gemm": (2 * 2 * C * 2 * C * T, "flop", "mfma"),   # [W1a | Mf] [x ; QZ]
         "mlp2_gemm": (2 * 2 * C * C * T, "flop", "mfma"),
         "final_gemm": (2 * C * C * T, "flop", "mfma"),
@@ -236,7 +235,12 @@ def main():
     if marks:   # matcher / pose stage GPU times over the timed region (diagnostic)
         mt = [a.elapsed_time(b) for a, b, _ in marks]
         pt = [b.elapsed_time(c) for _, b, c in marks]
+        gap = [marks[i][1].elapsed_time(marks[i + 1][0]) for i in range(len(marks) - 1)]
+        s2s = [marks[i][0].elapsed_time(marks[i + 1][0]) for i in range(len(marks) - 1)]
         stage_ms = {"matcher_mean": round(float(np.mean(mt)), 4),
+                    "gap_mean": round(float(np.mean(gap)), 4) if gap else None,
+                    "gap_max": round(float(np.max(gap)), 4) if gap else None,
+                    "start_to_start": [round(x, 3) for x in s2s],
                     "matcher_max": round(float(np.max(mt)), 4),
                     "pose_mean": round(float(np.mean(pt)), 4),
                     "pose_max": round(float(np.max(pt)), 4)}

@@ -43,7 +43,7 @@ constexpr int kHeadDim = 64;
 
 // ---- launch profiling (measurement hook, see onepose_profile_begin in the header) ----
 enum KernelKind {
-  K_TRANSPOSE = 0, K_GAT, K_KV_GEMM, K_Q_GEMM, K_KV_REDUCE, K_MFOLD, K_MLP1, K_STATS, K_MLP2,
+  K_TRANSPOSE = 0, K_GAT, K_QKV_GEMM, K_KV_REDUCE, K_MFOLD, K_MLP1, K_STATS, K_MLP2,
   K_FINAL, K_L2NORM, K_SCORE, K_SMX_REDUCE, K_CONF, K_MUTUAL, K_SELECT, K_PNP, K_PNP_REFIT,
   K_POSE_ERR, K_SAMPLE, K_NUM_KINDS
 };

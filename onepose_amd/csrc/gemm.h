@@ -17,16 +17,19 @@ namespace onepose {
 
 enum GemmEpi {
   EPI_BIAS = 0,    // y = acc + bias
-  EPI_KVPART = 1,  // 128-col tile = [k_h | v_h]: phi(k), v/vdiv -> per-tile KV_h = phi(k)^T v
-                   //   and sum phi(k) partials (linear-attention source reduction)
+  EPI_QKV = 1,     // 128-col tiles of [q (256) | k_0 v_0 | .. | k_3 v_3] (768 outputs):
+                   //   q tiles store phi(q) = elu(q)+1; [k_h | v_h] tiles reduce phi(k), v/vdiv
+                   //   to the tile's KV_h = phi(k)^T v and sum phi(k) partials (no store)
   EPI_STATS = 2,   // y = acc + bias, plus per-tile (mean, M2) of every column  (InstanceNorm)
   EPI_RESID = 3,   // y = R + (acc + bias)                                     (desc += delta)
   EPI_SCORE = 4,   // y = acc / scale, plus per-tile row/col (max, sum exp)     (dual softmax)
-  EPI_QZ = 5,      // 64-col tile = q_h: phi(q) * Z * Ns, Z = 1/(phi(q).ksum_h + 1e-6)
 };
 enum GemmPro {
   PRO_PLAIN = 0,
   PRO_NORM_RELU = 1,  // a = max((a - mean[k]) * rstd[k], 0)                    (norm + ReLU)
+  PRO_HEADZ = 2,      // K range [ksplit, K) = 4 heads x 64 of phi(q): each head's partial
+                      //   sum is scaled per row by Z*Ns = ns / (phi(q)_h . ksum_h + 1e-6)
+                      //   (linear attention's normaliser, computed from the staged tiles)
 };
 
 struct GemmProb {
@@ -53,13 +56,13 @@ struct GemmProb {
   float* stats;        // EPI_STATS: [batch][mtiles][2][N]  (mtiles = ceil(M / tile rows))
   float* rowstat;      // EPI_SCORE: [batch][M][ntiles][2]
   float* colstat;      // EPI_SCORE: [batch][N][mtiles][2]
-  float* kvpart;       // EPI_KVPART: [batch][mtiles][4][64][64]
-  float* kspart;       // EPI_KVPART: [batch][mtiles][256]
-  const float* ksum;   // EPI_QZ: [batch][256] of the attention source
+  float* kvpart;       // EPI_QKV: [batch][mtiles][4][64][64]
+  float* kspart;       // EPI_QKV: [batch][mtiles][256]
+  const float* ksum;   // PRO_HEADZ: [batch][256] sum phi(k) of the attention source
   int64_t ksum_bs;
   float scale;         // EPI_SCORE divisor (scale_factor)
-  float vdiv;          // EPI_KVPART: v divisor (source length)
-  float ns;            // EPI_QZ: source length (v_length)
+  float vdiv;          // EPI_QKV: v divisor (source length)
+  float ns;            // PRO_HEADZ: source length (v_length)
   int M, N, K, batch;
   int mtiles, ntiles, tiles;   // filled by gemm_launch
 };
@@ -72,12 +75,11 @@ struct GemmArgs {
 
 // Tile configurations: BM x BN output tile, K split into KS slices inside the workgroup.
 enum GemmTile {
-  TILE_64x64 = 0,      // score, mlp1 (STATS), mlp2 (RESID+NORM), final
-  TILE_32x64_K2 = 1,   // q (QZ: one head per tile), K split in two inside the workgroup
-  TILE_32x128 = 2,     // kv (KVPART: [k_h | v_h] per tile)
+  TILE_64x64 = 0,   // mlp1 (STATS + HEADZ), mlp2 (RESID + NORM), score, final
+  TILE_32x128 = 1,  // qkv (QKV: one head's [k_h | v_h] or two q heads per tile)
 };
 
-// Supported (epilogue, prologue, tile) combinations: KVPART/32x128, QZ/32x64_K2, STATS/64x64,
+// Supported (epilogue, prologue, tile) combinations: QKV/32x128, STATS+HEADZ/64x64,
 // RESID+NORM/64x64, SCORE/64x64, BIAS/64x64.  K must be a multiple of twice the tile's stage
 // depth (32 * KS).
 int gemm_launch(int epi, int pro, int tile, GemmArgs& args, hipStream_t stream, int kind);

@@ -184,14 +184,59 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args) {
         f.w[kk][j] = *reinterpret_cast<const float4*>(buf + w_off + j * 32 * PITCH + kk * 8);
     }
   };
-  auto mfma_kk = [&](const Frag& f, int kk) __attribute__((always_inline)) {
+  auto mfma_kk = [&](floatx16 (&tg)[FN], const Frag& f, int kk) __attribute__((always_inline)) {
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
-      acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(f.a[kk].x, f.w[kk][j].x, acc[j], 0, 0, 0);
-      acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(f.a[kk].y, f.w[kk][j].y, acc[j], 0, 0, 0);
-      acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(f.a[kk].z, f.w[kk][j].z, acc[j], 0, 0, 0);
-      acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(f.a[kk].w, f.w[kk][j].w, acc[j], 0, 0, 0);
+      tg[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(f.a[kk].x, f.w[kk][j].x, tg[j], 0, 0, 0);
+      tg[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(f.a[kk].y, f.w[kk][j].y, tg[j], 0, 0, 0);
+      tg[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(f.a[kk].z, f.w[kk][j].z, tg[j], 0, 0, 0);
+      tg[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(f.a[kk].w, f.w[kk][j].w, tg[j], 0, 0, 0);
     }
+  };
+
+  // PRO_HEADZ: the phi(q) part of K is 4 heads x 64 (two stages each) after the x part.
+  // Each head accumulates into acc_h; its rows are scaled by Z*Ns and added to acc when the
+  // head's two stages are done.  Z's dot products phi(q)_row . ksum_h are taken from the
+  // staged A tiles (thread = row, 8-wide k chunk) right after each stage's fragment read.
+  const int xs = c.ksplit / T::BKS;
+  floatx16 acc_h[FN];
+#pragma unroll
+  for (int j = 0; j < FN; ++j)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc_h[j][i] = 0.f;
+  float zp = 0.f;
+  const int zr = t >> 2, zq = t & 3;
+  __shared__ float zks[(PRO == PRO_HEADZ) ? 256 : 1];   // sum phi(k) of the source
+  if (PRO == PRO_HEADZ) zks[t] = F(ksum)[b * F(ksum_bs) + t];   // visible after 1st barrier
+  const float zns = F(ns);
+  auto zdot = [&](const float* buf, int sg) __attribute__((always_inline)) {
+    if (PRO == PRO_HEADZ && sg >= xs && sg < nk) {
+      static_assert(PRO != PRO_HEADZ || BM * 4 == T::NT, "HEADZ: four threads per row");
+      const float* ap = buf + zr * PITCH + zq * 8;
+      const float* kp = zks + (sg * T::BKS - c.ksplit) + zq * 8;   // LDS
+      const float4 a0 = *reinterpret_cast<const float4*>(ap);
+      const float4 a1 = *reinterpret_cast<const float4*>(ap + 4);
+      const float4 k0 = *reinterpret_cast<const float4*>(kp);
+      const float4 k1 = *reinterpret_cast<const float4*>(kp + 4);
+      zp += a0.x * k0.x + a0.y * k0.y + a0.z * k0.z + a0.w * k0.w + a1.x * k1.x + a1.y * k1.y +
+            a1.z * k1.z + a1.w * k1.w;
+    }
+  };
+  auto zfinal = [&]() __attribute__((always_inline)) {   // head's two partials are in zp
+    zp += __shfl_xor(zp, 1, 64);
+    zp += __shfl_xor(zp, 2, 64);
+    if (zq == 0) zrow[zr] = (1.0f / (zp + 1e-6f)) * zns;
+    zp = 0.f;
+  };
+  auto fold = [&]() __attribute__((always_inline)) {     // acc += Z*Ns (per row) * acc_h
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int row = wm * 32 + (i & 3) + 8 * (i >> 2) + 4 * (lane >> 5);
+        acc[j][i] += zrow[row] * acc_h[j][i];
+        acc_h[j][i] = 0.f;
+      }
   };
 
   load_stage<PRO, T>(c, m0, n0, 0, s0);
@@ -200,26 +245,40 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args) {
   __syncthreads();
   read_frag(lds, f0);
 
-  auto step = [&](int kt, Stage<T>& next, Stage<T>& spare, const Frag& cur, Frag& nxt)
-      __attribute__((always_inline)) {
+  auto step = [&](int kt, Stage<T>& next, Stage<T>& spare, const Frag& cur, Frag& nxt,
+                  floatx16 (&tg)[FN]) __attribute__((always_inline)) {
     // unconditional: past the end the last stage is re-read into the spare set and ignored
     load_stage<PRO, T>(c, m0, n0, min(kt + 2, nk - 1) * T::BKS, spare);
-    mfma_kk(cur, 0);
+    mfma_kk(tg, cur, 0);
     __builtin_amdgcn_sched_barrier(0);
     float* na = lds + ((kt + 1) & 1) * STAGE;
     store_stage<PRO, T>(na, na + BM * PITCH, next);   // (unused after the last step)
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int kk = 1; kk < KKW - 1; ++kk) mfma_kk(cur, kk);
+    for (int kk = 1; kk < KKW - 1; ++kk) mfma_kk(tg, cur, kk);
     __syncthreads();
     read_frag(na, nxt);                               // (unused after the last step)
+    zdot(na, kt + 1);
     __builtin_amdgcn_sched_barrier(0);
-    mfma_kk(cur, KKW - 1);
+    mfma_kk(tg, cur, KKW - 1);
     __builtin_amdgcn_sched_barrier(0);
   };
-  for (int kt = 0; kt < nk; kt += 2) {   // nk is even (checked at launch)
-    step(kt, s1, s0, f0, f1);
-    step(kt + 1, s0, s1, f1, f0);
+  if (PRO != PRO_HEADZ) {
+    for (int kt = 0; kt < nk; kt += 2) {   // nk is even (checked at launch)
+      step(kt, s1, s0, f0, f1, acc);
+      step(kt + 1, s0, s1, f1, f0, acc);
+    }
+  } else {
+    for (int kt = 0; kt < xs; kt += 2) {   // x part
+      step(kt, s1, s0, f0, f1, acc);
+      step(kt + 1, s0, s1, f1, f0, acc);
+    }
+    for (int kt = xs; kt < nk; kt += 2) {  // one head of phi(q) per two stages
+      step(kt, s1, s0, f0, f1, acc_h);
+      zfinal();                            // visible to every wave after the next barrier
+      step(kt + 1, s0, s1, f1, f0, acc_h);
+      fold();
+    }
   }
   __syncthreads();   // every wave done with the LDS stages before they are reused below
 
@@ -254,8 +313,8 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args) {
   const int ldy = F(ldy);
   float* tile = lds;   // [BM][BN+1] staging for the reducing epilogues
   constexpr int TP = BN + 1;
-  constexpr bool kStage =
-      EPI == EPI_STATS || EPI == EPI_SCORE || EPI == EPI_KVPART || EPI == EPI_QZ;
+  constexpr bool kStage = EPI == EPI_STATS || EPI == EPI_SCORE || EPI == EPI_QKV;
+  const bool q_tile = EPI == EPI_QKV && n0 < 256;   // phi(q) columns: stored, no reduction
 
   if (ks == 0) {
     float res[FN][16];
@@ -287,10 +346,10 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args) {
           y = acc[j][i] / F(scale);
         } else {
           y = acc[j][i] + bias;
-          if (EPI == EPI_QZ) y = elu1(y) + 1.0f;
-          if (EPI == EPI_KVPART) y = (col < 64) ? (elu1(y) + 1.0f) : (y / F(vdiv));
+          if (EPI == EPI_QKV) y = (q_tile || col < 64) ? (elu1(y) + 1.0f) : (y / F(vdiv));
         }
-        if (EPI == EPI_BIAS || EPI == EPI_STATS || EPI == EPI_SCORE || EPI == EPI_RESID) {
+        if (EPI == EPI_BIAS || EPI == EPI_STATS || EPI == EPI_SCORE || EPI == EPI_RESID ||
+            (EPI == EPI_QKV && q_tile)) {
           if (gm < M && col_ok) {
             if (EPI == EPI_RESID) y = res[j][i] + y;
             Y[(int64_t)gm * ldy + gn] = y;
@@ -300,7 +359,7 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args) {
       }
     }
   }
-  if (!kStage) return;
+  if (!kStage || q_tile) return;
   __syncthreads();
   const int rows = min(BM, M - m0);
 
@@ -363,30 +422,10 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args) {
       }
     }
   }
-  if (EPI == EPI_QZ) {
-    // Z[row] = 1 / (phi(q)_row . ksum_h + 1e-6), h = the head this 64-column tile holds
-    static_assert(EPI != EPI_QZ || BN == 64, "QZ tile is one head");
-    if (t < 4 * BM) {
-      const float* ks_h = F(ksum) + b * F(ksum_bs) + n0;
-      const int row = t >> 2, q = t & 3;   // 4 lanes per row, 16 channels each
-      float s = 0.f;
-#pragma unroll
-      for (int cc = 0; cc < 16; ++cc) s += tile[row * TP + q * 16 + cc] * ks_h[q * 16 + cc];
-      s += __shfl_xor(s, 1, 64);
-      s += __shfl_xor(s, 2, 64);
-      if (q == 0) zrow[row] = 1.0f / (s + 1e-6f);
-    }
-    __syncthreads();
-    const float ns = F(ns);
-    for (int e = t; e < BM * 64; e += T::NT) {
-      const int row = e >> 6, cc = e & 63;
-      if (m0 + row < M) Y[(int64_t)(m0 + row) * ldy + n0 + cc] = tile[row * TP + cc] * zrow[row] * ns;
-    }
-  }
-  if (EPI == EPI_KVPART) {
+  if (EPI == EPI_QKV) {
     // KV_h[d][q] = sum_rows phi(k)[row][d] * v[row][q]   (columns 0..63 | 64..127 of the tile)
-    static_assert(EPI != EPI_KVPART || (BN == 128 && T::NW == 4), "KVPART tile is [k_h | v_h]");
-    const int h = n0 / 128;
+    static_assert(EPI != EPI_QKV || (BN == 128 && T::NW == 4), "QKV tile is [k_h | v_h]");
+    const int h = (n0 - 256) / 128;
     if (t < 64) {
       float s = 0.f;
       for (int rr = 0; rr < rows; ++rr) s += tile[rr * TP + t];
@@ -421,7 +460,6 @@ __global__ __launch_bounds__(T::NT) void gemm_f32_kernel(GemmArgs args) {
 }
 
 using T64x64 = Tile<64, 64, 1, 4, 32>;
-using T32x64k2 = Tile<32, 64, 2, 4, 64>;
 using T32x128 = Tile<32, 128, 1, 4, 32>;
 
 template <int EPI, int PRO, class T>
@@ -435,7 +473,6 @@ struct TileDims {
 TileDims tile_dims(int tile) {
   switch (tile) {
     case TILE_64x64: return {64, 64, 32};
-    case TILE_32x64_K2: return {32, 64, 64};
     case TILE_32x128: return {32, 128, 32};
     default: return {0, 0, 0};
   }
@@ -483,8 +520,10 @@ int gemm_launch(int epi, int pro, int tile, GemmArgs& args, hipStream_t stream, 
     OP_REQUIRE(P.K % (2 * td.bks) == 0, "gemm: K=%d not a multiple of %d", P.K, 2 * td.bks);
     OP_REQUIRE(P.ksplit % td.bks == 0, "gemm: ksplit=%d", P.ksplit);
     OP_REQUIRE(P.lda0 % 4 == 0 && P.ldw % 4 == 0, "gemm: unaligned leading dimension");
-    OP_REQUIRE(epi != EPI_KVPART || (td.bn == 128 && P.N % 128 == 0), "gemm: KVPART tiling");
-    OP_REQUIRE(epi != EPI_QZ || (td.bn == 64 && P.N % 64 == 0), "gemm: QZ tiling");
+    OP_REQUIRE(epi != EPI_QKV || (td.bn == 128 && P.N == 768), "gemm: QKV tiling");
+    OP_REQUIRE(pro != PRO_HEADZ || (P.ksplit % 64 == 0 && P.K - P.ksplit == 256 &&
+                                    td.bks == 32 && P.ksum != nullptr),
+               "gemm: HEADZ needs 4 heads x 64 after ksplit");
     OP_REQUIRE(epi != EPI_STATS || td.bn == 64, "gemm: STATS tiling");
     P.mtiles = ceil_div(P.M, td.bm);
     P.ntiles = ceil_div(P.N, td.bn);
@@ -502,9 +541,8 @@ int gemm_launch(int epi, int pro, int tile, GemmArgs& args, hipStream_t stream, 
     OP_LAUNCHED();                                \
     return ONEPOSE_OK;                            \
   }
-  CASE(EPI_KVPART, PRO_PLAIN, TILE_32x128, T32x128)
-  CASE(EPI_QZ, PRO_PLAIN, TILE_32x64_K2, T32x64k2)
-  CASE(EPI_STATS, PRO_PLAIN, TILE_64x64, T64x64)
+  CASE(EPI_QKV, PRO_PLAIN, TILE_32x128, T32x128)
+  CASE(EPI_STATS, PRO_HEADZ, TILE_64x64, T64x64)
   CASE(EPI_RESID, PRO_NORM_RELU, TILE_64x64, T64x64)
   CASE(EPI_SCORE, PRO_PLAIN, TILE_64x64, T64x64)
   CASE(EPI_BIAS, PRO_PLAIN, TILE_64x64, T64x64)

@@ -36,7 +36,7 @@
 namespace onepose {
 
 // GEMM tile per layer GEMM (gemm.h; measured per shape on config 2).
-constexpr int kTileKV = TILE_32x128, kTileQ = TILE_32x64_K2, kTileMLP1 = TILE_64x64,
+constexpr int kTileKV = TILE_32x128, kTileMLP1 = TILE_64x64,
               kTileMLP2 = TILE_64x64, kTileFinal = TILE_64x64;
 
 // ------------------------------------------------------------------------------------
@@ -68,7 +68,7 @@ struct Prof {
 };
 Prof g_prof;
 const char* kKindNames[K_NUM_KINDS] = {
-    "transpose_in", "gat", "kv_gemm", "q_gemm", "kv_reduce", "m_fold", "mlp1_gemm",
+    "transpose_in", "gat", "qkv_gemm", "kv_reduce", "m_fold", "mlp1_gemm",
     "stats_finalize", "mlp2_gemm", "final_gemm", "l2norm", "score_gemm", "softmax_reduce",
     "conf", "mutual", "select", "pnp_ransac", "pnp_refit", "pose_error", "sample_desc"};
 }  // namespace
@@ -101,30 +101,29 @@ constexpr int kApLayers = 8;
 constexpr int kGatLayers = 4;
 
 // packed panel, floats (per attention layer):
-//   Wkv [512][256]: per head h: 64 rows of k_h then 64 rows of v_h (ref rows d*4+h)
-//   bkv [512], Wq [256][256] head-major rows, bq [256]
+//   Wqkv [768][256]: rows 0..255 q head-major (packed row h*64+d <- reference row d*4+h),
+//                    then per head h: 64 rows of k_h, 64 rows of v_h
+//   bqkv [768]
 //   W1a [512][256] = mlp.0.weight[:, :256]
 //   C   [512][256] = mlp.0.weight[:, 256:] @ merge.weight, columns head-major (h*64+q)
 //   b1f [512]      = mlp.0.bias + mlp.0.weight[:, 256:] @ merge.bias
 //   W2 [256][512], b2 [256]
-constexpr int64_t kApWkv = 512 * 256, kApBkv = 512, kApWq = 256 * 256, kApBq = 256;
+constexpr int64_t kApWqkv = 768 * 256, kApBqkv = 768;
 constexpr int64_t kApW1a = 512 * 256, kApC = 512 * 256, kApB1 = 512, kApW2 = 256 * 512,
                   kApB2 = 256;
-constexpr int64_t kApFloats = kApWkv + kApBkv + kApWq + kApBq + kApW1a + kApC + kApB1 + kApW2 + kApB2;
+constexpr int64_t kApFloats = kApWqkv + kApBqkv + kApW1a + kApC + kApB1 + kApW2 + kApB2;
 constexpr int64_t kGatFloats = 512;
 constexpr int64_t kFinalFloats = 256 * 256 + 256;
 constexpr int64_t kPackedFloats = kApLayers * kApFloats + kGatLayers * kGatFloats + kFinalFloats;
 
 struct ApW {
-  const float *wkv, *bkv, *wq, *bq, *w1a, *c, *b1, *w2, *b2;
+  const float *wqkv, *bqkv, *w1a, *c, *b1, *w2, *b2;
 };
 ApW ap_weights(const float* base, int ap) {
   const float* p = base + (int64_t)ap * kApFloats;
   ApW w;
-  w.wkv = p; p += kApWkv;
-  w.bkv = p; p += kApBkv;
-  w.wq = p; p += kApWq;
-  w.bq = p; p += kApBq;
+  w.wqkv = p; p += kApWqkv;
+  w.bqkv = p; p += kApBqkv;
   w.w1a = p; p += kApW1a;
   w.c = p; p += kApC;
   w.b1 = p; p += kApB1;
@@ -228,7 +227,7 @@ __global__ __launch_bounds__(256) void transpose_in_kernel(TransArgs args, int b
   }
 }
 
-// Linear-attention source state.  The kv GEMM's epilogue (EPI_KVPART) leaves, per 64-token
+// Linear-attention source state.  The qkv GEMM's epilogue (EPI_QKV) leaves, per 32-token
 // chunk, KVpart[h][d][q] = sum_m phi(k)[m][h,d] v[m][h,q]/Ns  (einsum 'bdhm,bqhm->bqdh', :96)
 // and kspart[h*64+d] = sum_m phi(k)[m][h,d]  (key.sum(3), :97); kv_reduce sums the chunks.
 struct KvProb {
@@ -648,7 +647,7 @@ struct Plan {
   float *x2[2], *x3[2];
   float *kvpart2, *kvpart3, *kspart2, *kspart3;
   float *kv, *ksum, *mf;
-  float *qz2, *qz3, *y12, *y13;
+  float *phiq2, *phiq3, *y12, *y13;
   float *stats2, *stats3, *mean, *rstd;
   float *f2, *f3, *s;
   float *rowpart, *colpart, *rowmax, *rowsum, *colmax, *colsum;
@@ -674,8 +673,8 @@ Plan make_plan(void* ws, int B, int n1, int n3, int L, bool with_conf) {
   p.kv = c.take<float>((size_t)2 * B * 16384);
   p.ksum = c.take<float>((size_t)2 * B * 256);
   p.mf = c.take<float>((size_t)2 * B * 512 * 256);
-  p.qz2 = c.take<float>(t2 * 256);
-  p.qz3 = c.take<float>(t3 * 256);
+  p.phiq2 = c.take<float>(t2 * 256);
+  p.phiq3 = c.take<float>(t3 * 256);
   p.y12 = c.take<float>(t2 * 512);
   p.y13 = c.take<float>(t3 * 512);
   p.stats2 = c.take<float>((size_t)B * ceil_div(n1, str) * 1024);
@@ -823,11 +822,11 @@ int onepose_matcher_pack(const float* const* tensors, int n_tensors, void* packe
       continue;
     }
     float* p = out + (int64_t)ap * kApFloats;
-    float* wkv = p;
-    float* bkv = wkv + kApWkv;
-    float* wq = bkv + kApBkv;
-    float* bq = wq + kApWq;
-    float* w1a = bq + kApBq;
+    float* wq = p;
+    float* wkv = wq + 256 * 256;
+    float* bq = p + kApWqkv;
+    float* bkv = bq + 256;
+    float* w1a = bq + kApBqkv;
     float* cw = w1a + kApW1a;
     float* b1 = cw + kApC;
     float* w2 = b1 + kApB1;
@@ -942,18 +941,20 @@ int match_impl(const void* packed_weights, const float* desc2d, int64_t desc2d_b
     // self: each side attends to itself; cross: 2D <-> 3D.  Source of side s: src(s).
     const int src2 = (kind == 1) ? 0 : 1, src3 = (kind == 1) ? 1 : 0;
     const int ns2 = src2 == 0 ? n1 : n3, ns3 = src3 == 0 ? n1 : n3;
-    {  // 1. [phi(k)_h | v_h / Ns] of both tensors -> per-chunk KV / ksum partials
+    {  // 1. [q | k_h v_h ...] of both tensors: phi(q) stored, per-chunk KV / ksum partials
       GemmArgs a;
       a.nprob = 2;
-      a.p[0] = gemm_prob(p.x2[c2], 256, w.wkv, 256, w.bkv, nullptr, 0, n1, 512, 256, B);
+      a.p[0] = gemm_prob(p.x2[c2], 256, w.wqkv, 256, w.bqkv, p.phiq2, 256, n1, 768, 256, B);
       a.p[0].vdiv = (float)n1;
       a.p[0].kvpart = p.kvpart2;
       a.p[0].kspart = p.kspart2;
-      a.p[1] = gemm_prob(p.x3[c3], 256, w.wkv, 256, w.bkv, nullptr, 0, n3, 512, 256, B);
+      a.p[0].y_bs = (int64_t)n1 * 256;
+      a.p[1] = gemm_prob(p.x3[c3], 256, w.wqkv, 256, w.bqkv, p.phiq3, 256, n3, 768, 256, B);
       a.p[1].vdiv = (float)n3;
       a.p[1].kvpart = p.kvpart3;
       a.p[1].kspart = p.kspart3;
-      if ((rc = gemm_launch(EPI_KVPART, PRO_PLAIN, kTileKV, a, st, K_KV_GEMM)) != ONEPOSE_OK)
+      a.p[1].y_bs = (int64_t)n3 * 256;
+      if ((rc = gemm_launch(EPI_QKV, PRO_PLAIN, kTileKV, a, st, K_QKV_GEMM)) != ONEPOSE_OK)
         return rc;
     }
     {  // 2. KV[src], ksum[src]
@@ -970,24 +971,12 @@ int match_impl(const void* packed_weights, const float* desc2d, int64_t desc2d_b
       fa.p[1] = {p.kv + (size_t)src3 * B * 16384, p.mf + (size_t)B * 512 * 256};
       OP_LAUNCH(K_MFOLD, st, m_fold_kernel, dim3(2 * B * 32), dim3(256), 0, st, fa, B);
     }
-    {  // 4. phi(q) * Z * Ns
-      GemmArgs a;
-      a.nprob = 2;
-      a.p[0] = gemm_prob(p.x2[c2], 256, w.wq, 256, w.bq, p.qz2, 256, n1, 256, 256, B);
-      a.p[0].ksum = p.ksum + (size_t)src2 * B * 256;
-      a.p[0].ksum_bs = 256;
-      a.p[0].ns = (float)ns2;
-      a.p[1] = gemm_prob(p.x3[c3], 256, w.wq, 256, w.bq, p.qz3, 256, n3, 256, 256, B);
-      a.p[1].ksum = p.ksum + (size_t)src3 * B * 256;
-      a.p[1].ksum_bs = 256;
-      a.p[1].ns = (float)ns3;
-      if ((rc = gemm_launch(EPI_QZ, PRO_PLAIN, kTileQ, a, st, K_Q_GEMM)) != ONEPOSE_OK) return rc;
-    }
-    {  // 5. MLP conv 1 on [x ; QZ] with [W1a | Mf] + InstanceNorm partials
+    {  // 4. MLP conv 1 on [x ; phi(q)] with [W1a | Mf], the phi(q) heads scaled by Z * Ns
+       //    in-kernel (PRO_HEADZ), + InstanceNorm partials
       GemmArgs a;
       a.nprob = 2;
       a.p[0] = gemm_prob(p.x2[c2], 256, w.w1a, 256, w.b1, p.y12, 512, n1, 512, 512, B);
-      a.p[0].A1 = p.qz2;
+      a.p[0].A1 = p.phiq2;
       a.p[0].lda1 = 256;
       a.p[0].a1_bs = (int64_t)n1 * 256;
       a.p[0].ksplit = 256;
@@ -995,8 +984,11 @@ int match_impl(const void* packed_weights, const float* desc2d, int64_t desc2d_b
       a.p[0].ldw1 = 256;
       a.p[0].w1_bs = 512 * 256;
       a.p[0].stats = p.stats2;
+      a.p[0].ksum = p.ksum + (size_t)src2 * B * 256;
+      a.p[0].ksum_bs = 256;
+      a.p[0].ns = (float)ns2;
       a.p[1] = gemm_prob(p.x3[c3], 256, w.w1a, 256, w.b1, p.y13, 512, n3, 512, 512, B);
-      a.p[1].A1 = p.qz3;
+      a.p[1].A1 = p.phiq3;
       a.p[1].lda1 = 256;
       a.p[1].a1_bs = (int64_t)n3 * 256;
       a.p[1].ksplit = 256;
@@ -1004,9 +996,13 @@ int match_impl(const void* packed_weights, const float* desc2d, int64_t desc2d_b
       a.p[1].ldw1 = 256;
       a.p[1].w1_bs = 512 * 256;
       a.p[1].stats = p.stats3;
-      if ((rc = gemm_launch(EPI_STATS, PRO_PLAIN, kTileMLP1, a, st, K_MLP1)) != ONEPOSE_OK) return rc;
+      a.p[1].ksum = p.ksum + (size_t)src3 * B * 256;
+      a.p[1].ksum_bs = 256;
+      a.p[1].ns = (float)ns3;
+      if ((rc = gemm_launch(EPI_STATS, PRO_HEADZ, kTileMLP1, a, st, K_MLP1)) != ONEPOSE_OK)
+        return rc;
     }
-    {  // 6. InstanceNorm statistics
+    {  // 5. InstanceNorm statistics
       StatsArgs sa;
       const int str = gemm_tile_rows(kTileMLP1);
       sa.p[0] = {p.stats2, p.mean, p.rstd, n1, ceil_div(n1, str), str};
@@ -1014,7 +1010,7 @@ int match_impl(const void* packed_weights, const float* desc2d, int64_t desc2d_b
                  ceil_div(n3, str), str};
       OP_LAUNCH(K_STATS, st, stats_finalize_kernel, dim3(2 * B * 32), dim3(256), 0, st, sa, B);
     }
-    {  // 7. MLP conv 2 on ReLU(InstanceNorm(.)) + residual: desc + delta
+    {  // 6. MLP conv 2 on ReLU(InstanceNorm(.)) + residual: desc + delta
       GemmArgs a;
       a.nprob = 2;
       a.p[0] = gemm_prob(p.y12, 512, w.w2, 512, w.b2, p.x2[c2 ^ 1], 256, n1, 256, 512, B);

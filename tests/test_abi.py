@@ -59,7 +59,7 @@ def _pack(sd):
     return buf
 
 
-AP_FLOATS = 512 * 256 + 512 + 256 * 256 + 256 + 512 * 256 + 512 * 256 + 512 + 256 * 512 + 256
+AP_FLOATS = 768 * 256 + 768 + 512 * 256 + 512 * 256 + 512 + 256 * 512 + 256
 
 
 def test_pack_layout():
@@ -75,10 +75,8 @@ def test_pack_layout():
         out = p[off:off + n]
         off += n
         return out
-    wkv = take(512 * 256).reshape(512, 256)
-    bkv = take(512)
-    wq = take(256 * 256).reshape(256, 256)
-    bq = take(256)
+    wqkv = take(768 * 256).reshape(768, 256)
+    bqkv = take(768)
     w1a = take(512 * 256).reshape(512, 256)
     cw = take(512 * 256).reshape(512, 256)
     b1 = take(512)
@@ -88,11 +86,11 @@ def test_pack_layout():
     v_w = sd["gnn.layers.1.attn.proj.2.weight"][:, :, 0]
     for h in range(4):
         for d in (0, 17, 63):
-            np.testing.assert_array_equal(wq[h * 64 + d], q_w[d * 4 + h])
-            np.testing.assert_array_equal(wkv[128 * h + d], k_w[d * 4 + h])
-            np.testing.assert_array_equal(wkv[128 * h + 64 + d], v_w[d * 4 + h])
-            assert bkv[128 * h + 64 + d] == sd["gnn.layers.1.attn.proj.2.bias"][d * 4 + h]
-            assert bq[h * 64 + d] == sd["gnn.layers.1.attn.proj.0.bias"][d * 4 + h]
+            np.testing.assert_array_equal(wqkv[h * 64 + d], q_w[d * 4 + h])
+            np.testing.assert_array_equal(wqkv[256 + 128 * h + d], k_w[d * 4 + h])
+            np.testing.assert_array_equal(wqkv[256 + 128 * h + 64 + d], v_w[d * 4 + h])
+            assert bqkv[256 + 128 * h + 64 + d] == sd["gnn.layers.1.attn.proj.2.bias"][d * 4 + h]
+            assert bqkv[h * 64 + d] == sd["gnn.layers.1.attn.proj.0.bias"][d * 4 + h]
     m0 = sd["gnn.layers.1.mlp.0.weight"][:, :, 0].astype(np.float64)
     merge = sd["gnn.layers.1.attn.merge.weight"][:, :, 0].astype(np.float64)
     np.testing.assert_array_equal(w1a, m0[:, :256])

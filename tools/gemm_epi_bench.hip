@@ -27,10 +27,9 @@ int main() {
   hipMemcpy(rstd, h.data(), 1024 * 4, hipMemcpyHostToDevice);
   hipMemcpy(ksum, h.data(), 512 * 4, hipMemcpyHostToDevice);
   struct Case { const char* name; int epi, pro, tile, N, K; };
-  Case cases[] = {{"kv   KVPART/32x128", EPI_KVPART, PRO_PLAIN, TILE_32x128, 512, 256},
-                  {"q    QZ/32x64k2", EPI_QZ, PRO_PLAIN, TILE_32x64_K2, 256, 256},
+  Case cases[] = {{"qkv  QKV/32x128", EPI_QKV, PRO_PLAIN, TILE_32x128, 768, 256},
                   {"q    BIAS/64x64", EPI_BIAS, PRO_PLAIN, TILE_64x64, 256, 256},
-                  {"mlp1 STATS/64x64", EPI_STATS, PRO_PLAIN, TILE_64x64, 512, 512},
+                  {"mlp1 STATS+HEADZ/64x64", EPI_STATS, PRO_HEADZ, TILE_64x64, 512, 512},
                   {"mlp1 BIAS/64x64", EPI_BIAS, PRO_PLAIN, TILE_64x64, 512, 512},
                   {"mlp2 RESID+NORM/64x64", EPI_RESID, PRO_NORM_RELU, TILE_64x64, 256, 512},
                   {"mlp2 BIAS/64x64", EPI_BIAS, PRO_PLAIN, TILE_64x64, 256, 512}};
@@ -47,6 +46,9 @@ int main() {
       g.kvpart = kvp + (i ? 32 * 16384 : 0); g.kspart = ksp + (i ? 32 * 256 : 0);
       g.ksum = ksum + i * 256;
       g.M = Ms[i]; g.N = c.N; g.K = c.K; g.batch = 1; g.scale = 1; g.vdiv = 1; g.ns = 1;
+      if (c.pro == PRO_HEADZ) {   // [x | phi(q)] = the two halves of one A row
+        g.ksplit = 256; g.A1 = g.A0 + 256; g.lda1 = c.K; g.a1_bs = 0;
+      }
     }
     for (int i = 0; i < 5; ++i) gemm_launch(c.epi, c.pro, c.tile, a, 0, 0);
     hipEvent_t e0, e1; hipEventCreate(&e0); hipEventCreate(&e1);

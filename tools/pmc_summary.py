@@ -10,12 +10,13 @@ import re
 import sys
 
 # GEMM template instance <EPI, PRO, BN> -> kernel kind (gemm.h enums; one instance per kind)
-GEMM_KIND = {(1, 0, 128): "kv_gemm", (5, 0, 64): "q_gemm", (2, 0, 64): "mlp1_gemm",
-             (3, 1, 64): "mlp2_gemm", (0, 0, 64): "final_gemm", (4, 0, 64): "score_gemm"}
+GEMM_KIND = {(1, 0, 32, 128): "qkv_gemm", (2, 2, 64, 64): "mlp1_gemm",
+             (3, 1, 64, 64): "mlp2_gemm", (0, 0, 64, 64): "final_gemm",
+             (4, 0, 64, 64): "score_gemm"}
 
 
 def kind_of(name):
-    m = re.search(r"gemm_f32_kernel<(\d+), (\d+), (\d+)>", name)
+    m = re.search(r"gemm_f32_kernel<(\d+), (\d+), [^<]*Tile<(\d+), (\d+),", name)
     if m:
         return GEMM_KIND.get(tuple(int(x) for x in m.groups()), name)
     m = re.search(r"onepose::(?:\(anonymous namespace\)::)?(\w+?)(?:<|\(|$)", name)
