@@ -53,6 +53,21 @@ def kernel_work(kind, B, n1, n3, L):
     return table.get(kind)
 
 
+def pmc_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the newest committed PMC summary
+    (profiles/r*/pmc/pmc_traffic.json, written by tools/gpu_pmc.sh + tools/pmc_summary.py:
+    FETCH_SIZE x2 (gfx950) + WRITE_SIZE, separate rocprofv3 passes).  None if absent."""
+    import glob
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "r*", "pmc", "pmc_traffic.json")))
+    if not files:
+        return None, None
+    d = json.load(open(files[-1]))
+    k = d.get("kernels", {}).get(kernel)
+    if not k or k.get("hbm_bytes") is None:
+        return None, None
+    return float(k["hbm_bytes"]), os.path.relpath(files[-1], REPO)
+
+
 def profile_kinds(lib):
     names = []
     k = 0
@@ -125,15 +140,13 @@ def main():
                          "and report those ms/step too (value always comes from the first)")
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    from onepose_amd import distributed as D
+    world, rank, local = D.env()
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     pg = None
-    if world > 1:
+    if D.init("nccl", dev):   # one process per GPU over RCCL; frames shard, results gather
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
         pg = dist
 
     from onepose_amd import _lib, matcher, synthetic
@@ -213,10 +226,7 @@ def main():
     result = torch.cat([last.pose.reshape(B, 12), last.R_err[:, None], last.t_err[:, None],
                         last.cmd.double(), last.n_inliers[:, None].double(),
                         last.status[:, None].double()], 1)
-    if pg:
-        gathered = torch.empty(world * B, result.shape[1], dtype=result.dtype, device=dev)
-        pg.all_gather_into_tensor(gathered, result)
-        result = gathered
+    result = D.gather_frames(result, world * B)   # the only cross-rank exchange
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     nk = len(names)
@@ -226,10 +236,7 @@ def main():
     n_dom = int(launches[dom_id])
     assert n_dom > 0 and tot_ms[dom_id] > 0, "dominant-kernel timing missing"
     dom_ms = float(tot_ms[dom_id] / n_dom)
-    if pg:
-        t = torch.tensor([elapsed], device=dev)
-        pg.all_reduce(t, op=pg.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = D.max_over_ranks(elapsed, dev)   # the slowest rank's clock
 
     stage_ms = None
     if marks:   # matcher / pose stage GPU times over the timed region (diagnostic)
@@ -259,9 +266,13 @@ def main():
     value = frames_total / elapsed
     work, unit, bound = kernel_work(dominant, B, n1, n3, L)
     achieved = work / (dom_ms * 1e-3) / 1e12
+    traffic, traffic_src = pmc_traffic(dominant) if (B, n1, n3, L) == (1, 1024, 4096, 8) \
+        else (None, None)
     roof = {"bound": "mfma", "achieved": round(achieved, 2), "peak": FP32_MFMA_PEAK_TFLOPS,
             "unit": "TFLOP/s", "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4),
-            "traffic": None, "kernel": dominant, "avg_launch_us": round(dom_ms * 1e3, 2),
+            "traffic": traffic, "traffic_unit": "HBM bytes per launch (PMC)",
+            "traffic_source": traffic_src, "kernel": dominant,
+            "avg_launch_us": round(dom_ms * 1e3, 2),
             "launches_timed": n_dom, "flop_per_launch": work,
             "timing": "device clock, first workgroup start to last workgroup end"}
 

@@ -3,8 +3,9 @@
  * GATsSPG 2D-3D matching + RANSAC-EPnP hot path.
  *
  * Plain pointers and sizes only.  Conventions:
- *   - every buffer belongs to the caller; the library never allocates or frees device
- *     memory and never synchronises, so every entry point is hipGraph-capturable;
+ *   - every buffer belongs to the caller; the launch entry points never allocate or free
+ *     device memory and never synchronise, so they are hipGraph-capturable (the measurement
+ *     hooks onepose_profile_* are the exception: they own their timing buffers);
  *   - "device" pointers are HIP device memory (e.g. torch tensors' data_ptr()),
  *     "host" pointers are ordinary CPU memory;
  *   - `stream` is a hipStream_t passed as void* (NULL = the default stream);

@@ -1,0 +1,87 @@
+"""Known-answer tests of the C RANSAC-EPnP oracle (oracle/epnp_ransac.c), CPU only.
+
+The reference solves pose with cv2.solvePnPRansac(SOLVEPNP_EPNP) (eval_utils.py:18-42,
+opencv_python==4.4.0.46 per requirements.txt:5).  cv2 is not installed and cannot be, so
+the oracle is parity-unpinned against OpenCV itself; these tests pin it on scenes with a
+known answer: exact data must give the ground-truth pose and the true inlier
+set, noisy data the noise-limited pose, too few points a failure status, and the random
+stream is the published cv::RNG multiply-with-carry recurrence."""
+import numpy as np
+import pytest
+
+from onepose_amd import synthetic as S
+from oracle import pnp_oracle as O
+
+
+def scene(seed, n, outlier_frac=0.3, px_noise=0.0):
+    rs = np.random.RandomState(seed)
+    K = S.crop_intrinsics()
+    R = S.random_rotation(rs)
+    t = np.array([rs.uniform(-0.03, 0.03), rs.uniform(-0.03, 0.03), rs.uniform(0.35, 0.55)])
+    pose = np.concatenate([R, t[:, None]], 1)
+    pts = rs.uniform(-0.1, 0.1, (n, 3)).astype(np.float32)
+    uv = S.project(K, pose, pts.astype(np.float64)) + rs.normal(0, px_noise, (n, 2))
+    out = rs.rand(n) < outlier_frac
+    uv[out] = rs.uniform(0, 512, (out.sum(), 2))
+    # a random outlier can land within the 5 px gate by chance; those are inliers by definition
+    near = np.linalg.norm(uv - S.project(K, pose, pts.astype(np.float64)), axis=1) <= 5.0
+    return uv.astype(np.float32), pts, K, pose, near
+
+
+def rot_err(Ra, Rb):
+    return np.arccos(np.clip((np.trace(Ra @ Rb.T) - 1) / 2, -1, 1))
+
+
+def test_cv_rng_stream():
+    """cv::RNG((uint64)-1): state = (u32)state * 4164903690 + (state >> 32), draw = (u32)state."""
+    state = 0xFFFFFFFFFFFFFFFF
+    want = []
+    for _ in range(64):
+        state = ((state & 0xFFFFFFFF) * 4164903690 + (state >> 32)) & 0xFFFFFFFFFFFFFFFF
+        want.append(state & 0xFFFFFFFF)
+    np.testing.assert_array_equal(O.rng_draws(64), np.array(want, np.uint32))
+
+
+@pytest.mark.parametrize("n", [6, 12, 50])
+def test_epnp_exact_correspondences(n):
+    p2, p3, K, pose, _ = scene(11 + n, n, outlier_frac=0.0)
+    R, t = O.epnp(p3.astype(np.float64), p2.astype(np.float64), K)
+    assert rot_err(R, pose[:, :3]) < 1e-5
+    assert np.linalg.norm(t - pose[:, 3]) < 1e-5
+
+
+@pytest.mark.parametrize("seed,outliers", [(1, 0.0), (2, 0.3), (3, 0.6)])
+def test_ransac_exact_scene_recovers_pose_and_inliers(seed, outliers):
+    p2, p3, K, pose, near = scene(seed, 400, outlier_frac=outliers)
+    st, est, mask, nin, _ = O.pnp_ransac(p2, p3 * 1000.0, K, scale=1000.0)
+    assert st == 0
+    np.testing.assert_array_equal(mask, near)
+    assert nin == near.sum()
+    assert rot_err(est[:, :3], pose[:, :3]) < 1e-4       # north-star bound, radians
+    assert np.linalg.norm(est[:, 3] - pose[:, 3]) < 1e-3
+
+
+def test_ransac_noisy_scene_is_noise_limited():
+    p2, p3, K, pose, near = scene(7, 700, outlier_frac=0.3, px_noise=0.5)
+    st, est, mask, nin, _ = O.pnp_ransac(p2, p3 * 1000.0, K, scale=1000.0)
+    assert st == 0
+    assert (mask & ~near).sum() <= 2                      # essentially no gross outliers kept
+    assert (near & mask).sum() >= 0.97 * near.sum()
+    assert np.degrees(rot_err(est[:, :3], pose[:, :3])) < 0.5
+    assert np.linalg.norm(est[:, 3] - pose[:, 3]) < 5e-3
+
+
+def test_ransac_too_few_points_fails():
+    p2, p3, K, _, _ = scene(5, 3, outlier_frac=0.0)
+    st, est, mask, nin, _ = O.pnp_ransac(p2, p3 * 1000.0, K, scale=1000.0)
+    assert st != 0 and nin == 0
+
+
+def test_pose_error_semantics():
+    """query_pose_error (eval_utils.py:45-63): cm and degrees, trace clamped at 3 only."""
+    R = S.random_rotation(np.random.RandomState(0))
+    gt = np.concatenate([R, np.array([[0.0], [0.0], [0.5]])], 1)
+    pr = gt.copy()
+    pr[2, 3] += 0.02
+    r, t = O.pose_error(pr, gt)
+    assert abs(t - 2.0) < 1e-9 and r < 1e-4
