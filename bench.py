@@ -212,7 +212,15 @@ def main():
                 pipe.enqueue()
         return pipe.slots[0]
 
-    run_steps(2)    # first replay of each graph (upload) stays out of the timed region
+    def result_rows(slot):   # per-frame result row: pose, errors, cm/deg flags, inliers, status
+        return torch.cat([slot.pose.reshape(B, 12), slot.R_err[:, None], slot.t_err[:, None],
+                          slot.cmd.double(), slot.n_inliers[:, None].double(),
+                          slot.status[:, None].double()], 1)
+
+    # first replay of each graph (upload) and the first use of every torch kernel the timed
+    # region launches (ROCm loads a kernel's code object lazily at its first launch, which
+    # can take tens of ms) stay out of the timed region
+    D.gather_frames(result_rows(run_steps(2)), world * B)
     torch.cuda.synchronize()
     # the dominant kernel's launches are timed on the device (first workgroup start -> last
     # workgroup end), accumulated over every launch inside the timed region
@@ -220,13 +228,14 @@ def main():
     if pg:
         pg.barrier()
     torch.cuda.synchronize()
+    ev_begin = torch.cuda.Event(enable_timing=True)
+    ev_end = torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
+    ev_begin.record()
     last = run_steps(args.steps, record=True)
     host_enqueue = time.perf_counter() - t0   # host time to issue the K steps
-    result = torch.cat([last.pose.reshape(B, 12), last.R_err[:, None], last.t_err[:, None],
-                        last.cmd.double(), last.n_inliers[:, None].double(),
-                        last.status[:, None].double()], 1)
-    result = D.gather_frames(result, world * B)   # the only cross-rank exchange
+    result = D.gather_frames(result_rows(last), world * B)   # the only cross-rank exchange
+    ev_end.record()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     nk = len(names)
@@ -244,10 +253,13 @@ def main():
         pt = [b.elapsed_time(c) for _, b, c in marks]
         gap = [marks[i][1].elapsed_time(marks[i + 1][0]) for i in range(len(marks) - 1)]
         s2s = [marks[i][0].elapsed_time(marks[i + 1][0]) for i in range(len(marks) - 1)]
-        stage_ms = {"matcher_mean": round(float(np.mean(mt)), 4),
+        stage_ms = {"gpu_region_ms": round(ev_begin.elapsed_time(ev_end), 3),
+                    "lead_ms": round(ev_begin.elapsed_time(marks[0][0]), 3),
+                    "tail_ms": round(marks[-1][2].elapsed_time(ev_end), 3),
+                    "matcher_mean": round(float(np.mean(mt)), 4),
                     "gap_mean": round(float(np.mean(gap)), 4) if gap else None,
                     "gap_max": round(float(np.max(gap)), 4) if gap else None,
-                    "start_to_start": [round(x, 3) for x in s2s],
+                    "step_mean": round(float(np.mean(s2s)), 4) if s2s else None,
                     "matcher_max": round(float(np.max(mt)), 4),
                     "pose_mean": round(float(np.mean(pt)), 4),
                     "pose_max": round(float(np.max(pt)), 4)}
