@@ -181,7 +181,8 @@ int onepose_profile_begin(uint64_t kind_mask, int capacity);
  * mlp2/final/score) is timed by its own workgroups on the device's constant-rate clock
  * (s_memrealtime): first workgroup start to last workgroup end; the last workgroup adds the
  * duration to a per-kind total and re-arms the slot, so graph replays and repeated launches
- * all accumulate.  Launches of one kind must not run concurrently while enabled.  A graph
+ * all accumulate.  Each launch (or captured graph node) draws its own accumulator from a
+ * per-kind pool of 256, so launches of one kind may run concurrently.  A graph
  * captured while enabled carries the accumulator address and keeps timing when replayed;
  * calling _begin_device again re-zeroes the accumulators (same addresses).
  * _end_device synchronises the device and returns, per kind k < n_kinds, the number of

@@ -64,8 +64,14 @@ struct Prof {
   std::vector<hipEvent_t> ev;
   std::vector<int> kinds;
   int n = 0;
-  StampAcc* acc = nullptr;   // device, one per kind
+  StampAcc* acc = nullptr;   // device, kStampPool per kind
+  int next[K_NUM_KINDS] = {};   // round-robin pool cursor per kind
 };
+// Each launch (or graph node captured while stamping) gets its own accumulator from the
+// kind's pool, so launches of one kind that run concurrently (several match streams)
+// never share one; a graph node keeps its accumulator across replays, which of the same
+// graph are serialised.
+constexpr int kStampPool = 256;
 Prof g_prof;
 const char* kKindNames[K_NUM_KINDS] = {
     "transpose_in", "gat", "qkv_gemm", "kv_reduce", "m_fold", "mlp1_gemm",
@@ -75,7 +81,8 @@ const char* kKindNames[K_NUM_KINDS] = {
 
 StampAcc* prof_stamp_slot(int kind) {
   if (!g_prof.device || !((g_prof.mask >> kind) & 1ull)) return nullptr;
-  return g_prof.acc + kind;
+  const int i = g_prof.next[kind]++ % kStampPool;
+  return g_prof.acc + (size_t)kind * kStampPool + i;
 }
 
 void prof_pre(int kind, hipStream_t s) {
@@ -728,11 +735,11 @@ int onepose_profile_begin(uint64_t kind_mask, int capacity) {
 
 int onepose_profile_begin_device(uint64_t kind_mask) {
   clear_error();
-  if (g_prof.acc == nullptr) OP_HIP(hipMalloc(&g_prof.acc, sizeof(StampAcc) * K_NUM_KINDS));
-  std::vector<StampAcc> init(K_NUM_KINDS);
+  const size_t n_acc = (size_t)K_NUM_KINDS * kStampPool;
+  if (g_prof.acc == nullptr) OP_HIP(hipMalloc(&g_prof.acc, sizeof(StampAcc) * n_acc));
+  std::vector<StampAcc> init(n_acc);
   for (auto& a : init) a = StampAcc{~0ull, 0ull, 0ull, 0u, 0u};
-  OP_HIP(hipMemcpy(g_prof.acc, init.data(), sizeof(StampAcc) * K_NUM_KINDS,
-                   hipMemcpyHostToDevice));
+  OP_HIP(hipMemcpy(g_prof.acc, init.data(), sizeof(StampAcc) * n_acc, hipMemcpyHostToDevice));
   g_prof.n = 0;
   g_prof.mask = kind_mask;
   g_prof.device = true;
@@ -745,8 +752,15 @@ int onepose_profile_end_device(int64_t* launches, double* total_ms, int n_kinds)
   g_prof.device = false;
   g_prof.mask = 0;
   OP_HIP(hipDeviceSynchronize());
-  std::vector<StampAcc> a(K_NUM_KINDS);
-  OP_HIP(hipMemcpy(a.data(), g_prof.acc, sizeof(StampAcc) * K_NUM_KINDS, hipMemcpyDeviceToHost));
+  std::vector<StampAcc> pool((size_t)K_NUM_KINDS * kStampPool);
+  OP_HIP(hipMemcpy(pool.data(), g_prof.acc, sizeof(StampAcc) * pool.size(),
+                   hipMemcpyDeviceToHost));
+  std::vector<StampAcc> a(K_NUM_KINDS, StampAcc{0ull, 0ull, 0ull, 0u, 0u});
+  for (int k = 0; k < K_NUM_KINDS; ++k)
+    for (int i = 0; i < kStampPool; ++i) {
+      a[k].total += pool[(size_t)k * kStampPool + i].total;
+      a[k].launches += pool[(size_t)k * kStampPool + i].launches;
+    }
   int dev = 0, khz = 0;
   OP_HIP(hipGetDevice(&dev));
   OP_HIP(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev));

@@ -154,21 +154,33 @@ class FramePipeline:
         return out
 
     def run_stream(self, steps: int, match_stream=None, pose_stream=None, graphs=None,
-                   marks=None):
+                   marks=None, match_streams: int = 1):
         """Enqueue `steps` frames (batches) with matcher(k+1) overlapping pose(k); with
-        `graphs` (from ``capture_stages``) each stage is one graph replay.  The match stream
-        waits for the pose stream at the end; the caller synchronises.  `marks` (a list)
-        receives per step (start, matcher done, pose done) timing events."""
-        ms = match_stream or torch.cuda.current_stream(self.device)
+        `graphs` (from ``capture_stages``) each stage is one graph replay.  With
+        `match_streams` = m > 1, consecutive frames' matchers run on m streams concurrently
+        (frame k on stream k % m; needs >= m + 1 buffer slots), filling the CUs that one
+        frame's kernels leave idle.  Every frame still runs every kernel.  All streams are
+        joined into the first match stream at the end; the caller synchronises.  `marks`
+        (a list) receives per step (start, matcher done, pose done) timing events."""
+        ms0 = match_stream or torch.cuda.current_stream(self.device)
         ps = pose_stream or getattr(self, "_pose_stream", None)
         if ps is None:
             ps = self._pose_stream = torch.cuda.Stream(self.device)
+        extra = getattr(self, "_match_streams", [])
+        while len(extra) < match_streams - 1:
+            extra.append(torch.cuda.Stream(self.device))
+        self._match_streams = extra
+        mss = [ms0] + extra[:match_streams - 1]
         n = len(self.slots)
+        assert n >= len(mss) + (1 if len(mss) > 1 else 0), "need more buffer slots than streams"
         matched = [torch.cuda.Event() for _ in range(n)]
         posed = [torch.cuda.Event() for _ in range(n)]
         used = [False] * n
+        for s in mss[1:]:
+            s.wait_stream(ms0)                    # inputs written on the caller's stream
         for k in range(steps):
             sl = k % n
+            ms = mss[k % len(mss)]
             mk = [torch.cuda.Event(enable_timing=True) for _ in range(3)] if marks is not None \
                 else None
             with torch.cuda.stream(ms):
@@ -195,5 +207,7 @@ class FramePipeline:
             used[sl] = True
             if mk:
                 marks.append(mk)
-        ms.wait_stream(ps)
+        for s in mss[1:]:
+            ms0.wait_stream(s)
+        ms0.wait_stream(ps)
         return ps

@@ -32,7 +32,7 @@ def setup():
     data, obj, frames = synthetic.make_matcher_inputs(N1, N3, L, seed=5, batch=2 * B)
     m = matcher.from_state_dict(sd)
     pipe = FramePipeline(m, data["keypoints3d"][0], data["descriptors3d_db"][0],
-                         data["descriptors2d_db"][0], B, N1, dev, scale=1000.0)
+                         data["descriptors2d_db"][0], B, N1, dev, scale=1000.0, slots=3)
     Ks = np.stack([f.K for f in frames])
     gts = np.stack([f.pose_gt for f in frames])
     batches = [(data["descriptors2d_query"][i:i + B], data["keypoints2d"][i:i + B],
@@ -82,6 +82,21 @@ def test_stream_schedule_with_stage_graphs_matches_eager(setup):
     ref = _outputs(pipe.slots[0])
     graphs = pipe.capture_stages()
     pipe.run_stream(7, graphs=graphs)
+    torch.cuda.synchronize()
+    for s in pipe.slots:
+        _assert_same(ref, _outputs(s))
+
+
+@pytest.mark.gpu
+def test_two_concurrent_matcher_streams_match_eager(setup):
+    """Consecutive frames' matchers on two streams (graphs), pose on a third: same bits."""
+    pipe, batches = setup
+    pipe.set_frames(*batches[1])
+    pipe.enqueue(0)
+    torch.cuda.synchronize()
+    ref = _outputs(pipe.slots[0])
+    graphs = pipe.capture_stages()
+    pipe.run_stream(9, graphs=graphs, match_streams=2)
     torch.cuda.synchronize()
     for s in pipe.slots:
         _assert_same(ref, _outputs(s))
