@@ -9,6 +9,9 @@ What is imported from the reference (read-only, nothing copied):
   * src.models.GATsSPG_architectures.GATs_SuperGlue.GATsSuperGlue  (torch only)
   * src.models.extractors.SuperPoint.superpoint.sample_descriptors (torch only)
   * src.evaluators.cmd_evaluator.Evaluator                         (numpy only)
+  * src.utils.data_utils.{pad_features3d_random, build_features3d_leaves} (numpy/torch; the
+    module's unrelated top-level cv2 / loguru imports are satisfied by empty placeholder
+    modules for the duration of the import only)
 
 Inputs are regenerated from seeds by ``onepose_amd.synthetic`` (numpy RandomState), so
 each fixture stores only outputs plus SHA-256 digests of the inputs and weights.
@@ -177,10 +180,58 @@ def evaluator_case():
     print("evaluator:", summ)
 
 
+def object_inputs(seed=21, n3=60, dim=256):
+    """Synthetic SfM object: per-3D-point observation counts 1..12, unit descriptors."""
+    rs = np.random.RandomState(seed)
+    idxs = rs.randint(1, 13, size=n3).astype(np.int64)
+    m = int(idxs.sum())
+    desc = rs.randn(dim, m).astype(np.float32)
+    desc /= np.linalg.norm(desc, axis=0, keepdims=True)
+    scores = rs.rand(m, 1).astype(np.float32)
+    avg = rs.randn(dim, n3).astype(np.float32)
+    avg_scores = rs.rand(n3, 1).astype(np.float32)
+    return idxs, desc, scores, avg, avg_scores
+
+
+def object_case():
+    """pad_features3d_random + build_features3d_leaves (data_utils.py:143-205) as
+    inference.py:113-130 calls them after seed_everything(12345): padded and truncated
+    targets, 8 and 3 leaves."""
+    import types
+    added = []
+    for name in ("cv2", "loguru"):   # data_utils.py:1,5 import these; the two functions don't
+        if name not in sys.modules:
+            sys.modules[name] = types.ModuleType(name)
+            added.append(name)
+    if "loguru" in added:
+        sys.modules["loguru"].logger = None
+    try:
+        from src.utils import data_utils as du
+    finally:
+        for name in added:
+            del sys.modules[name]
+    idxs, desc, scores, avg, avg_scores = object_inputs()
+    out = {"inputs_sha": sha(idxs, desc, scores, avg, avg_scores)}
+    for tag, n_target, num_leaf in (("pad8", 72, 8), ("trunc8", 50, 8), ("pad3", 64, 3)):
+        np.random.seed(12345)
+        a, a_s = du.pad_features3d_random(avg, avg_scores, n_target)
+        leaves, l_s = du.build_features3d_leaves(desc, scores, idxs, n_target, num_leaf)
+        out[f"{tag}_avg"] = a.numpy()
+        out[f"{tag}_avg_scores"] = a_s.numpy()
+        out[f"{tag}_leaves"] = leaves.numpy()
+        out[f"{tag}_leaf_scores"] = l_s.numpy()
+    np.savez_compressed(os.path.join(HERE, "object_leaves.npz"), **out)
+
+
 def main():
     assert os.path.isdir(REF), "the reference is only available in the build container"
     sys.path.insert(0, REF)
     torch.set_num_threads(8)
+    only = sys.argv[1:]
+    if only:   # e.g.  make_golden.py object_case
+        for name in only:
+            globals()[name]()
+        return
     matcher_case("matcher_c1_wc", 256, 512, 8, 1, 0, True, True, True)
     matcher_case("matcher_c1_rand", 256, 512, 8, 1, 1, False, False, True)
     matcher_case("matcher_b2", 128, 192, 8, 2, 2, True, True, False)
@@ -189,6 +240,7 @@ def main():
     empty_case()
     sample_desc_case()
     evaluator_case()
+    object_case()
 
 
 if __name__ == "__main__":

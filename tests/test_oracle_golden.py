@@ -72,3 +72,24 @@ def test_evaluator_matches_reference_fixture():
     np.testing.assert_allclose([s["cmd1"], s["cmd3"], s["cmd5"]], g["summary"])
     a, t = query_pose_error(g["preds"][1], g["gts"][1])
     assert np.isfinite(a) and np.isfinite(t)
+
+
+def test_object_leaves_match_reference():
+    """pad_features3d_random / build_features3d_leaves (data_utils.py:143-205), seeded as
+    inference.py does (seed_everything(12345)): the reference's outputs, bit for bit."""
+    import os
+    import sys
+    from conftest import REPO
+    sys.path.insert(0, os.path.join(REPO, "tests", "golden"))
+    from make_golden import object_inputs
+    from onepose_amd import data_utils as DU
+    g = golden("object_leaves")
+    idxs, desc, scores, avg, avg_scores = object_inputs()
+    for tag, n_target, num_leaf in (("pad8", 72, 8), ("trunc8", 50, 8), ("pad3", 64, 3)):
+        np.random.seed(12345)
+        a, a_s = DU.pad_features3d_random(avg, avg_scores, n_target)
+        leaves, l_s = DU.build_features3d_leaves(desc, scores, idxs, n_target, num_leaf)
+        np.testing.assert_array_equal(a.numpy(), g[f"{tag}_avg"])
+        np.testing.assert_array_equal(a_s.numpy(), g[f"{tag}_avg_scores"])
+        np.testing.assert_array_equal(leaves.numpy(), g[f"{tag}_leaves"])
+        np.testing.assert_array_equal(l_s.numpy(), g[f"{tag}_leaf_scores"])
