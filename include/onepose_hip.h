@@ -169,6 +169,43 @@ int onepose_pose_errors(const double* pose_pred, const double* pose_gt, int64_t 
                         void* stream);
 
 /* ------------------------------------------------------------------------------------ *
+ * SuperPoint keypoint detector + descriptor -- replaces SuperPoint.forward
+ * (src/models/extractors/SuperPoint/superpoint.py:170-224; the model extract_features.py:
+ * 27-40 builds, nms_radius 3, keypoint_threshold 0.005, remove_borders 4, max_keypoints
+ * 4096 there).  Weights: the 24 tensors conv1a.weight, conv1a.bias, ... convDb.bias in
+ * onepose_superpoint_tensor_name order, torch layouts ([cout][cin][k][k], [cout]), packed
+ * host-side into onepose_superpoint_packed_bytes() bytes (then copied to the device).
+ * image [batch][h][w] fp32 in [0,1] (h, w multiples of 8).  Outputs, per sample b:
+ *   keypoints [batch][max_keypoints][2] (x, y), scores [batch][max_keypoints],
+ *   descriptors [batch][256][max_keypoints], counts [batch] -- the first counts[b] entries
+ *   are the reference's keypoints in its order (raster order when at most max_keypoints
+ *   survive NMS + threshold + borders, torch.topk's descending order otherwise); the rest
+ *   are zero.  score_map [batch][h][w] and dense_desc [batch][h/8][w/8][256] (normalised)
+ *   are optional (may be null).  nms_radius <= 8; max_keypoints in [1, 16384], or >= h*w
+ * (the reference's -1: every pixel, no top-k).
+ * ------------------------------------------------------------------------------------ */
+int onepose_superpoint_num_tensors(void);
+const char* onepose_superpoint_tensor_name(int i);
+size_t onepose_superpoint_packed_bytes(void);
+int onepose_superpoint_pack(const float* const* tensors, int n_tensors, void* packed_host);
+size_t onepose_superpoint_workspace_bytes(int batch, int h, int w);
+int onepose_superpoint(const void* packed, const float* image, int batch, int h, int w,
+                       int nms_radius, float keypoint_threshold, int remove_borders,
+                       int max_keypoints, int align_corners, float* keypoints, float* scores,
+                       float* descriptors, int* counts, float* score_map, float* dense_desc,
+                       void* workspace, size_t workspace_bytes, void* stream);
+/* The detector's tail alone -- simple_nms, threshold, remove_borders, top_k_keypoints, the
+ * (y,x)->(x,y) flip and sample_descriptors (superpoint.py:47-113, 181-243) -- from a score
+ * map [batch][h][w] (softmax + pixel shuffle, before NMS) and a normalised dense descriptor
+ * map [batch][h/8][w/8][256].  Outputs and limits as onepose_superpoint. */
+size_t onepose_superpoint_detect_workspace_bytes(int batch, int h, int w);
+int onepose_superpoint_detect(const float* score_map, const float* dense_desc, int batch, int h,
+                              int w, int nms_radius, float keypoint_threshold, int remove_borders,
+                              int max_keypoints, int align_corners, float* keypoints,
+                              float* scores, float* descriptors, int* counts, void* workspace,
+                              size_t workspace_bytes, void* stream);
+
+/* ------------------------------------------------------------------------------------ *
  * Measurement hook (bench.py's roofline).  While enabled, every launch whose kernel kind
  * is in `kind_mask` (bit k = kind k, names from onepose_profile_kind_name) is bracketed by
  * two HIP events recorded on the launch's own stream.  Host-side state, not for use during

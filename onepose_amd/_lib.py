@@ -49,6 +49,18 @@ PROTOTYPES = {
                                    c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
     "onepose_pose_errors": (c_int, [c_void_p, c_void_p, c_int64, c_int, c_void_p, c_void_p,
                                     c_void_p, c_void_p]),
+    "onepose_superpoint_num_tensors": (c_int, []),
+    "onepose_superpoint_tensor_name": (c_char_p, [c_int]),
+    "onepose_superpoint_packed_bytes": (c_size_t, []),
+    "onepose_superpoint_pack": (c_int, [ctypes.POINTER(c_void_p), c_int, c_void_p]),
+    "onepose_superpoint_workspace_bytes": (c_size_t, [c_int, c_int, c_int]),
+    "onepose_superpoint": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_float, c_int,
+                                   c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                   c_void_p, c_void_p, c_size_t, c_void_p]),
+    "onepose_superpoint_detect_workspace_bytes": (c_size_t, [c_int, c_int, c_int]),
+    "onepose_superpoint_detect": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_float,
+                                          c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
+                                          c_void_p, c_void_p, c_size_t, c_void_p]),
     "onepose_profile_begin": (c_int, [ctypes.c_uint64, c_int]),
     "onepose_profile_begin_device": (c_int, [ctypes.c_uint64]),
     "onepose_profile_end_device": (c_int, [c_void_p, c_void_p, c_int]),

@@ -45,7 +45,7 @@ constexpr int kHeadDim = 64;
 enum KernelKind {
   K_TRANSPOSE = 0, K_GAT, K_QKV_GEMM, K_KV_REDUCE, K_MFOLD, K_MLP1, K_STATS, K_MLP2,
   K_FINAL, K_L2NORM, K_SCORE, K_SMX_REDUCE, K_CONF, K_MUTUAL, K_SELECT, K_PNP, K_PNP_REFIT,
-  K_POSE_ERR, K_SAMPLE, K_NUM_KINDS
+  K_POSE_ERR, K_SAMPLE, K_SP_CONV, K_SP_NMS, K_SP_SELECT, K_SP_DESC, K_NUM_KINDS
 };
 void prof_pre(int kind, hipStream_t s);
 void prof_post(int kind, hipStream_t s);

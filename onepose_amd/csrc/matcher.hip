@@ -76,7 +76,8 @@ Prof g_prof;
 const char* kKindNames[K_NUM_KINDS] = {
     "transpose_in", "gat", "qkv_gemm", "kv_reduce", "m_fold", "mlp1_gemm",
     "stats_finalize", "mlp2_gemm", "final_gemm", "l2norm", "score_gemm", "softmax_reduce",
-    "conf", "mutual", "select", "pnp_ransac", "pnp_refit", "pose_error", "sample_desc"};
+    "conf", "mutual", "select", "pnp_ransac", "pnp_refit", "pose_error", "sample_desc",
+    "sp_conv", "sp_nms", "sp_select", "sp_desc"};
 }  // namespace
 
 StampAcc* prof_stamp_slot(int kind) {

@@ -226,3 +226,46 @@ def make_matcher_inputs(n1: int, n3: int, num_leaf: int = 8, seed: int = 0, batc
         "descriptors3d_db": np.broadcast_to(avg[None], (batch,) + avg.shape).copy(),
         "descriptors2d_db": np.broadcast_to(leaves[None], (batch,) + leaves.shape).copy(),
     }, obj, frames
+
+
+# ------------------------------------------------------------------ SuperPoint
+SUPERPOINT_LAYERS = [   # (name, c_in, c_out, kernel)  superpoint.py:147-162
+    ("conv1a", 1, 64, 3), ("conv1b", 64, 64, 3), ("conv2a", 64, 64, 3), ("conv2b", 64, 64, 3),
+    ("conv3a", 64, 128, 3), ("conv3b", 128, 128, 3), ("conv4a", 128, 128, 3),
+    ("conv4b", 128, 128, 3), ("convPa", 128, 256, 3), ("convPb", 256, 65, 1),
+    ("convDa", 128, 256, 3), ("convDb", 256, 256, 1)]
+
+# the reference extraction config (extract_features.py:19-24); note 'keypoints_threshold'
+# is not a key SuperPoint reads, so its default keypoint_threshold 0.005 applies
+SUPERPOINT_CONF = {"descriptor_dim": 256, "nms_radius": 3, "max_keypoints": 4096,
+                   "keypoints_threshold": 0.6}
+
+
+def superpoint_state_dict(seed: int = 0) -> dict[str, np.ndarray]:
+    """Random SuperPoint weights (numpy RandomState, version-stable): He-uniform convs,
+    small biases.  The trained weights (superpoint_v1.pth) are not available offline."""
+    rs = np.random.RandomState(9000 + seed)
+    sd = {}
+    for name, cin, cout, k in SUPERPOINT_LAYERS:
+        bound = np.sqrt(6.0 / (cin * k * k))
+        sd[f"{name}.weight"] = rs.uniform(-bound, bound, (cout, cin, k, k)).astype(np.float32)
+        sd[f"{name}.bias"] = rs.uniform(-0.05, 0.05, cout).astype(np.float32)
+    return sd
+
+
+def superpoint_image(h: int, w: int, seed: int = 0) -> np.ndarray:
+    """A grayscale test image in [0, 1] ([h, w] float32): smooth blobs, edges and texture,
+    so the detector finds distinct local maxima."""
+    rs = np.random.RandomState(7000 + seed)
+    yy, xx = np.mgrid[0:h, 0:w].astype(np.float64)
+    img = np.zeros((h, w))
+    for _ in range(24):
+        cy, cx = rs.uniform(0, h), rs.uniform(0, w)
+        s = rs.uniform(2.0, 9.0)
+        img += rs.uniform(-1, 1) * np.exp(-((yy - cy) ** 2 + (xx - cx) ** 2) / (2 * s * s))
+    for _ in range(6):
+        a, b, c = rs.uniform(-1, 1, 3)
+        img += 0.3 * (a * (yy - h / 2) + b * (xx - w / 2) + c * h > 0)
+    img += 0.05 * rs.randn(h, w)
+    img = (img - img.min()) / (img.max() - img.min())
+    return img.astype(np.float32)

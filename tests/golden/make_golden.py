@@ -8,6 +8,7 @@ box; the fixtures travel instead):
 What is imported from the reference (read-only, nothing copied):
   * src.models.GATsSPG_architectures.GATs_SuperGlue.GATsSuperGlue  (torch only)
   * src.models.extractors.SuperPoint.superpoint.sample_descriptors (torch only)
+  * src.models.extractors.SuperPoint.superpoint.SuperPoint           (torch only)
   * src.evaluators.cmd_evaluator.Evaluator                         (numpy only)
   * src.utils.data_utils.{pad_features3d_random, build_features3d_leaves} (numpy/torch; the
     module's unrelated top-level cv2 / loguru imports are satisfied by empty placeholder
@@ -223,6 +224,41 @@ def object_case():
     np.savez_compressed(os.path.join(HERE, "object_leaves.npz"), **out)
 
 
+def superpoint_case():
+    """SuperPoint.forward (superpoint.py:170-224) with the extraction config of
+    extract_features.py:19-24 on seeded synthetic weights and images; also the dense score map
+    (after softmax + pixel shuffle, before NMS) and the normalised dense descriptors, computed
+    with the reference module's own layers in its forward order."""
+    from src.models.extractors.SuperPoint.superpoint import SuperPoint
+    out = {}
+    for tag, h, w, seed, max_kp in (("sq", 128, 128, 0, 4096), ("topk", 96, 160, 1, 300)):
+        conf = dict(synthetic.SUPERPOINT_CONF, max_keypoints=max_kp)
+        m = SuperPoint(conf).eval()
+        sd = synthetic.superpoint_state_dict(seed)
+        m.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
+        img = torch.from_numpy(synthetic.superpoint_image(h, w, seed))[None, None]
+        with torch.no_grad():
+            pred = m(img)
+            r = torch.relu
+            x = r(m.conv1b(r(m.conv1a(img))))
+            x = m.pool(x)
+            x = m.pool(r(m.conv2b(r(m.conv2a(x)))))
+            x = m.pool(r(m.conv3b(r(m.conv3a(x)))))
+            x = r(m.conv4b(r(m.conv4a(x))))
+            sc = torch.nn.functional.softmax(m.convPb(r(m.convPa(x))), 1)[:, :-1]
+            b, _, hc, wc = sc.shape
+            sc = sc.permute(0, 2, 3, 1).reshape(b, hc, wc, 8, 8)
+            sc = sc.permute(0, 1, 3, 2, 4).reshape(b, hc * 8, wc * 8)
+            dd = torch.nn.functional.normalize(m.convDb(r(m.convDa(x))), p=2, dim=1)
+        out[f"{tag}_keypoints"] = pred["keypoints"][0].numpy()
+        out[f"{tag}_scores"] = pred["scores"][0].numpy()
+        out[f"{tag}_descriptors"] = pred["descriptors"][0].numpy()
+        out[f"{tag}_score_map"] = sc[0].numpy()
+        out[f"{tag}_dense_desc"] = dd[0].numpy()
+        out[f"{tag}_weights_sha"] = sha(*[sd[k] for k in sorted(sd)])
+    np.savez_compressed(os.path.join(HERE, "superpoint.npz"), **out)
+
+
 def main():
     assert os.path.isdir(REF), "the reference is only available in the build container"
     sys.path.insert(0, REF)
@@ -241,6 +277,7 @@ def main():
     sample_desc_case()
     evaluator_case()
     object_case()
+    superpoint_case()
 
 
 if __name__ == "__main__":

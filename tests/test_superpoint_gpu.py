@@ -1,0 +1,128 @@
+"""SuperPoint on the GPU (onepose_superpoint / onepose_superpoint_detect) against the
+reference's own outputs (tests/golden/superpoint.npz) and the numpy oracle.
+
+Bars: the detector tail (NMS, threshold, borders, top-k, flip) is integer/selection work and
+must be bit-exact given the same score map; the convolutions are fp32 with a different
+summation order than the reference, so the score map is compared at rtol 1e-4 / atol 1e-6
+and the dense / sampled descriptors at atol 2e-5; the end-to-end keypoints of the golden
+cases must equal the reference's."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden
+from onepose_amd import synthetic
+from onepose_amd.superpoint import SuperPoint, detect_from_maps
+from oracle import superpoint_np as O
+
+pytestmark = pytest.mark.gpu
+CASES = {"sq": (128, 128, 0, 4096), "topk": (96, 160, 1, 300)}
+CONF = dict(nms_radius=3, keypoint_threshold=0.005, remove_borders=4)
+
+
+def model(seed, max_kp, device, **kw):
+    m = SuperPoint({**CONF, "max_keypoints": max_kp, **kw})
+    m.load_state_dict(synthetic.superpoint_state_dict(seed))
+    return m.eval().to(device)
+
+
+def first(raw, i=0):
+    n = int(raw["counts"][i])
+    return (raw["keypoints"][i, :n].cpu().numpy(), raw["scores"][i, :n].cpu().numpy(),
+            raw["descriptors"][i, :, :n].cpu().numpy(), n)
+
+
+@pytest.mark.parametrize("tag", sorted(CASES))
+def test_detect_tail_bit_exact_on_reference_maps(tag, device):
+    _, _, _, max_kp = CASES[tag]
+    g = golden("superpoint")
+    smap = torch.from_numpy(g[f"{tag}_score_map"])[None].to(device)
+    dense = torch.from_numpy(g[f"{tag}_dense_desc"]).permute(1, 2, 0)[None].contiguous().to(device)
+    raw = detect_from_maps(smap, dense, max_keypoints=max_kp, align_corners=False, **CONF)
+    kp, sc, desc, n = first(raw)
+    np.testing.assert_array_equal(kp, g[f"{tag}_keypoints"])
+    np.testing.assert_array_equal(sc, g[f"{tag}_scores"])
+    np.testing.assert_allclose(desc, g[f"{tag}_descriptors"], atol=1e-6)
+    k = raw["keypoints"].shape[1]
+    if n < k:   # capacity past the count is zero-filled
+        assert not raw["keypoints"][0, n:].any() and not raw["descriptors"][0, :, n:].any()
+
+
+@pytest.mark.parametrize("tag", sorted(CASES))
+def test_end_to_end_matches_reference(tag, device):
+    h, w, seed, max_kp = CASES[tag]
+    g = golden("superpoint")
+    m = model(seed, max_kp, device)
+    img = torch.from_numpy(synthetic.superpoint_image(h, w, seed))[None, None].to(device)
+    raw = m.detect_raw(img, score_map=True, dense=True)
+    np.testing.assert_allclose(raw["score_map"][0].cpu().numpy(), g[f"{tag}_score_map"],
+                               rtol=1e-4, atol=1e-6)
+    np.testing.assert_allclose(raw["dense"][0].permute(2, 0, 1).cpu().numpy(),
+                               g[f"{tag}_dense_desc"], atol=2e-5)
+    kp, sc, desc, _ = first(raw)
+    np.testing.assert_array_equal(kp, g[f"{tag}_keypoints"])
+    np.testing.assert_allclose(sc, g[f"{tag}_scores"], rtol=1e-4, atol=1e-7)
+    np.testing.assert_allclose(desc, g[f"{tag}_descriptors"], atol=2e-5)
+    # the reference interface: per-image lists
+    out = m(img)
+    assert len(out["keypoints"]) == 1
+    np.testing.assert_array_equal(out["keypoints"][0].cpu().numpy(), g[f"{tag}_keypoints"])
+    assert out["descriptors"][0].shape == (256, len(g[f"{tag}_keypoints"]))
+
+
+def test_tail_matches_oracle_on_own_score_map(device):
+    """At OnePose's 512x512 crop size: the GPU's keypoints are exactly the oracle tail applied
+    to the GPU's own score map (size-independent chain check), for top-k and raster order."""
+    m = model(2, 4096, device)
+    img = torch.from_numpy(synthetic.superpoint_image(512, 512, 2))[None, None].to(device)
+    for max_kp in (4096, 500, -1):
+        m.config["max_keypoints"] = max_kp
+        raw = m.detect_raw(img, score_map=True, dense=True)
+        smap = raw["score_map"][0].cpu().numpy()
+        kp_o, sc_o = O.select_keypoints(O.simple_nms(smap, 3), 0.005, 4, max_kp)
+        kp, sc, desc, n = first(raw)
+        np.testing.assert_array_equal(kp, kp_o)
+        np.testing.assert_array_equal(sc, sc_o)
+        dense = raw["dense"][0].permute(2, 0, 1).cpu().numpy()
+        d_o = O.sample_descriptors(kp_o[None], dense[None], 8, False)[0]
+        np.testing.assert_allclose(desc, d_o, atol=1e-6)
+
+
+def test_score_map_matches_oracle_256(device):
+    m = model(3, 1024, device)
+    img = synthetic.superpoint_image(256, 192, 3)
+    raw = m.detect_raw(torch.from_numpy(img)[None, None].to(device), score_map=True, dense=True)
+    sd = synthetic.superpoint_state_dict(3)
+    x = O.encoder(sd, img)
+    np.testing.assert_allclose(raw["score_map"][0].cpu().numpy(), O.score_map(sd, x),
+                               rtol=1e-4, atol=1e-6)
+    np.testing.assert_allclose(raw["dense"][0].permute(2, 0, 1).cpu().numpy(),
+                               O.dense_descriptors(sd, x), atol=2e-5)
+
+
+def test_batch_equals_single_images(device):
+    m = model(0, 400, device)
+    imgs = [synthetic.superpoint_image(128, 160, s) for s in (4, 5, 6)]
+    batch = m.detect_raw(torch.from_numpy(np.stack(imgs))[:, None].to(device))
+    for i, im in enumerate(imgs):
+        one = m.detect_raw(torch.from_numpy(im)[None, None].to(device))
+        for a, b in zip(first(batch, i), first(one)):
+            np.testing.assert_array_equal(np.asarray(a), np.asarray(b))
+
+
+def test_blank_image_has_no_keypoints(device):
+    m = model(0, 64, device)
+    raw = m.detect_raw(torch.zeros(1, 1, 64, 64, device=device), score_map=True)
+    smap = raw["score_map"][0].cpu().numpy()
+    kp_o, _ = O.select_keypoints(O.simple_nms(smap, 3), 0.005, 4, 64)
+    assert int(raw["counts"][0]) == len(kp_o)
+
+
+def test_rejects_unsupported_inputs(device):
+    m = model(0, 64, device)
+    with pytest.raises(ValueError):
+        m.detect_raw(torch.zeros(1, 1, 60, 64, device=device))
+    with pytest.raises(RuntimeError):
+        m.detect_raw(torch.zeros(1, 1, 64, 64))
+    with pytest.raises(ValueError):
+        SuperPoint({"max_keypoints": 0})
