@@ -57,28 +57,41 @@ struct ConvArgs {
   StampAcc* stamp;
 };
 
-constexpr int CBM = 64, CBK = 32, CPITCH = CBK + 4;
+constexpr int CBK = 32, CPITCH = CBK + 4;
 
-template <int BN>
+// Tile shape: WM x WN waves, each owning 32 rows x 32*FN output channels.
+template <int WM_, int WN_, int FN_>
+struct ConvTile {
+  static constexpr int WM = WM_, WN = WN_, FN = FN_;
+  static constexpr int BM = 32 * WM, BN = 32 * FN * WN, NT = 64 * WM * WN;
+  static constexpr int AV = BM * 8 / NT, WV = BN * 8 / NT;   // float4 loads per thread
+  static constexpr int STAGE = (BM + BN) * CPITCH;
+  static_assert(AV >= 1 && WV >= 1 && BM * 8 % NT == 0 && BN * 8 % NT == 0, "tile/threads");
+};
+using TileBig = ConvTile<2, 2, 1>;    // 64 x 64, 256 threads: the 512^2 .. 128^2 layers
+using TileSmall = ConvTile<1, 2, 1>;  // 32 x 64, 128 threads: the 64^2 layers (fills 256 CUs)
+using TileHead = ConvTile<1, 2, 2>;   // 32 x 128, 128 threads: convPb's 65 logits
+
+template <class TL>
 struct ConvStage {
-  float4 a[2];
-  float4 w[BN / 32];
-  bool ok[2];
+  float4 a[TL::AV];
+  float4 w[TL::WV];
+  int ok;   // bit i: A row i is inside the image (else zero padding)
 };
 
 // Pixel of tile row m: raster order, or (POOL) pooled pixel m>>2 and its 2x2 input m&3.
-template <bool POOL>
+template <bool POOL, int BM>
 __device__ __forceinline__ void row_pixel(const ConvArgs& a, int mt, int m, int& y, int& x,
                                           bool& valid) {
   if (!POOL) {
-    const int p = mt * CBM + m;
+    const int p = mt * BM + m;
     valid = p < a.H * a.W;
     const int pc = valid ? p : 0;
     y = pc / a.W;
     x = pc - y * a.W;
   } else {
     const int wp = a.W >> 1, hp = a.H >> 1;
-    const int pp = mt * (CBM / 4) + (m >> 2);
+    const int pp = mt * (BM / 4) + (m >> 2);
     valid = pp < hp * wp;
     const int pc = valid ? pp : 0;
     const int py = pc / wp, px = pc - py * wp;
@@ -87,52 +100,62 @@ __device__ __forceinline__ void row_pixel(const ConvArgs& a, int mt, int m, int&
   }
 }
 
-template <int BN, bool POOL, int EPI>
-__global__ __launch_bounds__(256) void conv_kernel(ConvArgs a) {
-  constexpr int FN = BN / 64;
-  constexpr int STAGE = (CBM + BN) * CPITCH;
-  __shared__ __attribute__((aligned(16))) float lds[2 * STAGE];
+template <int CIN, int KS, class TL, bool POOL, int EPI>
+__global__ __launch_bounds__(TL::NT) void conv_kernel(ConvArgs a) {
+  constexpr int BM = TL::BM, BN = TL::BN, NT = TL::NT, FN = TL::FN;
+  constexpr int CH = CIN / CBK, TAPS = KS * KS, NK = TAPS * CH, HALF = KS / 2;
+  static_assert(NK % 2 == 0, "stage count must be even");
+  __shared__ __attribute__((aligned(16))) float lds[2 * TL::STAGE];
   stamp_begin(a.stamp);
   const int b = blockIdx.y;
   const int mt = blockIdx.x / a.ntiles, nt = blockIdx.x - mt * a.ntiles;
   const int n0 = nt * BN;
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6, wm = wave >> 1, wn = wave & 1;
-  const float* X = a.x + b * a.x_bs;
-  const int taps = a.ks * a.ks, half = a.ks >> 1;
-  const int chunks = a.cin / CBK;
-  const int nk = taps * chunks;
-  const int kq = (t & 7) * 4;
-  int py[2], px[2];
-  bool pv[2];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int wm = wave / TL::WN, wn = wave - wm * TL::WN;
+  const int kq = (t & 7) * 4, r0 = t >> 3;
+  constexpr int RSTEP = NT / 8;   // rows covered by one load instruction
+  const float* X = a.x + (int64_t)b * a.x_bs + kq;
+  int py[TL::AV], px[TL::AV], roff[TL::AV];
+  bool pv[TL::AV];
 #pragma unroll
-  for (int i = 0; i < 2; ++i) row_pixel<POOL>(a, mt, (t >> 3) + 32 * i, py[i], px[i], pv[i]);
+  for (int i = 0; i < TL::AV; ++i) {
+    row_pixel<POOL, BM>(a, mt, r0 + RSTEP * i, py[i], px[i], pv[i]);
+    roff[i] = (py[i] * a.W + px[i]) * CIN;
+  }
+  const float* Wt = a.w + (n0 + r0) * (TAPS * CIN) + kq;
 
-  auto load = [&](int s, ConvStage<BN>& st) __attribute__((always_inline)) {
-    const int tap = s / chunks, c0 = (s - tap * chunks) * CBK;
-    const int dy = tap / a.ks - half, dx = tap - (tap / a.ks) * a.ks - half;
+  auto load = [&](int s, ConvStage<TL>& st) __attribute__((always_inline)) {
+    const int tap = s / CH, c0 = (s - tap * CH) * CBK;
+    const int dy = tap / KS - HALF, dx = tap - (tap / KS) * KS - HALF;
+    const int delta = (dy * a.W + dx) * CIN + c0;
+    int ok = 0;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int yy = py[i] + dy, xx = px[i] + dx;
-      st.ok[i] = pv[i] && yy >= 0 && yy < a.H && xx >= 0 && xx < a.W;   // zero padding
-      const int yc = min(max(yy, 0), a.H - 1), xc = min(max(xx, 0), a.W - 1);
-      st.a[i] = *reinterpret_cast<const float4*>(X + ((int64_t)yc * a.W + xc) * a.cin + c0 + kq);
+    for (int i = 0; i < TL::AV; ++i) {
+      const bool in = pv[i] & ((unsigned)(py[i] + dy) < (unsigned)a.H) &
+                      ((unsigned)(px[i] + dx) < (unsigned)a.W);
+      ok |= in ? (1 << i) : 0;
+      st.a[i] = *reinterpret_cast<const float4*>(X + roff[i] + (in ? delta : c0));
     }
+    st.ok = ok;
 #pragma unroll
-    for (int i = 0; i < BN / 32; ++i) {
-      const int o = n0 + (t >> 3) + 32 * i;   // cout_pad rows exist for every tile row
-      st.w[i] = *reinterpret_cast<const float4*>(a.w + ((int64_t)o * taps + tap) * a.cin + c0 + kq);
-    }
+    for (int i = 0; i < TL::WV; ++i)
+      st.w[i] = *reinterpret_cast<const float4*>(Wt + (i * RSTEP) * (TAPS * CIN) + tap * CIN + c0);
   };
-  auto store = [&](float* la, ConvStage<BN>& st) __attribute__((always_inline)) {
-    float* lw = la + CBM * CPITCH;
+  auto store = [&](float* la, const ConvStage<TL>& st) __attribute__((always_inline)) {
+    float* lw = la + BM * CPITCH;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
-      *reinterpret_cast<float4*>(la + ((t >> 3) + 32 * i) * CPITCH + kq) = st.ok[i] ? st.a[i] : z;
+    for (int i = 0; i < TL::AV; ++i) {
+      float4 v = st.a[i];
+      const bool in = (st.ok >> i) & 1;
+      v.x = in ? v.x : 0.f;
+      v.y = in ? v.y : 0.f;
+      v.z = in ? v.z : 0.f;
+      v.w = in ? v.w : 0.f;
+      *reinterpret_cast<float4*>(la + (r0 + RSTEP * i) * CPITCH + kq) = v;
     }
 #pragma unroll
-    for (int i = 0; i < BN / 32; ++i)
-      *reinterpret_cast<float4*>(lw + ((t >> 3) + 32 * i) * CPITCH + kq) = st.w[i];
+    for (int i = 0; i < TL::WV; ++i)
+      *reinterpret_cast<float4*>(lw + (r0 + RSTEP * i) * CPITCH + kq) = st.w[i];
   };
 
   floatx16 acc[FN];
@@ -141,17 +164,17 @@ __global__ __launch_bounds__(256) void conv_kernel(ConvArgs a) {
 #pragma unroll
     for (int i = 0; i < 16; ++i) acc[j][i] = 0.f;
 
-  ConvStage<BN> s0, s1;
+  ConvStage<TL> s0, s1;
   load(0, s0);
-  load(min(1, nk - 1), s1);
+  load(1, s1);
   store(lds, s0);
   __syncthreads();
-  auto step = [&](int kt, ConvStage<BN>& next, ConvStage<BN>& spare)
+  auto step = [&](int kt, ConvStage<TL>& next, ConvStage<TL>& spare)
       __attribute__((always_inline)) {
-    load(min(kt + 2, nk - 1), spare);
-    const float* la = lds + (kt & 1) * STAGE;
+    load(min(kt + 2, NK - 1), spare);
+    const float* la = lds + (kt & 1) * TL::STAGE;
     const float* pa = la + (wm * 32 + (lane & 31)) * CPITCH + (lane >> 5) * 4;
-    const float* pw = la + CBM * CPITCH + (wn * (BN / 2) + (lane & 31)) * CPITCH + (lane >> 5) * 4;
+    const float* pw = la + BM * CPITCH + (wn * 32 * FN + (lane & 31)) * CPITCH + (lane >> 5) * 4;
 #pragma unroll
     for (int kk = 0; kk < CBK / 8; ++kk) {
       const float4 av = *reinterpret_cast<const float4*>(pa + kk * 8);
@@ -164,53 +187,53 @@ __global__ __launch_bounds__(256) void conv_kernel(ConvArgs a) {
         acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av.w, wv.w, acc[j], 0, 0, 0);
       }
     }
-    store(lds + ((kt + 1) & 1) * STAGE, next);   // (unused after the last stage)
+    store(lds + ((kt + 1) & 1) * TL::STAGE, next);   // (unused after the last stage)
     __syncthreads();
   };
-  for (int kt = 0; kt < nk; kt += 2) {   // nk even: taps x cin/32 with cin % 64 == 0
+  for (int kt = 0; kt < NK; kt += 2) {
     step(kt, s1, s0);
     step(kt + 1, s0, s1);
   }
 
-  float* Y = a.y + b * a.y_bs;
+  float* Y = a.y + (int64_t)b * a.y_bs;
   if (EPI != CE_SOFTMAX) {
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
-      const int n = n0 + wn * (BN / 2) + j * 32 + (lane & 31);
+      const int n = n0 + wn * 32 * FN + j * 32 + (lane & 31);
       const bool n_ok = n < a.cout;
       const float bias = n_ok ? a.bias[n] : 0.f;
       if (!POOL) {
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
           const int m = wm * 32 + (i & 3) + 8 * (i >> 2) + 4 * (lane >> 5);
-          const int p = mt * CBM + m;
+          const int p = mt * BM + m;
           float v = acc[j][i] + bias;
           if (EPI == CE_RELU) v = fmaxf(v, 0.f);
-          if (n_ok && p < a.H * a.W) Y[(int64_t)p * a.cout + n] = v;
+          if (n_ok && p < a.H * a.W) Y[p * a.cout + n] = v;
         }
       } else {
         const int hp = a.H >> 1, wp = a.W >> 1;
 #pragma unroll
         for (int g = 0; g < 4; ++g) {   // registers 4g..4g+3 = one 2x2 window
           const int m = wm * 32 + 8 * g + 4 * (lane >> 5);
-          const int pp = mt * (CBM / 4) + (m >> 2);
+          const int pp = mt * (BM / 4) + (m >> 2);
           float v = fmaxf(fmaxf(acc[j][4 * g], acc[j][4 * g + 1]),
                           fmaxf(acc[j][4 * g + 2], acc[j][4 * g + 3])) + bias;
           if (EPI == CE_RELU) v = fmaxf(v, 0.f);   // relu(max(.)) == max(relu(.))
-          if (n_ok && pp < hp * wp) Y[(int64_t)pp * a.cout + n] = v;
+          if (n_ok && pp < hp * wp) Y[pp * a.cout + n] = v;
         }
       }
     }
     stamp_end(a.stamp);
     return;
   }
-  // CE_SOFTMAX: 64 cells x 65 logits -> softmax over 65, drop the dustbin, pixel shuffle
+  // CE_SOFTMAX: BM cells x 65 logits -> softmax over 65, drop the dustbin, pixel shuffle
   // (scores.permute(0,2,3,1).reshape(b,h,w,8,8).permute(0,1,3,2,4).reshape(b,8h,8w), :181-183)
-  static_assert(EPI != CE_SOFTMAX || BN == 128, "softmax head tile holds all 65 logits");
-  float* tile = lds;   // [64][129]
+  static_assert(EPI != CE_SOFTMAX || (BN == 128 && NT == 4 * BM), "softmax head tile");
+  float* tile = lds;   // [BM][129]
 #pragma unroll
   for (int j = 0; j < FN; ++j) {
-    const int n = wn * (BN / 2) + j * 32 + (lane & 31);
+    const int n = wn * 32 * FN + j * 32 + (lane & 31);
     const float bias = n < a.cout ? a.bias[n] : 0.f;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
@@ -226,53 +249,57 @@ __global__ __launch_bounds__(256) void conv_kernel(ConvArgs a) {
     for (int c = 0; c < 65; ++c) mx = fmaxf(mx, row[c]);
     float sum = 0.f;
     for (int c = 0; c < 65; ++c) sum += expf(row[c] - mx);
-    const int p = mt * CBM + m;
+    const int p = mt * BM + m;
     if (p < a.H * a.W) {
       const int cy = p / a.W, cx = p - cy * a.W;
       const int W8 = a.W * 8;
 #pragma unroll
       for (int cc = 0; cc < 16; ++cc) {
         const int c = q * 16 + cc;
-        Y[(int64_t)(cy * 8 + (c >> 3)) * W8 + cx * 8 + (c & 7)] = expf(row[c] - mx) / sum;
+        Y[(cy * 8 + (c >> 3)) * W8 + cx * 8 + (c & 7)] = expf(row[c] - mx) / sum;
       }
     }
   }
   stamp_end(a.stamp);
 }
 
-// conv1a (1 -> 64, 3x3, pad 1) + ReLU, direct: one thread per pixel, weights in LDS.
+// conv1a (1 -> 64, 3x3, pad 1) + ReLU, direct: 16 threads per pixel, 4 output channels each,
+// so a wave writes 4 whole NHWC pixels (1 KB) per store; each thread keeps its 36 weights.
 __global__ __launch_bounds__(256) void conv1a_kernel(const float* __restrict__ img, int64_t img_bs,
                                                      const float* __restrict__ w,
                                                      const float* __restrict__ bias, int H, int W,
                                                      float* __restrict__ y, int64_t y_bs) {
-  __shared__ float sw[64 * 9], sb[64];
-  for (int i = threadIdx.x; i < 64 * 9; i += 256) sw[i] = w[i];
-  if (threadIdx.x < 64) sb[threadIdx.x] = bias[threadIdx.x];
-  __syncthreads();
-  const int b = blockIdx.y;
-  const int p = blockIdx.x * 256 + threadIdx.x;
-  if (p >= H * W) return;
-  const int py = p / W, px = p - py * W;
-  const float* I = img + b * img_bs;
-  float v[9];
+  const int b = blockIdx.y, g = threadIdx.x & 15;
+  float wr[4][9], br[4];
 #pragma unroll
-  for (int k = 0; k < 9; ++k) {
-    const int yy = py + k / 3 - 1, xx = px + k % 3 - 1;
-    v[k] = (yy >= 0 && yy < H && xx >= 0 && xx < W) ? I[yy * W + xx] : 0.f;
+  for (int j = 0; j < 4; ++j) {
+#pragma unroll
+    for (int k = 0; k < 9; ++k) wr[j][k] = w[(4 * g + j) * 9 + k];
+    br[j] = bias[4 * g + j];
   }
-  float4* out = reinterpret_cast<float4*>(y + b * y_bs + (int64_t)p * 64);
+  const float* I = img + b * img_bs;
+  float* Y = y + b * y_bs;
+  constexpr int kPix = 4;   // pixels per thread group, amortising the weight loads
 #pragma unroll
-  for (int c4 = 0; c4 < 16; ++c4) {
-    float r[4];
+  for (int r = 0; r < kPix; ++r) {
+    const int p = (blockIdx.x * kPix + r) * 16 + (threadIdx.x >> 4);
+    if (p >= H * W) return;
+    const int py = p / W, px = p - py * W;
+    float v[9];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+      const int yy = py + k / 3 - 1, xx = px + k % 3 - 1;
+      v[k] = (yy >= 0 && yy < H && xx >= 0 && xx < W) ? I[yy * W + xx] : 0.f;
+    }
+    float o[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const int c = c4 * 4 + j;
       float s = 0.f;
 #pragma unroll
-      for (int k = 0; k < 9; ++k) s += v[k] * sw[c * 9 + k];
-      r[j] = fmaxf(s + sb[c], 0.f);
+      for (int k = 0; k < 9; ++k) s += v[k] * wr[j][k];
+      o[j] = fmaxf(s + br[j], 0.f);
     }
-    out[c4] = make_float4(r[0], r[1], r[2], r[3]);
+    *reinterpret_cast<float4*>(Y + (int64_t)p * 64 + 4 * g) = make_float4(o[0], o[1], o[2], o[3]);
   }
 }
 
@@ -336,8 +363,81 @@ __global__ __launch_bounds__(256) void nms_kernel(NmsArgs a) {
   }
 }
 
+// simple_nms fused: one 32x32 output tile per workgroup evaluates all five max-pool passes
+// in LDS over windows that shrink by R per pass, from scores loaded with a 5R halo.  Arrays
+// live in tile coordinates [E][E]; positions outside the image are -inf to every pool, as
+// max_pool2d's padding is.  Writes max_mask (0/1) for the tile.
+template <int R>
+__global__ __launch_bounds__(256) void nms_fused_kernel(NmsArgs a) {
+  constexpr int E = NT + 10 * R, K = 2 * R + 1;
+  __shared__ float S[E * E], M[E * E], SP[E * E], SS[E * E], TMP[E * E];
+  const int b = blockIdx.z, gy0 = blockIdx.y * NT - 5 * R, gx0 = blockIdx.x * NT - 5 * R;
+  const int64_t o = b * a.bs;
+  auto inside = [&](int y, int x) {
+    return (unsigned)(gy0 + y) < (unsigned)a.H && (unsigned)(gx0 + x) < (unsigned)a.W;
+  };
+  for (int e = threadIdx.x; e < E * E; e += 256) {
+    const int y = e / E, x = e - y * E;
+    S[e] = inside(y, x) ? a.s[o + (int64_t)(gy0 + y) * a.W + gx0 + x] : -INFINITY;
+  }
+  __syncthreads();
+  // max_pool(IN) over the window [lo, E - lo)^2 into TMP (rows then columns, via TMP rows)
+  auto pool = [&](const float* IN, int lo, auto&& finish) {
+    const int hi = E - lo, n = hi - lo;
+    float* rowm = TMP;   // rows [lo - R, hi + R) x cols [lo, hi)
+    for (int e = threadIdx.x; e < (n + 2 * R) * n; e += 256) {
+      const int y = lo - R + e / n, x = lo + e % n;
+      float m = -INFINITY;
+#pragma unroll
+      for (int d = 0; d < K; ++d) m = fmaxf(m, IN[y * E + x - R + d]);
+      rowm[y * E + x] = m;
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < n * n; e += 256) {
+      const int y = lo + e / n, x = lo + e % n;
+      float m = -INFINITY;
+#pragma unroll
+      for (int d = 0; d < K; ++d) m = fmaxf(m, rowm[(y - R + d) * E + x]);
+      finish(y * E + x, m, inside(y, x));
+    }
+    __syncthreads();
+  };
+  // mask = scores == max_pool(scores)
+  pool(S, R, [&](int i, float m, bool in) { M[i] = in ? (S[i] == m ? 1.f : 0.f) : -INFINITY; });
+  for (int it = 0; it < 2; ++it) {
+    // supp = max_pool(mask) > 0; ss = supp ? 0 : scores
+    pool(M, (2 + 2 * it) * R, [&](int i, float m, bool in) {
+      SP[i] = m > 0.f ? 1.f : 0.f;
+      SS[i] = in ? (m > 0.f ? 0.f : S[i]) : -INFINITY;
+    });
+    // mask |= (ss == max_pool(ss)) & ~supp
+    pool(SS, (3 + 2 * it) * R, [&](int i, float m, bool in) {
+      if (in && SS[i] == m && SP[i] == 0.f) M[i] = 1.f;
+    });
+  }
+  for (int e = threadIdx.x; e < NT * NT; e += 256) {
+    const int y = 5 * R + e / NT, x = 5 * R + e % NT;
+    if (inside(y, x)) a.mask[o + (int64_t)(gy0 + y) * a.W + gx0 + x] = M[y * E + x] > 0.f ? 1.f : 0.f;
+  }
+}
+
 // ---- keypoint selection: threshold + borders, raster-order compaction, top-k ----
+// Candidates (score > threshold after NMS, outside the border) are compacted in raster order
+// (torch.nonzero's order).  When more than max_keypoints survive, torch.topk(k) keeps the k
+// best in descending order: a 16384-bin histogram of the scores' order-preserving keys (binned
+// over the sample's own key range, so bins hold a handful of candidates) finds the cutoff
+// bin; every candidate at or above it is scattered into bin-descending order, and
+// its final position is its bin's start plus the number of bin mates with a larger key
+// (score, then lower raster index first).  Equal scores therefore keep raster order.
 constexpr int kSelChunk = 4096;
+constexpr int kCutBins = 16384;      // histogram bins over [min key, max key]
+constexpr int kCutBits = 14;
+constexpr int kMaxBinRank = 2048;    // larger tie bins take the single-workgroup sort path
+constexpr int kMaxSortKeys = 16384;  // LDS sort capacity of that path (128 KB of keys)
+constexpr int kUnroll = 8;           // candidate loads in flight per thread
+
+enum SelMode { SEL_DONE = 0, SEL_RANK = 1, SEL_SORT = 2 };
+
 struct SelArgs {
   const float* s;       // scores [B][H][W]
   const float* mask;    // NMS max_mask
@@ -348,15 +448,40 @@ struct SelArgs {
   int* chunk_count;     // [B][chunks]
   int* chunk_off;       // [B][chunks]
   int* total;           // [B]
+  int* mode;            // [B] SelMode
+  int* n_cut;           // [B] candidates at or above the cutoff bin
   float* cand_score;    // [B][H*W] raster-order candidates
   int* cand_idx;
+  unsigned long long* cut_key;   // [B][H*W] cutoff set, bin-descending
+  int2* cut_range;      // [B][H*W] the element's bin range in cut_key
   float* kpts;          // [B][max_kp][2] (x, y)
   float* kscores;       // [B][max_kp]
   int* counts;          // [B]
 };
 
+// Order-preserving uint key of a float (any sign), and its inverse.
+__device__ __forceinline__ unsigned ord_key(float v) {
+  const unsigned u = __float_as_uint(v);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float ord_val(unsigned k) {
+  return __uint_as_float((k & 0x80000000u) ? (k & 0x7FFFFFFFu) : ~k);
+}
+// Sort key: score descending, then raster index ascending.
+__device__ __forceinline__ unsigned long long sort_key(unsigned ordv, int idx) {
+  return ((unsigned long long)ordv << 32) | (0xFFFFFFFFu - (unsigned)idx);
+}
+__device__ __forceinline__ void emit(const SelArgs& a, int b, int slot,
+                                     unsigned long long key) {
+  const int p = (int)(0xFFFFFFFFu - (unsigned)(key & 0xFFFFFFFFull));
+  float* kp = a.kpts + ((int64_t)b * a.max_kp + slot) * 2;
+  kp[0] = (float)(p % a.W);   // flip (y, x) -> (x, y)
+  kp[1] = (float)(p / a.W);
+  a.kscores[(int64_t)b * a.max_kp + slot] = ord_val((unsigned)(key >> 32));
+}
+
 __device__ __forceinline__ bool is_cand(const SelArgs& a, int64_t o, int p, float& v) {
-  const int y = p / a.W, x = p - (p / a.W) * a.W;
+  const int y = p / a.W, x = p - y * a.W;
   // nms score = where(max_mask, scores, 0) > threshold; remove_borders (:66-76)
   v = a.mask[o + p] != 0.f ? a.s[o + p] : 0.f;
   return v > a.thr && y >= a.border && y < a.H - a.border && x >= a.border &&
@@ -378,15 +503,28 @@ __global__ __launch_bounds__(256) void sel_count_kernel(SelArgs a) {
   if (threadIdx.x == 0) a.chunk_count[b * a.chunks + ch] = red[0] + red[1] + red[2] + red[3];
 }
 
-__global__ __launch_bounds__(64) void sel_scan_kernel(SelArgs a) {
-  const int b = blockIdx.x;
-  if (threadIdx.x != 0) return;
-  int run = 0;
-  for (int c = 0; c < a.chunks; ++c) {
-    a.chunk_off[b * a.chunks + c] = run;
-    run += a.chunk_count[b * a.chunks + c];
+// Exclusive scan of the chunk counts (one workgroup per sample).
+__global__ __launch_bounds__(256) void sel_scan_kernel(SelArgs a) {
+  __shared__ int sc[256];
+  const int b = blockIdx.x, t = threadIdx.x;
+  const int per = (a.chunks + 255) / 256, c0 = t * per, c1 = min(c0 + per, a.chunks);
+  const int* cnt = a.chunk_count + (int64_t)b * a.chunks;
+  int sum = 0;
+  for (int c = c0; c < c1; ++c) sum += cnt[c];
+  sc[t] = sum;
+  __syncthreads();
+  for (int off = 1; off < 256; off <<= 1) {   // inclusive scan
+    const int v = t >= off ? sc[t - off] : 0;
+    __syncthreads();
+    sc[t] += v;
+    __syncthreads();
   }
-  a.total[b] = run;
+  int run = sc[t] - sum;
+  for (int c = c0; c < c1; ++c) {
+    a.chunk_off[(int64_t)b * a.chunks + c] = run;
+    run += cnt[c];
+  }
+  if (t == 255) a.total[b] = sc[255];
 }
 
 // Scatter candidates in raster order: each wave compacts 64 pixels with a ballot.
@@ -396,10 +534,10 @@ __global__ __launch_bounds__(256) void sel_scatter_kernel(SelArgs a) {
   const int64_t o = b * a.bs;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int p0 = ch * kSelChunk;
-  // pass 1: per (wave, round) counts; rounds cover 256 pixels each
-  constexpr int R = kSelChunk / 256;
+  constexpr int R = kSelChunk / 256;   // rounds of 256 pixels
   bool c[R];
   float v[R];
+#pragma unroll
   for (int rr = 0; rr < R; ++rr) {
     const int p = p0 + rr * 256 + wave * 64 + lane;
     c[rr] = p < a.H * a.W && is_cand(a, o, p, v[rr]);
@@ -419,6 +557,7 @@ __global__ __launch_bounds__(256) void sel_scatter_kernel(SelArgs a) {
   __syncthreads();
   float* cs = a.cand_score + o;
   int* ci = a.cand_idx + o;
+#pragma unroll
   for (int rr = 0; rr < R; ++rr) {
     const unsigned long long bal = __ballot(c[rr]);
     if (c[rr]) {
@@ -429,103 +568,153 @@ __global__ __launch_bounds__(256) void sel_scatter_kernel(SelArgs a) {
   }
 }
 
-// One workgroup per sample.  total <= max_kp: the candidates as they are (raster order, the
-// reference's nonzero order).  Otherwise torch.topk(k): radix-select the k-th largest score
-// on its bit pattern (scores > 0), gather the winners (ties by raster index) and bitonic-sort
-// them by (score desc, raster index asc) in LDS.
-__global__ __launch_bounds__(1024) void sel_final_kernel(SelArgs a) {
-  extern __shared__ unsigned long long keys[];   // [pow2 >= max_kp]
-  __shared__ int hist[256];
-  __shared__ unsigned prefix_s, mask_s;
-  __shared__ int need_s, ngt_s, neq_s;
+// One workgroup per sample: raster output when total <= k; otherwise the cutoff histogram and
+// the bin-grouped cutoff set for sel_rank (or SEL_SORT when a tie bin is too large).
+__global__ __launch_bounds__(1024) void sel_cut_kernel(SelArgs a) {
+  __shared__ int cnt[kCutBins];     // per-bin count, then a countdown cursor
+  __shared__ int start[kCutBins];   // candidates in higher bins
+  __shared__ int tsum[1024];
+  __shared__ int cut_bin, max_bin;
+  __shared__ unsigned kmin, kmax;
   const int b = blockIdx.x, t = threadIdx.x;
   const int total = a.total[b], k = a.max_kp;
   const int64_t o = b * a.bs;
   const float* cs = a.cand_score + o;
   const int* ci = a.cand_idx + o;
-  float* kp = a.kpts + (int64_t)b * k * 2;
-  float* ks = a.kscores + (int64_t)b * k;
   if (total <= k) {
     for (int i = t; i < k; i += 1024) {
       const bool on = i < total;
       const int p = on ? ci[i] : 0;
-      kp[2 * i] = on ? (float)(p % a.W) : 0.f;   // flip (y, x) -> (x, y)
-      kp[2 * i + 1] = on ? (float)(p / a.W) : 0.f;
-      ks[i] = on ? cs[i] : 0.f;
+      float* kp = a.kpts + ((int64_t)b * k + i) * 2;
+      kp[0] = on ? (float)(p % a.W) : 0.f;   // flip (y, x) -> (x, y)
+      kp[1] = on ? (float)(p / a.W) : 0.f;
+      a.kscores[(int64_t)b * k + i] = on ? cs[i] : 0.f;
     }
-    if (t == 0) a.counts[b] = total;
+    if (t == 0) {
+      a.counts[b] = total;
+      a.mode[b] = SEL_DONE;
+      a.n_cut[b] = 0;
+    }
     return;
   }
-  // radix select: the k-th largest bit pattern, 8 bits at a time from the top
+  for (int i = t; i < kCutBins; i += 1024) cnt[i] = 0;
   if (t == 0) {
-    prefix_s = 0u;
-    mask_s = 0u;
-    need_s = k;
+    max_bin = 0;
+    kmin = 0xFFFFFFFFu;
+    kmax = 0u;
   }
-  for (int shift = 24; shift >= 0; shift -= 8) {
-    for (int i = t; i < 256; i += 1024) hist[i] = 0;
-    __syncthreads();
-    const unsigned pre = prefix_s, msk = mask_s;
-    for (int i = t; i < total; i += 1024) {
-      const unsigned u = __float_as_uint(cs[i]);
-      if ((u & msk) == pre) atomicAdd(&hist[(u >> shift) & 255], 1);
-    }
-    __syncthreads();
-    if (t == 0) {
-      int need = need_s, d = 255;
-      for (; d > 0; --d) {
-        if (hist[d] >= need) break;
-        need -= hist[d];
-      }
-      prefix_s = pre | ((unsigned)d << shift);
-      mask_s = msk | (255u << shift);
-      need_s = need;   // how many of the bin's pattern (the threshold) are still needed
-    }
-    __syncthreads();
-  }
-  const unsigned thr_u = prefix_s;
-  if (t == 0) {
-    ngt_s = 0;
-    neq_s = 0;
-  }
-  int P = 1;
-  while (P < k) P <<= 1;
-  for (int i = t; i < P; i += 1024) keys[i] = 0ull;
   __syncthreads();
-  // winners: every score above the threshold, and the first need_s equal to it (raster order)
-  const int n_eq = need_s;
-  const int n_gt = k - n_eq;
-  for (int base = 0; base < total; base += 1024) {
-    const int i = base + t;
-    const unsigned u = i < total ? __float_as_uint(cs[i]) : 0u;
-    const bool gt = i < total && u > thr_u, eq = i < total && u == thr_u;
-    // equal ones must be taken in raster order: rank them within this round, in order
-    __shared__ int eq_rank[1024];
-    eq_rank[t] = eq ? 1 : 0;
+  {   // key range -> bin = (key - kmin) >> shift, monotone, at most kCutBins bins
+    unsigned lo = 0xFFFFFFFFu, hi = 0u;
+    for (int base = t; base < total; base += 1024 * kUnroll) {   // independent loads in flight
+      float v[kUnroll];
+#pragma unroll
+      for (int j = 0; j < kUnroll; ++j) v[j] = base + 1024 * j < total ? cs[base + 1024 * j] : cs[t];
+#pragma unroll
+      for (int j = 0; j < kUnroll; ++j) {
+        const unsigned u = ord_key(v[j]);
+        lo = min(lo, u);
+        hi = max(hi, u);
+      }
+    }
+    atomicMin(&kmin, lo);
+    atomicMax(&kmax, hi);
+  }
+  __syncthreads();
+  const unsigned k0 = kmin, span = kmax - kmin;
+  const int shift = span == 0u ? 0 : max(0, 32 - __clz((int)span) - kCutBits);
+  auto bin_of = [&](unsigned u) { return (int)((u - k0) >> shift); };
+  for (int base = t; base < total; base += 1024 * kUnroll) {
+    float v[kUnroll];
+#pragma unroll
+    for (int j = 0; j < kUnroll; ++j) v[j] = base + 1024 * j < total ? cs[base + 1024 * j] : 0.f;
+#pragma unroll
+    for (int j = 0; j < kUnroll; ++j)
+      if (base + 1024 * j < total) atomicAdd(&cnt[bin_of(ord_key(v[j]))], 1);
+  }
+  __syncthreads();
+  constexpr int PER = kCutBins / 1024;   // thread t owns bins [PER t, PER t + PER)
+  int own = 0;
+#pragma unroll
+  for (int j = 0; j < PER; ++j) own += cnt[PER * t + j];
+  tsum[t] = own;
+  __syncthreads();
+  for (int off = 1; off < 1024; off <<= 1) {   // inclusive suffix scan over threads
+    const int v = t + off < 1024 ? tsum[t + off] : 0;
     __syncthreads();
-    for (int off = 1; off < 1024; off <<= 1) {   // inclusive scan
-      const int v = t >= off ? eq_rank[t - off] : 0;
-      __syncthreads();
-      eq_rank[t] += v;
-      __syncthreads();
-    }
-    const int eq_before = neq_s;
-    if (gt) {
-      const int slot = atomicAdd(&ngt_s, 1);
-      keys[slot] = ((unsigned long long)u << 32) | (0xFFFFFFFFu - (unsigned)ci[i]);
-    }
-    if (eq) {
-      const int r = eq_before + eq_rank[t] - 1;
-      if (r < n_eq) keys[n_gt + r] = ((unsigned long long)u << 32) | (0xFFFFFFFFu - (unsigned)ci[i]);
-    }
-    __syncthreads();
-    if (t == 1023) neq_s = eq_before + eq_rank[1023];
+    tsum[t] += v;
     __syncthreads();
   }
-  // bitonic sort, descending by key (score desc, raster index asc)
+  {
+    int run = tsum[t] - own;
+    for (int j = PER - 1; j >= 0; --j) {
+      const int bin = PER * t + j, c = cnt[bin];
+      start[bin] = run;
+      if (run < k && run + c >= k) cut_bin = bin;
+      run += c;
+    }
+  }
+  __syncthreads();
+  const int cb = cut_bin;
+  const int n = start[cb] + cnt[cb];   // read before the scatter counts cnt down
+  {
+    int m = 0;
+    for (int j = 0; j < PER; ++j) {
+      const int bin = PER * t + j;
+      if (bin >= cb) m = max(m, cnt[bin]);
+    }
+    atomicMax(&max_bin, m);
+  }
+  __syncthreads();
+  if (t == 0) {
+    a.counts[b] = k;
+    a.n_cut[b] = n;
+    a.mode[b] = max_bin > kMaxBinRank ? SEL_SORT : SEL_RANK;
+  }
+  if (max_bin > kMaxBinRank) return;
+  unsigned long long* key = a.cut_key + o;
+  int2* range = a.cut_range + o;
+  for (int base = t; base < total; base += 1024 * kUnroll) {
+    float v[kUnroll];
+    int idx[kUnroll];
+#pragma unroll
+    for (int j = 0; j < kUnroll; ++j) {
+      const bool on = base + 1024 * j < total;
+      v[j] = on ? cs[base + 1024 * j] : 0.f;
+      idx[j] = on ? ci[base + 1024 * j] : 0;
+    }
+#pragma unroll
+    for (int j = 0; j < kUnroll; ++j) {
+      const unsigned u = ord_key(v[j]);
+      const int bin = bin_of(u);
+      if (base + 1024 * j >= total || bin < cb) continue;
+      const int s0 = start[bin], s1 = bin > 0 ? start[bin - 1] : total;   // bin's range
+      const int pos = s0 + atomicSub(&cnt[bin], 1) - 1;
+      key[pos] = sort_key(u, idx[j]);
+      range[pos] = make_int2(s0, s1);
+    }
+  }
+}
+
+// Final position of each cutoff-set element: its bin's start plus the bin mates with a
+// larger key.  Positions >= k are dropped (they can only come from the cutoff bin).
+__global__ __launch_bounds__(256) void sel_rank_kernel(SelArgs a) {
+  const int b = blockIdx.y, e = blockIdx.x * 256 + threadIdx.x;
+  if (a.mode[b] != SEL_RANK || e >= a.n_cut[b]) return;
+  const int64_t o = b * a.bs;
+  const unsigned long long* key = a.cut_key + o;
+  const unsigned long long me = key[e];
+  const int2 r = a.cut_range[o + e];
+  int rank = r.x;
+  for (int f = r.x; f < r.y; ++f) rank += key[f] > me ? 1 : 0;
+  if (rank < a.max_kp) emit(a, b, rank, me);
+}
+
+// Bitonic sort of keys[0, P) descending (P a power of two), whole workgroup.
+__device__ void bitonic_desc(unsigned long long* keys, int P) {
   for (int size = 2; size <= P; size <<= 1)
     for (int stride = size >> 1; stride > 0; stride >>= 1) {
-      for (int i = t; i < P; i += 1024) {
+      for (int i = threadIdx.x; i < P; i += blockDim.x) {
         const int j = i ^ stride;
         if (j > i) {
           const unsigned long long ki = keys[i], kj = keys[j];
@@ -538,14 +727,81 @@ __global__ __launch_bounds__(1024) void sel_final_kernel(SelArgs a) {
       }
       __syncthreads();
     }
-  for (int i = t; i < k; i += 1024) {
-    const unsigned long long key = keys[i];
-    const int p = (int)(0xFFFFFFFFu - (unsigned)(key & 0xFFFFFFFFull));
-    kp[2 * i] = (float)(p % a.W);
-    kp[2 * i + 1] = (float)(p / a.W);
-    ks[i] = __uint_as_float((unsigned)(key >> 32));
+}
+
+// SEL_SORT (a tie bin larger than kMaxBinRank): exact radix select of the k-th largest key
+// over the candidates, the first winners among equal keys in raster order, and a bitonic
+// sort of the k winners in LDS.  One workgroup per sample.
+__global__ __launch_bounds__(1024) void sel_sort_kernel(SelArgs a) {
+  extern __shared__ unsigned long long keys[];   // [kMaxSortKeys]
+  __shared__ int tsum[1024];
+  __shared__ int hist[256];
+  __shared__ unsigned prefix_s, mask_s;
+  __shared__ int need_s, ngt_s, neq_s;
+  const int b = blockIdx.x, t = threadIdx.x;
+  if (a.mode[b] != SEL_SORT) return;
+  const int total = a.total[b], k = a.max_kp;
+  const int64_t o = b * a.bs;
+  const float* cs = a.cand_score + o;
+  const int* ci = a.cand_idx + o;
+  if (t == 0) {
+    prefix_s = 0u;
+    mask_s = 0u;
+    need_s = k;
+    ngt_s = 0;
+    neq_s = 0;
   }
-  if (t == 0) a.counts[b] = k;
+  for (int shift = 24; shift >= 0; shift -= 8) {
+    for (int i = t; i < 256; i += 1024) hist[i] = 0;
+    __syncthreads();
+    const unsigned pre = prefix_s, msk = mask_s;
+    for (int i = t; i < total; i += 1024) {
+      const unsigned u = ord_key(cs[i]);
+      if ((u & msk) == pre) atomicAdd(&hist[(u >> shift) & 255], 1);
+    }
+    __syncthreads();
+    if (t == 0) {
+      int need = need_s, d = 255;
+      for (; d > 0; --d) {
+        if (hist[d] >= need) break;
+        need -= hist[d];
+      }
+      prefix_s = pre | ((unsigned)d << shift);
+      mask_s = msk | (255u << shift);
+      need_s = need;
+    }
+    __syncthreads();
+  }
+  const unsigned thr_u = prefix_s;
+  int P = 1;
+  while (P < k) P <<= 1;
+  for (int i = t; i < P; i += 1024) keys[i] = 0ull;
+  __syncthreads();
+  const int n_eq = need_s, n_gt = k - n_eq;
+  for (int base = 0; base < total; base += 1024) {   // equal keys: first n_eq in raster order
+    const int i = base + t;
+    const unsigned u = i < total ? ord_key(cs[i]) : 0u;
+    const bool gt = i < total && u > thr_u, eq = i < total && u == thr_u;
+    tsum[t] = eq ? 1 : 0;
+    __syncthreads();
+    for (int off = 1; off < 1024; off <<= 1) {
+      const int v = t >= off ? tsum[t - off] : 0;
+      __syncthreads();
+      tsum[t] += v;
+      __syncthreads();
+    }
+    const int eq_before = neq_s;
+    if (gt) keys[atomicAdd(&ngt_s, 1)] = sort_key(u, ci[i]);
+    if (eq) {
+      const int r = eq_before + tsum[t] - 1;
+      if (r < n_eq) keys[n_gt + r] = sort_key(u, ci[i]);
+    }
+    __syncthreads();
+    if (t == 1023) neq_s = eq_before + tsum[1023];
+    __syncthreads();
+  }
+  bitonic_desc(keys, P);
+  for (int i = t; i < k; i += 1024) emit(a, b, i, keys[i]);
 }
 
 // ---- descriptors: normalise the dense map per cell, then sample at the keypoints ----
@@ -561,7 +817,7 @@ __global__ __launch_bounds__(256) void desc_norm_kernel(float* d, int cells) {
 
 // sample_descriptors (superpoint.py:95-113) on the NHWC dense map [h][w][256]: one wave per
 // keypoint (4 channels per lane), the same arithmetic order as frame_ops.hip's NCHW kernel;
-// 64 keypoints per workgroup are written through LDS as [256][k] columns.
+// 16 keypoints per workgroup are written through LDS as [256][k] columns.
 __global__ __launch_bounds__(256) void sample_nhwc_kernel(const float* __restrict__ kpts,
                                                           const int* __restrict__ counts,
                                                           const float* __restrict__ dense,
@@ -569,12 +825,13 @@ __global__ __launch_bounds__(256) void sample_nhwc_kernel(const float* __restric
                                                           int align_corners,
                                                           float* __restrict__ out) {
 #pragma clang fp contract(off)
-  __shared__ float tile[256][65];
+  constexpr int KPB = 16;   // keypoints per workgroup
+  __shared__ float tile[256][KPB + 1];
   const int b = blockIdx.y, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int k0 = blockIdx.x * 64;
+  const int k0 = blockIdx.x * KPB;
   const int cnt = counts[b];
   const float* D = dense + (int64_t)b * h * w * 256;
-  for (int kk = wave; kk < 64; kk += 4) {
+  for (int kk = wave; kk < KPB; kk += 4) {
     const int k = k0 + kk;
     float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
     if (k < cnt) {
@@ -625,8 +882,8 @@ __global__ __launch_bounds__(256) void sample_nhwc_kernel(const float* __restric
   }
   __syncthreads();
   float* O = out + (int64_t)b * 256 * max_kp;
-  for (int e = threadIdx.x; e < 256 * 64; e += 256) {
-    const int c = e >> 6, kk = e & 63;
+  for (int e = threadIdx.x; e < 256 * KPB; e += 256) {
+    const int c = e / KPB, kk = e % KPB;
     if (k0 + kk < max_kp) O[(int64_t)c * max_kp + k0 + kk] = tile[c][kk];
   }
 }
@@ -635,7 +892,9 @@ __global__ __launch_bounds__(256) void sample_nhwc_kernel(const float* __restric
 struct DetPlan {   // NMS + selection scratch
   float *mask, *supp, *ss;        // [H][W]
   float* cand_score;
-  int *cand_idx, *chunk_count, *chunk_off, *total;
+  int *cand_idx, *chunk_count, *chunk_off, *total, *mode, *n_cut;
+  unsigned long long* cut_key;
+  int2* cut_range;
 };
 struct SpPlan {
   float *f0, *f1;                 // ping-pong feature maps (largest: H*W*64)
@@ -658,6 +917,10 @@ DetPlan det_plan(Carve& c, int B, int H, int W) {
   p.chunk_count = c.take<int>((size_t)B * chunks);
   p.chunk_off = c.take<int>((size_t)B * chunks);
   p.total = c.take<int>(B);
+  p.mode = c.take<int>(B);
+  p.n_cut = c.take<int>(B);
+  p.cut_key = c.take<unsigned long long>(B * hw);
+  p.cut_range = c.take<int2>(B * hw);
   return p;
 }
 
@@ -682,10 +945,14 @@ size_t det_bytes(int B, int H, int W) {
   return align_up(c.off, 256);
 }
 
-template <int BN, bool POOL, int EPI>
+template <int CIN, int KS, class TL, bool POOL, int EPI>
 int conv_launch(const float* x, int B, int H, int W, const float* packed, int layer, float* y,
                 hipStream_t st) {
   const SpLayer& L = kSp[layer];
+  if (L.cin != CIN || L.k != KS || L.cout_pad % TL::BN != 0) {
+    set_error("superpoint: layer %s does not fit its conv instantiation", kSpNames[layer]);
+    return ONEPOSE_ERR_INVALID;
+  }
   ConvArgs a;
   a.x = x;
   a.x_bs = (int64_t)H * W * L.cin;
@@ -698,12 +965,12 @@ int conv_launch(const float* x, int B, int H, int W, const float* packed, int la
   a.cout = L.cout;
   a.ks = L.k;
   const int pix = POOL ? (H / 2) * (W / 2) : H * W;
-  a.mtiles = ceil_div(pix, POOL ? CBM / 4 : CBM);
-  a.ntiles = L.cout_pad / BN;
+  a.mtiles = ceil_div(pix, POOL ? TL::BM / 4 : TL::BM);
+  a.ntiles = L.cout_pad / TL::BN;
   a.stamp = prof_stamp_slot(K_SP_CONV);
   a.y_bs = EPI == CE_SOFTMAX ? (int64_t)H * W * 64 : (int64_t)pix * L.cout;
-  OP_LAUNCH(K_SP_CONV, st, (conv_kernel<BN, POOL, EPI>), dim3(a.mtiles * a.ntiles, B), dim3(256),
-            0, st, a);
+  OP_LAUNCH(K_SP_CONV, st, (conv_kernel<CIN, KS, TL, POOL, EPI>), dim3(a.mtiles * a.ntiles, B),
+            dim3(TL::NT), 0, st, a);
   return ONEPOSE_OK;
 }
 
@@ -735,10 +1002,18 @@ int detect_impl(const float* score, const float* dense, int B, int h, int w, int
   //                                        mask |= (ss == mp(ss)) & ~supp }
   NmsArgs na{score, p.mask, p.supp, p.ss, h, w, nms_radius, (int64_t)h * w};
   const dim3 ng(ceil_div(w, NT), ceil_div(h, NT), B);
-  OP_LAUNCH(K_SP_NMS, st, nms_kernel<NMS_INIT>, ng, dim3(256), 0, st, na);
-  for (int it = 0; it < 2; ++it) {
-    OP_LAUNCH(K_SP_NMS, st, nms_kernel<NMS_SUPP>, ng, dim3(256), 0, st, na);
-    OP_LAUNCH(K_SP_NMS, st, nms_kernel<NMS_GROW>, ng, dim3(256), 0, st, na);
+  switch (nms_radius) {   // fused single pass for the radii OnePose uses; 5 launches beyond
+    case 0: OP_LAUNCH(K_SP_NMS, st, nms_fused_kernel<0>, ng, dim3(256), 0, st, na); break;
+    case 1: OP_LAUNCH(K_SP_NMS, st, nms_fused_kernel<1>, ng, dim3(256), 0, st, na); break;
+    case 2: OP_LAUNCH(K_SP_NMS, st, nms_fused_kernel<2>, ng, dim3(256), 0, st, na); break;
+    case 3: OP_LAUNCH(K_SP_NMS, st, nms_fused_kernel<3>, ng, dim3(256), 0, st, na); break;
+    case 4: OP_LAUNCH(K_SP_NMS, st, nms_fused_kernel<4>, ng, dim3(256), 0, st, na); break;
+    default:
+      OP_LAUNCH(K_SP_NMS, st, nms_kernel<NMS_INIT>, ng, dim3(256), 0, st, na);
+      for (int it = 0; it < 2; ++it) {
+        OP_LAUNCH(K_SP_NMS, st, nms_kernel<NMS_SUPP>, ng, dim3(256), 0, st, na);
+        OP_LAUNCH(K_SP_NMS, st, nms_kernel<NMS_GROW>, ng, dim3(256), 0, st, na);
+      }
   }
   SelArgs sa;
   sa.s = score;
@@ -753,29 +1028,33 @@ int detect_impl(const float* score, const float* dense, int B, int h, int w, int
   sa.chunk_count = p.chunk_count;
   sa.chunk_off = p.chunk_off;
   sa.total = p.total;
+  sa.mode = p.mode;
+  sa.n_cut = p.n_cut;
+  sa.cut_key = p.cut_key;
+  sa.cut_range = p.cut_range;
   sa.cand_score = p.cand_score;
   sa.cand_idx = p.cand_idx;
   sa.kpts = keypoints;
   sa.kscores = scores;
   sa.counts = counts;
   OP_LAUNCH(K_SP_SELECT, st, sel_count_kernel, dim3(sa.chunks, B), dim3(256), 0, st, sa);
-  OP_LAUNCH(K_SP_SELECT, st, sel_scan_kernel, dim3(B), dim3(64), 0, st, sa);
+  OP_LAUNCH(K_SP_SELECT, st, sel_scan_kernel, dim3(B), dim3(256), 0, st, sa);
   OP_LAUNCH(K_SP_SELECT, st, sel_scatter_kernel, dim3(sa.chunks, B), dim3(256), 0, st, sa);
-  size_t shm = 0;
-  if (max_kp <= kMaxSortKeypoints) {
-    int P2 = 1;
-    while (P2 < max_kp) P2 <<= 1;
-    shm = (size_t)P2 * 8;
+  OP_LAUNCH(K_SP_SELECT, st, sel_cut_kernel, dim3(B), dim3(1024), 0, st, sa);
+  if (max_kp <= kMaxSortKeypoints) {   // otherwise max_kp >= h*w: never more candidates
+    // the cutoff set holds at most k - 1 + kMaxBinRank elements in SEL_RANK mode
+    OP_LAUNCH(K_SP_SELECT, st, sel_rank_kernel, dim3(ceil_div(max_kp + kMaxBinRank, 256), B),
+              dim3(256), 0, st, sa);
+    static bool attr_set = false;
+    if (!attr_set) {
+      OP_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(sel_sort_kernel),
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, kMaxSortKeys * 8));
+      attr_set = true;
+    }
+    OP_LAUNCH(K_SP_SELECT, st, sel_sort_kernel, dim3(B), dim3(1024), (size_t)kMaxSortKeys * 8, st,
+              sa);
   }
-  static bool attr_set = false;
-  if (!attr_set) {
-    OP_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(sel_final_kernel),
-                               hipFuncAttributeMaxDynamicSharedMemorySize,
-                               kMaxSortKeypoints * 8));
-    attr_set = true;
-  }
-  OP_LAUNCH(K_SP_SELECT, st, sel_final_kernel, dim3(B), dim3(1024), shm, st, sa);
-  OP_LAUNCH(K_SP_DESC, st, sample_nhwc_kernel, dim3(ceil_div(max_kp, 64), B), dim3(256), 0, st,
+  OP_LAUNCH(K_SP_DESC, st, sample_nhwc_kernel, dim3(ceil_div(max_kp, 16), B), dim3(256), 0, st,
             keypoints, counts, dense, max_kp, h / 8, w / 8, 8, align_corners, descriptors);
   return ONEPOSE_OK;
 }
@@ -850,23 +1129,35 @@ int onepose_superpoint(const void* packed, const float* image, int batch, int h,
   const float* P = static_cast<const float*>(packed);
   const int B = batch;
   // shared encoder: conv1a, [1b+pool], 2a, [2b+pool], 3a, [3b+pool], 4a, 4b
-  OP_LAUNCH(K_SP_CONV, st, conv1a_kernel, dim3(ceil_div(h * w, 256), B), dim3(256), 0, st, image,
+  OP_LAUNCH(K_SP_CONV, st, conv1a_kernel, dim3(ceil_div(h * w, 64), B), dim3(256), 0, st, image,
             (int64_t)h * w, P + layer_offset(0), P + layer_offset(0) + 64 * 9, h, w, p.f0,
             (int64_t)h * w * 64);
-  if ((rc = conv_launch<64, true, CE_RELU>(p.f0, B, h, w, P, 1, p.f1, st))) return rc;
-  if ((rc = conv_launch<64, false, CE_RELU>(p.f1, B, h / 2, w / 2, P, 2, p.f0, st))) return rc;
-  if ((rc = conv_launch<64, true, CE_RELU>(p.f0, B, h / 2, w / 2, P, 3, p.f1, st))) return rc;
-  if ((rc = conv_launch<64, false, CE_RELU>(p.f1, B, h / 4, w / 4, P, 4, p.f0, st))) return rc;
-  if ((rc = conv_launch<64, true, CE_RELU>(p.f0, B, h / 4, w / 4, P, 5, p.f1, st))) return rc;
-  if ((rc = conv_launch<64, false, CE_RELU>(p.f1, B, h / 8, w / 8, P, 6, p.f0, st))) return rc;
-  if ((rc = conv_launch<64, false, CE_RELU>(p.f0, B, h / 8, w / 8, P, 7, p.x4, st))) return rc;
+  if ((rc = conv_launch<64, 3, TileBig, true, CE_RELU>(p.f0, B, h, w, P, 1, p.f1, st))) return rc;
+  if ((rc = conv_launch<64, 3, TileBig, false, CE_RELU>(p.f1, B, h / 2, w / 2, P, 2, p.f0, st)))
+    return rc;
+  if ((rc = conv_launch<64, 3, TileBig, true, CE_RELU>(p.f0, B, h / 2, w / 2, P, 3, p.f1, st)))
+    return rc;
+  if ((rc = conv_launch<64, 3, TileBig, false, CE_RELU>(p.f1, B, h / 4, w / 4, P, 4, p.f0, st)))
+    return rc;
+  if ((rc = conv_launch<128, 3, TileBig, true, CE_RELU>(p.f0, B, h / 4, w / 4, P, 5, p.f1, st)))
+    return rc;
+  if ((rc = conv_launch<128, 3, TileSmall, false, CE_RELU>(p.f1, B, h / 8, w / 8, P, 6, p.f0, st)))
+    return rc;
+  if ((rc = conv_launch<128, 3, TileSmall, false, CE_RELU>(p.f0, B, h / 8, w / 8, P, 7, p.x4, st)))
+    return rc;
   // score head: convPa + ReLU, convPb -> softmax(65)[:64] -> pixel shuffle -> [H][W]
-  if ((rc = conv_launch<64, false, CE_RELU>(p.x4, B, h / 8, w / 8, P, 8, p.head, st))) return rc;
-  if ((rc = conv_launch<128, false, CE_SOFTMAX>(p.head, B, h / 8, w / 8, P, 9, p.score, st)))
+  if ((rc = conv_launch<128, 3, TileSmall, false, CE_RELU>(p.x4, B, h / 8, w / 8, P, 8, p.head,
+                                                           st)))
+    return rc;
+  if ((rc = conv_launch<256, 1, TileHead, false, CE_SOFTMAX>(p.head, B, h / 8, w / 8, P, 9,
+                                                             p.score, st)))
     return rc;
   // descriptor head: convDa + ReLU, convDb, normalise (the score head's hidden map is dead)
-  if ((rc = conv_launch<64, false, CE_RELU>(p.x4, B, h / 8, w / 8, P, 10, p.head, st))) return rc;
-  if ((rc = conv_launch<64, false, CE_BIAS>(p.head, B, h / 8, w / 8, P, 11, p.dense, st)))
+  if ((rc = conv_launch<128, 3, TileSmall, false, CE_RELU>(p.x4, B, h / 8, w / 8, P, 10, p.head,
+                                                           st)))
+    return rc;
+  if ((rc = conv_launch<256, 1, TileSmall, false, CE_BIAS>(p.head, B, h / 8, w / 8, P, 11,
+                                                           p.dense, st)))
     return rc;
   const int cells = B * (h / 8) * (w / 8);
   OP_LAUNCH(K_SP_DESC, st, desc_norm_kernel, dim3(ceil_div(cells, 4)), dim3(256), 0, st, p.dense,

@@ -126,3 +126,48 @@ def test_rejects_unsupported_inputs(device):
         m.detect_raw(torch.zeros(1, 1, 64, 64))
     with pytest.raises(ValueError):
         SuperPoint({"max_keypoints": 0})
+
+
+def _dense(h, w, seed):
+    d = np.random.RandomState(seed).standard_normal((1, h // 8, w // 8, 256)).astype(np.float32)
+    return d / np.linalg.norm(d, axis=-1, keepdims=True)
+
+
+@pytest.mark.parametrize("spacing,max_kp", [(2, 1000), (5, 3000), (9, 100)])
+def test_topk_with_tied_scores_matches_oracle(spacing, max_kp, device):
+    """Equal scores straddling the top-k cutoff: the winners are the lowest raster indices.
+    spacing 2 puts 65k equal peaks in one histogram bin (the exact radix-select path);
+    the others exercise the histogram-cutoff path with ties at the boundary."""
+    h = w = 512
+    rs = np.random.RandomState(spacing)
+    s = np.zeros((h, w), np.float32)
+    ys, xs = np.meshgrid(np.arange(0, h, spacing), np.arange(0, w, spacing), indexing="ij")
+    levels = np.array([0.5, 0.25, 0.125], np.float32) if spacing > 2 else np.array([0.5], np.float32)
+    s[ys, xs] = levels[rs.randint(0, len(levels), ys.shape)]
+    dense = _dense(h, w, spacing)
+    raw = detect_from_maps(torch.from_numpy(s)[None].to(device), torch.from_numpy(dense).to(device),
+                           max_keypoints=max_kp, align_corners=False, **CONF)
+    kp_o, sc_o = O.select_keypoints(O.simple_nms(s, 3), 0.005, 4, max_kp)
+    kp, sc, desc, n = first(raw)
+    assert n == len(kp_o)
+    np.testing.assert_array_equal(kp, kp_o)
+    np.testing.assert_array_equal(sc, sc_o)
+    d_o = O.sample_descriptors(kp_o[None], dense.transpose(0, 3, 1, 2), 8, False)[0]
+    np.testing.assert_allclose(desc, d_o, atol=1e-6)
+
+
+@pytest.mark.parametrize("radius", [0, 1, 2, 4, 5, 8])
+def test_nms_radius_matches_oracle(radius, device):
+    """Fused single-launch NMS (radius <= 4) and the five-launch path (5..8), on the
+    reference's score map with a ragged 96x160 frame; raster-order output (no top-k)."""
+    g = golden("superpoint")
+    s = g["topk_score_map"]
+    dense = torch.from_numpy(g["topk_dense_desc"]).permute(1, 2, 0)[None].contiguous().to(device)
+    raw = detect_from_maps(torch.from_numpy(s)[None].to(device), dense, nms_radius=radius,
+                           keypoint_threshold=0.005, remove_borders=4, max_keypoints=-1,
+                           align_corners=False)
+    kp_o, sc_o = O.select_keypoints(O.simple_nms(s, radius), 0.005, 4, -1)
+    kp, sc, _, n = first(raw)
+    assert n == len(kp_o)
+    np.testing.assert_array_equal(kp, kp_o)
+    np.testing.assert_array_equal(sc, sc_o)
