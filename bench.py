@@ -8,6 +8,8 @@ before the timed region; nothing is cached across steps.
 
     python bench.py [--gpus N --steps K --warmup W]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N  (one rank/GPU)
+    python bench.py --e2e      (extra measurement: each step starts from 512x512 images --
+                                SuperPoint on the GPU produces the 1k query keypoints)
 
 Multi-GPU: frames are independent given the object, so each rank runs its own frames
 (weak scaling) and the only exchange is one all-gather of per-frame poses and cm/deg flags
@@ -32,6 +34,15 @@ FP32_MFMA_PEAK_TFLOPS = 157.3     # MI355X_MICROARCH.md: f32-input MFMA dense pe
 HBM_PEAK_GBS = 8000.0             # MI355X_MICROARCH.md: HBM3E spec
 # kernels that record device stamps (onepose_profile_begin_device): timeable inside graphs
 STAMPED = {"qkv_gemm", "mlp1_gemm", "mlp2_gemm", "final_gemm", "score_gemm"}
+
+
+def superpoint_conv_flops(h, w):
+    """Algorithmic FLOPs of SuperPoint's MFMA convolutions for one h x w image
+    (superpoint.py:147-162; conv1a, a direct kernel, excluded; convPb at its 65 outputs)."""
+    layers = [(1, 64, 64, 3), (2, 64, 64, 3), (2, 64, 64, 3), (4, 64, 128, 3), (4, 128, 128, 3),
+              (8, 128, 128, 3), (8, 128, 128, 3), (8, 128, 256, 3), (8, 256, 65, 1),
+              (8, 128, 256, 3), (8, 256, 256, 1)]   # (downsampling, cin, cout, k) from conv1b
+    return sum(2 * (h // d) * (w // d) * co * ci * k * k for d, ci, co, k in layers)
 
 
 def kernel_work(kind, B, n1, n3, L):
@@ -94,8 +105,9 @@ def run_profiled(lib, pipe, steps, mask, cap):
     return kinds[:n], ms[:n]
 
 
-def cpu_baseline(sd, data, frames, obj, seconds=15.0):
-    """The oracle (numpy matcher + C RANSAC-EPnP) on the host, bounded to ~`seconds`."""
+def cpu_baseline(sd, data, frames, obj, seconds=15.0, detector_image=None):
+    """The oracle (numpy matcher + C RANSAC-EPnP) on the host, bounded to ~`seconds`; with
+    `detector_image` also one SuperPoint oracle pass per frame (timed once)."""
     from oracle import matcher_np as M
     from oracle import pnp_oracle as O
     threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
@@ -111,9 +123,21 @@ def cpu_baseline(sd, data, frames, obj, seconds=15.0):
         if time.perf_counter() - t0 > seconds or n >= 8:
             break
     dt = time.perf_counter() - t0
-    return {"value": n / dt, "unit": "frames/s", "cores": threads, "kind": "port",
-            "sample": f"{n} frame(s) of the timed workload (matcher + RANSAC-EPnP) on the "
-                      f"oracle (numpy float32 GATsSPG restatement + C EPnP), {dt:.1f} s"}
+    per_frame = dt / n
+    sample = (f"{n} frame(s) of the timed workload (matcher + RANSAC-EPnP) on the oracle "
+              f"(numpy float32 GATsSPG restatement + C EPnP), {dt:.1f} s")
+    if detector_image is not None:
+        from onepose_amd import synthetic
+        from oracle import superpoint_np as SP
+        t1 = time.perf_counter()
+        SP.forward(synthetic.superpoint_state_dict(0), detector_image, nms_radius=3,
+                   keypoint_threshold=0.005, remove_borders=4,
+                   max_keypoints=data["keypoints2d"].shape[1])
+        t_sp = time.perf_counter() - t1
+        per_frame += t_sp
+        sample += f"; plus SuperPoint oracle (numpy) on one image: {t_sp:.1f} s"
+    return {"value": 1.0 / per_frame, "unit": "frames/s", "cores": threads, "kind": "port",
+            "sample": sample}
 
 
 def main():
@@ -138,6 +162,10 @@ def main():
     ap.add_argument("--eager", action="store_true",
                     help="launch every kernel from the host each step instead of replaying "
                          "captured HIP graphs")
+    ap.add_argument("--e2e", action="store_true",
+                    help="start each step from images: SuperPoint (max_keypoints = n1, nms 3, "
+                         "threshold 0.005) on the GPU produces the query keypoints/descriptors")
+    ap.add_argument("--image-size", type=int, default=512)
     ap.add_argument("--diag-repeats", type=int, default=0,
                     help="diagnostic: after the timed region, time it again this many times "
                          "and report those ms/step too (value always comes from the first)")
@@ -160,11 +188,22 @@ def main():
     sd = synthetic.make_state_dict(0)
     data, obj, frames = synthetic.make_matcher_inputs(n1, n3, L, seed=rank * 7919, batch=B)
     m = matcher.from_state_dict(sd)
+    detector, images = None, None
+    if args.e2e:
+        from onepose_amd.superpoint import SuperPoint
+        detector = SuperPoint({"nms_radius": 3, "keypoint_threshold": 0.005,
+                               "max_keypoints": n1, "remove_borders": 4})
+        detector.load_state_dict(synthetic.superpoint_state_dict(0))
+        S = args.image_size
+        images = np.stack([synthetic.superpoint_image(S, S, rank * 1000 + i) for i in range(B)])
     pipe = FramePipeline(m, data["keypoints3d"][0], data["descriptors3d_db"][0],
                          data["descriptors2d_db"][0], B, n1, dev, scale=1000.0,
-                         slots=max(2, args.match_streams + 1))
+                         slots=max(2, args.match_streams + 1), detector=detector,
+                         image_hw=(args.image_size, args.image_size))
     pipe.set_frames(data["descriptors2d_query"], data["keypoints2d"],
                     np.stack([f.K for f in frames]), np.stack([f.pose_gt for f in frames]))
+    if images is not None:
+        pipe.set_images(images)
 
     for _ in range(args.warmup):
         pipe.enqueue()
@@ -189,7 +228,9 @@ def main():
     overlap, graphs_on = not args.serial, not args.eager
     # stamping must be on while the graphs are captured (the accumulator address is a kernel
     # argument); begin_device again below re-zeroes the same accumulators
-    _lib.check(lib.onepose_profile_begin_device(1 << dom_id), "profile_begin_device")
+    sp_id = names.index("sp_conv")
+    stamp_mask = (1 << dom_id) | ((1 << sp_id) if args.e2e else 0)
+    _lib.check(lib.onepose_profile_begin_device(stamp_mask), "profile_begin_device")
     stage_graphs = pipe.capture_stages(torch.cuda.graph_pool_handle()) if graphs_on else None
     step_graph = pipe.capture(0) if graphs_on and not overlap else None
 
@@ -229,7 +270,7 @@ def main():
     torch.cuda.synchronize()
     # the dominant kernel's launches are timed on the device (first workgroup start -> last
     # workgroup end), accumulated over every launch inside the timed region
-    _lib.check(lib.onepose_profile_begin_device(1 << dom_id), "profile_begin_device")
+    _lib.check(lib.onepose_profile_begin_device(stamp_mask), "profile_begin_device")
     if pg:
         pg.barrier()
     torch.cuda.synchronize()
@@ -280,6 +321,21 @@ def main():
 
     res = result.cpu().numpy()
     frames_total = world * B * args.steps
+    det = None
+    if args.e2e:
+        S = args.image_size
+        conv_ms = float(tot_ms[sp_id])
+        conv_flop = superpoint_conv_flops(S, S) * B * args.steps
+        counts = torch.cat([o.det_counts for o in pipe.slots]).cpu().numpy()
+        det = {"image_hw": [S, S], "max_keypoints": n1,
+               "keypoints_saturated": bool((counts == n1).all()),
+               "conv_launches_timed": int(launches[sp_id]),
+               "conv_ms_per_frame": round(conv_ms / (B * args.steps), 4),
+               "conv_flop_per_frame": superpoint_conv_flops(S, S),
+               "conv_achieved_tflops": round(conv_flop / (conv_ms * 1e-3) / 1e12, 2),
+               "conv_frac_fp32_mfma": round(conv_flop / (conv_ms * 1e-3) / 1e12
+                                            / FP32_MFMA_PEAK_TFLOPS, 4),
+               "timing": "sum of SuperPoint MFMA-conv launch durations (device clock)"}
     value = frames_total / elapsed
     work, unit, bound = kernel_work(dominant, B, n1, n3, L)
     achieved = work / (dom_ms * 1e-3) / 1e12
@@ -303,8 +359,11 @@ def main():
             "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "fp32", "data": "synthetic",
-            "config": {"workload": f"config 2: {n1} kpts x {n3} 3D pts, L={L}, {B} frame(s) per "
-                                   f"GPU per step; matcher + RANSAC-EPnP + cm/deg; {sched}",
+            "config": {"workload": (f"config 2: {n1} kpts x {n3} 3D pts, L={L}, {B} frame(s) per "
+                                    f"GPU per step; "
+                                    + (f"SuperPoint on {args.image_size}x{args.image_size} images + "
+                                       if args.e2e else "")
+                                    + f"matcher + RANSAC-EPnP + cm/deg; {sched}"),
                        "n1": n1, "n3": n3, "num_leaf": L, "batch_per_gpu": B,
                        "parallelism": f"frame-dp{world}"},
             "pose": {"cmd1": float(res[:, 14].mean()), "cmd3": float(res[:, 15].mean()),
@@ -313,6 +372,7 @@ def main():
                      "n_inliers_mean": float(res[:, 17].mean()),
                      "status_ok": float((res[:, 18] == 0).mean())},
             "roofline": roof,
+            **({"detector": det} if det else {}),
             "host_enqueue_ms_per_step": round(host_enqueue / args.steps * 1e3, 4),
             **({"stage_ms": stage_ms} if stage_ms else {}),
             "kernel_ms_per_step": {k: round(v, 4) for k, v in sorted(total.items(),
@@ -320,7 +380,8 @@ def main():
             **({"diag_ms_per_step": diag} if diag else {}),
         }
         if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(sd, data, frames, obj)
+            out["cpu_baseline"] = cpu_baseline(sd, data, frames, obj,
+                                               detector_image=images[0] if args.e2e else None)
         print(json.dumps(out))
     if pg:
         pg.destroy_process_group()

@@ -14,6 +14,8 @@
 // survive, torch.topk's score-descending order otherwise; equal scores by raster index).
 #include "common.h"
 
+#include <cstdlib>
+
 namespace onepose {
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
@@ -59,18 +61,21 @@ struct ConvArgs {
 
 constexpr int CBK = 32, CPITCH = CBK + 4;
 
-// Tile shape: WM x WN waves, each owning 32 rows x 32*FN output channels.
-template <int WM_, int WN_, int FN_>
+// Tile shape: WM x WN waves, each owning 32 rows x 32*FN output channels, times KS groups of
+// such waves that split the K stages (taps x channel chunks) and reduce through LDS at the end.
+template <int WM_, int WN_, int FN_, int KS_>
 struct ConvTile {
-  static constexpr int WM = WM_, WN = WN_, FN = FN_;
-  static constexpr int BM = 32 * WM, BN = 32 * FN * WN, NT = 64 * WM * WN;
-  static constexpr int AV = BM * 8 / NT, WV = BN * 8 / NT;   // float4 loads per thread
+  static constexpr int WM = WM_, WN = WN_, FN = FN_, KS = KS_;
+  static constexpr int BM = 32 * WM, BN = 32 * FN * WN;
+  static constexpr int NTG = 64 * WM * WN, NT = NTG * KS;      // threads per group / total
+  static constexpr int AV = BM * 8 / NTG, WV = BN * 8 / NTG;   // float4 loads per thread
   static constexpr int STAGE = (BM + BN) * CPITCH;
-  static_assert(AV >= 1 && WV >= 1 && BM * 8 % NT == 0 && BN * 8 % NT == 0, "tile/threads");
+  static_assert(AV >= 1 && WV >= 1 && BM * 8 % NTG == 0 && BN * 8 % NTG == 0, "tile/threads");
+  static_assert(KS == 1 || (KS - 1) * WM * WN * FN * 16 * 64 <= KS * 2 * STAGE, "reduction");
 };
-using TileBig = ConvTile<2, 2, 1>;    // 64 x 64, 256 threads: the 512^2 .. 128^2 layers
-using TileSmall = ConvTile<1, 2, 1>;  // 32 x 64, 128 threads: the 64^2 layers (fills 256 CUs)
-using TileHead = ConvTile<1, 2, 2>;   // 32 x 128, 128 threads: convPb's 65 logits
+using TileBig = ConvTile<2, 2, 1, 1>;    // 64 x 64, 256 threads: the 512^2 .. 128^2 layers
+using TileSmall = ConvTile<1, 2, 1, 2>;  // 32 x 64, 2 K-groups: the 64^2 layers (fills CUs)
+using TileHead = ConvTile<1, 2, 2, 2>;   // 32 x 128, 2 K-groups: convPb's 65 logits
 
 template <class TL>
 struct ConvStage {
@@ -102,18 +107,20 @@ __device__ __forceinline__ void row_pixel(const ConvArgs& a, int mt, int m, int&
 
 template <int CIN, int KS, class TL, bool POOL, int EPI>
 __global__ __launch_bounds__(TL::NT) void conv_kernel(ConvArgs a) {
-  constexpr int BM = TL::BM, BN = TL::BN, NT = TL::NT, FN = TL::FN;
+  constexpr int BM = TL::BM, BN = TL::BN, NTG = TL::NTG, FN = TL::FN;
   constexpr int CH = CIN / CBK, TAPS = KS * KS, NK = TAPS * CH, HALF = KS / 2;
-  static_assert(NK % 2 == 0, "stage count must be even");
-  __shared__ __attribute__((aligned(16))) float lds[2 * TL::STAGE];
+  constexpr int NKG = NK / TL::KS;   // stages per K-group
+  static_assert(NK % TL::KS == 0 && NKG >= 2, "stages must split evenly over the K-groups");
+  __shared__ __attribute__((aligned(16))) float lds[TL::KS * 2 * TL::STAGE];
   stamp_begin(a.stamp);
   const int b = blockIdx.y;
   const int mt = blockIdx.x / a.ntiles, nt = blockIdx.x - mt * a.ntiles;
   const int n0 = nt * BN;
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int t = threadIdx.x, grp = t / NTG, tg = t - grp * NTG;
+  const int lane = t & 63, wave = tg >> 6;
   const int wm = wave / TL::WN, wn = wave - wm * TL::WN;
-  const int kq = (t & 7) * 4, r0 = t >> 3;
-  constexpr int RSTEP = NT / 8;   // rows covered by one load instruction
+  const int kq = (tg & 7) * 4, r0 = tg >> 3;
+  constexpr int RSTEP = NTG / 8;   // rows covered by one load instruction
   const float* X = a.x + (int64_t)b * a.x_bs + kq;
   int py[TL::AV], px[TL::AV], roff[TL::AV];
   bool pv[TL::AV];
@@ -123,6 +130,8 @@ __global__ __launch_bounds__(TL::NT) void conv_kernel(ConvArgs a) {
     roff[i] = (py[i] * a.W + px[i]) * CIN;
   }
   const float* Wt = a.w + (n0 + r0) * (TAPS * CIN) + kq;
+  float* glds = lds + grp * 2 * TL::STAGE;
+  const int s_base = grp * NKG;
 
   auto load = [&](int s, ConvStage<TL>& st) __attribute__((always_inline)) {
     const int tap = s / CH, c0 = (s - tap * CH) * CBK;
@@ -165,14 +174,14 @@ __global__ __launch_bounds__(TL::NT) void conv_kernel(ConvArgs a) {
     for (int i = 0; i < 16; ++i) acc[j][i] = 0.f;
 
   ConvStage<TL> s0, s1;
-  load(0, s0);
-  load(1, s1);
-  store(lds, s0);
+  load(s_base, s0);
+  load(s_base + 1, s1);
+  store(glds, s0);
   __syncthreads();
   auto step = [&](int kt, ConvStage<TL>& next, ConvStage<TL>& spare)
       __attribute__((always_inline)) {
-    load(min(kt + 2, NK - 1), spare);
-    const float* la = lds + (kt & 1) * TL::STAGE;
+    load(s_base + min(kt + 2, NKG - 1), spare);
+    const float* la = glds + (kt & 1) * TL::STAGE;
     const float* pa = la + (wm * 32 + (lane & 31)) * CPITCH + (lane >> 5) * 4;
     const float* pw = la + BM * CPITCH + (wn * 32 * FN + (lane & 31)) * CPITCH + (lane >> 5) * 4;
 #pragma unroll
@@ -187,40 +196,63 @@ __global__ __launch_bounds__(TL::NT) void conv_kernel(ConvArgs a) {
         acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av.w, wv.w, acc[j], 0, 0, 0);
       }
     }
-    store(lds + ((kt + 1) & 1) * TL::STAGE, next);   // (unused after the last stage)
+    store(glds + ((kt + 1) & 1) * TL::STAGE, next);   // (unused after the last stage)
     __syncthreads();
   };
-  for (int kt = 0; kt < NK; kt += 2) {
+  for (int kt = 0; kt + 1 < NKG; kt += 2) {
     step(kt, s1, s0);
     step(kt + 1, s0, s1);
+  }
+  if (NKG & 1) step(NKG - 1, s1, s0);
+  if (TL::KS > 1) {   // K-groups 1.. hand their partial sums to group 0 (fixed order)
+    constexpr int PER = TL::WM * TL::WN * FN * 16 * 64;
+    if (grp > 0) {
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+          lds[(grp - 1) * PER + ((wave * FN + j) * 16 + i) * 64 + lane] = acc[j][i];
+    }
+    __syncthreads();
+    if (grp == 0) {
+      for (int g = 1; g < TL::KS; ++g)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+#pragma unroll
+          for (int i = 0; i < 16; ++i)
+            acc[j][i] += lds[(g - 1) * PER + ((wave * FN + j) * 16 + i) * 64 + lane];
+    }
+    __syncthreads();
   }
 
   float* Y = a.y + (int64_t)b * a.y_bs;
   if (EPI != CE_SOFTMAX) {
+    if (grp == 0) {
 #pragma unroll
-    for (int j = 0; j < FN; ++j) {
-      const int n = n0 + wn * 32 * FN + j * 32 + (lane & 31);
-      const bool n_ok = n < a.cout;
-      const float bias = n_ok ? a.bias[n] : 0.f;
-      if (!POOL) {
+      for (int j = 0; j < FN; ++j) {
+        const int n = n0 + wn * 32 * FN + j * 32 + (lane & 31);
+        const bool n_ok = n < a.cout;
+        const float bias = n_ok ? a.bias[n] : 0.f;
+        if (!POOL) {
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const int m = wm * 32 + (i & 3) + 8 * (i >> 2) + 4 * (lane >> 5);
-          const int p = mt * BM + m;
-          float v = acc[j][i] + bias;
-          if (EPI == CE_RELU) v = fmaxf(v, 0.f);
-          if (n_ok && p < a.H * a.W) Y[p * a.cout + n] = v;
-        }
-      } else {
-        const int hp = a.H >> 1, wp = a.W >> 1;
+          for (int i = 0; i < 16; ++i) {
+            const int m = wm * 32 + (i & 3) + 8 * (i >> 2) + 4 * (lane >> 5);
+            const int p = mt * BM + m;
+            float v = acc[j][i] + bias;
+            if (EPI == CE_RELU) v = fmaxf(v, 0.f);
+            if (n_ok && p < a.H * a.W) Y[p * a.cout + n] = v;
+          }
+        } else {
+          const int hp = a.H >> 1, wp = a.W >> 1;
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {   // registers 4g..4g+3 = one 2x2 window
-          const int m = wm * 32 + 8 * g + 4 * (lane >> 5);
-          const int pp = mt * (BM / 4) + (m >> 2);
-          float v = fmaxf(fmaxf(acc[j][4 * g], acc[j][4 * g + 1]),
-                          fmaxf(acc[j][4 * g + 2], acc[j][4 * g + 3])) + bias;
-          if (EPI == CE_RELU) v = fmaxf(v, 0.f);   // relu(max(.)) == max(relu(.))
-          if (n_ok && pp < hp * wp) Y[pp * a.cout + n] = v;
+          for (int g = 0; g < 4; ++g) {   // registers 4g..4g+3 = one 2x2 window
+            const int m = wm * 32 + 8 * g + 4 * (lane >> 5);
+            const int pp = mt * (BM / 4) + (m >> 2);
+            float v = fmaxf(fmaxf(acc[j][4 * g], acc[j][4 * g + 1]),
+                            fmaxf(acc[j][4 * g + 2], acc[j][4 * g + 3])) + bias;
+            if (EPI == CE_RELU) v = fmaxf(v, 0.f);   // relu(max(.)) == max(relu(.))
+            if (n_ok && pp < hp * wp) Y[pp * a.cout + n] = v;
+          }
         }
       }
     }
@@ -229,21 +261,23 @@ __global__ __launch_bounds__(TL::NT) void conv_kernel(ConvArgs a) {
   }
   // CE_SOFTMAX: BM cells x 65 logits -> softmax over 65, drop the dustbin, pixel shuffle
   // (scores.permute(0,2,3,1).reshape(b,h,w,8,8).permute(0,1,3,2,4).reshape(b,8h,8w), :181-183)
-  static_assert(EPI != CE_SOFTMAX || (BN == 128 && NT == 4 * BM), "softmax head tile");
+  static_assert(EPI != CE_SOFTMAX || (BN == 128 && NTG == 4 * BM), "softmax head tile");
   float* tile = lds;   // [BM][129]
+  if (grp == 0) {
 #pragma unroll
-  for (int j = 0; j < FN; ++j) {
-    const int n = wn * 32 * FN + j * 32 + (lane & 31);
-    const float bias = n < a.cout ? a.bias[n] : 0.f;
+    for (int j = 0; j < FN; ++j) {
+      const int n = wn * 32 * FN + j * 32 + (lane & 31);
+      const float bias = n < a.cout ? a.bias[n] : 0.f;
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int m = wm * 32 + (i & 3) + 8 * (i >> 2) + 4 * (lane >> 5);
-      tile[m * 129 + n] = acc[j][i] + bias;
+      for (int i = 0; i < 16; ++i) {
+        const int m = wm * 32 + (i & 3) + 8 * (i >> 2) + 4 * (lane >> 5);
+        tile[m * 129 + n] = acc[j][i] + bias;
+      }
     }
   }
   __syncthreads();
-  {
-    const int m = t >> 2, q = t & 3;   // 4 threads per cell, 16 channels each
+  if (grp == 0) {
+    const int m = tg >> 2, q = tg & 3;   // 4 threads per cell, 16 channels each
     const float* row = tile + m * 129;
     float mx = -INFINITY;
     for (int c = 0; c < 65; ++c) mx = fmaxf(mx, row[c]);
@@ -974,6 +1008,24 @@ int conv_launch(const float* x, int B, int H, int W, const float* packed, int la
   return ONEPOSE_OK;
 }
 
+// Tile sweep hook for the 512^2..128^2 layers (ONEPOSE_SP_TILE, measurement only).
+template <int CIN, bool POOL>
+int big_conv(const float* x, int B, int H, int W, const float* packed, int layer, float* y,
+             hipStream_t st) {
+  static const int v = [] {
+    const char* e = getenv("ONEPOSE_SP_TILE");
+    return e ? atoi(e) : 0;
+  }();
+  switch (v) {
+    case 1: return conv_launch<CIN, 3, ConvTile<4, 1, 2, 1>, POOL, CE_RELU>(x, B, H, W, packed, layer, y, st);
+    case 2: return conv_launch<CIN, 3, ConvTile<2, 2, 1, 2>, POOL, CE_RELU>(x, B, H, W, packed, layer, y, st);
+    case 3: return conv_launch<CIN, 3, ConvTile<2, 1, 2, 1>, POOL, CE_RELU>(x, B, H, W, packed, layer, y, st);
+    case 5: return conv_launch<CIN, 3, ConvTile<4, 2, 1, 1>, POOL, CE_RELU>(x, B, H, W, packed, layer, y, st);
+    case 6: return conv_launch<CIN, 3, ConvTile<2, 2, 1, 3>, POOL, CE_RELU>(x, B, H, W, packed, layer, y, st);
+    default: return conv_launch<CIN, 3, TileBig, POOL, CE_RELU>(x, B, H, W, packed, layer, y, st);
+  }
+}
+
 constexpr int kMaxSortKeypoints = 16384;
 
 int check_detect_args(int batch, int h, int w, int nms_radius, int remove_borders,
@@ -1132,14 +1184,14 @@ int onepose_superpoint(const void* packed, const float* image, int batch, int h,
   OP_LAUNCH(K_SP_CONV, st, conv1a_kernel, dim3(ceil_div(h * w, 64), B), dim3(256), 0, st, image,
             (int64_t)h * w, P + layer_offset(0), P + layer_offset(0) + 64 * 9, h, w, p.f0,
             (int64_t)h * w * 64);
-  if ((rc = conv_launch<64, 3, TileBig, true, CE_RELU>(p.f0, B, h, w, P, 1, p.f1, st))) return rc;
-  if ((rc = conv_launch<64, 3, TileBig, false, CE_RELU>(p.f1, B, h / 2, w / 2, P, 2, p.f0, st)))
+  if ((rc = big_conv<64, true>(p.f0, B, h, w, P, 1, p.f1, st))) return rc;
+  if ((rc = big_conv<64, false>(p.f1, B, h / 2, w / 2, P, 2, p.f0, st)))
     return rc;
-  if ((rc = conv_launch<64, 3, TileBig, true, CE_RELU>(p.f0, B, h / 2, w / 2, P, 3, p.f1, st)))
+  if ((rc = big_conv<64, true>(p.f0, B, h / 2, w / 2, P, 3, p.f1, st)))
     return rc;
-  if ((rc = conv_launch<64, 3, TileBig, false, CE_RELU>(p.f1, B, h / 4, w / 4, P, 4, p.f0, st)))
+  if ((rc = big_conv<64, false>(p.f1, B, h / 4, w / 4, P, 4, p.f0, st)))
     return rc;
-  if ((rc = conv_launch<128, 3, TileBig, true, CE_RELU>(p.f0, B, h / 4, w / 4, P, 5, p.f1, st)))
+  if ((rc = big_conv<128, true>(p.f0, B, h / 4, w / 4, P, 5, p.f1, st)))
     return rc;
   if ((rc = conv_launch<128, 3, TileSmall, false, CE_RELU>(p.f1, B, h / 8, w / 8, P, 6, p.f0, st)))
     return rc;

@@ -1,7 +1,8 @@
 """Per-object frame pipeline: the whole per-frame hot path of ``inference.py:132-160`` on the
 device, with no host round trip and no per-frame re-upload of the object's 3D tensors.
 
-    matcher (onepose_match) -> correspondence selection -> RANSAC-EPnP -> cm/deg error
+    [SuperPoint (onepose_superpoint)] -> matcher (onepose_match) -> correspondence selection
+    -> RANSAC-EPnP -> cm/deg error
 
 The object's descriptors / leaves / 3D points are uploaded once (``inference.py:89-90``
 re-uploads them every frame).  All buffers are allocated at construction, so the enqueue
@@ -11,6 +12,14 @@ Streaming (``run_stream``): the pose stage of frame k needs one CU (one workgrou
 frame) while the matcher of frame k+1 needs the whole chip, so the two run on separate HIP
 streams with two buffer slots; events order matcher(k) -> pose(k) and pose(k) -> the
 matcher that next overwrites slot k % 2.  Every frame still runs every kernel.
+
+With a ``detector`` (``onepose_amd.superpoint.SuperPoint``) the pipeline starts from images
+(``extract_features.py`` + ``inference.py:143``): each slot owns an image buffer and the
+detector writes its keypoints / descriptors straight into that slot's matcher inputs
+([B, n1, 2] and [B, 256, n1], n1 = max_keypoints).  The matcher then runs at n1 keypoints, so
+the graph-replayed path is exact when the detector fills its top-k (``det_counts`` == n1, the
+512x512 crops' usual case); frames with fewer keypoints belong on ``inference.run_frames``,
+which runs each frame at its own size.
 """
 from __future__ import annotations
 
@@ -22,8 +31,17 @@ from .matcher import GATsSuperGlue
 
 
 class _Slot:
-    def __init__(self, B, n1, n3, dev, with_conf, lib, L, iters):
+    def __init__(self, B, n1, n3, dev, with_conf, lib, L, iters, image_hw=None):
         f32 = dict(dtype=torch.float32, device=dev)
+        if image_hw is not None:   # detector inputs / outputs (the matcher reads the latter)
+            h, w = image_hw
+            self.image = torch.zeros(B, h, w, **f32)
+            self.kpts2d = torch.zeros(B, n1, 2, **f32)
+            self.desc2d = torch.zeros(B, 256, n1, **f32)
+            self.det_scores = torch.empty(B, n1, **f32)
+            self.det_counts = torch.empty(B, dtype=torch.int32, device=dev)
+            self.ws_det_bytes = lib.onepose_superpoint_workspace_bytes(B, h, w)
+            self.ws_det = torch.empty(self.ws_det_bytes, dtype=torch.uint8, device=dev)
         self.matches0 = torch.empty(B, n1, dtype=torch.int64, device=dev)
         self.matches1 = torch.empty(B, n3, dtype=torch.int64, device=dev)
         self.mscores0 = torch.empty(B, n1, **f32)
@@ -49,7 +67,7 @@ class FramePipeline:
     def __init__(self, matcher: GATsSuperGlue, keypoints3d, desc3d, leaves, batch: int, n1: int,
                  device, scale: float = 1000.0, reprojection_error: float = 5.0,
                  iterations_count: int = 10000, confidence: float = 0.99, with_conf=True,
-                 slots: int = 2):
+                 slots: int = 2, detector=None, image_hw=(512, 512)):
         self.lib = _lib.load()
         self.device = torch.device(device)
         self.B, self.n1 = int(batch), int(n1)
@@ -78,8 +96,15 @@ class FramePipeline:
         self.kpts2d = torch.zeros(B, n1, 2, **f32)
         self.K = torch.zeros(B, 3, 3, dtype=torch.float64, device=dev)
         self.pose_gt = torch.zeros(B, 3, 4, dtype=torch.float64, device=dev)
-        self.slots = [_Slot(B, n1, self.n3, dev, with_conf, self.lib, self.L, self.iters)
-                      for _ in range(max(1, slots))]
+        self.detector = detector
+        if detector is not None:
+            cap = detector.capacity(*image_hw)
+            if cap != n1:
+                raise ValueError(f"detector max_keypoints {cap} != pipeline n1 {n1}")
+            self.det_weights = detector.to(dev).packed_weights()
+        self.image_hw = tuple(image_hw) if detector is not None else None
+        self.slots = [_Slot(B, n1, self.n3, dev, with_conf, self.lib, self.L, self.iters,
+                            self.image_hw) for _ in range(max(1, slots))]
 
     def __getattr__(self, name):
         # slot-0 outputs as attributes (pipe.pose, pipe.matches0, ...) for the common case
@@ -96,11 +121,42 @@ class FramePipeline:
         self.pose_gt.copy_(torch.as_tensor(np.asarray(pose_gt), dtype=torch.float64)[..., :3, :]
                            .expand_as(self.pose_gt))
 
+    def set_images(self, images, slot=None):
+        """Copy B images ([B, H, W] or [B, 1, H, W], float in [0, 1]) into one slot's image
+        buffer, or into every slot when slot is None."""
+        img = torch.as_tensor(np.asarray(images) if not torch.is_tensor(images) else images,
+                              dtype=torch.float32).reshape(self.B, *self.image_hw)
+        for o in (self.slots if slot is None else [self.slots[slot]]):
+            o.image.copy_(img)
+
+    def _inputs(self, o):
+        return (o.desc2d, o.kpts2d) if self.detector is not None else (self.desc2d, self.kpts2d)
+
+    def enqueue_detect(self, slot: int = 0):
+        """SuperPoint on the slot's images into the slot's matcher inputs."""
+        o = self.slots[slot]
+        c = self.detector.config
+        h, w = self.image_hw
+        from .superpoint import reference_align_corners
+        _lib.check(self.lib.onepose_superpoint(
+            self.det_weights.data_ptr(), o.image.data_ptr(), self.B, h, w, int(c["nms_radius"]),
+            float(c["keypoint_threshold"]), int(c["remove_borders"]), self.n1,
+            int(reference_align_corners()), o.kpts2d.data_ptr(), o.det_scores.data_ptr(),
+            o.desc2d.data_ptr(), o.det_counts.data_ptr(), 0, 0, o.ws_det.data_ptr(),
+            o.ws_det_bytes, _lib.stream_ptr(self.device)), "onepose_superpoint")
+
+    def enqueue_front(self, slot: int = 0):
+        """The stage that runs on a match stream: [detector ->] matcher."""
+        if self.detector is not None:
+            self.enqueue_detect(slot)
+        self.enqueue_match(slot)
+
     def enqueue_match(self, slot: int = 0):
         o = self.slots[slot]
         s = _lib.stream_ptr(self.device)
+        desc2d, _ = self._inputs(o)
         _lib.check(self.lib.onepose_match_prepared(
-            self.weights.data_ptr(), self.desc2d.data_ptr(), 256 * self.n1,
+            self.weights.data_ptr(), desc2d.data_ptr(), 256 * self.n1,
             self.desc3d.data_ptr(), 0, self.leaves_pm.data_ptr(), 0,
             self.B, self.n1, self.n3, self.L, self.scale_factor, self.threshold,
             o.matches0.data_ptr(), o.matches1.data_ptr(), o.mscores0.data_ptr(),
@@ -111,8 +167,9 @@ class FramePipeline:
         o = self.slots[slot]
         s = _lib.stream_ptr(self.device)
         lib = self.lib
+        _, kpts2d = self._inputs(o)
         _lib.check(lib.onepose_select_correspondences(
-            o.matches0.data_ptr(), self.kpts2d.data_ptr(), self.n1 * 2, self.kp3.data_ptr(), 0,
+            o.matches0.data_ptr(), kpts2d.data_ptr(), self.n1 * 2, self.kp3.data_ptr(), 0,
             self.B, self.n1, self.n3, self.scale, o.pts2d.data_ptr(), o.pts3d.data_ptr(),
             o.counts.data_ptr(), s), "select_correspondences")
         _lib.check(lib.onepose_pnp_ransac(
@@ -125,7 +182,7 @@ class FramePipeline:
             o.t_err.data_ptr(), o.cmd.data_ptr(), s), "pose_errors")
 
     def enqueue(self, slot: int = 0):
-        self.enqueue_match(slot)
+        self.enqueue_front(slot)
         self.enqueue_pose(slot)
 
     def capture(self, slot: int = 0, pool=None) -> "torch.cuda.CUDAGraph":
@@ -141,13 +198,13 @@ class FramePipeline:
         return g
 
     def capture_stages(self, pool=None):
-        """Capture, per buffer slot, the matcher stage and the pose stage as two HIP graphs
-        (for ``run_stream(graphs=...)``)."""
+        """Capture, per buffer slot, the front stage ([detector ->] matcher) and the pose stage
+        as two HIP graphs (for ``run_stream(graphs=...)``)."""
         out = []
         for sl in range(len(self.slots)):
             gm, gp = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
             with torch.cuda.graph(gm, pool=pool):
-                self.enqueue_match(sl)
+                self.enqueue_front(sl)
             with torch.cuda.graph(gp, pool=pool):
                 self.enqueue_pose(sl)
             out.append((gm, gp))
@@ -191,7 +248,7 @@ class FramePipeline:
                 if graphs:
                     graphs[sl][0].replay()
                 else:
-                    self.enqueue_match(sl)
+                    self.enqueue_front(sl)
                 matched[sl].record(ms)
                 if mk:
                     mk[1].record(ms)

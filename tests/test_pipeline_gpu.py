@@ -100,3 +100,48 @@ def test_two_concurrent_matcher_streams_match_eager(setup):
     torch.cuda.synchronize()
     for s in pipe.slots:
         _assert_same(ref, _outputs(s))
+
+
+@pytest.mark.gpu
+def test_detector_pipeline_from_images():
+    """Images -> SuperPoint -> matcher -> selection -> RANSAC-EPnP: the detector stage writes
+    exactly what SuperPoint.detect_raw returns, the matcher stage equals the module forward on
+    those keypoints, and graph replay / two matcher streams reproduce the eager results."""
+    from onepose_amd.superpoint import SuperPoint
+    dev = torch.device("cuda", 0)
+    n1, hw = 256, (256, 256)
+    sp = SuperPoint({"nms_radius": 3, "max_keypoints": n1})
+    sp.load_state_dict(synthetic.superpoint_state_dict(0))
+    sp.to(dev)
+    sd = synthetic.make_state_dict(0)
+    data, obj, frames = synthetic.make_matcher_inputs(n1, N3, L, seed=6, batch=1)
+    m = matcher.from_state_dict(sd)
+    pipe = FramePipeline(m, data["keypoints3d"][0], data["descriptors3d_db"][0],
+                         data["descriptors2d_db"][0], B, n1, dev, scale=1000.0, slots=3,
+                         detector=sp, image_hw=hw)
+    imgs = np.stack([synthetic.superpoint_image(*hw, s) for s in (10, 11)])
+    pipe.set_images(imgs)
+    pipe.K.copy_(torch.as_tensor(frames[0].K).expand_as(pipe.K))
+    pipe.pose_gt.copy_(torch.as_tensor(frames[0].pose_gt)[:3].expand_as(pipe.pose_gt))
+    pipe.enqueue(0)
+    torch.cuda.synchronize()
+    o = pipe.slots[0]
+    assert o.det_counts.tolist() == [n1] * B
+    raw = sp.detect_raw(torch.from_numpy(imgs)[:, None].to(dev))
+    np.testing.assert_array_equal(o.kpts2d.cpu().numpy(), raw["keypoints"].cpu().numpy())
+    np.testing.assert_array_equal(o.desc2d.cpu().numpy(), raw["descriptors"].cpu().numpy())
+    d3 = torch.as_tensor(data["descriptors3d_db"][0]).to(dev)[None]
+    db = torch.as_tensor(data["descriptors2d_db"][0]).to(dev)[None]
+    k3 = torch.as_tensor(data["keypoints3d"][0]).to(dev)[None]
+    for i in range(B):   # the module returns one frame's matches (GATs_SuperGlue.py:269-273)
+        pred, _ = m({"keypoints2d": raw["keypoints"][i:i + 1], "keypoints3d": k3,
+                     "descriptors2d_query": raw["descriptors"][i:i + 1],
+                     "descriptors3d_db": d3, "descriptors2d_db": db})
+        np.testing.assert_array_equal(o.matches0[i].cpu().numpy(),
+                                      pred["matches0"].cpu().numpy())
+    ref = _outputs(o)
+    graphs = pipe.capture_stages()
+    pipe.run_stream(6, graphs=graphs, match_streams=2)
+    torch.cuda.synchronize()
+    for s in pipe.slots:
+        _assert_same(ref, _outputs(s))
