@@ -53,3 +53,44 @@ def test_inference_core_on_disk(tmp_path, device):
     for (p, nin), f in zip(per, frames):
         assert nin >= 20                          # enough inliers for a well-posed EPnP
         assert np.linalg.norm(p[:, 3] - f.pose_gt[:, 3]) < 5e-3
+
+
+def test_inference_core_with_gpu_superpoint(tmp_path, device):
+    """The driver with onepose_amd.superpoint.SuperPoint as the extractor (inference.py:68-72
+    builds the reference's): textured crops give each frame its own keypoint count; the
+    summary equals run_frames over the detector's own per-frame outputs."""
+    from PIL import Image
+    from onepose_amd.superpoint import SuperPoint
+    obj = S.make_object(600, seed=9)
+    seq, sfm = tmp_path / "obj-2", tmp_path / "sfm" / "obj2"
+    for d in ("color", "intrin_ba", "poses_ba"):
+        (seq / d).mkdir(parents=True)
+    _, paths = I.get_default_paths(str(seq), str(sfm))
+    DU.save_object_annotations(paths["anno_dir"], obj.keypoints3d, obj.clt_descriptors,
+                               obj.clt_scores, obj.idxs)
+    frames = [S.make_frame(obj, 300, seed=60 + i) for i in range(3)]
+    imgs = []
+    for i, f in enumerate(frames):
+        im = (S.superpoint_image(128, 128, 20 + i) * 255).round().astype(np.uint8)
+        Image.fromarray(im, mode="L").save(seq / "color" / f"{i}.png")
+        imgs.append(im)
+        np.savetxt(seq / "intrin_ba" / f"{i}.txt", f.K)
+        np.savetxt(seq / "poses_ba" / f"{i}.txt", np.concatenate([f.pose_gt, [[0, 0, 0, 1]]]))
+    sp = SuperPoint({"nms_radius": 3, "keypoint_threshold": 0.005, "max_keypoints": 4096})
+    sp.load_state_dict(S.superpoint_state_dict(0))
+    sp.to(device)
+    m = matcher.from_state_dict(S.make_state_dict(0))
+    I.seed_reference_stream()
+    summary = I.inference_core(m, sp, str(seq), str(sfm), num_leaf=8, device=device)
+    dets = []
+    for im in imgs:
+        img = torch.from_numpy(im.astype(np.float32) / 255.0)[None, None].to(device)
+        d = sp(img)
+        dets.append((d["keypoints"][0].cpu().numpy(), d["descriptors"][0].cpu().numpy()))
+    assert len({len(k) for k, _ in dets}) > 1     # ragged keypoint counts
+    I.seed_reference_stream()
+    o = I.OnePoseObject.from_anno_dir(paths["anno_dir"], 8, device)
+    fr = [{"keypoints2d": k, "descriptors2d": d, "K": f.K, "pose_gt": f.pose_gt}
+          for (k, d), f in zip(dets, frames)]
+    summary2, _ = I.run_frames(m, o, fr)
+    assert summary2 == summary
