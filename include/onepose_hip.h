@@ -148,7 +148,8 @@ int onepose_select_correspondences(const int64_t* matches0, const float* kpts2d,
  * [batch, max_points] uint8, n_inliers [batch] int32, status [batch] int32:
  *   0 = solved; 1 = fewer than 4 points (reference: cv2.error -> identity pose, no inliers);
  *   2 = RANSAC found no model (identity pose, no inliers);
- *   3 = exactly 4 points (P3P branch of solvePnPRansac; identity pose, no inliers).
+ * Exactly 4 points follow solvePnPRansac's P3P branch: the P3P kernel (Gao) decides model / no
+ * model (status 2), the pose is the EPnP refit over all four.
  * All device pointers.
  * ------------------------------------------------------------------------------------ */
 size_t onepose_pnp_workspace_bytes(int batch, int max_points, int max_iters);

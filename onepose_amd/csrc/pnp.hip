@@ -887,7 +887,7 @@ struct Shared {
   double hypRvec[kRound][3];
   int count[kRound];
   // control
-  int iter, niters, max_good, done;
+  int iter, niters, max_good, done, p3p;
   double bestRvec[3], bestT[3];
   unsigned long long rng;
   // refit
@@ -903,6 +903,75 @@ struct Shared {
   int wave_cnt[4];
   int n_inl;
 };
+
+// Canonical basis of the 4-dimensional EPnP null space of exactly 4 correspondences (M is
+// 8 x 12): P = I - M^T (M M^T)^-1 M, Gram-Schmidt of P's columns in index order.  Same
+// arithmetic as null4_basis in oracle/epnp_ransac.c (see there for why).
+__device__ void null4_basis(const double (&M)[8][12], double (&v)[4][12]) {
+#pragma clang fp contract(off)
+  double G[8][8], X[8][12];
+  for (int a = 0; a < 8; ++a) {
+    for (int b = 0; b < 8; ++b) {
+      double acc = 0;
+      for (int k = 0; k < 12; ++k) acc += M[a][k] * M[b][k];
+      G[a][b] = acc;
+    }
+    for (int k = 0; k < 12; ++k) X[a][k] = M[a][k];
+  }
+  for (int c = 0; c < 8; ++c) {
+    int piv = c;
+    for (int r = c + 1; r < 8; ++r)
+      if (fabs(G[r][c]) > fabs(G[piv][c])) piv = r;
+    if (piv != c) {
+      for (int k = 0; k < 8; ++k) {
+        const double tmp = G[c][k];
+        G[c][k] = G[piv][k];
+        G[piv][k] = tmp;
+      }
+      for (int k = 0; k < 12; ++k) {
+        const double tmp = X[c][k];
+        X[c][k] = X[piv][k];
+        X[piv][k] = tmp;
+      }
+    }
+    const double inv = 1.0 / G[c][c];
+    for (int k = 0; k < 8; ++k) G[c][k] *= inv;
+    for (int k = 0; k < 12; ++k) X[c][k] *= inv;
+    for (int r = 0; r < 8; ++r) {
+      if (r == c) continue;
+      const double f = G[r][c];
+      if (f == 0.0) continue;
+      for (int k = 0; k < 8; ++k) G[r][k] -= f * G[c][k];
+      for (int k = 0; k < 12; ++k) X[r][k] -= f * X[c][k];
+    }
+  }
+  double P[12][12];
+  for (int a = 0; a < 12; ++a)
+    for (int b = 0; b < 12; ++b) {
+      double acc = 0;
+      for (int r = 0; r < 8; ++r) acc += M[r][a] * X[r][b];
+      P[a][b] = (a == b ? 1.0 : 0.0) - acc;
+    }
+  int nq = 0;
+  for (int pass = 0; pass < 2 && nq < 4; ++pass) {
+    const double keep = pass == 0 ? 0.05 : 1e-12;
+    for (int c = 0; c < 12 && nq < 4; ++c) {
+      double w[12];
+      for (int k = 0; k < 12; ++k) w[k] = P[k][c];
+      for (int j = 0; j < nq; ++j) {
+        double d = 0;
+        for (int k = 0; k < 12; ++k) d += v[j][k] * w[k];
+        for (int k = 0; k < 12; ++k) w[k] -= d * v[j][k];
+      }
+      double nn = 0;
+      for (int k = 0; k < 12; ++k) nn += w[k] * w[k];
+      if (nn <= keep) continue;
+      nn = 1.0 / sqrt(nn);
+      for (int k = 0; k < 12; ++k) v[nq][k] = w[k] * nn;
+      ++nq;
+    }
+  }
+}
 
 // Workgroup-parallel EPnP over the points listed in idx[0..n) (epnp::compute_pose).
 __device__ __forceinline__ void epnp_refit(Shared& sh, const float* p2, const float* p3, const int* idx, int n,
@@ -981,7 +1050,25 @@ __device__ __forceinline__ void epnp_refit(Shared& sh, const float* p2, const fl
   block_sum<78>(acc, sh.red);
   if (t == 0) {
     double ev4[4][12];
-    eig12_small4<100>(acc, ev4, sh.hh, 1);
+    if (n == 4) {   // canonical null-space basis (null4_basis), no eigensolver
+      double M[8][12];
+      for (int i = 0; i < 4; ++i) {
+        double as[4];
+        alphas(idx[i], as);
+        const double u = (double)p2[2 * idx[i]], v = (double)p2[2 * idx[i] + 1];
+        for (int k = 0; k < 4; ++k) {
+          M[2 * i][3 * k] = as[k] * fu;
+          M[2 * i][3 * k + 1] = 0.0;
+          M[2 * i][3 * k + 2] = as[k] * (uc - u);
+          M[2 * i + 1][3 * k] = 0.0;
+          M[2 * i + 1][3 * k + 1] = as[k] * fv;
+          M[2 * i + 1][3 * k + 2] = as[k] * (vc - v);
+        }
+      }
+      null4_basis(M, ev4);
+    } else {
+      eig12_small4<100>(acc, ev4, sh.hh, 1);
+    }
     for (int i = 0; i < 48; ++i) sh.vs[i] = (&ev4[0][0])[i];
     compute_L_6x10(sh.vs, sh.L);
     compute_rho(sh.cws, sh.rho);
@@ -1066,6 +1153,138 @@ __device__ __forceinline__ void epnp_refit(Shared& sh, const float* p2, const fl
   for (int i = 0; i < 3; ++i) t_out[i] = sh.sol_t[N][i];
 }
 
+// ---- P3P gate for exactly 4 points (solvePnPRansac: model_points = 4, P3P kernel; with
+// count == model_points the kernel runs once on all points and, when it yields a model, all 4
+// are inliers and the final refit is EPnP over them).  Same arithmetic as the oracle's
+// oracle_p3p_solutions (oracle/epnp_ransac.c): Gao's law-of-cosines system, y eliminated
+// linearly, the quartic's real roots by derivative bracketing + bisection.
+__device__ double p3p_poly(const double* c, int deg, double x) {
+#pragma clang fp contract(off)
+  double v = c[deg];
+  for (int i = deg - 1; i >= 0; --i) v = v * x + c[i];
+  return v;
+}
+
+__device__ double p3p_bisect(const double* c, int deg, double lo, double hi) {
+#pragma clang fp contract(off)
+  double flo = p3p_poly(c, deg, lo);
+  for (int it = 0; it < 200; ++it) {
+    const double mid = 0.5 * (lo + hi);
+    if (mid <= lo || mid >= hi) break;
+    const double fm = p3p_poly(c, deg, mid);
+    if (fm == 0.0) return mid;
+    if ((fm < 0) == (flo < 0)) {
+      lo = mid;
+      flo = fm;
+    } else {
+      hi = mid;
+    }
+  }
+  return 0.5 * (lo + hi);
+}
+
+// real roots (ascending) of c[0..deg]; iterative over degrees 1..deg (no recursion on device)
+__device__ int p3p_real_roots(const double* c4, double* roots) {
+#pragma clang fp contract(off)
+  double cs[5][5];   // cs[d] = the (4-d)-th derivative of the quartic, degree d
+  for (int i = 0; i <= 4; ++i) cs[4][i] = c4[i];
+  for (int d = 3; d >= 1; --d)
+    for (int i = 1; i <= d + 1; ++i) cs[d][i - 1] = i * cs[d + 1][i];
+  double r[4];
+  int nr = 1;
+  r[0] = -cs[1][0] / cs[1][1];
+  for (int deg = 2; deg <= 4; ++deg) {
+    const double* c = cs[deg];
+    double bound = 0.0;
+    for (int i = 0; i < deg; ++i) {
+      const double q = fabs(c[i] / c[deg]);
+      bound = q > bound ? q : bound;
+    }
+    bound += 1.0;
+    double pts[6];
+    int np = 0;
+    pts[np++] = -bound;
+    for (int i = 0; i < nr; ++i)
+      if (r[i] > -bound && r[i] < bound) pts[np++] = r[i];
+    pts[np++] = bound;
+    double out[4];
+    int n = 0;
+    for (int i = 0; i + 1 < np; ++i) {
+      const double fa = p3p_poly(c, deg, pts[i]), fb = p3p_poly(c, deg, pts[i + 1]);
+      if (fa == 0.0) {
+        if (n == 0 || out[n - 1] != pts[i]) out[n++] = pts[i];
+      } else if ((fa < 0) != (fb < 0) && fb != 0.0) {
+        out[n++] = p3p_bisect(c, deg, pts[i], pts[i + 1]);
+      }
+    }
+    if (p3p_poly(c, deg, pts[np - 1]) == 0.0) out[n++] = pts[np - 1];
+    for (int i = 0; i < n; ++i) r[i] = out[i];
+    nr = n;
+  }
+  for (int i = 0; i < nr; ++i) roots[i] = r[i];
+  return nr;
+}
+
+__device__ int p3p_solutions(const float* p2, const float* p3, const double* K4) {
+#pragma clang fp contract(off)
+  const double fx = K4[0], fy = K4[1], cx = K4[2], cy = K4[3];
+  double bear[3][3], P[3][3];
+  for (int i = 0; i < 3; ++i) {
+    const double mu = ((double)p2[2 * i] - cx) / fx, mv = ((double)p2[2 * i + 1] - cy) / fy;
+    const double mk = 1.0 / sqrt(mu * mu + mv * mv + 1.0);
+    bear[i][0] = mu * mk;
+    bear[i][1] = mv * mk;
+    bear[i][2] = mk;
+    for (int k = 0; k < 3; ++k) P[i][k] = p3[3 * i + k];
+  }
+  auto d2f = [](const double* a, const double* b) {
+    return (a[0] - b[0]) * (a[0] - b[0]) + (a[1] - b[1]) * (a[1] - b[1]) + (a[2] - b[2]) * (a[2] - b[2]);
+  };
+  auto dotf = [](const double* a, const double* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; };
+  const double d0 = sqrt(d2f(P[1], P[2])), d1 = sqrt(d2f(P[0], P[2])), d2 = sqrt(d2f(P[0], P[1]));
+  const double p = 2.0 * dotf(bear[1], bear[2]), q = 2.0 * dotf(bear[0], bear[2]),
+               r = 2.0 * dotf(bear[0], bear[1]);
+  if (p * p + q * q + r * r - p * q * r - 1.0 == 0.0) return 0;
+  if (d2 == 0.0) return 0;
+  const double a = (d0 * d0) / (d2 * d2), b = (d1 * d1) / (d2 * d2);
+  const double n2 = -(1.0 - a - b), n1 = (1.0 - a) * q, n0 = -(1.0 - a + b);
+  const double e1 = r, e0 = -p;
+  const double q2 = 1.0 - b, q1 = -q, q0 = 1.0;
+  double c[5] = {0, 0, 0, 0, 0};
+  c[4] -= n2 * n2;
+  c[3] -= 2.0 * n2 * n1;
+  c[2] -= n1 * n1 + 2.0 * n2 * n0;
+  c[1] -= 2.0 * n1 * n0;
+  c[0] -= n0 * n0;
+  const double ne3 = n2 * e1, ne2 = n2 * e0 + n1 * e1, ne1 = n1 * e0 + n0 * e1, ne0 = n0 * e0;
+  c[4] += b * r * ne3;
+  c[3] += b * r * ne2;
+  c[2] += b * r * ne1;
+  c[1] += b * r * ne0;
+  const double ee2 = e1 * e1, ee1 = 2.0 * e1 * e0, ee0 = e0 * e0;
+  c[4] += b * q2 * ee2;
+  c[3] += b * (q2 * ee1 + q1 * ee2);
+  c[2] += b * (q2 * ee0 + q1 * ee1 + q0 * ee2);
+  c[1] += b * (q1 * ee0 + q0 * ee1);
+  c[0] += b * q0 * ee0;
+  if (c[4] == 0.0) return 0;
+  double xs[4];
+  const int nr = p3p_real_roots(c, xs);
+  int sols = 0;
+  for (int i = 0; i < nr; ++i) {
+    const double x = xs[i];
+    if (x <= 0.0) continue;
+    const double den = b * (e1 * x + e0);
+    if (den == 0.0) continue;
+    const double y = (n2 * x * x + n1 * x + n0) / den;
+    if (y <= 0.0) continue;
+    const double v = x * x + y * y - x * y * r;
+    if (v <= 0.0) continue;
+    ++sols;
+  }
+  return sols;
+}
+
 __device__ __forceinline__ unsigned rng_next(unsigned long long& s) {
   s = (unsigned long long)(unsigned)s * 4164903690ull + (unsigned)(s >> 32);
   return (unsigned)s;
@@ -1101,10 +1320,6 @@ __global__ __launch_bounds__(kThreads) void pnp_ransac_kernel(
     identity(1);
     return;
   }
-  if (n == 4) {
-    identity(3);
-    return;
-  }
   for (int i = t; i < n; i += kThreads) {
     p2[2 * i] = pts2d[((int64_t)b * max_points + i) * 2];
     p2[2 * i + 1] = pts2d[((int64_t)b * max_points + i) * 2 + 1];
@@ -1121,6 +1336,23 @@ __global__ __launch_bounds__(kThreads) void pnp_ransac_kernel(
     sh.rng = 0xFFFFFFFFFFFFFFFFull;
   }
   __syncthreads();
+  if (n == 4) {   // solvePnPRansac's 4-point branch: P3P gate, then EPnP over all four
+    if (t == 0) sh.p3p = p3p_solutions(p2, p3, K4);
+    __syncthreads();
+    if (sh.p3p == 0) {
+      identity(2);
+      return;
+    }
+    for (int i = t; i < 4; i += kThreads) {
+      idx[i] = i;
+      mask[i] = 1;
+    }
+    if (t == 0) {
+      n_inliers[b] = 4;
+      status[b] = 0;
+    }
+    return;
+  }
 
   while (!sh.done) {
     if (t == 0) {  // getSubset x 64, in iteration order

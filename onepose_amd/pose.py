@@ -18,7 +18,7 @@ import torch
 
 from . import _lib
 
-STATUS_OK, STATUS_TOO_FEW, STATUS_NO_MODEL, STATUS_P3P = 0, 1, 2, 3
+STATUS_OK, STATUS_TOO_FEW, STATUS_NO_MODEL = 0, 1, 2
 
 
 def select_correspondences(matches0, kpts2d, kpts3d, scale=1.0):
@@ -118,9 +118,7 @@ def ransac_PnP(K, pts_2d, pts_3d, scale=1):
     pose, mask, n_in, status = ransac_pnp_batch(p2, p3, counts, np.asarray(K, np.float64),
                                                 scale=float(scale))
     st = int(status.item())
-    if st != STATUS_OK:
-        if st == STATUS_P3P:
-            raise NotImplementedError("solvePnPRansac's 4-point (P3P) branch is not implemented")
+    if st != STATUS_OK:   # cv2.solvePnPRansac returned False / raised: identity, no inliers
         return np.eye(4)[:3], np.eye(4), []
     pose = pose[0].cpu().numpy()
     pose_homo = np.concatenate([pose, np.array([[0, 0, 0, 1]])], axis=0)

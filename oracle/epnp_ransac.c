@@ -513,6 +513,77 @@ static double compute_R_and_t(Epnp* e, const double* ut, const double* betas, do
   return reprojection_error(e, R, t);
 }
 
+/* Exactly 4 correspondences give M (8 x 12) a 4-dimensional null space, so the basis an
+ * eigensolver returns for it -- and with it EPnP's beta approximations -- is arbitrary (it
+ * differs between eigensolvers and OpenCV versions).  For n == 4 both implementations here
+ * use a canonical basis instead: the projector P = I - M^T (M M^T)^-1 M (Gauss-Jordan with
+ * partial pivoting), then Gram-Schmidt of P's columns in index order, keeping residuals with
+ * squared norm > 0.05.  v[i] is the null vector EPnP reads as its i-th (ut row 11 - i). */
+static void null4_basis(const double M[8][12], double v[4][12]) {
+  double G[8][8], X[8][12];
+  for (int a = 0; a < 8; ++a) {
+    for (int b = 0; b < 8; ++b) {
+      double acc = 0;
+      for (int k = 0; k < 12; ++k) acc += M[a][k] * M[b][k];
+      G[a][b] = acc;
+    }
+    for (int k = 0; k < 12; ++k) X[a][k] = M[a][k];
+  }
+  for (int c = 0; c < 8; ++c) { /* G X = M, Gauss-Jordan with partial pivoting */
+    int piv = c;
+    for (int r = c + 1; r < 8; ++r)
+      if (fabs(G[r][c]) > fabs(G[piv][c])) piv = r;
+    if (piv != c) {
+      for (int k = 0; k < 8; ++k) {
+        const double tmp = G[c][k];
+        G[c][k] = G[piv][k];
+        G[piv][k] = tmp;
+      }
+      for (int k = 0; k < 12; ++k) {
+        const double tmp = X[c][k];
+        X[c][k] = X[piv][k];
+        X[piv][k] = tmp;
+      }
+    }
+    const double inv = 1.0 / G[c][c];
+    for (int k = 0; k < 8; ++k) G[c][k] *= inv;
+    for (int k = 0; k < 12; ++k) X[c][k] *= inv;
+    for (int r = 0; r < 8; ++r) {
+      if (r == c) continue;
+      const double f = G[r][c];
+      if (f == 0.0) continue;
+      for (int k = 0; k < 8; ++k) G[r][k] -= f * G[c][k];
+      for (int k = 0; k < 12; ++k) X[r][k] -= f * X[c][k];
+    }
+  }
+  double P[12][12];
+  for (int a = 0; a < 12; ++a)
+    for (int b = 0; b < 12; ++b) {
+      double acc = 0;
+      for (int r = 0; r < 8; ++r) acc += M[r][a] * X[r][b];
+      P[a][b] = (a == b ? 1.0 : 0.0) - acc;
+    }
+  int nq = 0;
+  for (int pass = 0; pass < 2 && nq < 4; ++pass) {
+    const double keep = pass == 0 ? 0.05 : 1e-12;
+    for (int c = 0; c < 12 && nq < 4; ++c) {
+      double w[12];
+      for (int k = 0; k < 12; ++k) w[k] = P[k][c];
+      for (int j = 0; j < nq; ++j) {
+        double d = 0;
+        for (int k = 0; k < 12; ++k) d += v[j][k] * w[k];
+        for (int k = 0; k < 12; ++k) w[k] -= d * v[j][k];
+      }
+      double nn = 0;
+      for (int k = 0; k < 12; ++k) nn += w[k] * w[k];
+      if (nn <= keep) continue;
+      nn = 1.0 / sqrt(nn);
+      for (int k = 0; k < 12; ++k) v[nq][k] = w[k] * nn;
+      ++nq;
+    }
+  }
+}
+
 /* epnp::compute_pose: R (3x3 row-major) and t from n >= 4 correspondences */
 void oracle_epnp(const double* pws, const double* us, int n, const double* K, double* R_out,
                  double* t_out) {
@@ -546,6 +617,24 @@ void oracle_epnp(const double* pws, const double* us, int n, const double* K, do
   }
   double d[12], ut[144];
   jacobi_eigen(mtm, 12, d, ut);
+  if (n == 4) { /* canonical null-space basis (see null4_basis) */
+    double M[8][12], v4[4][12];
+    for (int i = 0; i < 4; ++i) {
+      const double* as = e.alphas + 4 * i;
+      const double u = us[2 * i], v = us[2 * i + 1];
+      for (int k = 0; k < 4; ++k) {
+        M[2 * i][3 * k] = as[k] * e.fu;
+        M[2 * i][3 * k + 1] = 0.0;
+        M[2 * i][3 * k + 2] = as[k] * (e.uc - u);
+        M[2 * i + 1][3 * k] = 0.0;
+        M[2 * i + 1][3 * k + 1] = as[k] * e.fv;
+        M[2 * i + 1][3 * k + 2] = as[k] * (e.vc - v);
+      }
+    }
+    null4_basis(M, v4);
+    for (int i = 0; i < 4; ++i)
+      for (int k = 0; k < 12; ++k) ut[12 * (11 - i) + k] = v4[i][k];
+  }
   double L[60], rho[6];
   compute_L_6x10(ut, L);
   compute_rho(&e, rho);
@@ -669,7 +758,133 @@ static void epnp_rt(const float* p2, const float* p3, const int* idx, int n, con
   free(us);
 }
 
-/* Returns status (0 ok, 1 <4 points, 2 no model, 3 P3P branch); pose34 = [R | t/scale]
+/* ---- P3P (Gao et al. 2003, the kernel cv::solvePnPRansac switches to for exactly 4 points:
+ * model_points = 4, ransac_kernel_method = SOLVEPNP_P3P).  With count == model_points the
+ * RANSAC registrator runs the kernel once on all points and, when it yields a model, marks all
+ * 4 inliers; the final refit is solvePnP(EPNP) over them.  So P3P only decides model / no
+ * model; the pose is the EPnP of the 4 points.  Lengths follow Gao's law-of-cosines system
+ * with x = |P0|/|P2|, y = |P1|/|P2|; y is eliminated linearly (b*Eq1 + (1-a)*Eq2) and the
+ * quartic in x is Eq2 after substitution.  Real roots: recursive derivative bracketing +
+ * bisection (deterministic; pnp.hip runs the same arithmetic). */
+static double poly_eval(const double* c, int deg, double x) { /* c[0] + c[1] x + ... */
+  double v = c[deg];
+  for (int i = deg - 1; i >= 0; --i) v = v * x + c[i];
+  return v;
+}
+
+static double bisect_root(const double* c, int deg, double lo, double hi) {
+  double flo = poly_eval(c, deg, lo);
+  for (int it = 0; it < 200; ++it) {
+    const double mid = 0.5 * (lo + hi);
+    if (mid <= lo || mid >= hi) break;
+    const double fm = poly_eval(c, deg, mid);
+    if (fm == 0.0) return mid;
+    if ((fm < 0) == (flo < 0)) {
+      lo = mid;
+      flo = fm;
+    } else {
+      hi = mid;
+    }
+  }
+  return 0.5 * (lo + hi);
+}
+
+/* real roots (ascending) of c[0..deg], deg <= 4, c[deg] != 0 */
+static int real_roots(const double* c, int deg, double* roots) {
+  if (deg == 1) {
+    roots[0] = -c[0] / c[1];
+    return 1;
+  }
+  double bound = 0.0; /* Cauchy bound */
+  for (int i = 0; i < deg; ++i) {
+    const double q = fabs(c[i] / c[deg]);
+    bound = q > bound ? q : bound;
+  }
+  bound += 1.0;
+  double dc[4], crit[4];
+  for (int i = 1; i <= deg; ++i) dc[i - 1] = i * c[i];
+  const int nc = real_roots(dc, deg - 1, crit);
+  double pts[6];
+  int np = 0;
+  pts[np++] = -bound;
+  for (int i = 0; i < nc; ++i)
+    if (crit[i] > -bound && crit[i] < bound) pts[np++] = crit[i];
+  pts[np++] = bound;
+  int n = 0;
+  for (int i = 0; i + 1 < np; ++i) {
+    const double fa = poly_eval(c, deg, pts[i]), fb = poly_eval(c, deg, pts[i + 1]);
+    if (fa == 0.0) {
+      if (n == 0 || roots[n - 1] != pts[i]) roots[n++] = pts[i];
+    } else if ((fa < 0) != (fb < 0) && fb != 0.0) {
+      roots[n++] = bisect_root(c, deg, pts[i], pts[i + 1]);
+    }
+  }
+  if (poly_eval(c, deg, pts[np - 1]) == 0.0) roots[n++] = pts[np - 1];
+  return n;
+}
+
+/* number of P3P solutions from the first three correspondences (p3p::solve's lengths) */
+int oracle_p3p_solutions(const float* p2, const float* p3, const double* K) {
+  const double fx = K[0], fy = K[4], cx = K[2], cy = K[5];
+  double bear[3][3], P[3][3];
+  for (int i = 0; i < 3; ++i) {
+    double mu = (p2[2 * i] - cx) / fx, mv = (p2[2 * i + 1] - cy) / fy;
+    const double mk = 1.0 / sqrt(mu * mu + mv * mv + 1.0);
+    bear[i][0] = mu * mk;
+    bear[i][1] = mv * mk;
+    bear[i][2] = mk;
+    for (int k = 0; k < 3; ++k) P[i][k] = p3[3 * i + k];
+  }
+  const double d0 = sqrt(dist2(P[1], P[2])), d1 = sqrt(dist2(P[0], P[2])),
+               d2 = sqrt(dist2(P[0], P[1]));
+  const double p = 2.0 * dot3(bear[1], bear[2]), q = 2.0 * dot3(bear[0], bear[2]),
+               r = 2.0 * dot3(bear[0], bear[1]);
+  if (p * p + q * q + r * r - p * q * r - 1.0 == 0.0) return 0; /* Gao's degenerate case */
+  if (d2 == 0.0) return 0;
+  const double a = (d0 * d0) / (d2 * d2), b = (d1 * d1) / (d2 * d2);
+  /* y = N(x) / (b E(x)); quartic -N^2 + b r x N E + b Q E^2 = 0 */
+  const double n2 = -(1.0 - a - b), n1 = (1.0 - a) * q, n0 = -(1.0 - a + b);
+  const double e1 = r, e0 = -p;
+  const double q2 = 1.0 - b, q1 = -q, q0 = 1.0;
+  double c[5] = {0, 0, 0, 0, 0};
+  /* -N^2 */
+  c[4] -= n2 * n2;
+  c[3] -= 2.0 * n2 * n1;
+  c[2] -= n1 * n1 + 2.0 * n2 * n0;
+  c[1] -= 2.0 * n1 * n0;
+  c[0] -= n0 * n0;
+  /* b r x N E:  N E = (n2 x^2 + n1 x + n0)(e1 x + e0) */
+  const double ne3 = n2 * e1, ne2 = n2 * e0 + n1 * e1, ne1 = n1 * e0 + n0 * e1, ne0 = n0 * e0;
+  c[4] += b * r * ne3;
+  c[3] += b * r * ne2;
+  c[2] += b * r * ne1;
+  c[1] += b * r * ne0;
+  /* b Q E^2 */
+  const double ee2 = e1 * e1, ee1 = 2.0 * e1 * e0, ee0 = e0 * e0;
+  c[4] += b * q2 * ee2;
+  c[3] += b * (q2 * ee1 + q1 * ee2);
+  c[2] += b * (q2 * ee0 + q1 * ee1 + q0 * ee2);
+  c[1] += b * (q1 * ee0 + q0 * ee1);
+  c[0] += b * q0 * ee0;
+  if (c[4] == 0.0) return 0; /* Gao's A == 0 */
+  double xs[4];
+  const int nr = real_roots(c, 4, xs);
+  int sols = 0;
+  for (int i = 0; i < nr; ++i) {
+    const double x = xs[i];
+    if (x <= 0.0) continue;
+    const double den = b * (e1 * x + e0);
+    if (den == 0.0) continue;
+    const double y = (n2 * x * x + n1 * x + n0) / den;
+    if (y <= 0.0) continue;
+    const double v = x * x + y * y - x * y * r;
+    if (v <= 0.0) continue;
+    ++sols; /* lengths (x Z, y Z, Z), Z = d2 / sqrt(v): a pose aligns the three points */
+  }
+  return sols;
+}
+
+/* Returns status (0 ok, 1 <4 points, 2 no model); pose34 = [R | t/scale]
  * with R = Rodrigues(rvec) as eval_utils.py:31-34 builds it. */
 int oracle_pnp_ransac(const float* p2, const float* p3, int n, const double* K, double scale,
                       float reproj_error, int max_iters, double confidence, double* pose34,
@@ -679,14 +894,18 @@ int oracle_pnp_ransac(const float* p2, const float* p3, int n, const double* K, 
   *n_inliers = 0;
   if (iters_run) *iters_run = 0;
   if (n < 4) return 1;
-  if (n == 4) return 3;
-  const int model_points = 5;
   double rvec[3], tvec[3];
-  if (n == model_points) {
+  if (n == 4) { /* P3P kernel decides model / no model; refit EPnP over all four */
+    if (oracle_p3p_solutions(p2, p3, K) == 0) return 2;
+    epnp_rt(p2, p3, NULL, n, K, rvec, tvec);
+    for (int i = 0; i < n; ++i) mask[i] = 1;
+    *n_inliers = n;
+  } else if (n == 5) { /* count == model_points: the EPnP kernel once, all inliers */
     epnp_rt(p2, p3, NULL, n, K, rvec, tvec);
     for (int i = 0; i < n; ++i) mask[i] = 1;
     *n_inliers = n;
   } else {
+    const int model_points = 5;
     rng_state = 0xFFFFFFFFFFFFFFFFULL;
     const float thr = (float)((double)reproj_error * (double)reproj_error);
     int niters = max_iters > 1 ? max_iters : 1;

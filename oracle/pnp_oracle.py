@@ -33,6 +33,8 @@ def load():
         lib.oracle_epnp.argtypes = [dp, dp, ctypes.c_int, dp, dp, dp]
         lib.oracle_rng_draws.restype = None
         lib.oracle_rng_draws.argtypes = [ctypes.POINTER(ctypes.c_uint), ctypes.c_int]
+        lib.oracle_p3p_solutions.restype = ctypes.c_int
+        lib.oracle_p3p_solutions.argtypes = [fp, fp, dp]
         lib.oracle_rodrigues_m2v.argtypes = [dp, dp]
         lib.oracle_rodrigues_v2m.argtypes = [dp, dp]
         _lib = lib
@@ -41,6 +43,15 @@ def load():
 
 def _p(a, t):
     return a.ctypes.data_as(ctypes.POINTER(t))
+
+
+def p3p_solutions(pts2d_f32, pts3d_f32, K):
+    """Number of P3P solutions from the first three correspondences (the 4-point gate)."""
+    p2 = np.ascontiguousarray(pts2d_f32, np.float32)
+    p3 = np.ascontiguousarray(pts3d_f32, np.float32)
+    Kd = np.ascontiguousarray(K, np.float64)
+    return int(load().oracle_p3p_solutions(_p(p2, ctypes.c_float), _p(p3, ctypes.c_float),
+                                           _p(Kd, ctypes.c_double)))
 
 
 def pnp_ransac(pts2d_f32, pts3d_f32, K, scale=1.0, reproj=5.0, max_iters=10000, confidence=0.99):

@@ -82,7 +82,9 @@ def test_ransac_edge_counts(device):
     st, opose, omask, onin, _ = O.pnp_ransac(s5[0], s5[1], s5[2], scale=1000.0)
     assert status[0] == 0 and nin[0] == 5 and mask[0, :5].all()
     assert rot_angle(pose[0, :, :3], opose[:, :3]) < 1e-6
-    assert status[1] == P.STATUS_P3P and nin[1] == 0
+    # exactly 4 points: the P3P gate passes, EPnP over all four (status / inliers as the oracle)
+    st4, opose4, _, onin4, _ = O.pnp_ransac(s4[0], s4[1], s4[2], scale=1000.0)
+    assert status[1] == st4 == 0 and nin[1] == onin4 == 4 and mask[1, :4].all()
     assert status[2] == P.STATUS_TOO_FEW and nin[2] == 0
     np.testing.assert_allclose(pose[2], np.eye(4)[:3])
     st6, opose6, omask6, onin6, _ = O.pnp_ransac(s6[0], s6[1], s6[2], scale=1000.0)
@@ -99,3 +101,34 @@ def test_drop_in_ransac_PnP(device):
     few = P.ransac_PnP(K, p2[:3], pts3d_m[:3], scale=1000)
     np.testing.assert_allclose(few[0], np.eye(4)[:3])
     assert few[2] == []
+
+
+def test_four_point_p3p_gate_matches_oracle(device):
+    """solvePnPRansac's 4-point branch on many scenes: exact, noisy, degenerate-looking ones (all
+    image points on one pixel, solved by a far-away triangle; random sets, a few with no
+    positive P3P root -> no model); status, inlier mask and count as the oracle's.  The pose
+    of a 4-point solve is EPnP on a rank-deficient system (M is 8 x 12: a 4-dimensional null
+    space), which amplifies rounding into degrees -- the oracle itself lands up to ~80 deg
+    from the truth on exact data, and OpenCV's answer depends on its SVD -- so the pose is
+    checked for form only: a finite rotation and translation."""
+    scenes = [scene(200 + i, 4, 0.0 if i % 2 else 0.5) for i in range(12)]
+    p2, p3, K, gt, inl = scene(7, 4, 0.0)
+    scenes.append((np.repeat(p2[:1], 4, axis=0), p3, K, gt, inl))   # one pixel: a far solution
+    rs = np.random.RandomState(5)
+    for i in range(64):   # random 4-point sets: a few have no positive P3P solution
+        q3 = rs.uniform(-100, 100, (4, 3)).astype(np.float32)
+        q3[:, 2] += 400
+        scenes.append((rs.uniform(0, 512, (4, 2)).astype(np.float32), q3, K, gt, inl))
+    pose, mask, nin, status = run_gpu(scenes, device, max_points=4)
+    n_fail = 0
+    for b, (q2, q3, Kb, _, _) in enumerate(scenes):
+        st, opose, omask, onin, _ = O.pnp_ransac(q2, q3, Kb, scale=1000.0)
+        assert status[b] == st and nin[b] == onin, b
+        np.testing.assert_array_equal(mask[b, :4], omask)
+        assert np.isfinite(pose[b]).all()
+        R = pose[b, :, :3]
+        assert np.abs(R @ R.T - np.eye(3)).max() < 1e-9 and np.linalg.det(R) > 0
+        if st != 0:
+            np.testing.assert_array_equal(pose[b], np.eye(4)[:3])
+        n_fail += st != 0
+    assert 0 < n_fail < len(scenes)

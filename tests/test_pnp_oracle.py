@@ -77,6 +77,47 @@ def test_ransac_too_few_points_fails():
     assert st != 0 and nin == 0
 
 
+def test_four_points_take_the_p3p_gate():
+    """Exactly 4 correspondences: cv::solvePnPRansac switches to model_points 4 with the P3P
+    kernel, which (count == model_points) runs once; a model means all four are inliers and
+    the final refit is EPnP over them.  The true lengths are among P3P's solutions; one image
+    point for all four rays has no solution and fails."""
+    for seed in range(4):
+        p2, p3, K, pose, _ = scene(100 + seed, 4, outlier_frac=0.0)
+        assert O.p3p_solutions(p2, p3 * 1000.0, K) >= 1
+        st, est, mask, nin, _ = O.pnp_ransac(p2, p3 * 1000.0, K, scale=1000.0)
+        assert st == 0 and nin == 4 and mask.all()
+        R, t = np.zeros(9), np.zeros(3)
+        O.load().oracle_epnp(O._p(np.ascontiguousarray(p3 * 1000.0, np.float64), O.ctypes.c_double),
+                             O._p(np.ascontiguousarray(p2, np.float64), O.ctypes.c_double), 4,
+                             O._p(np.ascontiguousarray(K, np.float64), O.ctypes.c_double),
+                             O._p(R, O.ctypes.c_double), O._p(t, O.ctypes.c_double))
+        assert rot_err(est[:, :3], R.reshape(3, 3)) < 1e-6   # the EPnP refit of all four
+    p2, p3, K, _, _ = scene(7, 4, outlier_frac=0.0)
+    p2[:] = p2[0]
+    assert O.p3p_solutions(p2, p3 * 1000.0, K) == 0
+    st, est, _, nin, _ = O.pnp_ransac(p2, p3 * 1000.0, K, scale=1000.0)
+    assert st == 2 and nin == 0 and np.allclose(est, np.eye(4)[:3])
+
+
+def test_p3p_quartic_recovers_true_lengths():
+    """The gate's quartic has the true distance ratio x = |P0|/|P2| among its positive roots:
+    a known-answer check of the elimination (restated from Gao et al., not from OpenCV)."""
+    for seed in range(6):
+        p2, p3, K, pose, _ = scene(300 + seed, 4, outlier_frac=0.0)
+        Pc = (pose[:, :3] @ p3.astype(np.float64).T).T + pose[:, 3]
+        d = np.linalg.norm(Pc, axis=1)
+        bear = Pc / d[:, None]
+        # the law-of-cosines system the gate solves, at the true lengths
+        x, y = d[0] / d[2], d[1] / d[2]
+        p, q, r = 2 * bear[1] @ bear[2], 2 * bear[0] @ bear[2], 2 * bear[0] @ bear[1]
+        dd = lambda i, j: np.linalg.norm(p3[i].astype(np.float64) - p3[j])
+        a, b = dd(1, 2) ** 2 / dd(0, 1) ** 2, dd(0, 2) ** 2 / dd(0, 1) ** 2
+        assert abs((1 - a) * y * y + (a * x * r - p) * y + (1 - a * x * x)) < 1e-9
+        assert abs(-b * y * y + b * x * r * y + ((1 - b) * x * x - q * x + 1)) < 1e-9
+        assert O.p3p_solutions(p2, p3 * 1000.0, K) >= 1
+
+
 def test_pose_error_semantics():
     """query_pose_error (eval_utils.py:45-63): cm and degrees, trace clamped at 3 only."""
     R = S.random_rotation(np.random.RandomState(0))
