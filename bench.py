@@ -31,6 +31,7 @@ sys.path.insert(0, REPO)
 
 METRIC = "query frames/sec (1k kpts × 4k 3D pts) + cm/deg pose err, 1/2/4/8 GPU"
 FP32_MFMA_PEAK_TFLOPS = 157.3     # MI355X_MICROARCH.md: f32-input MFMA dense peak
+BF16_MFMA_PEAK_TFLOPS = 2500.0    # MI355X_MICROARCH.md: "~2.5 PF dense" bf16 MFMA
 HBM_PEAK_GBS = 8000.0             # MI355X_MICROARCH.md: HBM3E spec
 # kernels that record device stamps (onepose_profile_begin_device): timeable inside graphs
 STAMPED = {"qkv_gemm", "mlp1_gemm", "mlp2_gemm", "final_gemm", "score_gemm"}
@@ -162,6 +163,9 @@ def main():
     ap.add_argument("--eager", action="store_true",
                     help="launch every kernel from the host each step instead of replaying "
                          "captured HIP graphs")
+    ap.add_argument("--precision", choices=["fp32", "bf16"], default="fp32",
+                    help="matcher attention-layer GEMMs: fp32 MFMA (the reference's numerics, "
+                         "default) or bf16 MFMA with fp32 accumulation (BASELINE config 5)")
     ap.add_argument("--e2e", action="store_true",
                     help="start each step from images: SuperPoint (max_keypoints = n1, nms 3, "
                          "threshold 0.005) on the GPU produces the query keypoints/descriptors")
@@ -187,7 +191,8 @@ def main():
     B, n1, n3, L = args.batch, args.n1, args.n3, args.leaf
     sd = synthetic.make_state_dict(0)
     data, obj, frames = synthetic.make_matcher_inputs(n1, n3, L, seed=rank * 7919, batch=B)
-    m = matcher.from_state_dict(sd)
+    m = matcher.from_state_dict(sd, {**synthetic.DEFAULT_HPARAMS,
+                                     "attention_precision": args.precision})
     detector, images = None, None
     if args.e2e:
         from onepose_amd.superpoint import SuperPoint
@@ -339,16 +344,22 @@ def main():
     value = frames_total / elapsed
     work, unit, bound = kernel_work(dominant, B, n1, n3, L)
     achieved = work / (dom_ms * 1e-3) / 1e12
-    traffic, traffic_src = pmc_traffic(dominant) if (B, n1, n3, L) == (1, 1024, 4096, 8) \
-        else (None, None)
-    roof = {"bound": "mfma", "achieved": round(achieved, 2), "peak": FP32_MFMA_PEAK_TFLOPS,
-            "unit": "TFLOP/s", "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4),
+    bf_dom = args.precision == "bf16" and dominant in ("qkv_gemm", "mlp1_gemm", "mlp2_gemm")
+    peak = BF16_MFMA_PEAK_TFLOPS if bf_dom else FP32_MFMA_PEAK_TFLOPS
+    traffic, traffic_src = pmc_traffic(dominant) \
+        if (B, n1, n3, L) == (1, 1024, 4096, 8) and args.precision == "fp32" else (None, None)
+    roof = {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak,
+            "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
             "traffic": traffic, "traffic_unit": "HBM bytes per launch (PMC)",
             "traffic_source": traffic_src, "kernel": dominant,
             "avg_launch_us": round(dom_ms * 1e3, 2),
             "launches_timed": n_dom, "flop_per_launch": work,
             "timing": "device clock, first workgroup start to last workgroup end"}
 
+    cfg_name = {(1024, 4096): "config 2", (1024, 16384): "config 3",
+                (2048, 8192): "config 5"}.get((n1, n3), "custom")
+    if args.precision == "bf16":
+        cfg_name += " (bf16-MFMA attention)"
     if rank == 0:
         sched = (f"matchers of consecutive steps on {args.match_streams} concurrent stream(s), "
                  "each step's pose stage on its own stream overlapping the next matchers"
@@ -358,8 +369,10 @@ def main():
             "metric": METRIC, "value": round(value, 2), "unit": "frames/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "fp32", "data": "synthetic",
-            "config": {"workload": (f"config 2: {n1} kpts x {n3} 3D pts, L={L}, {B} frame(s) per "
+            "scaling": "weak", "vs_baseline": None,
+            "dtype": "fp32" if args.precision == "fp32" else "bf16 attention GEMMs, fp32 rest",
+            "data": "synthetic",
+            "config": {"workload": (f"{cfg_name}: {n1} kpts x {n3} 3D pts, L={L}, {B} frame(s) per "
                                     f"GPU per step; "
                                     + (f"SuperPoint on {args.image_size}x{args.image_size} images + "
                                        if args.e2e else "")

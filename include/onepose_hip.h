@@ -35,6 +35,16 @@ enum {
   ONEPOSE_ERR_WORKSPACE = 4     /* workspace too small                                  */
 };
 
+/* Matcher arithmetic (onepose_match_ex / onepose_match_prepared_ex). */
+enum {
+  ONEPOSE_PREC_FP32 = 0,        /* every contraction on fp32-input MFMA: the reference's
+                                   numerics up to summation order (bit-exact indices)   */
+  ONEPOSE_PREC_BF16_ATTN = 1    /* the attention layers' GEMMs (q/k/v projection, merge+MLP)
+                                   take bf16-rounded operands on v_mfma_f32_32x32x16_bf16
+                                   with fp32 accumulation (BASELINE config 5); GAT, final
+                                   projection, scores and dual softmax stay fp32       */
+};
+
 /* Thread-local description of the last error ("" when none). */
 const char* onepose_last_error(void);
 /* ABI version, bumped on any signature change. */
@@ -99,6 +109,26 @@ int onepose_match(const void* packed_weights,
 size_t onepose_leaves_prepared_bytes(int batch, int n3, int num_leaf);
 int onepose_prepare_leaves(const float* leaves, int64_t leaves_bstride, int batch, int n3,
                            int num_leaf, float* out, void* stream);
+/* The same two calls with a precision mode (ONEPOSE_PREC_*); the plain forms are
+ * ONEPOSE_PREC_FP32. */
+int onepose_match_ex(const void* packed_weights,
+                     const float* desc2d, int64_t desc2d_bstride,
+                     const float* desc3d, int64_t desc3d_bstride,
+                     const float* leaves, int64_t leaves_bstride,
+                     int batch, int n1, int n3, int num_leaf,
+                     float scale_factor, float match_threshold, int precision,
+                     int64_t* matches0, int64_t* matches1,
+                     float* mscores0, float* mscores1, float* conf,
+                     void* workspace, size_t workspace_bytes, void* stream);
+int onepose_match_prepared_ex(const void* packed_weights,
+                              const float* desc2d, int64_t desc2d_bstride,
+                              const float* desc3d, int64_t desc3d_bstride,
+                              const float* leaves_prepared, int64_t prepared_bstride,
+                              int batch, int n1, int n3, int num_leaf,
+                              float scale_factor, float match_threshold, int precision,
+                              int64_t* matches0, int64_t* matches1,
+                              float* mscores0, float* mscores1, float* conf,
+                              void* workspace, size_t workspace_bytes, void* stream);
 int onepose_match_prepared(const void* packed_weights,
                            const float* desc2d, int64_t desc2d_bstride,
                            const float* desc3d, int64_t desc3d_bstride,

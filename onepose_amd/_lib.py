@@ -35,6 +35,14 @@ PROTOTYPES = {
                                        c_int64, c_int, c_int, c_int, c_int, c_float, c_float,
                                        c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                        c_void_p, c_size_t, c_void_p]),
+    "onepose_match_ex": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_int64, c_void_p,
+                                 c_int64, c_int, c_int, c_int, c_int, c_float, c_float, c_int,
+                                 c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                 c_void_p, c_size_t, c_void_p]),
+    "onepose_match_prepared_ex": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_int64,
+                                          c_void_p, c_int64, c_int, c_int, c_int, c_int, c_float,
+                                          c_float, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
+                                          c_void_p, c_void_p, c_size_t, c_void_p]),
     "onepose_leaves_prepared_bytes": (c_size_t, [c_int, c_int, c_int]),
     "onepose_prepare_leaves": (c_int, [c_void_p, c_int64, c_int, c_int, c_int, c_void_p,
                                        c_void_p]),

@@ -82,7 +82,10 @@ enum GemmTile {
 // Supported (epilogue, prologue, tile) combinations: QKV/32x128, STATS+HEADZ/64x64,
 // RESID+NORM/64x64, SCORE/64x64, BIAS/64x64.  K must be a multiple of twice the tile's stage
 // depth (32 * KS).
-int gemm_launch(int epi, int pro, int tile, GemmArgs& args, hipStream_t stream, int kind);
+// bf16 = true: operands rounded to bf16 as the stage is read, v_mfma_f32_32x32x16_bf16 with
+// fp32 accumulation (QKV, STATS+HEADZ, RESID+NORM only: the attention-layer GEMMs).
+int gemm_launch(int epi, int pro, int tile, GemmArgs& args, hipStream_t stream, int kind,
+                bool bf16 = false);
 // Rows per M-tile of a configuration (the chunk size of the STATS / KVPART partials).
 int gemm_tile_rows(int tile);
 

@@ -1,4 +1,4 @@
-// fp32 MFMA grouped token-GEMM (see gemm.h).
+// fp32 (or bf16-input) MFMA grouped token-GEMM (see gemm.h).
 //
 // A workgroup (4 or 8 waves) owns a BM x BN output tile.  Its waves form a
 // WM x WN x KS grid: each wave owns a 32 x (FN*32) block of v_mfma_f32_32x32x2_f32
@@ -23,8 +23,38 @@
 namespace onepose {
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
 namespace {
+
+// Per-wave MFMA operand fragments of one stage: fp32 (v_mfma_f32_32x32x2_f32, a float4 feeds
+// four MFMAs over k = 8 kk + 4 h + j) or bf16 (v_mfma_f32_32x32x16_bf16: lane half h holds
+// k = 16 kk + 8 h + j, j < 8, converted round-to-nearest-even when read from the fp32 stage).
+template <bool BF, int KKW, int FN>
+struct FragT {
+  float4 a[KKW];
+  float4 w[KKW][FN];
+};
+template <int KKW, int FN>
+struct FragT<true, KKW, FN> {
+  bf16x8 a[KKW];
+  bf16x8 w[KKW][FN];
+};
+
+__device__ __forceinline__ bf16x8 to_bf16x8(const float* p) {
+  const float4 lo = *reinterpret_cast<const float4*>(p);
+  const float4 hi = *reinterpret_cast<const float4*>(p + 4);
+  bf16x8 r;
+  r[0] = (__bf16)lo.x;
+  r[1] = (__bf16)lo.y;
+  r[2] = (__bf16)lo.z;
+  r[3] = (__bf16)lo.w;
+  r[4] = (__bf16)hi.x;
+  r[5] = (__bf16)hi.y;
+  r[6] = (__bf16)hi.z;
+  r[7] = (__bf16)hi.w;
+  return r;
+}
 
 template <int BM_, int BN_, int KS_, int NW_, int BKS_>
 struct Tile {
@@ -107,7 +137,7 @@ __device__ __forceinline__ void store_stage(float* lds_a, float* lds_w, Stage<T>
     *reinterpret_cast<float4*>(lds_w + ((t + T::NT * i) / T::KQ) * T::PITCH + kq) = s.w[i];
 }
 
-template <int EPI, int PRO, class T>
+template <int EPI, int PRO, class T, bool BF>
 __device__ __forceinline__ void gemm_body(const GemmArgs& args) {
   constexpr int BM = T::BM, BN = T::BN, FN = T::FN, STAGE = T::STAGE, PITCH = T::PITCH;
   __shared__ __attribute__((aligned(16))) float lds[2 * STAGE];
@@ -166,31 +196,40 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args) {
   // Global loads run two stages ahead (register stage + LDS stage).
   const int nk = c.K / T::BKS;
   Stage<T> s0, s1;
-  constexpr int KKW = T::KKW;
-  struct Frag {
-    float4 a[KKW];
-    float4 w[KKW][FN];
-  };
+  constexpr int KG = BF ? 16 : 8;                  // k per MFMA group
+  constexpr int KKW = T::BKS / T::KS / KG;         // groups per wave per stage
+  static_assert(KKW >= 2, "two MFMA groups per stage (pipeline shape)");
+  using Frag = FragT<BF, KKW, FN>;
   Frag f0, f1;
-  const int kofs = ks * KKW * 8 + (lane >> 5) * 4;
+  const int kofs = ks * (T::BKS / T::KS) + (lane >> 5) * (KG / 2);
   const int a_off = (wm * 32 + (lane & 31)) * PITCH + kofs;
   const int w_off = BM * PITCH + (wn * FN * 32 + (lane & 31)) * PITCH + kofs;
   auto read_frag = [&](const float* buf, Frag& f) __attribute__((always_inline)) {
 #pragma unroll
     for (int kk = 0; kk < KKW; ++kk) {
-      f.a[kk] = *reinterpret_cast<const float4*>(buf + a_off + kk * 8);
+      if constexpr (BF) {
+        f.a[kk] = to_bf16x8(buf + a_off + kk * KG);
 #pragma unroll
-      for (int j = 0; j < FN; ++j)
-        f.w[kk][j] = *reinterpret_cast<const float4*>(buf + w_off + j * 32 * PITCH + kk * 8);
+        for (int j = 0; j < FN; ++j) f.w[kk][j] = to_bf16x8(buf + w_off + j * 32 * PITCH + kk * KG);
+      } else {
+        f.a[kk] = *reinterpret_cast<const float4*>(buf + a_off + kk * KG);
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          f.w[kk][j] = *reinterpret_cast<const float4*>(buf + w_off + j * 32 * PITCH + kk * KG);
+      }
     }
   };
   auto mfma_kk = [&](floatx16 (&tg)[FN], const Frag& f, int kk) __attribute__((always_inline)) {
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
-      tg[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(f.a[kk].x, f.w[kk][j].x, tg[j], 0, 0, 0);
-      tg[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(f.a[kk].y, f.w[kk][j].y, tg[j], 0, 0, 0);
-      tg[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(f.a[kk].z, f.w[kk][j].z, tg[j], 0, 0, 0);
-      tg[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(f.a[kk].w, f.w[kk][j].w, tg[j], 0, 0, 0);
+      if constexpr (BF) {
+        tg[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.a[kk], f.w[kk][j], tg[j], 0, 0, 0);
+      } else {
+        tg[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(f.a[kk].x, f.w[kk][j].x, tg[j], 0, 0, 0);
+        tg[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(f.a[kk].y, f.w[kk][j].y, tg[j], 0, 0, 0);
+        tg[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(f.a[kk].z, f.w[kk][j].z, tg[j], 0, 0, 0);
+        tg[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(f.a[kk].w, f.w[kk][j].w, tg[j], 0, 0, 0);
+      }
     }
   };
 
@@ -452,19 +491,20 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args) {
 #undef F
 }
 
-template <int EPI, int PRO, class T>
-__global__ __launch_bounds__(T::NT) void gemm_f32_kernel(GemmArgs args) {
+template <int EPI, int PRO, class T, bool BF>
+__global__ __launch_bounds__(T::NT) __attribute__((amdgpu_waves_per_eu(3)))
+void gemm_kernel(GemmArgs args) {
   stamp_begin(args.stamp);
-  gemm_body<EPI, PRO, T>(args);
+  gemm_body<EPI, PRO, T, BF>(args);
   stamp_end(args.stamp);
 }
 
 using T64x64 = Tile<64, 64, 1, 4, 32>;
 using T32x128 = Tile<32, 128, 1, 4, 32>;
 
-template <int EPI, int PRO, class T>
+template <int EPI, int PRO, class T, bool BF>
 void launch_one(GemmArgs& args, int grid, hipStream_t stream) {
-  hipLaunchKernelGGL((gemm_f32_kernel<EPI, PRO, T>), dim3(grid), dim3(T::NT), 0, stream, args);
+  hipLaunchKernelGGL((gemm_kernel<EPI, PRO, T, BF>), dim3(grid), dim3(T::NT), 0, stream, args);
 }
 
 struct TileDims {
@@ -506,7 +546,8 @@ GemmProb gemm_prob(const float* A, int lda, const float* W, int ldw, const float
   return g;
 }
 
-int gemm_launch(int epi, int pro, int tile, GemmArgs& args, hipStream_t stream, int kind) {
+int gemm_launch(int epi, int pro, int tile, GemmArgs& args, hipStream_t stream, int kind,
+                bool bf16) {
   const TileDims td = tile_dims(tile);
   OP_REQUIRE(td.bm > 0, "gemm: unknown tile %d", tile);
   int grid = 0;
@@ -532,22 +573,26 @@ int gemm_launch(int epi, int pro, int tile, GemmArgs& args, hipStream_t stream, 
   }
   if (grid == 0) return ONEPOSE_OK;
   args.stamp = nullptr;
-#define CASE(E, PR, TI, T)                        \
-  if (epi == E && pro == PR && tile == TI) {      \
-    prof_pre(kind, stream);                       \
-    args.stamp = prof_stamp_slot(kind);           \
-    launch_one<E, PR, T>(args, grid, stream);     \
-    prof_post(kind, stream);                      \
-    OP_LAUNCHED();                                \
-    return ONEPOSE_OK;                            \
+#define CASE(E, PR, TI, T, BF)                           \
+  if (epi == E && pro == PR && tile == TI && bf16 == BF) { \
+    prof_pre(kind, stream);                              \
+    args.stamp = prof_stamp_slot(kind);                  \
+    launch_one<E, PR, T, BF>(args, grid, stream);        \
+    prof_post(kind, stream);                             \
+    OP_LAUNCHED();                                       \
+    return ONEPOSE_OK;                                   \
   }
-  CASE(EPI_QKV, PRO_PLAIN, TILE_32x128, T32x128)
-  CASE(EPI_STATS, PRO_HEADZ, TILE_64x64, T64x64)
-  CASE(EPI_RESID, PRO_NORM_RELU, TILE_64x64, T64x64)
-  CASE(EPI_SCORE, PRO_PLAIN, TILE_64x64, T64x64)
-  CASE(EPI_BIAS, PRO_PLAIN, TILE_64x64, T64x64)
+  CASE(EPI_QKV, PRO_PLAIN, TILE_32x128, T32x128, false)
+  CASE(EPI_STATS, PRO_HEADZ, TILE_64x64, T64x64, false)
+  CASE(EPI_RESID, PRO_NORM_RELU, TILE_64x64, T64x64, false)
+  CASE(EPI_SCORE, PRO_PLAIN, TILE_64x64, T64x64, false)
+  CASE(EPI_BIAS, PRO_PLAIN, TILE_64x64, T64x64, false)
+  // bf16-MFMA attention layers (precision mode ONEPOSE_PREC_BF16_ATTN)
+  CASE(EPI_QKV, PRO_PLAIN, TILE_32x128, T32x128, true)
+  CASE(EPI_STATS, PRO_HEADZ, TILE_64x64, T64x64, true)
+  CASE(EPI_RESID, PRO_NORM_RELU, TILE_64x64, T64x64, true)
 #undef CASE
-  set_error("gemm: unsupported epilogue/prologue/tile %d/%d/%d", epi, pro, tile);
+  set_error("gemm: unsupported epilogue/prologue/tile/bf16 %d/%d/%d/%d", epi, pro, tile, (int)bf16);
   return ONEPOSE_ERR_INVALID;
 }
 

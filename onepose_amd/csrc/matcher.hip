@@ -919,8 +919,9 @@ int match_impl(const void* packed_weights, const float* desc2d, int64_t desc2d_b
                const float* desc3d, int64_t desc3d_bstride, const float* leaves_pm,
                int64_t leaves_pm_bs, int batch, int n1, int n3, int num_leaf, float scale_factor,
                float match_threshold, int64_t* matches0, int64_t* matches1, float* mscores0,
-               float* mscores1, float* conf, const Plan& p, hipStream_t st) {
+               float* mscores1, float* conf, const Plan& p, hipStream_t st, int precision) {
   const bool with_conf = conf != nullptr;
+  const bool bf = precision == ONEPOSE_PREC_BF16_ATTN;   // attention-layer GEMMs on bf16 MFMA
   const float* wbase = static_cast<const float*>(packed_weights);
   const int B = batch;
   float* S = with_conf ? conf : p.s;
@@ -969,7 +970,7 @@ int match_impl(const void* packed_weights, const float* desc2d, int64_t desc2d_b
       a.p[1].kvpart = p.kvpart3;
       a.p[1].kspart = p.kspart3;
       a.p[1].y_bs = (int64_t)n3 * 256;
-      if ((rc = gemm_launch(EPI_QKV, PRO_PLAIN, kTileKV, a, st, K_QKV_GEMM)) != ONEPOSE_OK)
+      if ((rc = gemm_launch(EPI_QKV, PRO_PLAIN, kTileKV, a, st, K_QKV_GEMM, bf)) != ONEPOSE_OK)
         return rc;
     }
     {  // 2. KV[src], ksum[src]
@@ -1014,7 +1015,7 @@ int match_impl(const void* packed_weights, const float* desc2d, int64_t desc2d_b
       a.p[1].ksum = p.ksum + (size_t)src3 * B * 256;
       a.p[1].ksum_bs = 256;
       a.p[1].ns = (float)ns3;
-      if ((rc = gemm_launch(EPI_STATS, PRO_HEADZ, kTileMLP1, a, st, K_MLP1)) != ONEPOSE_OK)
+      if ((rc = gemm_launch(EPI_STATS, PRO_HEADZ, kTileMLP1, a, st, K_MLP1, bf)) != ONEPOSE_OK)
         return rc;
     }
     {  // 5. InstanceNorm statistics
@@ -1042,7 +1043,7 @@ int match_impl(const void* packed_weights, const float* desc2d, int64_t desc2d_b
       a.p[1].pro_mean = p.mean + (size_t)B * 512;
       a.p[1].pro_rstd = p.rstd + (size_t)B * 512;
       a.p[1].pro_bs = 512;
-      if ((rc = gemm_launch(EPI_RESID, PRO_NORM_RELU, kTileMLP2, a, st, K_MLP2)) != ONEPOSE_OK)
+      if ((rc = gemm_launch(EPI_RESID, PRO_NORM_RELU, kTileMLP2, a, st, K_MLP2, bf)) != ONEPOSE_OK)
         return rc;
     }
     c2 ^= 1;
@@ -1129,13 +1130,15 @@ int onepose_prepare_leaves(const float* leaves, int64_t leaves_bstride, int batc
   return ONEPOSE_OK;
 }
 
-int onepose_match(const void* packed_weights, const float* desc2d, int64_t desc2d_bstride,
-                  const float* desc3d, int64_t desc3d_bstride, const float* leaves,
-                  int64_t leaves_bstride, int batch, int n1, int n3, int num_leaf,
-                  float scale_factor, float match_threshold, int64_t* matches0,
-                  int64_t* matches1, float* mscores0, float* mscores1, float* conf,
-                  void* workspace, size_t workspace_bytes, void* stream_) {
+int onepose_match_ex(const void* packed_weights, const float* desc2d, int64_t desc2d_bstride,
+                     const float* desc3d, int64_t desc3d_bstride, const float* leaves,
+                     int64_t leaves_bstride, int batch, int n1, int n3, int num_leaf,
+                     float scale_factor, float match_threshold, int precision,
+                     int64_t* matches0, int64_t* matches1, float* mscores0, float* mscores1,
+                     float* conf, void* workspace, size_t workspace_bytes, void* stream_) {
   clear_error();
+  OP_REQUIRE(precision == ONEPOSE_PREC_FP32 || precision == ONEPOSE_PREC_BF16_ATTN,
+             "match: precision %d", precision);
   int rc = check_match_args(packed_weights, desc2d, desc3d, leaves, batch, n1, n3, num_leaf,
                             scale_factor, matches0, matches1, mscores0, mscores1, workspace);
   if (rc != ONEPOSE_OK) return rc;
@@ -1154,17 +1157,31 @@ int onepose_match(const void* packed_weights, const float* desc2d, int64_t desc2
   const int64_t pm_bs = leaves_bstride == 0 ? 0 : (int64_t)n3 * num_leaf * 256;
   return match_impl(packed_weights, desc2d, desc2d_bstride, desc3d, desc3d_bstride, p.leaves_pm,
                     pm_bs, batch, n1, n3, num_leaf, scale_factor, match_threshold, matches0,
-                    matches1, mscores0, mscores1, conf, p, st);
+                    matches1, mscores0, mscores1, conf, p, st, precision);
 }
 
-int onepose_match_prepared(const void* packed_weights, const float* desc2d,
-                           int64_t desc2d_bstride, const float* desc3d, int64_t desc3d_bstride,
-                           const float* leaves_prepared, int64_t prepared_bstride, int batch,
-                           int n1, int n3, int num_leaf, float scale_factor,
-                           float match_threshold, int64_t* matches0, int64_t* matches1,
-                           float* mscores0, float* mscores1, float* conf, void* workspace,
-                           size_t workspace_bytes, void* stream_) {
+int onepose_match(const void* packed_weights, const float* desc2d, int64_t desc2d_bstride,
+                  const float* desc3d, int64_t desc3d_bstride, const float* leaves,
+                  int64_t leaves_bstride, int batch, int n1, int n3, int num_leaf,
+                  float scale_factor, float match_threshold, int64_t* matches0,
+                  int64_t* matches1, float* mscores0, float* mscores1, float* conf,
+                  void* workspace, size_t workspace_bytes, void* stream_) {
+  return onepose_match_ex(packed_weights, desc2d, desc2d_bstride, desc3d, desc3d_bstride, leaves,
+                          leaves_bstride, batch, n1, n3, num_leaf, scale_factor, match_threshold,
+                          ONEPOSE_PREC_FP32, matches0, matches1, mscores0, mscores1, conf,
+                          workspace, workspace_bytes, stream_);
+}
+
+int onepose_match_prepared_ex(const void* packed_weights, const float* desc2d,
+                              int64_t desc2d_bstride, const float* desc3d, int64_t desc3d_bstride,
+                              const float* leaves_prepared, int64_t prepared_bstride, int batch,
+                              int n1, int n3, int num_leaf, float scale_factor,
+                              float match_threshold, int precision, int64_t* matches0,
+                              int64_t* matches1, float* mscores0, float* mscores1, float* conf,
+                              void* workspace, size_t workspace_bytes, void* stream_) {
   clear_error();
+  OP_REQUIRE(precision == ONEPOSE_PREC_FP32 || precision == ONEPOSE_PREC_BF16_ATTN,
+             "match: precision %d", precision);
   int rc = check_match_args(packed_weights, desc2d, desc3d, leaves_prepared, batch, n1, n3,
                             num_leaf, scale_factor, matches0, matches1, mscores0, mscores1,
                             workspace);
@@ -1178,7 +1195,21 @@ int onepose_match_prepared(const void* packed_weights, const float* desc2d,
   return match_impl(packed_weights, desc2d, desc2d_bstride, desc3d, desc3d_bstride,
                     leaves_prepared, prepared_bstride, batch, n1, n3, num_leaf, scale_factor,
                     match_threshold, matches0, matches1, mscores0, mscores1, conf, p,
-                    static_cast<hipStream_t>(stream_));
+                    static_cast<hipStream_t>(stream_), precision);
+}
+
+int onepose_match_prepared(const void* packed_weights, const float* desc2d,
+                           int64_t desc2d_bstride, const float* desc3d, int64_t desc3d_bstride,
+                           const float* leaves_prepared, int64_t prepared_bstride, int batch,
+                           int n1, int n3, int num_leaf, float scale_factor,
+                           float match_threshold, int64_t* matches0, int64_t* matches1,
+                           float* mscores0, float* mscores1, float* conf, void* workspace,
+                           size_t workspace_bytes, void* stream_) {
+  return onepose_match_prepared_ex(packed_weights, desc2d, desc2d_bstride, desc3d, desc3d_bstride,
+                                   leaves_prepared, prepared_bstride, batch, n1, n3, num_leaf,
+                                   scale_factor, match_threshold, ONEPOSE_PREC_FP32, matches0,
+                                   matches1, mscores0, mscores1, conf, workspace, workspace_bytes,
+                                   stream_);
 }
 
 }  // extern "C"

@@ -101,6 +101,9 @@ class AttentionalGNN(nn.Module):
         self.names = list(layer_names)
 
 
+PRECISIONS = {"fp32": 0, "bf16": 1}   # ONEPOSE_PREC_FP32 / ONEPOSE_PREC_BF16_ATTN
+
+
 class GATsSuperGlue(nn.Module):
     def __init__(self, hparams):
         super().__init__()
@@ -120,6 +123,12 @@ class GATsSuperGlue(nn.Module):
         self.register_parameter("bin_score", nn.Parameter(torch.tensor(1.0)))
         self._packed = None
         self._packed_key = None
+        # onepose_amd extension (not a reference hparam): "fp32" (default, the reference's
+        # numerics) or "bf16" (attention-layer GEMMs on bf16 MFMA, BASELINE config 5)
+        prec = _hp(hparams, "attention_precision", "fp32")
+        if prec not in PRECISIONS:
+            raise ValueError(f"attention_precision {prec!r} not in {sorted(PRECISIONS)}")
+        self.precision = PRECISIONS[prec]
 
     # ---------------------------------------------------------------- weight packing
     def _weight_tensors(self):
@@ -198,10 +207,10 @@ class GATsSuperGlue(nn.Module):
             conf = torch.empty(B, n1, n3, dtype=torch.float32, device=dev)
             ws_bytes = lib.onepose_match_workspace_bytes(B, n1, n3, nleaf, 1)
             ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
-            rc = lib.onepose_match(
+            rc = lib.onepose_match_ex(
                 w.data_ptr(), d2.data_ptr(), s2, d3.data_ptr(), s3, db.data_ptr(), sl,
                 B, n1, n3, nleaf, float(_hp(self.hparams, "scale_factor")),
-                float(_hp(self.hparams, "match_threshold")),
+                float(_hp(self.hparams, "match_threshold")), self.precision,
                 m0.data_ptr(), m1.data_ptr(), ms0.data_ptr(), ms1.data_ptr(), conf.data_ptr(),
                 ws.data_ptr(), ws_bytes, _lib.stream_ptr(dev))
             _lib.check(rc, "onepose_match")

@@ -74,6 +74,7 @@ class FramePipeline:
         self.scale, self.reproj = float(scale), float(reprojection_error)
         self.iters, self.conf_level = int(iterations_count), float(confidence)
         hp = matcher.hparams
+        self.precision = matcher.precision
         self.scale_factor = float(hp["scale_factor"] if isinstance(hp, dict) else hp.scale_factor)
         self.threshold = float(hp["match_threshold"] if isinstance(hp, dict) else hp.match_threshold)
         dev = self.device
@@ -155,10 +156,10 @@ class FramePipeline:
         o = self.slots[slot]
         s = _lib.stream_ptr(self.device)
         desc2d, _ = self._inputs(o)
-        _lib.check(self.lib.onepose_match_prepared(
+        _lib.check(self.lib.onepose_match_prepared_ex(
             self.weights.data_ptr(), desc2d.data_ptr(), 256 * self.n1,
             self.desc3d.data_ptr(), 0, self.leaves_pm.data_ptr(), 0,
-            self.B, self.n1, self.n3, self.L, self.scale_factor, self.threshold,
+            self.B, self.n1, self.n3, self.L, self.scale_factor, self.threshold, self.precision,
             o.matches0.data_ptr(), o.matches1.data_ptr(), o.mscores0.data_ptr(),
             o.mscores1.data_ptr(), _lib.ptr(o.conf), o.ws_match.data_ptr(),
             o.ws_match_bytes, s), "onepose_match_prepared")

@@ -151,3 +151,28 @@ def test_prepared_leaves_path_is_identical(device, n1, n3, L):
         outs.append({k: v.cpu().numpy() for k, v in o.items()})
     for k in outs[0]:
         np.testing.assert_array_equal(outs[0][k], outs[1][k], err_msg=k)
+
+
+@pytest.mark.parametrize("n1,n3", [(1024, 4096), (2048, 8192)])
+def test_bf16_attention_mode_tracks_fp32(n1, n3, device):
+    """BASELINE config 5's bf16-MFMA attention (attention_precision="bf16"): the same matches
+    as the fp32 path on the well-conditioned synthetic object except where the fp32 decision
+    margin is small, confident rows all agree, and scores stay close.  bf16 rounding is not
+    bit-exact by construction; the fp32 path is the parity reference."""
+    from onepose_amd import synthetic as S
+    sd = S.make_state_dict(0)
+    data, _, _ = S.make_matcher_inputs(n1, n3, 8, seed=11, batch=1)
+    inp = {k: torch.as_tensor(v).to(device) for k, v in data.items()}
+    m32 = matcher.from_state_dict(sd)
+    m16 = matcher.from_state_dict(sd, {**S.DEFAULT_HPARAMS, "attention_precision": "bf16"})
+    p32, c32 = m32(inp)
+    p16, c16 = m16(inp)
+    a, b = p32["matches0"].cpu().numpy(), p16["matches0"].cpu().numpy()
+    s32 = p32["matching_scores0"].cpu().numpy()
+    agree = (a == b).mean()
+    matched = a > -1
+    assert matched.sum() > 0.2 * n1
+    assert agree >= 0.99, agree
+    confident = s32 > 0.5
+    assert (a[confident] == b[confident]).all()
+    assert np.abs(c32.cpu().numpy() - c16.cpu().numpy()).max() < 0.05
