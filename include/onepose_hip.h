@@ -140,6 +140,40 @@ int onepose_match_prepared(const void* packed_weights,
                            void* workspace, size_t workspace_bytes, void* stream);
 
 /* ------------------------------------------------------------------------------------ *
+ * N3-sharded single frame (SURVEY.md §8e optional / §8f rank 4): one frame's 3D points split
+ * over `world` ranks (one process per GPU), rank r holding points [start_r, start_r + count_r)
+ * with start_r = floor(n3_total * r / world) (onepose_shard_range).  Every rank holds the
+ * whole 2D side.  Per attention layer the 3D side's KV / sum phi(k) and its InstanceNorm
+ * (n, mean, M2) cross ranks; after the score GEMM the row softmax statistics, the row winners
+ * and the column winners do -- each as an all-gather of one fixed-size block per rank,
+ * merged in rank order on the device.  The caller supplies the exchange buffers (send: one
+ * block of xchg_bytes, recv: world blocks) and a callback that, for `bytes_per_rank` <=
+ * xchg_bytes, makes recv hold every rank's first `bytes_per_rank` bytes of send (rank-major,
+ * block stride = bytes_per_rank) ordered on `stream` (an RCCL all-gather enqueued there, or a
+ * synchronous exchange); it returns 0 on success.
+ * Inputs: desc2d [batch,256,n1]; desc3d_shard [batch,256,count_r]; the shard's leaves
+ * prepared point-major (onepose_prepare_leaves on the shard).  Outputs on every rank, for the
+ * whole frame: matches0 / mscores0 [batch,n1], matches1 / mscores1 [batch,n3_total] (indices
+ * global); conf_shard [batch,n1,count_r] optional.
+ * ------------------------------------------------------------------------------------ */
+typedef int (*onepose_allgather_fn)(size_t bytes_per_rank, void* stream, void* user);
+void onepose_shard_range(int n3_total, int world, int rank, int* start, int* count);
+size_t onepose_match_sharded_xchg_bytes(int batch, int n1, int n3_total, int world);
+size_t onepose_match_sharded_workspace_bytes(int batch, int n1, int n3_total, int world, int rank,
+                                             int num_leaf, int with_conf);
+int onepose_match_sharded(const void* packed_weights,
+                          const float* desc2d, int64_t desc2d_bstride,
+                          const float* desc3d_shard, int64_t desc3d_bstride,
+                          const float* leaves_shard_prepared, int64_t prepared_bstride,
+                          int batch, int n1, int n3_total, int num_leaf, int world, int rank,
+                          float scale_factor, float match_threshold, int precision,
+                          void* xchg_send, void* xchg_recv, size_t xchg_bytes,
+                          onepose_allgather_fn allgather, void* user,
+                          int64_t* matches0, int64_t* matches1,
+                          float* mscores0, float* mscores1, float* conf_shard,
+                          void* workspace, size_t workspace_bytes, void* stream);
+
+/* ------------------------------------------------------------------------------------ *
  * SuperPoint descriptor sampling  --  replaces sample_descriptors
  *   (src/models/extractors/SuperPoint/superpoint.py:95-113)
  * keypoints [batch, n, 2] (x, y) pixels, dense [batch, c, h, w] -> out [batch, c, n],

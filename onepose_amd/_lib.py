@@ -17,6 +17,9 @@ c_int, c_int64, c_size_t, c_float, c_double = (ctypes.c_int, ctypes.c_int64, cty
                                                ctypes.c_float, ctypes.c_double)
 c_void_p, c_char_p = ctypes.c_void_p, ctypes.c_char_p
 
+# onepose_allgather_fn: int (*)(size_t bytes_per_rank, void* stream, void* user)
+ALLGATHER_FN = ctypes.CFUNCTYPE(c_int, c_size_t, c_void_p, c_void_p)
+
 # name -> (restype, argtypes); mirrors include/onepose_hip.h
 PROTOTYPES = {
     "onepose_last_error": (c_char_p, []),
@@ -43,6 +46,16 @@ PROTOTYPES = {
                                           c_void_p, c_int64, c_int, c_int, c_int, c_int, c_float,
                                           c_float, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                                           c_void_p, c_void_p, c_size_t, c_void_p]),
+    "onepose_shard_range": (None, [c_int, c_int, c_int, ctypes.POINTER(c_int),
+                                   ctypes.POINTER(c_int)]),
+    "onepose_match_sharded_xchg_bytes": (c_size_t, [c_int, c_int, c_int, c_int]),
+    "onepose_match_sharded_workspace_bytes": (c_size_t, [c_int, c_int, c_int, c_int, c_int,
+                                                         c_int, c_int]),
+    "onepose_match_sharded": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_int64, c_void_p,
+                                      c_int64, c_int, c_int, c_int, c_int, c_int, c_int,
+                                      c_float, c_float, c_int, c_void_p, c_void_p, c_size_t,
+                                      ALLGATHER_FN, c_void_p, c_void_p, c_void_p, c_void_p,
+                                      c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
     "onepose_leaves_prepared_bytes": (c_size_t, [c_int, c_int, c_int]),
     "onepose_prepare_leaves": (c_int, [c_void_p, c_int64, c_int, c_int, c_int, c_void_p,
                                        c_void_p]),

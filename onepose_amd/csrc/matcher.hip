@@ -33,6 +33,8 @@
 
 #include "gemm.h"
 
+#include <algorithm>
+
 namespace onepose {
 
 // GEMM tile per layer GEMM (gemm.h; measured per shape on config 2).
@@ -380,6 +382,115 @@ __global__ __launch_bounds__(256) void stats_finalize_kernel(StatsArgs args, int
   }
 }
 
+// ---- N3-sharded frames (onepose_match_sharded): per-rank partials and their merges ----
+// Every exchange is an all-gather of a fixed-size block per rank (rank-major in `recv`), merged
+// in rank order, so results do not depend on the collective's reduction order.
+
+// dst[i] = sum_r recv[r * block + off + i]   (KV and sum phi(k) of the sharded 3D side)
+__global__ __launch_bounds__(256) void shard_sum_kernel(const float* recv, int world,
+                                                        int64_t block, int64_t off, int64_t count,
+                                                        float* dst) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= count) return;
+  float s = 0.f;
+  for (int r = 0; r < world; ++r) s += recv[r * block + off + i];
+  dst[i] = s;
+}
+
+// This rank's (n, mean, M2) per channel of the 3D side's MLP hidden layer: out[b][c][3] doubles
+__global__ __launch_bounds__(256) void stats_partial_kernel(StatsProb P, int batch, double* out) {
+  __shared__ double red[3][16][17];
+  const int g = blockIdx.x & 31, b = blockIdx.x >> 5;
+  const int t = threadIdx.x, tg = t >> 4, cl = t & 15, c = g * 16 + cl;
+  const float* part = P.part + (int64_t)b * P.mtiles * 1024;
+  double n = 0.0, mean = 0.0, m2 = 0.0;
+  for (int ti = tg; ti < P.mtiles; ti += 16) {
+    const double nb = (double)min(P.rows, P.m - ti * P.rows);
+    chan_merge(n, mean, m2, nb, part[ti * 1024 + c], part[ti * 1024 + 512 + c]);
+  }
+  red[0][tg][cl] = n;
+  red[1][tg][cl] = mean;
+  red[2][tg][cl] = m2;
+  __syncthreads();
+  if (tg == 0) {
+    for (int k = 1; k < 16; ++k) chan_merge(n, mean, m2, red[0][k][cl], red[1][k][cl], red[2][k][cl]);
+    double* o = out + ((int64_t)b * 512 + c) * 3;
+    o[0] = n;
+    o[1] = mean;
+    o[2] = m2;
+  }
+}
+
+// Chan-merge the ranks' (n, mean, M2) in rank order -> InstanceNorm mean / rstd
+__global__ __launch_bounds__(256) void stats_merge_kernel(const double* recv, int world,
+                                                          int64_t block, int batch, float* mean,
+                                                          float* rstd) {
+  const int i = blockIdx.x * 256 + threadIdx.x;   // (b, c)
+  if (i >= batch * 512) return;
+  double n = 0.0, mu = 0.0, m2 = 0.0;
+  for (int r = 0; r < world; ++r) {
+    const double* q = recv + r * block + (int64_t)i * 3;
+    chan_merge(n, mu, m2, q[0], q[1], q[2]);
+  }
+  mean[i] = (float)mu;
+  rstd[i] = (float)(1.0 / sqrt(m2 / n + 1e-5));
+}
+
+// Row softmax statistics over every rank's columns: max of maxima, rescaled sum of sums
+__global__ __launch_bounds__(256) void rowstat_merge_kernel(const float* recv, int world,
+                                                            int64_t block, int64_t rows,
+                                                            float* rowmax, float* rowsum) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= rows) return;
+  float mx = -INFINITY;
+  for (int r = 0; r < world; ++r) mx = fmaxf(mx, recv[r * block + i]);
+  float s = 0.f;
+  for (int r = 0; r < world; ++r) {
+    const float m = recv[r * block + i];
+    s += recv[r * block + rows + i] * expf(m - mx);
+  }
+  rowmax[i] = mx;
+  rowsum[i] = s;
+}
+
+// Row winners (packed value | global column) across ranks: unsigned max
+__global__ __launch_bounds__(256) void best_max_kernel(const unsigned long long* recv, int world,
+                                                       int64_t block, int64_t count,
+                                                       unsigned long long* dst) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= count) return;
+  unsigned long long k = 0ull;
+  for (int r = 0; r < world; ++r) k = recv[r * block + i] > k ? recv[r * block + i] : k;
+  dst[i] = k;
+}
+
+// colbest [B][n3s] -> send [B][max_shard] (padded rank block)
+__global__ __launch_bounds__(256) void colbest_pack_kernel(const unsigned long long* src, int batch,
+                                                           int n3s, int max_shard,
+                                                           unsigned long long* send) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (int64_t)batch * max_shard) return;
+  const int b = (int)(i / max_shard), j = (int)(i - (int64_t)b * max_shard);
+  send[i] = j < n3s ? src[(int64_t)b * n3s + j] : 0ull;
+}
+
+// Every rank's column winners at their global columns: full [B][n3_total]
+__global__ __launch_bounds__(256) void colbest_assemble_kernel(const unsigned long long* recv,
+                                                               int world, int64_t block,
+                                                               int batch, int n3_total,
+                                                               int max_shard,
+                                                               unsigned long long* full) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;   // (b, global column)
+  if (i >= (int64_t)batch * n3_total) return;
+  const int b = (int)(i / n3_total), col = (int)(i - (int64_t)b * n3_total);
+  // rank owning col: start_r = floor(n3_total * r / world)
+  int r = (int)(((int64_t)col * world) / n3_total);
+  while (r + 1 < world && (int64_t)n3_total * (r + 1) / world <= col) ++r;
+  while (r > 0 && (int64_t)n3_total * r / world > col) --r;
+  const int start = (int)((int64_t)n3_total * r / world);
+  full[i] = recv[r * block + (int64_t)b * max_shard + (col - start)];
+}
+
 // GraphAttentionLayer (GATs.py:62-123) with include_self=True, with_linear_transform=False,
 // additional=False, concat=True, W a folded (h.(W a) == (h W) a):
 //   s3 = h3.wa_hi, s2_j = leaf_j.wa_lo, e = LeakyReLU_0.2(s3 + [s3, s2_1..L])
@@ -533,7 +644,8 @@ __global__ __launch_bounds__(256) void conf_kernel(float* S, int n1, int n3,
                                                    const float* rowmax, const float* rowsum,
                                                    const float* colmax, const float* colsum,
                                                    unsigned long long* rowbest,
-                                                   unsigned long long* colbest, int write_conf) {
+                                                   unsigned long long* colbest, int write_conf,
+                                                   int col_offset) {
   __shared__ unsigned long long cb[4][256];
   const int ct = (n3 + 255) / 256;
   const int tilec = blockIdx.x % ct, tiler = blockIdx.x / ct;
@@ -579,7 +691,7 @@ __global__ __launch_bounds__(256) void conf_kernel(float* S, int n1, int n3,
     for (int j = 0; j < 4; ++j) {
       c[j] = (expf(v[i][j] - cmx[j]) * cinv[j]) * (expf(v[i][j] - rmx) * rinv);
       if (cok[j]) {
-        const unsigned long long rk = pack_best(c[j], col[j]);
+        const unsigned long long rk = pack_best(c[j], col[j] + col_offset);
         key = rk > key ? rk : key;
         const unsigned long long ck = pack_best(c[j], n);
         cbest[j] = ck > cbest[j] ? ck : cbest[j];
@@ -914,13 +1026,55 @@ extern "C" {
 namespace onepose {
 namespace {
 
+// N3-sharded execution context (onepose_match_sharded); null for a whole frame.
+struct ShardCtx {
+  int world, rank, n3_total, offset, max_shard;
+  char* send;          // caller's exchange buffers: this rank's block / world blocks, rank-major
+  char* recv;
+  size_t cap;          // bytes per rank block
+  onepose_allgather_fn fn;
+  void* user;
+  unsigned long long* colbest_full;   // [B][n3_total]
+};
+
+void shard_range(int n3_total, int world, int rank, int* start, int* count) {
+  const int s0 = (int)((int64_t)n3_total * rank / world);
+  const int s1 = (int)((int64_t)n3_total * (rank + 1) / world);
+  *start = s0;
+  *count = s1 - s0;
+}
+
+size_t shard_xchg_bytes(int B, int n1, int n3_total, int world) {
+  const size_t max_shard = (size_t)(n3_total + world - 1) / world;
+  size_t b = (size_t)B * (16384 + 256) * sizeof(float);      // KV + sum phi(k)
+  b = std::max(b, (size_t)B * 512 * 3 * sizeof(double));     // InstanceNorm (n, mean, M2)
+  b = std::max(b, (size_t)B * n1 * 8);                       // row (max, sum) / row winners
+  b = std::max(b, (size_t)B * max_shard * 8);                // column winners
+  return align_up(b, 256);
+}
+
+int shard_exchange(const ShardCtx& sh, size_t bytes, hipStream_t st) {
+  if (bytes > sh.cap) {
+    set_error("match_sharded: exchange of %zu bytes > buffer %zu", bytes, sh.cap);
+    return ONEPOSE_ERR_WORKSPACE;
+  }
+  const int rc = sh.fn(bytes, static_cast<void*>(st), sh.user);
+  if (rc != 0) {
+    set_error("match_sharded: all-gather callback returned %d", rc);
+    return ONEPOSE_ERR_HIP;
+  }
+  return ONEPOSE_OK;
+}
+
 // The matcher forward on point-major leaves [*, n3*L, 256] (leaves_pm_bs elements per sample).
 int match_impl(const void* packed_weights, const float* desc2d, int64_t desc2d_bstride,
                const float* desc3d, int64_t desc3d_bstride, const float* leaves_pm,
                int64_t leaves_pm_bs, int batch, int n1, int n3, int num_leaf, float scale_factor,
                float match_threshold, int64_t* matches0, int64_t* matches1, float* mscores0,
-               float* mscores1, float* conf, const Plan& p, hipStream_t st, int precision) {
+               float* mscores1, float* conf, const Plan& p, hipStream_t st, int precision,
+               const ShardCtx* sh = nullptr) {
   const bool with_conf = conf != nullptr;
+  const int n3g = sh ? sh->n3_total : n3;   // the 3D side's full length (softmax / attention)
   const bool bf = precision == ONEPOSE_PREC_BF16_ATTN;   // attention-layer GEMMs on bf16 MFMA
   const float* wbase = static_cast<const float*>(packed_weights);
   const int B = batch;
@@ -956,7 +1110,7 @@ int match_impl(const void* packed_weights, const float* desc2d, int64_t desc2d_b
     int rc;
     // self: each side attends to itself; cross: 2D <-> 3D.  Source of side s: src(s).
     const int src2 = (kind == 1) ? 0 : 1, src3 = (kind == 1) ? 1 : 0;
-    const int ns2 = src2 == 0 ? n1 : n3, ns3 = src3 == 0 ? n1 : n3;
+    const int ns2 = src2 == 0 ? n1 : n3g, ns3 = src3 == 0 ? n1 : n3g;
     {  // 1. [q | k_h v_h ...] of both tensors: phi(q) stored, per-chunk KV / ksum partials
       GemmArgs a;
       a.nprob = 2;
@@ -966,7 +1120,7 @@ int match_impl(const void* packed_weights, const float* desc2d, int64_t desc2d_b
       a.p[0].kspart = p.kspart2;
       a.p[0].y_bs = (int64_t)n1 * 256;
       a.p[1] = gemm_prob(p.x3[c3], 256, w.wqkv, 256, w.bqkv, p.phiq3, 256, n3, 768, 256, B);
-      a.p[1].vdiv = (float)n3;
+      a.p[1].vdiv = (float)n3g;
       a.p[1].kvpart = p.kvpart3;
       a.p[1].kspart = p.kspart3;
       a.p[1].y_bs = (int64_t)n3 * 256;
@@ -979,6 +1133,18 @@ int match_impl(const void* packed_weights, const float* desc2d, int64_t desc2d_b
       kva.p[1] = {p.kvpart3, p.kspart3, ceil_div(n3, gemm_tile_rows(kTileKV))};
       OP_LAUNCH(K_KV_REDUCE, st, kv_reduce_kernel, dim3(2 * B * 65), dim3(256), 0, st, kva, p.kv,
                 p.ksum, B);
+      if (sh) {   // the 3D side's KV / sum phi(k) over every rank's points
+        const int64_t nkv = (int64_t)B * 16384, nks = (int64_t)B * 256;
+        OP_HIP(hipMemcpyAsync(sh->send, p.kv + nkv, nkv * 4, hipMemcpyDeviceToDevice, st));
+        OP_HIP(hipMemcpyAsync(sh->send + nkv * 4, p.ksum + nks, nks * 4, hipMemcpyDeviceToDevice,
+                              st));
+        if ((rc = shard_exchange(*sh, (nkv + nks) * 4, st)) != ONEPOSE_OK) return rc;
+        const float* rv = reinterpret_cast<const float*>(sh->recv);
+        OP_LAUNCH(K_KV_REDUCE, st, shard_sum_kernel, dim3((unsigned)ceil_div((int)nkv, 256)),
+                  dim3(256), 0, st, rv, sh->world, nkv + nks, (int64_t)0, nkv, p.kv + nkv);
+        OP_LAUNCH(K_KV_REDUCE, st, shard_sum_kernel, dim3((unsigned)ceil_div((int)nks, 256)),
+                  dim3(256), 0, st, rv, sh->world, nkv + nks, nkv, nks, p.ksum + nks);
+      }
     }
     {  // 3. folded message weights per side
       FoldArgs fa;
@@ -1024,7 +1190,18 @@ int match_impl(const void* packed_weights, const float* desc2d, int64_t desc2d_b
       sa.p[0] = {p.stats2, p.mean, p.rstd, n1, ceil_div(n1, str), str};
       sa.p[1] = {p.stats3, p.mean + (size_t)B * 512, p.rstd + (size_t)B * 512, n3,
                  ceil_div(n3, str), str};
-      OP_LAUNCH(K_STATS, st, stats_finalize_kernel, dim3(2 * B * 32), dim3(256), 0, st, sa, B);
+      if (!sh) {
+        OP_LAUNCH(K_STATS, st, stats_finalize_kernel, dim3(2 * B * 32), dim3(256), 0, st, sa, B);
+      } else {   // 2D side local; 3D side Chan-merged over the ranks' (n, mean, M2)
+        OP_LAUNCH(K_STATS, st, stats_finalize_kernel, dim3(B * 32), dim3(256), 0, st, sa, B);
+        OP_LAUNCH(K_STATS, st, stats_partial_kernel, dim3(B * 32), dim3(256), 0, st, sa.p[1], B,
+                  reinterpret_cast<double*>(sh->send));
+        const int64_t nst = (int64_t)B * 512 * 3;
+        if ((rc = shard_exchange(*sh, nst * 8, st)) != ONEPOSE_OK) return rc;
+        OP_LAUNCH(K_STATS, st, stats_merge_kernel, dim3(ceil_div(B * 512, 256)), dim3(256), 0, st,
+                  reinterpret_cast<const double*>(sh->recv), sh->world, nst, B,
+                  p.mean + (size_t)B * 512, p.rstd + (size_t)B * 512);
+      }
     }
     {  // 6. MLP conv 2 on ReLU(InstanceNorm(.)) + residual: desc + delta
       GemmArgs a;
@@ -1077,15 +1254,44 @@ int match_impl(const void* packed_weights, const float* desc2d, int64_t desc2d_b
     OP_LAUNCH(K_SMX_REDUCE, st, softmax_reduce_kernel, dim3((unsigned)((total + 3) / 4)), dim3(256),
                        0, st, p.rowpart, ch3, p.colpart, ch2, B, n1, n3, p.rowmax, p.rowsum,
                        p.colmax, p.colsum, p.rowbest, p.colbest);
+    const int64_t nr = (int64_t)B * n1;
+    if (sh) {   // row softmax over every rank's columns
+      OP_HIP(hipMemcpyAsync(sh->send, p.rowmax, nr * 4, hipMemcpyDeviceToDevice, st));
+      OP_HIP(hipMemcpyAsync(sh->send + nr * 4, p.rowsum, nr * 4, hipMemcpyDeviceToDevice, st));
+      if ((rc = shard_exchange(*sh, nr * 8, st)) != ONEPOSE_OK) return rc;
+      OP_LAUNCH(K_SMX_REDUCE, st, rowstat_merge_kernel, dim3((unsigned)((nr + 255) / 256)),
+                dim3(256), 0, st, reinterpret_cast<const float*>(sh->recv), sh->world, 2 * nr, nr,
+                p.rowmax, p.rowsum);
+    }
+    const int coff = sh ? sh->offset : 0;
     const dim3 cgrid(ceil_div(n1, 32) * ceil_div(n3, 256), B);
     if (n3 % 4 == 0)
       OP_LAUNCH(K_CONF, st, conf_kernel<true>, cgrid, dim3(256), 0, st, S, n1, n3, p.rowmax,
-                p.rowsum, p.colmax, p.colsum, p.rowbest, p.colbest, with_conf ? 1 : 0);
+                p.rowsum, p.colmax, p.colsum, p.rowbest, p.colbest, with_conf ? 1 : 0, coff);
     else
       OP_LAUNCH(K_CONF, st, conf_kernel<false>, cgrid, dim3(256), 0, st, S, n1, n3, p.rowmax,
-                p.rowsum, p.colmax, p.colsum, p.rowbest, p.colbest, with_conf ? 1 : 0);
-    OP_LAUNCH(K_MUTUAL, st, mutual_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st,
-                       p.rowbest, p.colbest, B, n1, n3, match_threshold, matches0, matches1,
+                p.rowsum, p.colmax, p.colsum, p.rowbest, p.colbest, with_conf ? 1 : 0, coff);
+    const unsigned long long* colbest = p.colbest;
+    if (sh) {   // row winners over all columns; every rank's column winners at global columns
+      OP_HIP(hipMemcpyAsync(sh->send, p.rowbest, nr * 8, hipMemcpyDeviceToDevice, st));
+      if ((rc = shard_exchange(*sh, nr * 8, st)) != ONEPOSE_OK) return rc;
+      OP_LAUNCH(K_MUTUAL, st, best_max_kernel, dim3((unsigned)((nr + 255) / 256)), dim3(256), 0, st,
+                reinterpret_cast<const unsigned long long*>(sh->recv), sh->world, nr, nr,
+                p.rowbest);
+      const int64_t nc = (int64_t)B * sh->max_shard;
+      OP_LAUNCH(K_MUTUAL, st, colbest_pack_kernel, dim3((unsigned)((nc + 255) / 256)), dim3(256), 0,
+                st, p.colbest, B, n3, sh->max_shard,
+                reinterpret_cast<unsigned long long*>(sh->send));
+      if ((rc = shard_exchange(*sh, nc * 8, st)) != ONEPOSE_OK) return rc;
+      const int64_t nf = (int64_t)B * n3g;
+      OP_LAUNCH(K_MUTUAL, st, colbest_assemble_kernel, dim3((unsigned)((nf + 255) / 256)),
+                dim3(256), 0, st, reinterpret_cast<const unsigned long long*>(sh->recv), sh->world,
+                nc, B, n3g, sh->max_shard, sh->colbest_full);
+      colbest = sh->colbest_full;
+    }
+    const int64_t tot_g = (int64_t)B * (n1 + n3g);
+    OP_LAUNCH(K_MUTUAL, st, mutual_kernel, dim3((unsigned)((tot_g + 255) / 256)), dim3(256), 0, st,
+                       p.rowbest, colbest, B, n1, n3g, match_threshold, matches0, matches1,
                        mscores0, mscores1);
   }
   return ONEPOSE_OK;
@@ -1210,6 +1416,82 @@ int onepose_match_prepared(const void* packed_weights, const float* desc2d,
                                    scale_factor, match_threshold, ONEPOSE_PREC_FP32, matches0,
                                    matches1, mscores0, mscores1, conf, workspace, workspace_bytes,
                                    stream_);
+}
+
+void onepose_shard_range(int n3_total, int world, int rank, int* start, int* count) {
+  if (!start || !count || world <= 0 || rank < 0 || rank >= world || n3_total < 0) {
+    if (start) *start = 0;
+    if (count) *count = 0;
+    return;
+  }
+  shard_range(n3_total, world, rank, start, count);
+}
+
+size_t onepose_match_sharded_xchg_bytes(int batch, int n1, int n3_total, int world) {
+  if (batch <= 0 || n1 <= 0 || n3_total <= 0 || world <= 0) return 0;
+  return shard_xchg_bytes(batch, n1, n3_total, world);
+}
+
+size_t onepose_match_sharded_workspace_bytes(int batch, int n1, int n3_total, int world, int rank,
+                                             int num_leaf, int with_conf) {
+  if (batch <= 0 || n1 <= 0 || n3_total <= 0 || world <= 0 || rank < 0 || rank >= world) return 0;
+  int s0, n3s;
+  shard_range(n3_total, world, rank, &s0, &n3s);
+  if (n3s <= 0) return 0;
+  return make_plan(nullptr, batch, n1, n3s, num_leaf, with_conf != 0).bytes +
+         align_up((size_t)batch * n3_total * 8, 256);
+}
+
+int onepose_match_sharded(const void* packed_weights, const float* desc2d, int64_t desc2d_bstride,
+                          const float* desc3d_shard, int64_t desc3d_bstride,
+                          const float* leaves_shard_prepared, int64_t prepared_bstride, int batch,
+                          int n1, int n3_total, int num_leaf, int world, int rank,
+                          float scale_factor, float match_threshold, int precision,
+                          void* xchg_send, void* xchg_recv, size_t xchg_bytes,
+                          onepose_allgather_fn allgather, void* user, int64_t* matches0,
+                          int64_t* matches1, float* mscores0, float* mscores1, float* conf_shard,
+                          void* workspace, size_t workspace_bytes, void* stream_) {
+  clear_error();
+  OP_REQUIRE(precision == ONEPOSE_PREC_FP32 || precision == ONEPOSE_PREC_BF16_ATTN,
+             "match_sharded: precision %d", precision);
+  OP_REQUIRE(world >= 1 && rank >= 0 && rank < world, "match_sharded: rank %d of %d", rank, world);
+  OP_REQUIRE(xchg_send && xchg_recv && allgather, "match_sharded: null exchange buffer/callback");
+  int off, n3s;
+  shard_range(n3_total, world, rank, &off, &n3s);
+  OP_REQUIRE(n3s >= 1, "match_sharded: empty shard (n3_total %d, world %d)", n3_total, world);
+  int rc = check_match_args(packed_weights, desc2d, desc3d_shard, leaves_shard_prepared, batch, n1,
+                            n3s, num_leaf, scale_factor, matches0, matches1, mscores0, mscores1,
+                            workspace);
+  if (rc != ONEPOSE_OK) return rc;
+  const size_t need_x = shard_xchg_bytes(batch, n1, n3_total, world);
+  if (xchg_bytes < need_x) {
+    set_error("match_sharded: exchange buffers %zu < %zu bytes per rank", xchg_bytes, need_x);
+    return ONEPOSE_ERR_WORKSPACE;
+  }
+  const size_t need = onepose_match_sharded_workspace_bytes(batch, n1, n3_total, world, rank,
+                                                            num_leaf, conf_shard != nullptr);
+  if (workspace_bytes < need) {
+    set_error("match_sharded: workspace %zu < %zu bytes", workspace_bytes, need);
+    return ONEPOSE_ERR_WORKSPACE;
+  }
+  const Plan p = make_plan(workspace, batch, n1, n3s, num_leaf, conf_shard != nullptr);
+  ShardCtx sh;
+  sh.world = world;
+  sh.rank = rank;
+  sh.n3_total = n3_total;
+  sh.offset = off;
+  sh.max_shard = (n3_total + world - 1) / world;
+  sh.send = static_cast<char*>(xchg_send);
+  sh.recv = static_cast<char*>(xchg_recv);
+  sh.cap = xchg_bytes;
+  sh.fn = allgather;
+  sh.user = user;
+  sh.colbest_full = reinterpret_cast<unsigned long long*>(static_cast<char*>(workspace) +
+                                                          align_up(p.bytes, 256));
+  return match_impl(packed_weights, desc2d, desc2d_bstride, desc3d_shard, desc3d_bstride,
+                    leaves_shard_prepared, prepared_bstride, batch, n1, n3s, num_leaf, scale_factor,
+                    match_threshold, matches0, matches1, mscores0, mscores1, conf_shard, p,
+                    static_cast<hipStream_t>(stream_), precision, &sh);
 }
 
 }  // extern "C"
