@@ -177,10 +177,15 @@ def main():
 
     from onepose_amd import distributed as D
     world, rank, local = D.env()
+    # ONEPOSE_REHEARSE_ONE_GPU=1: every rank on device 0 over gloo -- rehearses the N>1 code
+    # path (sharding, barrier, result gather, max-over-ranks) on a one-GPU box; not a
+    # scaling measurement
+    rehearse = os.environ.get("ONEPOSE_REHEARSE_ONE_GPU") == "1"
+    local = 0 if rehearse else local
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     pg = None
-    if D.init("nccl", dev):   # one process per GPU over RCCL; frames shard, results gather
+    if D.init("gloo" if rehearse else "nccl", dev):   # one process per GPU over RCCL
         import torch.distributed as dist
         pg = dist
 
