@@ -24,12 +24,13 @@ namespace onepose {
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 
 namespace {
 
 // Per-wave MFMA operand fragments of one stage: fp32 (v_mfma_f32_32x32x2_f32, a float4 feeds
 // four MFMAs over k = 8 kk + 4 h + j) or bf16 (v_mfma_f32_32x32x16_bf16: lane half h holds
-// k = 16 kk + 8 h + j, j < 8, converted round-to-nearest-even when read from the fp32 stage).
+// k = 16 kk + 8 h + j, j < 8, from a bf16 LDS image rounded to nearest even when stored).
 template <bool BF, int KKW, int FN>
 struct FragT {
   float4 a[KKW];
@@ -41,20 +42,6 @@ struct FragT<true, KKW, FN> {
   bf16x8 w[KKW][FN];
 };
 
-__device__ __forceinline__ bf16x8 to_bf16x8(const float* p) {
-  const float4 lo = *reinterpret_cast<const float4*>(p);
-  const float4 hi = *reinterpret_cast<const float4*>(p + 4);
-  bf16x8 r;
-  r[0] = (__bf16)lo.x;
-  r[1] = (__bf16)lo.y;
-  r[2] = (__bf16)lo.z;
-  r[3] = (__bf16)lo.w;
-  r[4] = (__bf16)hi.x;
-  r[5] = (__bf16)hi.y;
-  r[6] = (__bf16)hi.z;
-  r[7] = (__bf16)hi.w;
-  return r;
-}
 
 template <int BM_, int BN_, int KS_, int NW_, int BKS_>
 struct Tile {
@@ -69,6 +56,10 @@ struct Tile {
   static constexpr int A4 = BM * KQ / NT;       // float4 of A per thread per stage
   static constexpr int W4 = BN * KQ / NT;
   static constexpr int STAGE = (BM + BN) * PITCH;
+  // bf16 mode: the stage is stored as bf16 rows of BKS + 8 elements (80 B at BKS 32: 16-byte
+  // aligned, and 16 rows at one k hit 16 distinct 4-bank groups -> conflict-free b128 reads)
+  static constexpr int PITCHB = BKS + 8;
+  static constexpr int STAGEB = (BM + BN) * PITCHB;   // bf16 elements (even)
   static_assert(WM * WN * KS == NW && FN >= 1 && A4 >= 1 && W4 >= 1 && KKW >= 2, "tile shape");
   static_assert(NT % KQ == 0 && BM * KQ % NT == 0 && BN * KQ % NT == 0, "one k-quad per thread");
 };
@@ -117,30 +108,42 @@ __device__ __forceinline__ void load_stage(const Ctx& c, int m0, int n0, int k0,
   }
 }
 
-template <int PRO, class T>
-__device__ __forceinline__ void store_stage(float* lds_a, float* lds_w, Stage<T>& s) {
+// Stage registers -> LDS image at `base` ([BM + BN] rows: A then W), applying the prologue;
+// fp32 rows of PITCH floats, or (BF) bf16 rows of PITCHB elements rounded to nearest even.
+template <int PRO, class T, bool BF>
+__device__ __forceinline__ void store_stage(float* base, Stage<T>& s) {
   const int t = threadIdx.x;
   const int kq = (t % T::KQ) * 4;
 #pragma unroll
-  for (int i = 0; i < T::A4; ++i) {
-    float4 v = s.a[i];
-    if (PRO == PRO_NORM_RELU) {
+  for (int i = 0; i < T::A4 + T::W4; ++i) {
+    const bool is_a = i < T::A4;
+    float4 v = is_a ? s.a[i] : s.w[i - T::A4];
+    if (PRO == PRO_NORM_RELU && is_a) {
       v.x = fmaxf((v.x - s.mean.x) * s.rstd.x, 0.f);
       v.y = fmaxf((v.y - s.mean.y) * s.rstd.y, 0.f);
       v.z = fmaxf((v.z - s.mean.z) * s.rstd.z, 0.f);
       v.w = fmaxf((v.w - s.mean.w) * s.rstd.w, 0.f);
     }
-    *reinterpret_cast<float4*>(lds_a + ((t + T::NT * i) / T::KQ) * T::PITCH + kq) = v;
+    const int row = (is_a ? 0 : T::BM) + (t + T::NT * (is_a ? i : i - T::A4)) / T::KQ;
+    if constexpr (BF) {
+      bf16x4 q;
+      q[0] = (__bf16)v.x;
+      q[1] = (__bf16)v.y;
+      q[2] = (__bf16)v.z;
+      q[3] = (__bf16)v.w;
+      *reinterpret_cast<bf16x4*>(reinterpret_cast<__bf16*>(base) + row * T::PITCHB + kq) = q;
+    } else {
+      *reinterpret_cast<float4*>(base + row * T::PITCH + kq) = v;
+    }
   }
-#pragma unroll
-  for (int i = 0; i < T::W4; ++i)
-    *reinterpret_cast<float4*>(lds_w + ((t + T::NT * i) / T::KQ) * T::PITCH + kq) = s.w[i];
 }
 
 template <int EPI, int PRO, class T, bool BF>
 __device__ __forceinline__ void gemm_body(const GemmArgs& args) {
-  constexpr int BM = T::BM, BN = T::BN, FN = T::FN, STAGE = T::STAGE, PITCH = T::PITCH;
-  __shared__ __attribute__((aligned(16))) float lds[2 * STAGE];
+  constexpr int BM = T::BM, BN = T::BN, FN = T::FN, PITCH = T::PITCH;
+  constexpr int STAGE = BF ? T::STAGEB / 2 : T::STAGE;   // one LDS stage, in floats
+  constexpr int LDSF = 2 * STAGE > BM * (BN + 1) ? 2 * STAGE : BM * (BN + 1);
+  __shared__ __attribute__((aligned(16))) float lds[LDSF];
   __shared__ float zrow[BM];
   __shared__ float part[(EPI == EPI_STATS) ? (T::NT / 64) * BN * 2 : 1];
 
@@ -202,15 +205,18 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args) {
   using Frag = FragT<BF, KKW, FN>;
   Frag f0, f1;
   const int kofs = ks * (T::BKS / T::KS) + (lane >> 5) * (KG / 2);
-  const int a_off = (wm * 32 + (lane & 31)) * PITCH + kofs;
-  const int w_off = BM * PITCH + (wn * FN * 32 + (lane & 31)) * PITCH + kofs;
+  constexpr int RP = BF ? T::PITCHB : PITCH;   // LDS row pitch in elements
+  const int a_off = (wm * 32 + (lane & 31)) * RP + kofs;
+  const int w_off = BM * RP + (wn * FN * 32 + (lane & 31)) * RP + kofs;
   auto read_frag = [&](const float* buf, Frag& f) __attribute__((always_inline)) {
 #pragma unroll
     for (int kk = 0; kk < KKW; ++kk) {
       if constexpr (BF) {
-        f.a[kk] = to_bf16x8(buf + a_off + kk * KG);
+        const __bf16* b16 = reinterpret_cast<const __bf16*>(buf);
+        f.a[kk] = *reinterpret_cast<const bf16x8*>(b16 + a_off + kk * KG);
 #pragma unroll
-        for (int j = 0; j < FN; ++j) f.w[kk][j] = to_bf16x8(buf + w_off + j * 32 * PITCH + kk * KG);
+        for (int j = 0; j < FN; ++j)
+          f.w[kk][j] = *reinterpret_cast<const bf16x8*>(b16 + w_off + j * 32 * RP + kk * KG);
       } else {
         f.a[kk] = *reinterpret_cast<const float4*>(buf + a_off + kk * KG);
 #pragma unroll
@@ -251,10 +257,18 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args) {
   auto zdot = [&](const float* buf, int sg) __attribute__((always_inline)) {
     if (PRO == PRO_HEADZ && sg >= xs && sg < nk) {
       static_assert(PRO != PRO_HEADZ || BM * 4 == T::NT, "HEADZ: four threads per row");
-      const float* ap = buf + zr * PITCH + zq * 8;
       const float* kp = zks + (sg * T::BKS - c.ksplit) + zq * 8;   // LDS
-      const float4 a0 = *reinterpret_cast<const float4*>(ap);
-      const float4 a1 = *reinterpret_cast<const float4*>(ap + 4);
+      float4 a0, a1;
+      if constexpr (BF) {   // the phi(q) the bf16 MFMAs see
+        const bf16x8 q = *reinterpret_cast<const bf16x8*>(
+            reinterpret_cast<const __bf16*>(buf) + zr * T::PITCHB + zq * 8);
+        a0 = make_float4((float)q[0], (float)q[1], (float)q[2], (float)q[3]);
+        a1 = make_float4((float)q[4], (float)q[5], (float)q[6], (float)q[7]);
+      } else {
+        const float* ap = buf + zr * PITCH + zq * 8;
+        a0 = *reinterpret_cast<const float4*>(ap);
+        a1 = *reinterpret_cast<const float4*>(ap + 4);
+      }
       const float4 k0 = *reinterpret_cast<const float4*>(kp);
       const float4 k1 = *reinterpret_cast<const float4*>(kp + 4);
       zp += a0.x * k0.x + a0.y * k0.y + a0.z * k0.z + a0.w * k0.w + a1.x * k1.x + a1.y * k1.y +
@@ -280,7 +294,7 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args) {
 
   load_stage<PRO, T>(c, m0, n0, 0, s0);
   load_stage<PRO, T>(c, m0, n0, T::BKS, s1);
-  store_stage<PRO, T>(lds, lds + BM * PITCH, s0);
+  store_stage<PRO, T, BF>(lds, s0);
   __syncthreads();
   read_frag(lds, f0);
 
@@ -291,7 +305,7 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args) {
     mfma_kk(tg, cur, 0);
     __builtin_amdgcn_sched_barrier(0);
     float* na = lds + ((kt + 1) & 1) * STAGE;
-    store_stage<PRO, T>(na, na + BM * PITCH, next);   // (unused after the last step)
+    store_stage<PRO, T, BF>(na, next);                // (unused after the last step)
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int kk = 1; kk < KKW - 1; ++kk) mfma_kk(tg, cur, kk);
@@ -324,7 +338,7 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args) {
   // ---- k-slice reduction: slices 1..KS-1 add into slice 0 in order (deterministic) ----
   if (T::KS > 1) {
     float* red = lds;   // [KS-1][WM*WN][FN][16][64]
-    static_assert((T::KS - 1) * T::WM * T::WN * FN * 16 * 64 <= 2 * STAGE, "reduction fits");
+    static_assert((T::KS - 1) * T::WM * T::WN * FN * 16 * 64 <= LDSF, "reduction fits");
     const int blk = wave % (T::WM * T::WN);
     if (ks > 0) {
 #pragma unroll
