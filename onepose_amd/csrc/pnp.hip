@@ -902,7 +902,94 @@ struct Shared {
   double flip;
   int wave_cnt[4];
   int n_inl;
+  // refit eigensolver (jacobi12_block)
+  double jA[144], jV[144], jc[6], js[6], jscale;
+  int jp[6], jq[6], jrot[12];
 };
+
+// Eigenvectors of the four smallest eigenvalues of the symmetric 12x12 M^T M (packed lower
+// triangle `acc`, identical on every thread), ascending -> ev4 (thread 0), for the EPnP
+// refit.  Cyclic Jacobi in parallel rounds: the circle method pairs the 12 indices into 6
+// disjoint (p, q) per round, 11 rounds per sweep; a round computes the 6 rotations, then
+// applies them to A's columns and V's columns, then to A's rows.  Workgroup-collective (every
+// thread calls it); ~15 us against ~160 us for one thread's eig12_small4.  EPnP's result does
+// not depend on the eigenvectors' signs, and any accurate eigensolver gives the oracle's
+// vectors up to sign when the eigenvalues are separated.
+__device__ void jacobi12_block(Shared& sh, const double* acc, double (&ev4)[4][12]) {
+  const int t = threadIdx.x;
+  for (int i = t; i < 144; i += kThreads) {
+    const int r = i / 12, c = i - r * 12;
+    sh.jA[i] = r >= c ? acc[LI(r, c)] : acc[LI(c, r)];
+    sh.jV[i] = r == c ? 1.0 : 0.0;
+  }
+  if (t < 12) sh.jrot[t] = 0;
+  if (t == 0) {   // trace: the scale of "converged" off-diagonals (M^T M is PSD)
+    double tr = 0.0;
+    for (int i = 0; i < 12; ++i) tr += fabs(acc[LI(i, i)]);
+    sh.jscale = tr;
+  }
+  __syncthreads();
+  for (int sweep = 0; sweep < 12; ++sweep) {
+    for (int round = 0; round < 11; ++round) {
+      if (t < 6) {   // pair t: (round, 11) or ((round + t) % 11, (round - t + 11) % 11)
+        int p = t == 0 ? round : (round + t) % 11;
+        int q = t == 0 ? 11 : (round - t + 11) % 11;
+        if (p > q) {
+          const int x = p;
+          p = q;
+          q = x;
+        }
+        const double apq = sh.jA[p * 12 + q];
+        double c = 1.0, sn = 0.0;
+        if (fabs(apq) > 1e-22 * sh.jscale) sh.jrot[sweep] = 1;   // not yet converged
+        if (apq != 0.0) {
+          const double theta = (sh.jA[q * 12 + q] - sh.jA[p * 12 + p]) / (2.0 * apq);
+          const double tt = (theta >= 0.0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
+          c = 1.0 / sqrt(tt * tt + 1.0);
+          sn = tt * c;
+        }
+        sh.jp[t] = p;
+        sh.jq[t] = q;
+        sh.jc[t] = c;
+        sh.js[t] = sn;
+      }
+      __syncthreads();
+      for (int task = t; task < 144; task += kThreads) {   // A J and V J (columns p, q)
+        const int k = task / 24, w = task - k * 24, i = w % 12;
+        double* M = w < 12 ? sh.jA : sh.jV;
+        const int p = sh.jp[k], q = sh.jq[k];
+        const double c = sh.jc[k], sn = sh.js[k];
+        const double aip = M[i * 12 + p], aiq = M[i * 12 + q];
+        M[i * 12 + p] = c * aip - sn * aiq;
+        M[i * 12 + q] = sn * aip + c * aiq;
+      }
+      __syncthreads();
+      for (int task = t; task < 72; task += kThreads) {    // J^T (A J) (rows p, q)
+        const int k = task / 12, j = task - k * 12;
+        const int p = sh.jp[k], q = sh.jq[k];
+        const double c = sh.jc[k], sn = sh.js[k];
+        const double apj = sh.jA[p * 12 + j], aqj = sh.jA[q * 12 + j];
+        sh.jA[p * 12 + j] = c * apj - sn * aqj;
+        sh.jA[q * 12 + j] = sn * apj + c * aqj;
+      }
+      __syncthreads();
+    }
+    if (!sh.jrot[sweep]) break;   // a sweep without a rotation: converged (uniform)
+  }
+  if (t == 0) {   // the four smallest eigenvalues, ascending (ties by index)
+    int order[12];
+    for (int i = 0; i < 12; ++i) order[i] = i;
+    for (int i = 0; i < 4; ++i)
+      for (int j = i + 1; j < 12; ++j)
+        if (sh.jA[order[j] * 13] < sh.jA[order[i] * 13]) {
+          const int x = order[i];
+          order[i] = order[j];
+          order[j] = x;
+        }
+    for (int i = 0; i < 4; ++i)
+      for (int k = 0; k < 12; ++k) ev4[i][k] = sh.jV[k * 12 + order[i]];
+  }
+}
 
 // Canonical basis of the 4-dimensional EPnP null space of exactly 4 correspondences (M is
 // 8 x 12): P = I - M^T (M M^T)^-1 M, Gram-Schmidt of P's columns in index order.  Same
@@ -974,6 +1061,19 @@ __device__ void null4_basis(const double (&M)[8][12], double (&v)[4][12]) {
 }
 
 // Workgroup-parallel EPnP over the points listed in idx[0..n) (epnp::compute_pose).
+#ifdef ONEPOSE_PNP_PHASES
+__device__ unsigned long long g_pnp_phase[16];
+#define PNP_PHASE(i) \
+  do {               \
+    __syncthreads(); \
+    if (threadIdx.x == 0 && blockIdx.x == 0) g_pnp_phase[i] = wall_clock64(); \
+  } while (0)
+#else
+#define PNP_PHASE(i) \
+  do {               \
+  } while (0)
+#endif
+
 __device__ __forceinline__ void epnp_refit(Shared& sh, const float* p2, const float* p3, const int* idx, int n,
                            const double* K4, double* R_out, double* t_out) {
   const int t = threadIdx.x;
@@ -1047,9 +1147,15 @@ __device__ __forceinline__ void epnp_refit(Shared& sh, const float* p2, const fl
 #pragma unroll
       for (int b = 0; b <= a; ++b) acc[LI(a, b)] += r1[a] * r1[b] + r2[a] * r2[b];
   }
+  PNP_PHASE(1);
   block_sum<78>(acc, sh.red);
+  PNP_PHASE(2);
+  // n >= 6: parallel Jacobi.  n = 5 (M 10 x 12: a 2-dimensional null space whose basis the
+  // refit's result depends on, as OpenCV's does on its SVD) keeps the per-lane solver the
+  // RANSAC hypotheses use; n = 4 takes null4_basis.
+  double ev4[4][12];
+  if (n >= 6) jacobi12_block(sh, acc, ev4);   // workgroup-collective; thread 0 holds ev4
   if (t == 0) {
-    double ev4[4][12];
     if (n == 4) {   // canonical null-space basis (null4_basis), no eigensolver
       double M[8][12];
       for (int i = 0; i < 4; ++i) {
@@ -1066,7 +1172,7 @@ __device__ __forceinline__ void epnp_refit(Shared& sh, const float* p2, const fl
         }
       }
       null4_basis(M, ev4);
-    } else {
+    } else if (n == 5) {
       eig12_small4<100>(acc, ev4, sh.hh, 1);
     }
     for (int i = 0; i < 48; ++i) sh.vs[i] = (&ev4[0][0])[i];
@@ -1074,6 +1180,7 @@ __device__ __forceinline__ void epnp_refit(Shared& sh, const float* p2, const fl
     compute_rho(sh.cws, sh.rho);
   }
   __syncthreads();
+  PNP_PHASE(3);
   for (int which = 1; which <= 3; ++which) {
     if (t == 0) {
       double betas[4];
@@ -1146,6 +1253,7 @@ __device__ __forceinline__ void epnp_refit(Shared& sh, const float* p2, const fl
     if (t == 0) sh.sol_err[which] = err[0] / n;
     __syncthreads();
   }
+  PNP_PHASE(4);
   int N = 1;
   if (sh.sol_err[2] < sh.sol_err[1]) N = 2;
   if (sh.sol_err[3] < sh.sol_err[N]) N = 3;
@@ -1478,7 +1586,9 @@ __global__ __launch_bounds__(kThreads) void pnp_refit_kernel(
   const float* p2 = pts2d + (int64_t)b * max_points * 2;
   const float* p3 = pts3d + (int64_t)b * max_points * 3;
   double Rf[9], tf[3], rv[3], Rr[9];
+  PNP_PHASE(0);
   epnp_refit(sh, p2, p3, idx_ws + (int64_t)b * max_points, nin, K4, Rf, tf);
+  PNP_PHASE(5);
   rodrigues_m2v(Rf, rv);
   rodrigues_v2m(rv, Rr);
   if (t == 0) {
