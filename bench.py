@@ -46,10 +46,19 @@ def superpoint_conv_flops(h, w):
     return sum(2 * (h // d) * (w // d) * co * ci * k * k for d, ci, co, k in layers)
 
 
-def kernel_work(kind, B, n1, n3, L):
+def frame_flops(n1, n3, L, cached):
+    """algorithmic MFMA FLOPs per frame, F, or F_dep when the object-only
+    prefix (GAT 0 + the 3D half of self-attention 1) is cached per object."""
+    f = 11141120 * (n1 + n3) + 512 * n1 * n3 + 2048 * (L + 2) * n3
+    return f - 1376256 * n3 - 512 * (L + 2) * n3 if cached else f
+
+
+def kernel_work(kind, B, n1, n3, L, cached=False):
     """Algorithmic work of ONE launch of each matcher kernel kind: (amount, unit, bound).
-    GEMM-shaped kernels: FLOPs; byte-moving kernels: bytes that must cross HBM."""
-    T = B * (n1 + n3)
+    GEMM-shaped kernels: FLOPs; byte-moving kernels: bytes that must cross HBM.  With the
+    object cache, one of a frame's 8 launches of each attention GEMM has the 2D side only, so
+    the figure is the frame's work of that kind / 8 (the average launch)."""
+    T = B * (n1 + n3) - (B * n3 / 8 if cached else 0)
     C = 256
     table = {
         "qkv_gemm": (2 * 3 * C * C * T, "flop", "mfma"),      # [q | k v] = Wqkv x
@@ -166,6 +175,9 @@ def main():
     ap.add_argument("--precision", choices=["fp32", "bf16"], default="fp32",
                     help="matcher attention-layer GEMMs: fp32 MFMA (the reference's numerics, "
                          "default) or bf16 MFMA with fp32 accumulation (BASELINE config 5)")
+    ap.add_argument("--no-object-cache", action="store_true",
+                    help="run GAT 0 and the 3D half of self-attention 1 every frame instead of "
+                         "once per object (onepose_match_prepared_ex instead of _cached)")
     ap.add_argument("--e2e", action="store_true",
                     help="start each step from images: SuperPoint (max_keypoints = n1, nms 3, "
                          "threshold 0.005) on the GPU produces the query keypoints/descriptors")
@@ -209,7 +221,9 @@ def main():
     pipe = FramePipeline(m, data["keypoints3d"][0], data["descriptors3d_db"][0],
                          data["descriptors2d_db"][0], B, n1, dev, scale=1000.0,
                          slots=max(2, args.match_streams + 1), detector=detector,
-                         image_hw=(args.image_size, args.image_size))
+                         image_hw=(args.image_size, args.image_size),
+                         object_cache=not args.no_object_cache)
+    cached = pipe.object_cache is not None
     pipe.set_frames(data["descriptors2d_query"], data["keypoints2d"],
                     np.stack([f.K for f in frames]), np.stack([f.pose_gt for f in frames]))
     if images is not None:
@@ -227,7 +241,7 @@ def main():
         per_kind.setdefault(names[k], []).append(float(t))
     total = {k: sum(v) / 3.0 for k, v in per_kind.items()}
     # the dominant kernel is timed by device stamps, which the token GEMMs record
-    dominant = max((k for k in total if kernel_work(k, B, n1, n3, L) and k in STAMPED),
+    dominant = max((k for k in total if kernel_work(k, B, n1, n3, L, cached) and k in STAMPED),
                    key=lambda k: total[k])
     dom_id = names.index(dominant)
 
@@ -347,7 +361,7 @@ def main():
                                             / FP32_MFMA_PEAK_TFLOPS, 4),
                "timing": "sum of SuperPoint MFMA-conv launch durations (device clock)"}
     value = frames_total / elapsed
-    work, unit, bound = kernel_work(dominant, B, n1, n3, L)
+    work, unit, bound = kernel_work(dominant, B, n1, n3, L, cached)
     achieved = work / (dom_ms * 1e-3) / 1e12
     bf_dom = args.precision == "bf16" and dominant in ("qkv_gemm", "mlp1_gemm", "mlp2_gemm")
     peak = BF16_MFMA_PEAK_TFLOPS if bf_dom else FP32_MFMA_PEAK_TFLOPS
@@ -361,6 +375,12 @@ def main():
             "launches_timed": n_dom, "flop_per_launch": work,
             "timing": "device clock, first workgroup start to last workgroup end"}
 
+    # SURVEY.md §8d "fraction = F * frames/s / peak" for the whole frame's contractions
+    ff = frame_flops(n1, n3, L, cached)
+    frame_roof = {"flop_per_frame": ff, "formula": "F_dep (object prefix cached)" if cached
+                  else "F", "achieved_tflops": round(ff * value / 1e12, 2),
+                  "peak": peak, "frac": round(ff * value / 1e12 / peak, 4)}
+
     cfg_name = {(1024, 4096): "config 2", (1024, 16384): "config 3",
                 (2048, 8192): "config 5"}.get((n1, n3), "custom")
     if args.precision == "bf16":
@@ -370,6 +390,8 @@ def main():
                  "each step's pose stage on its own stream overlapping the next matchers"
                  if overlap else "serial steps")
         sched += "; stages replayed as HIP graphs" if graphs_on else "; host-launched kernels"
+        sched += ("; object prefix (GAT 0 + 3D half of self-attention 1) prepared once per object"
+                  if cached else "; every layer run per frame")
         out = {
             "metric": METRIC, "value": round(value, 2), "unit": "frames/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup,
@@ -390,6 +412,7 @@ def main():
                      "n_inliers_mean": float(res[:, 17].mean()),
                      "status_ok": float((res[:, 18] == 0).mean())},
             "roofline": roof,
+            "frame_roofline": frame_roof,
             **({"detector": det} if det else {}),
             "host_enqueue_ms_per_step": round(host_enqueue / args.steps * 1e3, 4),
             **({"stage_ms": stage_ms} if stage_ms else {}),

@@ -140,6 +140,35 @@ int onepose_match_prepared(const void* packed_weights,
                            void* workspace, size_t workspace_bytes, void* stream);
 
 /* ------------------------------------------------------------------------------------ *
+ * Per-object cache (SURVEY.md §8b ops_object_prepare, §8f rank 2).  Two parts of the forward
+ * depend on the object alone: GAT layer 0 (GATs.py:62-123, the 3D descriptors and their
+ * leaves) and the 3D half of self-attention 1 (GATs_SuperGlue.py:67-85 -- the 3D side attends
+ * only to itself there).  onepose_object_prepare runs them once per object and leaves the
+ * 3D state entering layer 2 in `cache` ([n3][256] fp32, onepose_object_cache_bytes);
+ * onepose_match_cached then runs every frame from there.  Its results are bit-identical to
+ * onepose_match_prepared_ex's on the same object (the same kernels and tiles produce the
+ * cached state), provided the cache was prepared with the same `precision`.
+ *   desc3d:          [256][n3] reference layout (descriptors3d_db of one object)
+ *   leaves_prepared: [n3*L][256] point-major (onepose_prepare_leaves of the object)
+ * The cache is shared by every sample of a batch (one object per call).
+ * ------------------------------------------------------------------------------------ */
+size_t onepose_object_cache_bytes(int n3);
+size_t onepose_object_prepare_workspace_bytes(int n3, int num_leaf);
+int onepose_object_prepare(const void* packed_weights, const float* desc3d,
+                           const float* leaves_prepared, int n3, int num_leaf, int precision,
+                           float* cache, void* workspace, size_t workspace_bytes, void* stream);
+/* Workspace: onepose_match_workspace_bytes(batch, n1, n3, num_leaf, conf != NULL). */
+int onepose_match_cached(const void* packed_weights,
+                         const float* desc2d, int64_t desc2d_bstride,
+                         const float* object_cache,
+                         const float* leaves_prepared, int64_t prepared_bstride,
+                         int batch, int n1, int n3, int num_leaf,
+                         float scale_factor, float match_threshold, int precision,
+                         int64_t* matches0, int64_t* matches1,
+                         float* mscores0, float* mscores1, float* conf,
+                         void* workspace, size_t workspace_bytes, void* stream);
+
+/* ------------------------------------------------------------------------------------ *
  * N3-sharded single frame (SURVEY.md §8e optional / §8f rank 4): one frame's 3D points split
  * over `world` ranks (one process per GPU), rank r holding points [start_r, start_r + count_r)
  * with start_r = floor(n3_total * r / world) (onepose_shard_range).  Every rank holds the

@@ -46,6 +46,14 @@ PROTOTYPES = {
                                           c_void_p, c_int64, c_int, c_int, c_int, c_int, c_float,
                                           c_float, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                                           c_void_p, c_void_p, c_size_t, c_void_p]),
+    "onepose_object_cache_bytes": (c_size_t, [c_int]),
+    "onepose_object_prepare_workspace_bytes": (c_size_t, [c_int, c_int]),
+    "onepose_object_prepare": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
+                                       c_void_p, c_void_p, c_size_t, c_void_p]),
+    "onepose_match_cached": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_int64,
+                                     c_int, c_int, c_int, c_int, c_float, c_float, c_int,
+                                     c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                     c_void_p, c_size_t, c_void_p]),
     "onepose_shard_range": (None, [c_int, c_int, c_int, ctypes.POINTER(c_int),
                                    ctypes.POINTER(c_int)]),
     "onepose_match_sharded_xchg_bytes": (c_size_t, [c_int, c_int, c_int, c_int]),

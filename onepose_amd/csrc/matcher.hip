@@ -1066,13 +1066,138 @@ int shard_exchange(const ShardCtx& sh, size_t bytes, hipStream_t st) {
   return ONEPOSE_OK;
 }
 
+// One side of an attention layer: its input state (x_bs 0 = shared by the batch: the object
+// cache), where the residual output goes, its per-layer scratch, and which slot's KV it
+// attends to.  Slot i of kv / ksum / mf / mean / rstd belongs to side i of the launch.
+struct Side {
+  const float* x;
+  int64_t x_bs;
+  float* xo;
+  float *phiq, *kvpart, *kspart, *y1, *stats;
+  int n;        // tokens (this rank's)
+  float len;    // the side's full length as an attention source (Ns, v / Ns)
+  int src;      // slot of the side this one attends to
+};
+
+// AttentionPropagation (GATs_SuperGlue.py:123-132) for 1 or 2 sides in grouped launches.
+// Each side's arithmetic is independent of the others' (per-problem tiles, per-slot
+// reductions), so a side gives the same bits alone or grouped.  Sharded runs have two
+// sides, slot 1 being the 3D shard.
+int attention_layer(const ApW& w, const Side* sd, int nside, int B, const Plan& p,
+                    hipStream_t st, bool bf, const ShardCtx* sh) {
+  int rc;
+  {  // 1. [q | k_h v_h ...]: phi(q) stored, per-chunk KV / ksum partials
+    GemmArgs a;
+    a.nprob = nside;
+    for (int i = 0; i < nside; ++i) {
+      const Side& s = sd[i];
+      a.p[i] = gemm_prob(s.x, 256, w.wqkv, 256, w.bqkv, s.phiq, 256, s.n, 768, 256, B);
+      a.p[i].a0_bs = s.x_bs;
+      a.p[i].vdiv = s.len;
+      a.p[i].kvpart = s.kvpart;
+      a.p[i].kspart = s.kspart;
+      a.p[i].y_bs = (int64_t)s.n * 256;
+    }
+    if ((rc = gemm_launch(EPI_QKV, PRO_PLAIN, kTileKV, a, st, K_QKV_GEMM, bf)) != ONEPOSE_OK)
+      return rc;
+  }
+  {  // 2. KV[slot], ksum[slot]
+    KvArgs kva;
+    for (int i = 0; i < nside; ++i)
+      kva.p[i] = {sd[i].kvpart, sd[i].kspart, ceil_div(sd[i].n, gemm_tile_rows(kTileKV))};
+    OP_LAUNCH(K_KV_REDUCE, st, kv_reduce_kernel, dim3(nside * B * 65), dim3(256), 0, st, kva,
+              p.kv, p.ksum, B);
+    if (sh) {   // the 3D side's KV / sum phi(k) over every rank's points
+      const int64_t nkv = (int64_t)B * 16384, nks = (int64_t)B * 256;
+      OP_HIP(hipMemcpyAsync(sh->send, p.kv + nkv, nkv * 4, hipMemcpyDeviceToDevice, st));
+      OP_HIP(hipMemcpyAsync(sh->send + nkv * 4, p.ksum + nks, nks * 4, hipMemcpyDeviceToDevice,
+                            st));
+      if ((rc = shard_exchange(*sh, (nkv + nks) * 4, st)) != ONEPOSE_OK) return rc;
+      const float* rv = reinterpret_cast<const float*>(sh->recv);
+      OP_LAUNCH(K_KV_REDUCE, st, shard_sum_kernel, dim3((unsigned)ceil_div((int)nkv, 256)),
+                dim3(256), 0, st, rv, sh->world, nkv + nks, (int64_t)0, nkv, p.kv + nkv);
+      OP_LAUNCH(K_KV_REDUCE, st, shard_sum_kernel, dim3((unsigned)ceil_div((int)nks, 256)),
+                dim3(256), 0, st, rv, sh->world, nkv + nks, nkv, nks, p.ksum + nks);
+    }
+  }
+  {  // 3. folded message weights per side
+    FoldArgs fa;
+    fa.c = w.c;
+    for (int i = 0; i < nside; ++i)
+      fa.p[i] = {p.kv + (size_t)sd[i].src * B * 16384, p.mf + (size_t)i * B * 512 * 256};
+    OP_LAUNCH(K_MFOLD, st, m_fold_kernel, dim3(nside * B * 32), dim3(256), 0, st, fa, B);
+  }
+  {  // 4. MLP conv 1 on [x ; phi(q)] with [W1a | Mf], the phi(q) heads scaled by Z * Ns
+     //    in-kernel (PRO_HEADZ), + InstanceNorm partials
+    GemmArgs a;
+    a.nprob = nside;
+    for (int i = 0; i < nside; ++i) {
+      const Side& s = sd[i];
+      a.p[i] = gemm_prob(s.x, 256, w.w1a, 256, w.b1, s.y1, 512, s.n, 512, 512, B);
+      a.p[i].a0_bs = s.x_bs;
+      a.p[i].A1 = s.phiq;
+      a.p[i].lda1 = 256;
+      a.p[i].a1_bs = (int64_t)s.n * 256;
+      a.p[i].ksplit = 256;
+      a.p[i].W1 = p.mf + (size_t)i * B * 512 * 256;
+      a.p[i].ldw1 = 256;
+      a.p[i].w1_bs = 512 * 256;
+      a.p[i].stats = s.stats;
+      a.p[i].ksum = p.ksum + (size_t)s.src * B * 256;
+      a.p[i].ksum_bs = 256;
+      a.p[i].ns = sd[s.src].len;
+    }
+    if ((rc = gemm_launch(EPI_STATS, PRO_HEADZ, kTileMLP1, a, st, K_MLP1, bf)) != ONEPOSE_OK)
+      return rc;
+  }
+  {  // 5. InstanceNorm statistics
+    StatsArgs sa;
+    const int str = gemm_tile_rows(kTileMLP1);
+    for (int i = 0; i < nside; ++i)
+      sa.p[i] = {sd[i].stats, p.mean + (size_t)i * B * 512, p.rstd + (size_t)i * B * 512,
+                 sd[i].n, ceil_div(sd[i].n, str), str};
+    if (!sh) {
+      OP_LAUNCH(K_STATS, st, stats_finalize_kernel, dim3(nside * B * 32), dim3(256), 0, st, sa,
+                B);
+    } else {   // 2D side local; 3D side Chan-merged over the ranks' (n, mean, M2)
+      OP_LAUNCH(K_STATS, st, stats_finalize_kernel, dim3(B * 32), dim3(256), 0, st, sa, B);
+      OP_LAUNCH(K_STATS, st, stats_partial_kernel, dim3(B * 32), dim3(256), 0, st, sa.p[1], B,
+                reinterpret_cast<double*>(sh->send));
+      const int64_t nst = (int64_t)B * 512 * 3;
+      if ((rc = shard_exchange(*sh, nst * 8, st)) != ONEPOSE_OK) return rc;
+      OP_LAUNCH(K_STATS, st, stats_merge_kernel, dim3(ceil_div(B * 512, 256)), dim3(256), 0, st,
+                reinterpret_cast<const double*>(sh->recv), sh->world, nst, B,
+                p.mean + (size_t)B * 512, p.rstd + (size_t)B * 512);
+    }
+  }
+  {  // 6. MLP conv 2 on ReLU(InstanceNorm(.)) + residual: desc + delta
+    GemmArgs a;
+    a.nprob = nside;
+    for (int i = 0; i < nside; ++i) {
+      const Side& s = sd[i];
+      a.p[i] = gemm_prob(s.y1, 512, w.w2, 512, w.b2, s.xo, 256, s.n, 256, 512, B);
+      a.p[i].R = s.x;
+      a.p[i].ldr = 256;
+      a.p[i].r_bs = s.x_bs;
+      a.p[i].pro_mean = p.mean + (size_t)i * B * 512;
+      a.p[i].pro_rstd = p.rstd + (size_t)i * B * 512;
+      a.p[i].pro_bs = 512;
+    }
+    if ((rc = gemm_launch(EPI_RESID, PRO_NORM_RELU, kTileMLP2, a, st, K_MLP2, bf)) != ONEPOSE_OK)
+      return rc;
+  }
+  return ONEPOSE_OK;
+}
+
 // The matcher forward on point-major leaves [*, n3*L, 256] (leaves_pm_bs elements per sample).
+// obj_cache (onepose_match_cached): the 3D side entering layer 2, [n3][256] shared by the
+// batch (onepose_object_prepare) -- GAT 0 and the 3D half of self-attention 1 are skipped.
 int match_impl(const void* packed_weights, const float* desc2d, int64_t desc2d_bstride,
                const float* desc3d, int64_t desc3d_bstride, const float* leaves_pm,
                int64_t leaves_pm_bs, int batch, int n1, int n3, int num_leaf, float scale_factor,
                float match_threshold, int64_t* matches0, int64_t* matches1, float* mscores0,
                float* mscores1, float* conf, const Plan& p, hipStream_t st, int precision,
-               const ShardCtx* sh = nullptr) {
+               const ShardCtx* sh = nullptr, const float* obj_cache = nullptr) {
   const bool with_conf = conf != nullptr;
   const int n3g = sh ? sh->n3_total : n3;   // the 3D side's full length (softmax / attention)
   const bool bf = precision == ONEPOSE_PREC_BF16_ATTN;   // attention-layer GEMMs on bf16 MFMA
@@ -1085,146 +1210,52 @@ int match_impl(const void* packed_weights, const float* desc2d, int64_t desc2d_b
   {
     TransArgs ta;
     ta.p[0] = {desc2d, desc2d_bstride, n1, ceil_div(n1, 64) * 4, p.x2[0]};
-    ta.p[1] = {desc3d, desc3d_bstride, n3, ceil_div(n3, 64) * 4, p.x3[0]};
+    ta.p[1] = {desc3d, desc3d_bstride, n3, obj_cache ? 0 : ceil_div(n3, 64) * 4, p.x3[0]};
     OP_LAUNCH(K_TRANSPOSE, st, transpose_in_kernel, dim3((ta.p[0].tiles + ta.p[1].tiles) * B),
               dim3(256), 0, st, ta, B);
   }
 
+  // Current states: side x is read from x?r (batch stride x?bs) and written to p.x?[c? ^ 1].
   int c2 = 0, c3 = 0, ap = 0, gat = 0;
+  const float* x2r = p.x2[0];
+  const float* x3r = obj_cache ? obj_cache : p.x3[0];
+  int64_t x3bs = obj_cache ? 0 : (int64_t)n3 * 256;
   const int ch2 = ceil_div(n1, 64), ch3 = ceil_div(n3, 64);
   for (int layer = 0; layer < kLayers; ++layer) {
     const int kind = layer % 3;  // 0 GATs, 1 self, 2 cross
+    const bool cached3 = obj_cache && layer < 2;   // the 3D side comes from the cache
     if (kind == 0) {
-      const dim3 ggrid(ceil_div(B * n3, 4));
-      if (num_leaf <= 8)
-        OP_LAUNCH(K_GAT, st, gat_kernel<8>, ggrid, dim3(256), 0, st, p.x3[c3], leaves,
-                  leaves_bstride, gat_weights(wbase, gat), p.x3[c3 ^ 1], n3, num_leaf, B);
-      else
-        OP_LAUNCH(K_GAT, st, gat_kernel<16>, ggrid, dim3(256), 0, st, p.x3[c3], leaves,
-                  leaves_bstride, gat_weights(wbase, gat), p.x3[c3 ^ 1], n3, num_leaf, B);
-      c3 ^= 1;
+      if (!cached3) {
+        const dim3 ggrid(ceil_div(B * n3, 4));
+        if (num_leaf <= 8)
+          OP_LAUNCH(K_GAT, st, gat_kernel<8>, ggrid, dim3(256), 0, st, x3r, leaves,
+                    leaves_bstride, gat_weights(wbase, gat), p.x3[c3 ^ 1], n3, num_leaf, B);
+        else
+          OP_LAUNCH(K_GAT, st, gat_kernel<16>, ggrid, dim3(256), 0, st, x3r, leaves,
+                    leaves_bstride, gat_weights(wbase, gat), p.x3[c3 ^ 1], n3, num_leaf, B);
+        x3r = p.x3[c3 ^ 1];
+        c3 ^= 1;
+      }
       ++gat;
       continue;
     }
     const ApW w = ap_weights(wbase, ap++);
-    int rc;
-    // self: each side attends to itself; cross: 2D <-> 3D.  Source of side s: src(s).
-    const int src2 = (kind == 1) ? 0 : 1, src3 = (kind == 1) ? 1 : 0;
-    const int ns2 = src2 == 0 ? n1 : n3g, ns3 = src3 == 0 ? n1 : n3g;
-    {  // 1. [q | k_h v_h ...] of both tensors: phi(q) stored, per-chunk KV / ksum partials
-      GemmArgs a;
-      a.nprob = 2;
-      a.p[0] = gemm_prob(p.x2[c2], 256, w.wqkv, 256, w.bqkv, p.phiq2, 256, n1, 768, 256, B);
-      a.p[0].vdiv = (float)n1;
-      a.p[0].kvpart = p.kvpart2;
-      a.p[0].kspart = p.kspart2;
-      a.p[0].y_bs = (int64_t)n1 * 256;
-      a.p[1] = gemm_prob(p.x3[c3], 256, w.wqkv, 256, w.bqkv, p.phiq3, 256, n3, 768, 256, B);
-      a.p[1].vdiv = (float)n3g;
-      a.p[1].kvpart = p.kvpart3;
-      a.p[1].kspart = p.kspart3;
-      a.p[1].y_bs = (int64_t)n3 * 256;
-      if ((rc = gemm_launch(EPI_QKV, PRO_PLAIN, kTileKV, a, st, K_QKV_GEMM, bf)) != ONEPOSE_OK)
-        return rc;
-    }
-    {  // 2. KV[src], ksum[src]
-      KvArgs kva;
-      kva.p[0] = {p.kvpart2, p.kspart2, ceil_div(n1, gemm_tile_rows(kTileKV))};
-      kva.p[1] = {p.kvpart3, p.kspart3, ceil_div(n3, gemm_tile_rows(kTileKV))};
-      OP_LAUNCH(K_KV_REDUCE, st, kv_reduce_kernel, dim3(2 * B * 65), dim3(256), 0, st, kva, p.kv,
-                p.ksum, B);
-      if (sh) {   // the 3D side's KV / sum phi(k) over every rank's points
-        const int64_t nkv = (int64_t)B * 16384, nks = (int64_t)B * 256;
-        OP_HIP(hipMemcpyAsync(sh->send, p.kv + nkv, nkv * 4, hipMemcpyDeviceToDevice, st));
-        OP_HIP(hipMemcpyAsync(sh->send + nkv * 4, p.ksum + nks, nks * 4, hipMemcpyDeviceToDevice,
-                              st));
-        if ((rc = shard_exchange(*sh, (nkv + nks) * 4, st)) != ONEPOSE_OK) return rc;
-        const float* rv = reinterpret_cast<const float*>(sh->recv);
-        OP_LAUNCH(K_KV_REDUCE, st, shard_sum_kernel, dim3((unsigned)ceil_div((int)nkv, 256)),
-                  dim3(256), 0, st, rv, sh->world, nkv + nks, (int64_t)0, nkv, p.kv + nkv);
-        OP_LAUNCH(K_KV_REDUCE, st, shard_sum_kernel, dim3((unsigned)ceil_div((int)nks, 256)),
-                  dim3(256), 0, st, rv, sh->world, nkv + nks, nkv, nks, p.ksum + nks);
-      }
-    }
-    {  // 3. folded message weights per side
-      FoldArgs fa;
-      fa.c = w.c;
-      fa.p[0] = {p.kv + (size_t)src2 * B * 16384, p.mf};
-      fa.p[1] = {p.kv + (size_t)src3 * B * 16384, p.mf + (size_t)B * 512 * 256};
-      OP_LAUNCH(K_MFOLD, st, m_fold_kernel, dim3(2 * B * 32), dim3(256), 0, st, fa, B);
-    }
-    {  // 4. MLP conv 1 on [x ; phi(q)] with [W1a | Mf], the phi(q) heads scaled by Z * Ns
-       //    in-kernel (PRO_HEADZ), + InstanceNorm partials
-      GemmArgs a;
-      a.nprob = 2;
-      a.p[0] = gemm_prob(p.x2[c2], 256, w.w1a, 256, w.b1, p.y12, 512, n1, 512, 512, B);
-      a.p[0].A1 = p.phiq2;
-      a.p[0].lda1 = 256;
-      a.p[0].a1_bs = (int64_t)n1 * 256;
-      a.p[0].ksplit = 256;
-      a.p[0].W1 = p.mf;
-      a.p[0].ldw1 = 256;
-      a.p[0].w1_bs = 512 * 256;
-      a.p[0].stats = p.stats2;
-      a.p[0].ksum = p.ksum + (size_t)src2 * B * 256;
-      a.p[0].ksum_bs = 256;
-      a.p[0].ns = (float)ns2;
-      a.p[1] = gemm_prob(p.x3[c3], 256, w.w1a, 256, w.b1, p.y13, 512, n3, 512, 512, B);
-      a.p[1].A1 = p.phiq3;
-      a.p[1].lda1 = 256;
-      a.p[1].a1_bs = (int64_t)n3 * 256;
-      a.p[1].ksplit = 256;
-      a.p[1].W1 = p.mf + (size_t)B * 512 * 256;
-      a.p[1].ldw1 = 256;
-      a.p[1].w1_bs = 512 * 256;
-      a.p[1].stats = p.stats3;
-      a.p[1].ksum = p.ksum + (size_t)src3 * B * 256;
-      a.p[1].ksum_bs = 256;
-      a.p[1].ns = (float)ns3;
-      if ((rc = gemm_launch(EPI_STATS, PRO_HEADZ, kTileMLP1, a, st, K_MLP1, bf)) != ONEPOSE_OK)
-        return rc;
-    }
-    {  // 5. InstanceNorm statistics
-      StatsArgs sa;
-      const int str = gemm_tile_rows(kTileMLP1);
-      sa.p[0] = {p.stats2, p.mean, p.rstd, n1, ceil_div(n1, str), str};
-      sa.p[1] = {p.stats3, p.mean + (size_t)B * 512, p.rstd + (size_t)B * 512, n3,
-                 ceil_div(n3, str), str};
-      if (!sh) {
-        OP_LAUNCH(K_STATS, st, stats_finalize_kernel, dim3(2 * B * 32), dim3(256), 0, st, sa, B);
-      } else {   // 2D side local; 3D side Chan-merged over the ranks' (n, mean, M2)
-        OP_LAUNCH(K_STATS, st, stats_finalize_kernel, dim3(B * 32), dim3(256), 0, st, sa, B);
-        OP_LAUNCH(K_STATS, st, stats_partial_kernel, dim3(B * 32), dim3(256), 0, st, sa.p[1], B,
-                  reinterpret_cast<double*>(sh->send));
-        const int64_t nst = (int64_t)B * 512 * 3;
-        if ((rc = shard_exchange(*sh, nst * 8, st)) != ONEPOSE_OK) return rc;
-        OP_LAUNCH(K_STATS, st, stats_merge_kernel, dim3(ceil_div(B * 512, 256)), dim3(256), 0, st,
-                  reinterpret_cast<const double*>(sh->recv), sh->world, nst, B,
-                  p.mean + (size_t)B * 512, p.rstd + (size_t)B * 512);
-      }
-    }
-    {  // 6. MLP conv 2 on ReLU(InstanceNorm(.)) + residual: desc + delta
-      GemmArgs a;
-      a.nprob = 2;
-      a.p[0] = gemm_prob(p.y12, 512, w.w2, 512, w.b2, p.x2[c2 ^ 1], 256, n1, 256, 512, B);
-      a.p[0].R = p.x2[c2];
-      a.p[0].ldr = 256;
-      a.p[0].r_bs = (int64_t)n1 * 256;
-      a.p[0].pro_mean = p.mean;
-      a.p[0].pro_rstd = p.rstd;
-      a.p[0].pro_bs = 512;
-      a.p[1] = gemm_prob(p.y13, 512, w.w2, 512, w.b2, p.x3[c3 ^ 1], 256, n3, 256, 512, B);
-      a.p[1].R = p.x3[c3];
-      a.p[1].ldr = 256;
-      a.p[1].r_bs = (int64_t)n3 * 256;
-      a.p[1].pro_mean = p.mean + (size_t)B * 512;
-      a.p[1].pro_rstd = p.rstd + (size_t)B * 512;
-      a.p[1].pro_bs = 512;
-      if ((rc = gemm_launch(EPI_RESID, PRO_NORM_RELU, kTileMLP2, a, st, K_MLP2, bf)) != ONEPOSE_OK)
-        return rc;
-    }
+    // self: each side attends to itself; cross: 2D <-> 3D
+    Side sd[2];
+    sd[0] = {x2r, (int64_t)n1 * 256, p.x2[c2 ^ 1], p.phiq2, p.kvpart2, p.kspart2, p.y12,
+             p.stats2, n1, (float)n1, kind == 1 ? 0 : 1};
+    sd[1] = {x3r, x3bs, p.x3[c3 ^ 1], p.phiq3, p.kvpart3, p.kspart3, p.y13, p.stats3, n3,
+             (float)n3g, kind == 1 ? 1 : 0};
+    const int nside = cached3 ? 1 : 2;
+    int rc = attention_layer(w, sd, nside, B, p, st, bf, sh);
+    if (rc != ONEPOSE_OK) return rc;
+    x2r = p.x2[c2 ^ 1];
     c2 ^= 1;
-    c3 ^= 1;
+    if (!cached3) {
+      x3r = p.x3[c3 ^ 1];
+      x3bs = (int64_t)n3 * 256;
+      c3 ^= 1;
+    }
   }
 
   int rc;
@@ -1232,8 +1263,8 @@ int match_impl(const void* packed_weights, const float* desc2d, int64_t desc2d_b
     const float* fw = final_weights(wbase);
     GemmArgs a;
     a.nprob = 2;
-    a.p[0] = gemm_prob(p.x2[c2], 256, fw, 256, fw + 65536, p.f2, 256, n1, 256, 256, B);
-    a.p[1] = gemm_prob(p.x3[c3], 256, fw, 256, fw + 65536, p.f3, 256, n3, 256, 256, B);
+    a.p[0] = gemm_prob(x2r, 256, fw, 256, fw + 65536, p.f2, 256, n1, 256, 256, B);
+    a.p[1] = gemm_prob(x3r, 256, fw, 256, fw + 65536, p.f3, 256, n3, 256, 256, B);
     if ((rc = gemm_launch(EPI_BIAS, PRO_PLAIN, kTileFinal, a, st, K_FINAL)) != ONEPOSE_OK) return rc;
     const int rows = B * (n1 + n3);
     OP_LAUNCH(K_L2NORM, st, l2norm_kernel, dim3(ceil_div(rows, 4)), dim3(256), 0, st, p.f2, B * n1,
@@ -1295,6 +1326,34 @@ int match_impl(const void* packed_weights, const float* desc2d, int64_t desc2d_b
                        mscores0, mscores1);
   }
   return ONEPOSE_OK;
+}
+
+// The frame-independent prefix of the 3D side (onepose_object_prepare): transpose, GAT 0
+// (GATs.py:62-123 on the object's own leaves) and the 3D half of self-attention 1 (the 3D
+// side attends only to itself there) -> cache [n3][256], the state entering layer 2.
+// The same kernels and tiles as the grouped forward, so the cached state is bit-identical
+// to what onepose_match computes in place.
+int object_prepare_impl(const void* packed_weights, const float* desc3d, const float* leaves_pm,
+                        int n3, int num_leaf, int precision, float* cache, const Plan& p,
+                        hipStream_t st) {
+  const float* wbase = static_cast<const float*>(packed_weights);
+  {
+    TransArgs ta;
+    ta.p[0] = {desc3d, 0, n3, ceil_div(n3, 64) * 4, p.x3[0]};
+    ta.p[1] = {desc3d, 0, n3, 0, p.x3[0]};
+    OP_LAUNCH(K_TRANSPOSE, st, transpose_in_kernel, dim3(ta.p[0].tiles), dim3(256), 0, st, ta, 1);
+  }
+  const dim3 ggrid(ceil_div(n3, 4));
+  if (num_leaf <= 8)
+    OP_LAUNCH(K_GAT, st, gat_kernel<8>, ggrid, dim3(256), 0, st, p.x3[0], leaves_pm, (int64_t)0,
+              gat_weights(wbase, 0), p.x3[1], n3, num_leaf, 1);
+  else
+    OP_LAUNCH(K_GAT, st, gat_kernel<16>, ggrid, dim3(256), 0, st, p.x3[0], leaves_pm, (int64_t)0,
+              gat_weights(wbase, 0), p.x3[1], n3, num_leaf, 1);
+  const Side s3 = {p.x3[1], (int64_t)n3 * 256, cache, p.phiq3, p.kvpart3, p.kspart3, p.y13,
+                   p.stats3, n3, (float)n3, 0};
+  return attention_layer(ap_weights(wbase, 0), &s3, 1, 1, p, st,
+                         precision == ONEPOSE_PREC_BF16_ATTN, nullptr);
 }
 
 int check_match_args(const void* packed_weights, const float* desc2d, const float* desc3d,
@@ -1416,6 +1475,62 @@ int onepose_match_prepared(const void* packed_weights, const float* desc2d,
                                    scale_factor, match_threshold, ONEPOSE_PREC_FP32, matches0,
                                    matches1, mscores0, mscores1, conf, workspace, workspace_bytes,
                                    stream_);
+}
+
+size_t onepose_object_cache_bytes(int n3) {
+  if (n3 <= 0) return 0;
+  return (size_t)n3 * 256 * sizeof(float);
+}
+
+size_t onepose_object_prepare_workspace_bytes(int n3, int num_leaf) {
+  clear_error();
+  if (n3 <= 0 || num_leaf < 1 || num_leaf > 16) return 0;
+  return make_plan(nullptr, 1, 1, n3, num_leaf, false).bytes;
+}
+
+int onepose_object_prepare(const void* packed_weights, const float* desc3d,
+                           const float* leaves_prepared, int n3, int num_leaf, int precision,
+                           float* cache, void* workspace, size_t workspace_bytes, void* stream_) {
+  clear_error();
+  OP_REQUIRE(packed_weights && desc3d && leaves_prepared && cache, "object_prepare: null pointer");
+  OP_REQUIRE(precision == ONEPOSE_PREC_FP32 || precision == ONEPOSE_PREC_BF16_ATTN,
+             "object_prepare: precision %d", precision);
+  OP_REQUIRE(n3 >= 1 && num_leaf >= 1 && num_leaf <= 16, "object_prepare: n3=%d num_leaf=%d", n3,
+             num_leaf);
+  OP_REQUIRE(workspace != nullptr, "object_prepare: null workspace");
+  const size_t need = onepose_object_prepare_workspace_bytes(n3, num_leaf);
+  if (workspace_bytes < need) {
+    set_error("object_prepare: workspace %zu < %zu bytes", workspace_bytes, need);
+    return ONEPOSE_ERR_WORKSPACE;
+  }
+  const Plan p = make_plan(workspace, 1, 1, n3, num_leaf, false);
+  return object_prepare_impl(packed_weights, desc3d, leaves_prepared, n3, num_leaf, precision,
+                             cache, p, static_cast<hipStream_t>(stream_));
+}
+
+int onepose_match_cached(const void* packed_weights, const float* desc2d, int64_t desc2d_bstride,
+                         const float* object_cache, const float* leaves_prepared,
+                         int64_t prepared_bstride, int batch, int n1, int n3, int num_leaf,
+                         float scale_factor, float match_threshold, int precision,
+                         int64_t* matches0, int64_t* matches1, float* mscores0, float* mscores1,
+                         float* conf, void* workspace, size_t workspace_bytes, void* stream_) {
+  clear_error();
+  OP_REQUIRE(precision == ONEPOSE_PREC_FP32 || precision == ONEPOSE_PREC_BF16_ATTN,
+             "match_cached: precision %d", precision);
+  int rc = check_match_args(packed_weights, desc2d, object_cache, leaves_prepared, batch, n1, n3,
+                            num_leaf, scale_factor, matches0, matches1, mscores0, mscores1,
+                            workspace);
+  if (rc != ONEPOSE_OK) return rc;
+  const Plan need = make_plan(nullptr, batch, n1, n3, num_leaf, conf != nullptr);
+  if (workspace_bytes < need.bytes) {
+    set_error("match_cached: workspace %zu < %zu bytes", workspace_bytes, need.bytes);
+    return ONEPOSE_ERR_WORKSPACE;
+  }
+  const Plan p = make_plan(workspace, batch, n1, n3, num_leaf, conf != nullptr);
+  return match_impl(packed_weights, desc2d, desc2d_bstride, object_cache, 0, leaves_prepared,
+                    prepared_bstride, batch, n1, n3, num_leaf, scale_factor, match_threshold,
+                    matches0, matches1, mscores0, mscores1, conf, p,
+                    static_cast<hipStream_t>(stream_), precision, nullptr, object_cache);
 }
 
 void onepose_shard_range(int n3_total, int world, int rank, int* start, int* count) {

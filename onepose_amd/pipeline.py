@@ -5,7 +5,11 @@ device, with no host round trip and no per-frame re-upload of the object's 3D te
     -> RANSAC-EPnP -> cm/deg error
 
 The object's descriptors / leaves / 3D points are uploaded once (``inference.py:89-90``
-re-uploads them every frame).  All buffers are allocated at construction, so the enqueue
+re-uploads them every frame).  With ``object_cache`` (default) the object-only prefix of the
+forward -- GAT 0 and the 3D half of self-attention 1 -- is also run once
+(``onepose_object_prepare``); each frame's matcher (``onepose_match_cached``) starts from that
+state and returns the same bits as the uncached forward (SURVEY.md §8b / §8d F_dep).
+All buffers are allocated at construction, so the enqueue
 methods only launch kernels on the current stream and can be captured in a HIP graph.
 
 Streaming (``run_stream``): the pose stage of frame k needs one CU (one workgroup per
@@ -67,7 +71,7 @@ class FramePipeline:
     def __init__(self, matcher: GATsSuperGlue, keypoints3d, desc3d, leaves, batch: int, n1: int,
                  device, scale: float = 1000.0, reprojection_error: float = 5.0,
                  iterations_count: int = 10000, confidence: float = 0.99, with_conf=True,
-                 slots: int = 2, detector=None, image_hw=(512, 512)):
+                 slots: int = 2, detector=None, image_hw=(512, 512), object_cache: bool = True):
         self.lib = _lib.load()
         self.device = torch.device(device)
         self.B, self.n1 = int(batch), int(n1)
@@ -91,6 +95,19 @@ class FramePipeline:
         _lib.check(self.lib.onepose_prepare_leaves(
             self.leaves.data_ptr(), 0, 1, self.n3, self.L, self.leaves_pm.data_ptr(),
             _lib.stream_ptr(dev)), "prepare_leaves")
+        # the object-only prefix of the forward (GAT 0 + the 3D half of self-attention 1),
+        # computed once: every frame starts from it (onepose_match_cached, bit-identical)
+        self.object_cache = None
+        if object_cache:
+            self.object_cache = torch.empty(self.n3 * 256, **f32)
+            wsb = self.lib.onepose_object_prepare_workspace_bytes(self.n3, self.L)
+            ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
+            _lib.check(self.lib.onepose_object_prepare(
+                self.weights.data_ptr(), self.desc3d.data_ptr(), self.leaves_pm.data_ptr(),
+                self.n3, self.L, self.precision, self.object_cache.data_ptr(), ws.data_ptr(), wsb,
+                _lib.stream_ptr(dev)), "object_prepare")
+            torch.cuda.current_stream(dev).synchronize()
+            del ws
         B = self.B
         # per-frame inputs (filled by the caller)
         self.desc2d = torch.zeros(B, 256, n1, **f32)
@@ -156,6 +173,15 @@ class FramePipeline:
         o = self.slots[slot]
         s = _lib.stream_ptr(self.device)
         desc2d, _ = self._inputs(o)
+        if self.object_cache is not None:
+            _lib.check(self.lib.onepose_match_cached(
+                self.weights.data_ptr(), desc2d.data_ptr(), 256 * self.n1,
+                self.object_cache.data_ptr(), self.leaves_pm.data_ptr(), 0,
+                self.B, self.n1, self.n3, self.L, self.scale_factor, self.threshold,
+                self.precision, o.matches0.data_ptr(), o.matches1.data_ptr(),
+                o.mscores0.data_ptr(), o.mscores1.data_ptr(), _lib.ptr(o.conf),
+                o.ws_match.data_ptr(), o.ws_match_bytes, s), "onepose_match_cached")
+            return
         _lib.check(self.lib.onepose_match_prepared_ex(
             self.weights.data_ptr(), desc2d.data_ptr(), 256 * self.n1,
             self.desc3d.data_ptr(), 0, self.leaves_pm.data_ptr(), 0,

@@ -176,3 +176,54 @@ def test_bf16_attention_mode_tracks_fp32(n1, n3, device):
     confident = s32 > 0.5
     assert (a[confident] == b[confident]).all()
     assert np.abs(c32.cpu().numpy() - c16.cpu().numpy()).max() < 0.05
+
+
+@pytest.mark.parametrize("n1,n3,L,B,prec", [(200, 777, 8, 1, 0), (1024, 4096, 8, 2, 0),
+                                             (128, 256, 12, 1, 0), (1024, 4096, 8, 1, 1)])
+def test_object_cache_is_bit_identical(device, n1, n3, L, B, prec):
+    """onepose_object_prepare + onepose_match_cached (GAT 0 and the 3D half of self-attention
+    1 run once per object) vs onepose_match_prepared_ex on the same object: every output
+    bit-equal, for a ragged cloud, a batch sharing the object, the L=12 GAT and bf16 mode."""
+    from onepose_amd import _lib
+    lib = _lib.load()
+    sd = synthetic.make_state_dict(0)
+    data, _, _ = synthetic.make_matcher_inputs(n1, n3, L, seed=11, batch=B)
+    m = matcher.from_state_dict(sd)
+    w = m.packed_weights(device)
+    f32 = dict(dtype=torch.float32, device=device)
+    s = _lib.stream_ptr(device)
+    d2 = torch.from_numpy(data["descriptors2d_query"]).to(device).contiguous()
+    d3 = torch.from_numpy(data["descriptors3d_db"][0]).to(device).contiguous()
+    lv = torch.from_numpy(data["descriptors2d_db"][0]).to(device).contiguous()
+    pm = torch.empty(lib.onepose_leaves_prepared_bytes(1, n3, L) // 4, **f32)
+    _lib.check(lib.onepose_prepare_leaves(lv.data_ptr(), 0, 1, n3, L, pm.data_ptr(), s), "leaves")
+    cache = torch.empty(lib.onepose_object_cache_bytes(n3) // 4, **f32)
+    wsb = lib.onepose_object_prepare_workspace_bytes(n3, L)
+    ws = torch.empty(wsb, dtype=torch.uint8, device=device)
+    _lib.check(lib.onepose_object_prepare(w.data_ptr(), d3.data_ptr(), pm.data_ptr(), n3, L, prec,
+                                          cache.data_ptr(), ws.data_ptr(), wsb, s), "prepare")
+    ws_bytes = lib.onepose_match_workspace_bytes(B, n1, n3, L, 1)
+    sf, thr = float(m.hparams["scale_factor"]), float(m.hparams["match_threshold"])
+    outs = []
+    for cached in (False, True):
+        o = dict(m0=torch.empty(B, n1, dtype=torch.int64, device=device),
+                 m1=torch.empty(B, n3, dtype=torch.int64, device=device),
+                 s0=torch.empty(B, n1, **f32), s1=torch.empty(B, n3, **f32),
+                 conf=torch.empty(B, n1, n3, **f32))
+        wsm = torch.empty(ws_bytes, dtype=torch.uint8, device=device)
+        tail = (B, n1, n3, L, sf, thr, prec, o["m0"].data_ptr(), o["m1"].data_ptr(),
+                o["s0"].data_ptr(), o["s1"].data_ptr(), o["conf"].data_ptr(), wsm.data_ptr(),
+                ws_bytes, s)
+        if cached:
+            rc = lib.onepose_match_cached(w.data_ptr(), d2.data_ptr(), 256 * n1, cache.data_ptr(),
+                                          pm.data_ptr(), 0, *tail)
+        else:
+            rc = lib.onepose_match_prepared_ex(w.data_ptr(), d2.data_ptr(), 256 * n1,
+                                               d3.data_ptr(), 0, pm.data_ptr(), 0, *tail)
+        _lib.check(rc, "match")
+        torch.cuda.synchronize()
+        outs.append({k: v.cpu().numpy() for k, v in o.items()})
+    for k in outs[0]:
+        np.testing.assert_array_equal(outs[0][k], outs[1][k], err_msg=k)
+    if n1 == 1024 and prec == 0:
+        assert (outs[1]["m0"] > -1).sum() > 100
