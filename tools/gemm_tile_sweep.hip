@@ -81,5 +81,10 @@ int main() {
   row<Tile<32, 64, 1, 2, 32>>("32x64 k1 2w bks32", A, W, Y, bias);
   row<Tile<32, 128, 1, 4, 32>>("32x128 k1 4w bks32", A, W, Y, bias);
   row<Tile<64, 32, 1, 2, 32>>("64x32 k1 2w bks32", A, W, Y, bias);
+  row<Tile<32, 64, 2, 4, 64>>("32x64 k2 4w bks64", A, W, Y, bias);
+  row<Tile<64, 32, 2, 4, 64>>("64x32 k2 4w bks64", A, W, Y, bias);
+  row<Tile<32, 64, 1, 2, 32>>("32x64 k1 2w bks32", A, W, Y, bias);
+  row<Tile<64, 64, 2, 8, 64>>("64x64 k2 8w bks64", A, W, Y, bias);
+  row<Tile<32, 128, 2, 8, 64>>("32x128 k2 8w bks64", A, W, Y, bias);
   return 0;
 }

@@ -10,15 +10,15 @@ import re
 import sys
 
 # GEMM template instance <EPI, PRO, BN> -> kernel kind (gemm.h enums; one instance per kind)
-GEMM_KIND = {(1, 0, 32, 128): "qkv_gemm", (2, 2, 64, 64): "mlp1_gemm",
-             (3, 1, 64, 64): "mlp2_gemm", (0, 0, 64, 64): "final_gemm",
-             (4, 0, 64, 64): "score_gemm"}
+GEMM_KIND = {(1, 0): "qkv_gemm", (2, 2): "mlp1_gemm", (3, 1): "mlp2_gemm", (0, 0): "final_gemm",
+             (4, 0): "score_gemm"}
 
 
 def kind_of(name):
-    m = re.search(r"gemm_f32_kernel<(\d+), (\d+), [^<]*Tile<(\d+), (\d+),", name)
+    m = re.search(r"gemm_(?:f32_)?kernel<(\d+), (\d+), [^<]*Tile<[^>]*>(?:, (true|false))?", name)
     if m:
-        return GEMM_KIND.get(tuple(int(x) for x in m.groups()), name)
+        k = GEMM_KIND.get((int(m.group(1)), int(m.group(2))), name)
+        return k + ("_bf16" if m.group(3) == "true" else "")
     m = re.search(r"onepose::(?:\(anonymous namespace\)::)?(\w+?)(?:<|\(|$)", name)
     return m.group(1) if m else name
 
@@ -33,6 +33,54 @@ def load(root, counter):
             k = kind_of(row["Kernel_Name"])
             per.setdefault(k, []).append(float(row["Counter_Value"]))
     return per
+
+
+SQ = ["SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY",
+      "SQ_ACTIVE_INST_ANY", "SQ_VALU_MFMA_BUSY_CYCLES", "GRBM_GUI_ACTIVE"]
+
+
+def load_all(root):
+    """{kind: {counter: [per-dispatch values]}} plus kernel durations (ns) from the trace."""
+    per, dur = {}, {}
+    for f in glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True):
+        for row in csv.DictReader(open(f)):
+            k = kind_of(row["Kernel_Name"])
+            d = per.setdefault(k, {}).setdefault(row["Counter_Name"], {})
+            d[row.get("Dispatch_Id", len(d))] = d.get(row.get("Dispatch_Id", len(d)), 0.0) + \
+                float(row["Counter_Value"])
+    for f in glob.glob(os.path.join(root, "**", "*kernel_trace.csv"), recursive=True):
+        for row in csv.DictReader(open(f)):
+            k = kind_of(row["Kernel_Name"])
+            dur.setdefault(k, []).append(int(row["End_Timestamp"]) - int(row["Start_Timestamp"]))
+    return {k: {c: list(v.values()) for c, v in cs.items()} for k, cs in per.items()}, dur
+
+
+def main_sq(root, cus=256, simds=4):
+    """Wave-state fractions (of SQ_WAVE_CYCLES) and MFMA-busy per SIMD:
+    SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 XCDs x 1024 SIMDs): the fraction of the
+    dispatch's SIMD-cycles in which a matrix core was busy."""
+    per, dur = load_all(root)
+    out = {"note": "per kernel kind, averaged over dispatches; wait/active fractions of "
+                   "SQ_WAVE_CYCLES; mfma_busy = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE/8 "
+                   "x 1024 SIMDs); clock_ghz = GRBM_GUI_ACTIVE/8 / kernel-trace duration",
+           "kernels": {}}
+    for k, cs in sorted(per.items()):
+        avg = {c: sum(v) / len(v) for c, v in cs.items() if v}
+        w = avg.get("SQ_WAVE_CYCLES")
+        g = avg.get("GRBM_GUI_ACTIVE")
+        e = {"dispatches": max(len(v) for v in cs.values())}
+        if w:
+            for c in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY"):
+                if c in avg:
+                    e[c.lower()[3:] + "_frac"] = round(avg[c] / w, 4)
+        if g and "SQ_VALU_MFMA_BUSY_CYCLES" in avg:
+            e["mfma_busy"] = round(avg["SQ_VALU_MFMA_BUSY_CYCLES"] / (g / 8 * cus * simds), 4)
+        if g and k in dur:
+            e["avg_us"] = round(sum(dur[k]) / len(dur[k]) / 1e3, 2)
+            e["clock_ghz"] = round(g / 8 / (sum(dur[k]) / len(dur[k])), 3)
+        e["raw_avg"] = {c: round(v, 1) for c, v in avg.items()}
+        out["kernels"][k] = e
+    print(json.dumps(out, indent=1))
 
 
 def main(root):
@@ -51,4 +99,7 @@ def main(root):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    if sys.argv[1] == "--sq":
+        main_sq(sys.argv[2])
+    else:
+        main(sys.argv[1])
