@@ -77,10 +77,12 @@ struct GemmArgs {
 enum GemmTile {
   TILE_64x64 = 0,   // mlp1 (STATS + HEADZ), mlp2 (RESID + NORM), score, final
   TILE_32x128 = 1,  // qkv (QKV: one head's [k_h | v_h] or two q heads per tile)
+  TILE_64x32K2 = 2, // mlp2 fp32 (RESID + NORM): 64 x 32 outputs, K split over two wave pairs
+                    //   (N = 256 gives 2x the 64x64 tile count: 640 tiles at config 2)
 };
 
 // Supported (epilogue, prologue, tile) combinations: QKV/32x128, STATS+HEADZ/64x64,
-// RESID+NORM/64x64, SCORE/64x64, BIAS/64x64.  K must be a multiple of twice the tile's stage
+// RESID+NORM/64x64 and /64x32K2 (fp32), SCORE/64x64, BIAS/64x64.  K must be a multiple of twice the tile's stage
 // depth (32 * KS).
 // bf16 = true: operands rounded to bf16 as the stage is read, v_mfma_f32_32x32x16_bf16 with
 // fp32 accumulation (QKV, STATS+HEADZ, RESID+NORM only: the attention-layer GEMMs).

@@ -515,6 +515,7 @@ void gemm_kernel(GemmArgs args) {
 
 using T64x64 = Tile<64, 64, 1, 4, 32>;
 using T32x128 = Tile<32, 128, 1, 4, 32>;
+using T64x32K2 = Tile<64, 32, 2, 4, 64>;
 
 template <int EPI, int PRO, class T, bool BF>
 void launch_one(GemmArgs& args, int grid, hipStream_t stream) {
@@ -528,6 +529,7 @@ TileDims tile_dims(int tile) {
   switch (tile) {
     case TILE_64x64: return {64, 64, 32};
     case TILE_32x128: return {32, 128, 32};
+    case TILE_64x32K2: return {64, 32, 64};
     default: return {0, 0, 0};
   }
 }
@@ -599,6 +601,7 @@ int gemm_launch(int epi, int pro, int tile, GemmArgs& args, hipStream_t stream, 
   CASE(EPI_QKV, PRO_PLAIN, TILE_32x128, T32x128, false)
   CASE(EPI_STATS, PRO_HEADZ, TILE_64x64, T64x64, false)
   CASE(EPI_RESID, PRO_NORM_RELU, TILE_64x64, T64x64, false)
+  CASE(EPI_RESID, PRO_NORM_RELU, TILE_64x32K2, T64x32K2, false)
   CASE(EPI_SCORE, PRO_PLAIN, TILE_64x64, T64x64, false)
   CASE(EPI_BIAS, PRO_PLAIN, TILE_64x64, T64x64, false)
   // bf16-MFMA attention layers (precision mode ONEPOSE_PREC_BF16_ATTN)

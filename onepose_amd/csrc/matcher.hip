@@ -39,7 +39,7 @@ namespace onepose {
 
 // GEMM tile per layer GEMM (gemm.h; measured per shape on config 2).
 constexpr int kTileKV = TILE_32x128, kTileMLP1 = TILE_64x64,
-              kTileMLP2 = TILE_64x64, kTileFinal = TILE_64x64;
+              kTileMLP2 = TILE_64x64, kTileMLP2F32 = TILE_64x32K2, kTileFinal = TILE_64x64;
 
 // ------------------------------------------------------------------------------------
 // errors
@@ -1183,7 +1183,8 @@ int attention_layer(const ApW& w, const Side* sd, int nside, int B, const Plan& 
       a.p[i].pro_rstd = p.rstd + (size_t)i * B * 512;
       a.p[i].pro_bs = 512;
     }
-    if ((rc = gemm_launch(EPI_RESID, PRO_NORM_RELU, kTileMLP2, a, st, K_MLP2, bf)) != ONEPOSE_OK)
+    if ((rc = gemm_launch(EPI_RESID, PRO_NORM_RELU, bf ? kTileMLP2 : kTileMLP2F32, a, st, K_MLP2,
+                          bf)) != ONEPOSE_OK)
       return rc;
   }
   return ONEPOSE_OK;
