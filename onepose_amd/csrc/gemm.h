@@ -80,6 +80,9 @@ enum GemmTile {
   TILE_64x32K2 = 2, // mlp2 fp32 (RESID + NORM): 64 x 32 outputs, K split over two wave pairs
                     //   (N = 256 gives 2x the 64x64 tile count: 640 tiles at config 2)
 };
+// (STATS + HEADZ also compile for 64x32 / 2 waves and for 64x64 / 8 waves with K split in
+// two and 64-deep stages, one head per stage; both measured slower than 64x64 for mlp1 in the
+// two-stream frame: DESIGN.md section 3.)
 
 // Supported (epilogue, prologue, tile) combinations: QKV/32x128, STATS+HEADZ/64x64,
 // RESID+NORM/64x64 and /64x32K2 (fp32), SCORE/64x64, BIAS/64x64.  K must be a multiple of twice the tile's stage

@@ -144,8 +144,8 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args) {
   constexpr int STAGE = BF ? T::STAGEB / 2 : T::STAGE;   // one LDS stage, in floats
   constexpr int LDSF = 2 * STAGE > BM * (BN + 1) ? 2 * STAGE : BM * (BN + 1);
   __shared__ __attribute__((aligned(16))) float lds[LDSF];
-  __shared__ float zrow[BM];
-  __shared__ float part[(EPI == EPI_STATS) ? (T::NT / 64) * BN * 2 : 1];
+  __shared__ float zrow[2 * BM];
+  __shared__ float part[(EPI == EPI_STATS) ? T::NT * 2 : 1];
 
   // XCD-aware tile order: blocks are dealt round-robin over the 8 XCDs, so hand each XCD a
   // contiguous run of logical tiles -- the N-tiles of one M-tile then share that XCD's L2.
@@ -239,10 +239,17 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args) {
     }
   };
 
-  // PRO_HEADZ: the phi(q) part of K is 4 heads x 64 (two stages each) after the x part.
-  // Each head accumulates into acc_h; its rows are scaled by Z*Ns and added to acc when the
-  // head's two stages are done.  Z's dot products phi(q)_row . ksum_h are taken from the
-  // staged A tiles (thread = row, 8-wide k chunk) right after each stage's fragment read.
+  // PRO_HEADZ: the phi(q) part of K is 4 heads x 64 (HS = 64 / BKS stages each) after the
+  // x part.  Each head accumulates into acc_h; its rows are scaled by Z*Ns and added to acc
+  // when the head's stages are done.  Z's dot products phi(q)_row . ksum_h are taken from
+  // the staged A tiles (TPR threads per row, ZK-wide k chunks) right after each stage's
+  // fragment read.  zrow is double-buffered by head parity (one head per stage at BKS 64
+  // leaves no barrier between one head's fold and the next head's Z).
+  constexpr int HS = 64 / T::BKS;
+  constexpr int TPR = T::NT / BM, ZK = T::BKS / TPR;
+  static_assert(PRO != PRO_HEADZ || (HS >= 1 && T::BKS * HS == 64 && T::NT % BM == 0 &&
+                                     ZK % 8 == 0 && ZK * TPR == T::BKS && 64 % TPR == 0),
+                "HEADZ tiling");
   const int xs = c.ksplit / T::BKS;
   floatx16 acc_h[FN];
 #pragma unroll
@@ -250,44 +257,48 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args) {
 #pragma unroll
     for (int i = 0; i < 16; ++i) acc_h[j][i] = 0.f;
   float zp = 0.f;
-  const int zr = t >> 2, zq = t & 3;
+  const int zr = t / TPR, zq = t % TPR;
   __shared__ float zks[(PRO == PRO_HEADZ) ? 256 : 1];   // sum phi(k) of the source
-  if (PRO == PRO_HEADZ) zks[t] = F(ksum)[b * F(ksum_bs) + t];   // visible after 1st barrier
+  if (PRO == PRO_HEADZ)
+    for (int i = t; i < 256; i += T::NT) zks[i] = F(ksum)[b * F(ksum_bs) + i];   // 1st barrier
   const float zns = F(ns);
   auto zdot = [&](const float* buf, int sg) __attribute__((always_inline)) {
     if (PRO == PRO_HEADZ && sg >= xs && sg < nk) {
-      static_assert(PRO != PRO_HEADZ || BM * 4 == T::NT, "HEADZ: four threads per row");
-      const float* kp = zks + (sg * T::BKS - c.ksplit) + zq * 8;   // LDS
-      float4 a0, a1;
-      if constexpr (BF) {   // the phi(q) the bf16 MFMAs see
-        const bf16x8 q = *reinterpret_cast<const bf16x8*>(
-            reinterpret_cast<const __bf16*>(buf) + zr * T::PITCHB + zq * 8);
-        a0 = make_float4((float)q[0], (float)q[1], (float)q[2], (float)q[3]);
-        a1 = make_float4((float)q[4], (float)q[5], (float)q[6], (float)q[7]);
-      } else {
-        const float* ap = buf + zr * PITCH + zq * 8;
-        a0 = *reinterpret_cast<const float4*>(ap);
-        a1 = *reinterpret_cast<const float4*>(ap + 4);
+#pragma unroll
+      for (int cc = 0; cc < ZK / 8; ++cc) {
+        const int k8 = zq * ZK + cc * 8;
+        const float* kp = zks + (sg * T::BKS - c.ksplit) + k8;   // LDS
+        float4 a0, a1;
+        if constexpr (BF) {   // the phi(q) the bf16 MFMAs see
+          const bf16x8 q = *reinterpret_cast<const bf16x8*>(
+              reinterpret_cast<const __bf16*>(buf) + zr * T::PITCHB + k8);
+          a0 = make_float4((float)q[0], (float)q[1], (float)q[2], (float)q[3]);
+          a1 = make_float4((float)q[4], (float)q[5], (float)q[6], (float)q[7]);
+        } else {
+          const float* ap = buf + zr * PITCH + k8;
+          a0 = *reinterpret_cast<const float4*>(ap);
+          a1 = *reinterpret_cast<const float4*>(ap + 4);
+        }
+        const float4 k0 = *reinterpret_cast<const float4*>(kp);
+        const float4 k1 = *reinterpret_cast<const float4*>(kp + 4);
+        zp += a0.x * k0.x + a0.y * k0.y + a0.z * k0.z + a0.w * k0.w + a1.x * k1.x +
+              a1.y * k1.y + a1.z * k1.z + a1.w * k1.w;
       }
-      const float4 k0 = *reinterpret_cast<const float4*>(kp);
-      const float4 k1 = *reinterpret_cast<const float4*>(kp + 4);
-      zp += a0.x * k0.x + a0.y * k0.y + a0.z * k0.z + a0.w * k0.w + a1.x * k1.x + a1.y * k1.y +
-            a1.z * k1.z + a1.w * k1.w;
     }
   };
-  auto zfinal = [&]() __attribute__((always_inline)) {   // head's two partials are in zp
-    zp += __shfl_xor(zp, 1, 64);
-    zp += __shfl_xor(zp, 2, 64);
-    if (zq == 0) zrow[zr] = (1.0f / (zp + 1e-6f)) * zns;
+  auto zfinal = [&](int par) __attribute__((always_inline)) {   // the head's partials are in zp
+#pragma unroll
+    for (int o = 1; o < TPR; o <<= 1) zp += __shfl_xor(zp, o, 64);
+    if (zq == 0) zrow[par * BM + zr] = (1.0f / (zp + 1e-6f)) * zns;
     zp = 0.f;
   };
-  auto fold = [&]() __attribute__((always_inline)) {     // acc += Z*Ns (per row) * acc_h
+  auto fold = [&](int par) __attribute__((always_inline)) {     // acc += Z*Ns (per row) * acc_h
 #pragma unroll
     for (int j = 0; j < FN; ++j)
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const int row = wm * 32 + (i & 3) + 8 * (i >> 2) + 4 * (lane >> 5);
-        acc[j][i] += zrow[row] * acc_h[j][i];
+        acc[j][i] += zrow[par * BM + row] * acc_h[j][i];
         acc_h[j][i] = 0.f;
       }
   };
@@ -326,11 +337,22 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args) {
       step(kt, s1, s0, f0, f1, acc);
       step(kt + 1, s0, s1, f1, f0, acc);
     }
-    for (int kt = xs; kt < nk; kt += 2) {  // one head of phi(q) per two stages
-      step(kt, s1, s0, f0, f1, acc_h);
-      zfinal();                            // visible to every wave after the next barrier
-      step(kt + 1, s0, s1, f1, f0, acc_h);
-      fold();
+    if constexpr (HS == 2) {
+      for (int kt = xs; kt < nk; kt += 2) {  // one head of phi(q) per two stages
+        step(kt, s1, s0, f0, f1, acc_h);
+        zfinal(0);                           // visible to every wave after the next barrier
+        step(kt + 1, s0, s1, f1, f0, acc_h);
+        fold(0);
+      }
+    } else {
+      for (int kt = xs; kt < nk; kt += 2) {  // one head per stage; its Z partials were taken
+        zfinal(0);                           // while the previous step read the stage
+        step(kt, s1, s0, f0, f1, acc_h);
+        fold(0);
+        zfinal(1);
+        step(kt + 1, s0, s1, f1, f0, acc_h);
+        fold(1);
+      }
     }
   }
   __syncthreads();   // every wave done with the LDS stages before they are reused below
@@ -418,9 +440,9 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args) {
 
   if (EPI == EPI_STATS) {
     // per column: NRG row groups -> (mean, M2 about the group mean), Chan-merged in order
-    static_assert(EPI != EPI_STATS || BN == 64, "stats tile is 64 columns");
-    constexpr int NRG = T::NT / 64, RG = BM / NRG;
-    const int col = t & 63, rg = t >> 6;
+    static_assert(EPI != EPI_STATS || (T::NT % BN == 0 && BM % (T::NT / BN) == 0), "stats tile");
+    constexpr int NRG = T::NT / BN, RG = BM / NRG;
+    const int col = t % BN, rg = t / BN;
     const int r0 = rg * RG, r1 = min(r0 + RG, rows);
     const int cnt = max(r1 - r0, 0);
     float s = 0.f;
@@ -431,15 +453,15 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args) {
       const float d = tile[rr * TP + col] - gmean;
       m2 += d * d;
     }
-    part[(rg * 64 + col) * 2] = gmean;
-    part[(rg * 64 + col) * 2 + 1] = m2;
+    part[(rg * BN + col) * 2] = gmean;
+    part[(rg * BN + col) * 2 + 1] = m2;
     __syncthreads();
-    if (t < 64 && n0 + t < N) {
+    if (t < BN && n0 + t < N) {
       float n = 0.f, mean = 0.f, M2 = 0.f;
       for (int g = 0; g < NRG; ++g) {
         const float nb = (float)max(min(g * RG + RG, rows) - g * RG, 0);
         if (nb == 0.f) continue;
-        const float mb = part[(g * 64 + t) * 2], m2b = part[(g * 64 + t) * 2 + 1];
+        const float mb = part[(g * BN + t) * 2], m2b = part[(g * BN + t) * 2 + 1];
         const float nn = n + nb, delta = mb - mean;
         mean += delta * (nb / nn);
         M2 += m2b + delta * delta * (n * nb / nn);
@@ -517,6 +539,7 @@ using T64x64 = Tile<64, 64, 1, 4, 32>;
 using T32x128 = Tile<32, 128, 1, 4, 32>;
 using T64x32K2 = Tile<64, 32, 2, 4, 64>;
 
+
 template <int EPI, int PRO, class T, bool BF>
 void launch_one(GemmArgs& args, int grid, hipStream_t stream) {
   hipLaunchKernelGGL((gemm_kernel<EPI, PRO, T, BF>), dim3(grid), dim3(T::NT), 0, stream, args);
@@ -530,6 +553,7 @@ TileDims tile_dims(int tile) {
     case TILE_64x64: return {64, 64, 32};
     case TILE_32x128: return {32, 128, 32};
     case TILE_64x32K2: return {64, 32, 64};
+
     default: return {0, 0, 0};
   }
 }
@@ -579,9 +603,8 @@ int gemm_launch(int epi, int pro, int tile, GemmArgs& args, hipStream_t stream, 
     OP_REQUIRE(P.lda0 % 4 == 0 && P.ldw % 4 == 0, "gemm: unaligned leading dimension");
     OP_REQUIRE(epi != EPI_QKV || (td.bn == 128 && P.N == 768), "gemm: QKV tiling");
     OP_REQUIRE(pro != PRO_HEADZ || (P.ksplit % 64 == 0 && P.K - P.ksplit == 256 &&
-                                    td.bks == 32 && P.ksum != nullptr),
+                                    (td.bks == 32 || td.bks == 64) && P.ksum != nullptr),
                "gemm: HEADZ needs 4 heads x 64 after ksplit");
-    OP_REQUIRE(epi != EPI_STATS || td.bn == 64, "gemm: STATS tiling");
     P.mtiles = ceil_div(P.M, td.bm);
     P.ntiles = ceil_div(P.N, td.bn);
     P.tiles = P.mtiles * P.ntiles * P.batch;
