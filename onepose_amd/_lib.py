@@ -11,7 +11,8 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libonepose_hip.so")
+# ONEPOSE_LIB: an alternative in-tree build of the same library (A/B measurement, tools/ab.sh)
+LIB_PATH = os.environ.get("ONEPOSE_LIB") or os.path.join(_HERE, "libonepose_hip.so")
 
 c_int, c_int64, c_size_t, c_float, c_double = (ctypes.c_int, ctypes.c_int64, ctypes.c_size_t,
                                                ctypes.c_float, ctypes.c_double)

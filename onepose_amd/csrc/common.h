@@ -122,6 +122,17 @@ __device__ __forceinline__ float wave_max(float v) {
 // F.elu as ATen computes it (x > 0 ? x : exp(x) - 1), GATs.py:102 / GATs_SuperGlue.py:90-91
 __device__ __forceinline__ float elu1(float x) { return x > 0.f ? x : (expf(x) - 1.0f); }
 
+// Chan et al. pairwise merge of (count, mean, M2) statistics (InstanceNorm moments).
+__device__ __forceinline__ void chan_merge(double& n, double& mean, double& m2, double nb,
+                                           double mb, double m2b) {
+  if (nb == 0.0) return;
+  const double nn = n + nb;
+  const double delta = mb - mean;
+  mean += delta * (nb / nn);
+  m2 += m2b + delta * delta * (n * nb / nn);
+  n = nn;
+}
+
 // Bijection hardware block id -> logical id giving each XCD (hardware blocks b, b+8, ...)
 // a contiguous range of logical ids.  Placement is a speed hint only, never correctness.
 __device__ __forceinline__ int xcd_contiguous(int bid, int grid) {

@@ -54,6 +54,11 @@ struct GemmProb {
   const float* pro_rstd;
   int64_t pro_bs;
   float* stats;        // EPI_STATS: [batch][mtiles][2][N]  (mtiles = ceil(M / tile rows))
+  unsigned* st_cnt;    // EPI_STATS: [batch][ntiles] arrival counters, zero before the launch;
+                       //   null = partials only.  The last M-tile to arrive at a column block
+                       //   merges its partials into st_mean / st_rstd [batch][N] (InstanceNorm)
+  float* st_mean;
+  float* st_rstd;
   float* rowstat;      // EPI_SCORE: [batch][M][ntiles][2]
   float* colstat;      // EPI_SCORE: [batch][N][mtiles][2]
   float* kvpart;       // EPI_QKV: [batch][mtiles][4][64][64]

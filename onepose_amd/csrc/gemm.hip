@@ -468,8 +468,88 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args) {
         n = nn;
       }
       float* st_out = F(stats) + ((int64_t)b * mtiles + mt) * 2 * N;
-      st_out[n0 + t] = mean;
-      st_out[N + n0 + t] = M2;
+      if (F(st_cnt) != nullptr) {   // handed to this launch's last tile: write-through (sc1)
+        __hip_atomic_store(st_out + n0 + t, mean, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(st_out + N + n0 + t, M2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      } else {
+        st_out[n0 + t] = mean;
+        st_out[N + n0 + t] = M2;
+      }
+    }
+    // InstanceNorm finalize in-launch (replaces a separate reduction launch): every M-tile of
+    // this (sample, column block) takes a ticket after its write-through (sc1) partial stores
+    // have drained; the one drawing mtiles - 1 reads all mtiles partials with sc1 loads and
+    // reduces them in tile order, so the result does not depend on which tile arrives last.
+    // Every store and load of the handed-off partials is sc1, so neither an agent-scope
+    // release (it would write back the XCD's L2, this tile's Y in it) nor an acquire (an L1
+    // invalidate, ~1.7 us) is needed.  The counters are zeroed by the forward's first kernel.
+    unsigned* tickets = F(st_cnt);
+    if (tickets != nullptr) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();   // every wave's partial stores drained; `part` no longer read
+      int* last = reinterpret_cast<int*>(part);
+      if (t == 0) {
+        const unsigned ticket = __hip_atomic_fetch_add(tickets + b * ntiles + nt, 1u, __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_AGENT);
+        last[0] = ticket == (unsigned)(mtiles - 1) ? 1 : 0;
+      }
+      __syncthreads();
+      if (last[0]) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // (no instruction: keeps the
+                                                                 // loads below the ticket)
+        // two passes over the partials (sc1 loads, 16 tiles in flight per thread):
+        //   mean = sum n_i mean_i / n,   M2 = sum (M2_i + n_i (mean_i - mean)^2)   in double
+        // (no per-merge division, unlike a pairwise Chan merge); NG tile-interleaved groups
+        // per column, added in group order through LDS
+        static_assert(EPI != EPI_STATS || T::NT % BN == 0, "finalize groups");
+        constexpr int NG = T::NT / BN;
+        const int col = t % BN, grp = t / BN;
+        float* sp = F(stats) + (int64_t)b * mtiles * 2 * N + min(n0 + col, N - 1);
+        double* red = reinterpret_cast<double*>(lds);   // [2][NG][BN]
+        auto ld = [&](int ti, int half) __attribute__((always_inline)) {
+          return __hip_atomic_load(sp + (int64_t)ti * 2 * N + half * N, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+        };
+        double s0 = 0.0, s1 = 0.0;
+        for (int t0 = grp; t0 < mtiles; t0 += 16 * NG) {
+          float mv[16];
+#pragma unroll
+          for (int u = 0; u < 16; ++u) mv[u] = ld(min(t0 + u * NG, mtiles - 1), 0);
+#pragma unroll
+          for (int u = 0; u < 16; ++u) {
+            const int ti = t0 + u * NG;
+            if (ti < mtiles) s0 += (double)min(BM, M - ti * BM) * (double)mv[u];
+          }
+        }
+        red[grp * BN + col] = s0;
+        __syncthreads();
+        for (int g = 0; g < NG; ++g) s1 += red[g * BN + col];
+        const double gmean = s1 / (double)M;
+        s0 = 0.0;
+        for (int t0 = grp; t0 < mtiles; t0 += 16 * NG) {
+          float mv[16], qv[16];
+#pragma unroll
+          for (int u = 0; u < 16; ++u) {
+            const int ti = min(t0 + u * NG, mtiles - 1);
+            mv[u] = ld(ti, 0);
+            qv[u] = ld(ti, 1);
+          }
+#pragma unroll
+          for (int u = 0; u < 16; ++u) {
+            const int ti = t0 + u * NG;
+            const double d = (double)mv[u] - gmean;
+            if (ti < mtiles) s0 += (double)qv[u] + (double)min(BM, M - ti * BM) * d * d;
+          }
+        }
+        red[(NG + grp) * BN + col] = s0;
+        __syncthreads();
+        if (grp == 0 && n0 + col < N) {
+          double m2 = 0.0;
+          for (int g = 0; g < NG; ++g) m2 += red[(NG + g) * BN + col];
+          F(st_mean)[(int64_t)b * N + n0 + col] = (float)gmean;
+          F(st_rstd)[(int64_t)b * N + n0 + col] = (float)(1.0 / sqrt(m2 / (double)M + 1e-5));
+        }
+      }
     }
   }
   if (EPI == EPI_SCORE) {

@@ -21,7 +21,7 @@
 //   3. m_fold: Mf = C_h KV_h^T with C = W1b Wm  (merge conv folded into MLP conv 1)
 //   4. q GEMM, epilogue phi(q) * Z * Ns
 //   5. MLP conv 1 = [W1a | Mf] [x ; QZ] + (b1 + W1b bm), epilogue InstanceNorm partials
-//   6. InstanceNorm statistics
+//   6. InstanceNorm statistics (finalized by the last M-tile of each column block of step 5)
 //   7. MLP conv 2 on ReLU(norm(.)) + residual
 // Steps 3-5 are an exact re-association of message = merge(attention), MLP(cat[x, msg])
 // (the linear attention output and the merge conv are linear in the message): the fp32
@@ -198,6 +198,8 @@ struct TransProb {
 };
 struct TransArgs {
   TransProb p[2];
+  unsigned* zero;   // the forward's in-launch arrival counters, zeroed here (first kernel)
+  int nzero;
 };
 __global__ __launch_bounds__(256) void transpose_in_kernel(TransArgs args, int batch) {
   __shared__ float tile[64][65];
@@ -205,6 +207,8 @@ __global__ __launch_bounds__(256) void transpose_in_kernel(TransArgs args, int b
   const bool second = bid >= args.p[0].tiles * batch;
   const TransProb& P = second ? args.p[1] : args.p[0];
   if (second) bid -= args.p[0].tiles * batch;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < args.nzero; i += gridDim.x * 256)
+    args.zero[i] = 0u;
   const int b = bid / P.tiles, r = bid - b * P.tiles;
   const int n0 = (r >> 2) * 64, c0 = (r & 3) * 64, n = P.n;
   const float* s = P.src + b * P.bs;
@@ -337,10 +341,9 @@ __global__ __launch_bounds__(256) void m_fold_kernel(FoldArgs args, int batch) {
   for (int i = 0; i < 16; ++i) out[((i & 3) + 8 * (i >> 2) + 4 * half) * 256] = acc[i];
 }
 
-// InstanceNorm1d statistics (GATs_SuperGlue.py:145; biased variance, eps 1e-5): combine the
-// per-64-row-tile (mean, M2) partials (Chan et al., double).  One workgroup per (side,
-// sample, 64-channel group); four tile-interleaved partial combines per channel, merged in
-// a fixed order.
+// InstanceNorm1d statistics (GATs_SuperGlue.py:145; biased variance, eps 1e-5): per-64-row-tile
+// (mean, M2) partials from MLP conv 1, Chan-merged (double) in tile order by the last tile of
+// each column block inside that launch (gemm.hip, EPI_STATS with st_cnt).
 struct StatsProb {
   const float* part;  // [B][mtiles][2][512]
   float* mean;        // [B][512]
@@ -350,38 +353,6 @@ struct StatsProb {
 struct StatsArgs {
   StatsProb p[2];
 };
-__device__ __forceinline__ void chan_merge(double& n, double& mean, double& m2, double nb,
-                                           double mb, double m2b) {
-  if (nb == 0.0) return;
-  const double nn = n + nb;
-  const double delta = mb - mean;
-  mean += delta * (nb / nn);
-  m2 += m2b + delta * delta * (n * nb / nn);
-  n = nn;
-}
-__global__ __launch_bounds__(256) void stats_finalize_kernel(StatsArgs args, int batch) {
-  // workgroup = (side, sample, 16 channels); thread = (channel, tile group of every 16th tile)
-  __shared__ double red[3][16][17];
-  const int g = blockIdx.x & 31, b = (blockIdx.x >> 5) % batch, side = (blockIdx.x >> 5) / batch;
-  const StatsProb& P = side ? args.p[1] : args.p[0];
-  const int t = threadIdx.x, tg = t >> 4, cl = t & 15, c = g * 16 + cl;
-  const float* part = P.part + (int64_t)b * P.mtiles * 1024;
-  double n = 0.0, mean = 0.0, m2 = 0.0;
-  for (int ti = tg; ti < P.mtiles; ti += 16) {
-    const double nb = (double)min(P.rows, P.m - ti * P.rows);
-    chan_merge(n, mean, m2, nb, part[ti * 1024 + c], part[ti * 1024 + 512 + c]);
-  }
-  red[0][tg][cl] = n;
-  red[1][tg][cl] = mean;
-  red[2][tg][cl] = m2;
-  __syncthreads();
-  if (tg == 0) {
-    for (int k = 1; k < 16; ++k) chan_merge(n, mean, m2, red[0][k][cl], red[1][k][cl], red[2][k][cl]);
-    P.mean[b * 512 + c] = (float)mean;
-    P.rstd[b * 512 + c] = (float)(1.0 / sqrt(m2 / n + 1e-5));
-  }
-}
-
 // ---- N3-sharded frames (onepose_match_sharded): per-rank partials and their merges ----
 // Every exchange is an all-gather of a fixed-size block per rank (rank-major in `recv`), merged
 // in rank order, so results do not depend on the collective's reduction order.
@@ -763,12 +734,16 @@ __global__ __launch_bounds__(256) void mutual_kernel(const unsigned long long* r
 // ------------------------------------------------------------------------------------
 namespace {
 
+constexpr int kCntPerSide = 512 / 64;   // mlp1 column blocks (TILE_64x64, N = 512)
+
 struct Plan {
   float *x2[2], *x3[2];
   float *kvpart2, *kvpart3, *kspart2, *kspart3;
   float *kv, *ksum, *mf;
   float *phiq2, *phiq3, *y12, *y13;
   float *stats2, *stats3, *mean, *rstd;
+  unsigned* cnt;      // in-launch arrival counters: [attention layer][side][B][mlp1 N-tiles]
+  int ncnt;
   float *f2, *f3, *s;
   float *rowpart, *colpart, *rowmax, *rowsum, *colmax, *colsum;
   unsigned long long *rowbest, *colbest;
@@ -801,6 +776,8 @@ Plan make_plan(void* ws, int B, int n1, int n3, int L, bool with_conf) {
   p.stats3 = c.take<float>((size_t)B * ceil_div(n3, str) * 1024);
   p.mean = c.take<float>((size_t)2 * B * 512);
   p.rstd = c.take<float>((size_t)2 * B * 512);
+  p.ncnt = kApLayers * 2 * B * kCntPerSide;
+  p.cnt = c.take<unsigned>((size_t)p.ncnt);
   p.f2 = c.take<float>(t2 * 256);
   p.f3 = c.take<float>(t3 * 256);
   p.s = with_conf ? nullptr : c.take<float>((size_t)B * n1 * n3);
@@ -1084,7 +1061,7 @@ struct Side {
 // reductions), so a side gives the same bits alone or grouped.  Sharded runs have two
 // sides, slot 1 being the 3D shard.
 int attention_layer(const ApW& w, const Side* sd, int nside, int B, const Plan& p,
-                    hipStream_t st, bool bf, const ShardCtx* sh) {
+                    unsigned* cnt, hipStream_t st, bool bf, const ShardCtx* sh) {
   int rc;
   {  // 1. [q | k_h v_h ...]: phi(q) stored, per-chunk KV / ksum partials
     GemmArgs a;
@@ -1143,6 +1120,9 @@ int attention_layer(const ApW& w, const Side* sd, int nside, int B, const Plan& 
       a.p[i].ldw1 = 256;
       a.p[i].w1_bs = 512 * 256;
       a.p[i].stats = s.stats;
+      a.p[i].st_cnt = cnt + (size_t)i * B * kCntPerSide;
+      a.p[i].st_mean = p.mean + (size_t)i * B * 512;
+      a.p[i].st_rstd = p.rstd + (size_t)i * B * 512;
       a.p[i].ksum = p.ksum + (size_t)s.src * B * 256;
       a.p[i].ksum_bs = 256;
       a.p[i].ns = sd[s.src].len;
@@ -1150,17 +1130,15 @@ int attention_layer(const ApW& w, const Side* sd, int nside, int B, const Plan& 
     if ((rc = gemm_launch(EPI_STATS, PRO_HEADZ, kTileMLP1, a, st, K_MLP1, bf)) != ONEPOSE_OK)
       return rc;
   }
-  {  // 5. InstanceNorm statistics
+  // 5. InstanceNorm statistics: finalized inside MLP conv 1 by each column block's last
+  //    M-tile (st_cnt); a sharded 3D side is re-merged over the ranks' (n, mean, M2)
+  if (sh) {
     StatsArgs sa;
     const int str = gemm_tile_rows(kTileMLP1);
     for (int i = 0; i < nside; ++i)
       sa.p[i] = {sd[i].stats, p.mean + (size_t)i * B * 512, p.rstd + (size_t)i * B * 512,
                  sd[i].n, ceil_div(sd[i].n, str), str};
-    if (!sh) {
-      OP_LAUNCH(K_STATS, st, stats_finalize_kernel, dim3(nside * B * 32), dim3(256), 0, st, sa,
-                B);
-    } else {   // 2D side local; 3D side Chan-merged over the ranks' (n, mean, M2)
-      OP_LAUNCH(K_STATS, st, stats_finalize_kernel, dim3(B * 32), dim3(256), 0, st, sa, B);
+    {
       OP_LAUNCH(K_STATS, st, stats_partial_kernel, dim3(B * 32), dim3(256), 0, st, sa.p[1], B,
                 reinterpret_cast<double*>(sh->send));
       const int64_t nst = (int64_t)B * 512 * 3;
@@ -1212,6 +1190,8 @@ int match_impl(const void* packed_weights, const float* desc2d, int64_t desc2d_b
     TransArgs ta;
     ta.p[0] = {desc2d, desc2d_bstride, n1, ceil_div(n1, 64) * 4, p.x2[0]};
     ta.p[1] = {desc3d, desc3d_bstride, n3, obj_cache ? 0 : ceil_div(n3, 64) * 4, p.x3[0]};
+    ta.zero = p.cnt;
+    ta.nzero = p.ncnt;
     OP_LAUNCH(K_TRANSPOSE, st, transpose_in_kernel, dim3((ta.p[0].tiles + ta.p[1].tiles) * B),
               dim3(256), 0, st, ta, B);
   }
@@ -1248,7 +1228,8 @@ int match_impl(const void* packed_weights, const float* desc2d, int64_t desc2d_b
     sd[1] = {x3r, x3bs, p.x3[c3 ^ 1], p.phiq3, p.kvpart3, p.kspart3, p.y13, p.stats3, n3,
              (float)n3g, kind == 1 ? 1 : 0};
     const int nside = cached3 ? 1 : 2;
-    int rc = attention_layer(w, sd, nside, B, p, st, bf, sh);
+    int rc = attention_layer(w, sd, nside, B, p, p.cnt + (size_t)(ap - 1) * 2 * B * kCntPerSide,
+                             st, bf, sh);
     if (rc != ONEPOSE_OK) return rc;
     x2r = p.x2[c2 ^ 1];
     c2 ^= 1;
@@ -1342,6 +1323,8 @@ int object_prepare_impl(const void* packed_weights, const float* desc3d, const f
     TransArgs ta;
     ta.p[0] = {desc3d, 0, n3, ceil_div(n3, 64) * 4, p.x3[0]};
     ta.p[1] = {desc3d, 0, n3, 0, p.x3[0]};
+    ta.zero = p.cnt;
+    ta.nzero = p.ncnt;
     OP_LAUNCH(K_TRANSPOSE, st, transpose_in_kernel, dim3(ta.p[0].tiles), dim3(256), 0, st, ta, 1);
   }
   const dim3 ggrid(ceil_div(n3, 4));
@@ -1353,7 +1336,7 @@ int object_prepare_impl(const void* packed_weights, const float* desc3d, const f
               gat_weights(wbase, 0), p.x3[1], n3, num_leaf, 1);
   const Side s3 = {p.x3[1], (int64_t)n3 * 256, cache, p.phiq3, p.kvpart3, p.kspart3, p.y13,
                    p.stats3, n3, (float)n3, 0};
-  return attention_layer(ap_weights(wbase, 0), &s3, 1, 1, p, st,
+  return attention_layer(ap_weights(wbase, 0), &s3, 1, 1, p, p.cnt, st,
                          precision == ONEPOSE_PREC_BF16_ATTN, nullptr);
 }
 
@@ -1391,6 +1374,8 @@ int onepose_prepare_leaves(const float* leaves, int64_t leaves_bstride, int batc
   TransArgs ta;
   ta.p[0] = {leaves, leaves_bstride, ncol, ceil_div(ncol, 64) * 4, out};
   ta.p[1] = {leaves, 0, 1, 0, out};
+  ta.zero = nullptr;
+  ta.nzero = 0;
   OP_LAUNCH(K_TRANSPOSE, st, transpose_in_kernel, dim3(ta.p[0].tiles * batch), dim3(256), 0, st,
             ta, batch);
   return ONEPOSE_OK;
