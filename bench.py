@@ -172,7 +172,7 @@ def main():
     ap.add_argument("--eager", action="store_true",
                     help="launch every kernel from the host each step instead of replaying "
                          "captured HIP graphs")
-    ap.add_argument("--precision", choices=["fp32", "bf16"], default="fp32",
+    ap.add_argument("--precision", choices=["fp32", "bf16", "fp32_split"], default="fp32",
                     help="matcher attention-layer GEMMs: fp32 MFMA (the reference's numerics, "
                          "default) or bf16 MFMA with fp32 accumulation (BASELINE config 5)")
     ap.add_argument("--no-object-cache", action="store_true",

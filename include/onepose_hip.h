@@ -39,10 +39,14 @@ enum {
 enum {
   ONEPOSE_PREC_FP32 = 0,        /* every contraction on fp32-input MFMA: the reference's
                                    numerics up to summation order (bit-exact indices)   */
-  ONEPOSE_PREC_BF16_ATTN = 1    /* the attention layers' GEMMs (q/k/v projection, merge+MLP)
+  ONEPOSE_PREC_BF16_ATTN = 1,   /* the attention layers' GEMMs (q/k/v projection, merge+MLP)
                                    take bf16-rounded operands on v_mfma_f32_32x32x16_bf16
                                    with fp32 accumulation (BASELINE config 5); GAT, final
                                    projection, scores and dual softmax stay fp32       */
+  ONEPOSE_PREC_FP32_SPLIT = 2   /* every GEMM in fp32 by an exact 3-way bf16 split of both
+                                   operands (x = hi + mid + lo) and the six bf16 MFMA
+                                   products a_i b_j with i + j <= 2, fp32 accumulation:
+                                   fp32-accurate (the dropped terms are < 2^-22 |a b|)  */
 };
 
 /* Thread-local description of the last error ("" when none). */

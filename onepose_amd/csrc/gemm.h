@@ -78,6 +78,9 @@ struct GemmArgs {
   StampAcc* stamp;   // device-stamp profiling accumulator (set by gemm_launch) or null
 };
 
+// Operand modes (gemm.hip): exact fp32 MFMA, bf16 (rounded), fp32 by exact 3-way bf16 split.
+enum GemmPm { PM_F32 = 0, PM_BF16 = 1, PM_SPLIT3 = 2 };
+
 // Tile configurations: BM x BN output tile, K split into KS slices inside the workgroup.
 enum GemmTile {
   TILE_64x64 = 0,   // mlp1 (STATS + HEADZ), mlp2 (RESID + NORM), score, final
@@ -92,10 +95,12 @@ enum GemmTile {
 // Supported (epilogue, prologue, tile) combinations: QKV/32x128, STATS+HEADZ/64x64,
 // RESID+NORM/64x64 and /64x32K2 (fp32), SCORE/64x64, BIAS/64x64.  K must be a multiple of twice the tile's stage
 // depth (32 * KS).
-// bf16 = true: operands rounded to bf16 as the stage is read, v_mfma_f32_32x32x16_bf16 with
-// fp32 accumulation (QKV, STATS+HEADZ, RESID+NORM only: the attention-layer GEMMs).
+// pm = PM_BF16: operands rounded to bf16 as the stage is stored, v_mfma_f32_32x32x16_bf16 with
+// fp32 accumulation (QKV, STATS+HEADZ, RESID+NORM 64x64 only: the attention-layer GEMMs).
+// pm = PM_SPLIT3: every operand split exactly into three bf16 pieces, six bf16 MFMAs per
+// 16-deep group (fp32-accurate; all 64x64 and 32x128 combinations).
 int gemm_launch(int epi, int pro, int tile, GemmArgs& args, hipStream_t stream, int kind,
-                bool bf16 = false);
+                int pm = PM_F32);
 // Rows per M-tile of a configuration (the chunk size of the STATS / KVPART partials).
 int gemm_tile_rows(int tile);
 

@@ -28,18 +28,30 @@ typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 
 namespace {
 
+// Operand modes (gemm.h): PM_F32 fp32 LDS image + v_mfma_f32_32x32x2_f32; PM_BF16 one bf16
+// image (rounded) + v_mfma_f32_32x32x16_bf16; PM_SPLIT3 three bf16 images per operand, the
+// exact split x = hi + mid + lo (hi = bf16(x), mid = bf16(x - hi), lo = x - hi - mid: every
+// step is exact in fp32 and lo fits bf16's 8 bits), and six bf16 MFMAs per 16-deep group,
+// a_i b_j for i + j <= 2 (the dropped a_mid b_lo, a_lo b_mid, a_lo b_lo are <= 2^-23 of |a b|
+// together), accumulated in fp32: an fp32-accurate product at 6 x 32 instead of 8 x 64 MFMA
+// cycles per 16-deep group.
 // Per-wave MFMA operand fragments of one stage: fp32 (v_mfma_f32_32x32x2_f32, a float4 feeds
 // four MFMAs over k = 8 kk + 4 h + j) or bf16 (v_mfma_f32_32x32x16_bf16: lane half h holds
 // k = 16 kk + 8 h + j, j < 8, from a bf16 LDS image rounded to nearest even when stored).
-template <bool BF, int KKW, int FN>
+template <int PM, int KKW, int FN>
 struct FragT {
   float4 a[KKW];
   float4 w[KKW][FN];
 };
 template <int KKW, int FN>
-struct FragT<true, KKW, FN> {
+struct FragT<PM_BF16, KKW, FN> {
   bf16x8 a[KKW];
   bf16x8 w[KKW][FN];
+};
+template <int KKW, int FN>
+struct FragT<PM_SPLIT3, KKW, FN> {   // hi / mid / lo pieces
+  bf16x8 a[3][KKW];
+  bf16x8 w[3][KKW][FN];
 };
 
 
@@ -109,8 +121,9 @@ __device__ __forceinline__ void load_stage(const Ctx& c, int m0, int n0, int k0,
 }
 
 // Stage registers -> LDS image at `base` ([BM + BN] rows: A then W), applying the prologue;
-// fp32 rows of PITCH floats, or (BF) bf16 rows of PITCHB elements rounded to nearest even.
-template <int PRO, class T, bool BF>
+// fp32 rows of PITCH floats, or bf16 rows of PITCHB elements (PM_BF16: rounded to nearest even;
+// PM_SPLIT3: the hi, mid and lo images one after another, STAGEB elements apart).
+template <int PRO, class T, int PM>
 __device__ __forceinline__ void store_stage(float* base, Stage<T>& s) {
   const int t = threadIdx.x;
   const int kq = (t % T::KQ) * 4;
@@ -125,23 +138,41 @@ __device__ __forceinline__ void store_stage(float* base, Stage<T>& s) {
       v.w = fmaxf((v.w - s.mean.w) * s.rstd.w, 0.f);
     }
     const int row = (is_a ? 0 : T::BM) + (t + T::NT * (is_a ? i : i - T::A4)) / T::KQ;
-    if constexpr (BF) {
+    if constexpr (PM == PM_BF16) {
       bf16x4 q;
       q[0] = (__bf16)v.x;
       q[1] = (__bf16)v.y;
       q[2] = (__bf16)v.z;
       q[3] = (__bf16)v.w;
       *reinterpret_cast<bf16x4*>(reinterpret_cast<__bf16*>(base) + row * T::PITCHB + kq) = q;
+    } else if constexpr (PM == PM_SPLIT3) {
+      bf16x4 q0, q1, q2;
+      const float x[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const __bf16 h = (__bf16)x[c];
+        const float r = x[c] - (float)h;
+        const __bf16 m = (__bf16)r;
+        q0[c] = h;
+        q1[c] = m;
+        q2[c] = (__bf16)(r - (float)m);
+      }
+      __bf16* b16 = reinterpret_cast<__bf16*>(base) + row * T::PITCHB + kq;
+      *reinterpret_cast<bf16x4*>(b16) = q0;
+      *reinterpret_cast<bf16x4*>(b16 + T::STAGEB) = q1;
+      *reinterpret_cast<bf16x4*>(b16 + 2 * T::STAGEB) = q2;
     } else {
       *reinterpret_cast<float4*>(base + row * T::PITCH + kq) = v;
     }
   }
 }
 
-template <int EPI, int PRO, class T, bool BF>
+template <int EPI, int PRO, class T, int PM>
 __device__ __forceinline__ void gemm_body(const GemmArgs& args) {
   constexpr int BM = T::BM, BN = T::BN, FN = T::FN, PITCH = T::PITCH;
-  constexpr int STAGE = BF ? T::STAGEB / 2 : T::STAGE;   // one LDS stage, in floats
+  constexpr bool BF = PM != PM_F32;   // bf16 LDS images and MFMAs
+  constexpr int STAGE = PM == PM_F32 ? T::STAGE : PM == PM_BF16 ? T::STAGEB / 2
+                                                                : 3 * T::STAGEB / 2;   // floats
   constexpr int LDSF = 2 * STAGE > BM * (BN + 1) ? 2 * STAGE : BM * (BN + 1);
   __shared__ __attribute__((aligned(16))) float lds[LDSF];
   __shared__ float zrow[2 * BM];
@@ -202,7 +233,7 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args) {
   constexpr int KG = BF ? 16 : 8;                  // k per MFMA group
   constexpr int KKW = T::BKS / T::KS / KG;         // groups per wave per stage
   static_assert(KKW >= 2, "two MFMA groups per stage (pipeline shape)");
-  using Frag = FragT<BF, KKW, FN>;
+  using Frag = FragT<PM, KKW, FN>;
   Frag f0, f1;
   const int kofs = ks * (T::BKS / T::KS) + (lane >> 5) * (KG / 2);
   constexpr int RP = BF ? T::PITCHB : PITCH;   // LDS row pitch in elements
@@ -211,12 +242,21 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args) {
   auto read_frag = [&](const float* buf, Frag& f) __attribute__((always_inline)) {
 #pragma unroll
     for (int kk = 0; kk < KKW; ++kk) {
-      if constexpr (BF) {
+      if constexpr (PM == PM_BF16) {
         const __bf16* b16 = reinterpret_cast<const __bf16*>(buf);
         f.a[kk] = *reinterpret_cast<const bf16x8*>(b16 + a_off + kk * KG);
 #pragma unroll
         for (int j = 0; j < FN; ++j)
           f.w[kk][j] = *reinterpret_cast<const bf16x8*>(b16 + w_off + j * 32 * RP + kk * KG);
+      } else if constexpr (PM == PM_SPLIT3) {
+#pragma unroll
+        for (int pc = 0; pc < 3; ++pc) {
+          const __bf16* b16 = reinterpret_cast<const __bf16*>(buf) + pc * T::STAGEB;
+          f.a[pc][kk] = *reinterpret_cast<const bf16x8*>(b16 + a_off + kk * KG);
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+            f.w[pc][kk][j] = *reinterpret_cast<const bf16x8*>(b16 + w_off + j * 32 * RP + kk * KG);
+        }
       } else {
         f.a[kk] = *reinterpret_cast<const float4*>(buf + a_off + kk * KG);
 #pragma unroll
@@ -228,8 +268,15 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args) {
   auto mfma_kk = [&](floatx16 (&tg)[FN], const Frag& f, int kk) __attribute__((always_inline)) {
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
-      if constexpr (BF) {
+      if constexpr (PM == PM_BF16) {
         tg[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.a[kk], f.w[kk][j], tg[j], 0, 0, 0);
+      } else if constexpr (PM == PM_SPLIT3) {   // smallest terms first
+        tg[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.a[2][kk], f.w[0][kk][j], tg[j], 0, 0, 0);
+        tg[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.a[1][kk], f.w[1][kk][j], tg[j], 0, 0, 0);
+        tg[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.a[0][kk], f.w[2][kk][j], tg[j], 0, 0, 0);
+        tg[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.a[1][kk], f.w[0][kk][j], tg[j], 0, 0, 0);
+        tg[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.a[0][kk], f.w[1][kk][j], tg[j], 0, 0, 0);
+        tg[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.a[0][kk], f.w[0][kk][j], tg[j], 0, 0, 0);
       } else {
         tg[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(f.a[kk].x, f.w[kk][j].x, tg[j], 0, 0, 0);
         tg[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(f.a[kk].y, f.w[kk][j].y, tg[j], 0, 0, 0);
@@ -269,11 +316,21 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args) {
         const int k8 = zq * ZK + cc * 8;
         const float* kp = zks + (sg * T::BKS - c.ksplit) + k8;   // LDS
         float4 a0, a1;
-        if constexpr (BF) {   // the phi(q) the bf16 MFMAs see
+        if constexpr (PM == PM_BF16) {   // the phi(q) the bf16 MFMAs see
           const bf16x8 q = *reinterpret_cast<const bf16x8*>(
               reinterpret_cast<const __bf16*>(buf) + zr * T::PITCHB + k8);
           a0 = make_float4((float)q[0], (float)q[1], (float)q[2], (float)q[3]);
           a1 = make_float4((float)q[4], (float)q[5], (float)q[6], (float)q[7]);
+        } else if constexpr (PM == PM_SPLIT3) {   // hi + mid + lo = the fp32 value, exactly
+          const __bf16* b16 = reinterpret_cast<const __bf16*>(buf) + zr * T::PITCHB + k8;
+          const bf16x8 q0 = *reinterpret_cast<const bf16x8*>(b16);
+          const bf16x8 q1 = *reinterpret_cast<const bf16x8*>(b16 + T::STAGEB);
+          const bf16x8 q2 = *reinterpret_cast<const bf16x8*>(b16 + 2 * T::STAGEB);
+          float x[8];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) x[e] = ((float)q0[e] + (float)q1[e]) + (float)q2[e];
+          a0 = make_float4(x[0], x[1], x[2], x[3]);
+          a1 = make_float4(x[4], x[5], x[6], x[7]);
         } else {
           const float* ap = buf + zr * PITCH + k8;
           a0 = *reinterpret_cast<const float4*>(ap);
@@ -305,18 +362,20 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args) {
 
   load_stage<PRO, T>(c, m0, n0, 0, s0);
   load_stage<PRO, T>(c, m0, n0, T::BKS, s1);
-  store_stage<PRO, T, BF>(lds, s0);
+  store_stage<PRO, T, PM>(lds, s0);
   __syncthreads();
   read_frag(lds, f0);
 
   auto step = [&](int kt, Stage<T>& next, Stage<T>& spare, const Frag& cur, Frag& nxt,
                   floatx16 (&tg)[FN]) __attribute__((always_inline)) {
     // unconditional: past the end the last stage is re-read into the spare set and ignored
+#ifndef ONEPOSE_GEMM_PROBE_NOLOAD   // (tools/gemm_probe.hip: the loop without its global loads)
     load_stage<PRO, T>(c, m0, n0, min(kt + 2, nk - 1) * T::BKS, spare);
+#endif
     mfma_kk(tg, cur, 0);
     __builtin_amdgcn_sched_barrier(0);
     float* na = lds + ((kt + 1) & 1) * STAGE;
-    store_stage<PRO, T, BF>(na, next);                // (unused after the last step)
+    store_stage<PRO, T, PM>(na, next);                // (unused after the last step)
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int kk = 1; kk < KKW - 1; ++kk) mfma_kk(tg, cur, kk);
@@ -485,8 +544,8 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args) {
     // invalidate, ~1.7 us) is needed.  The counters are zeroed by the forward's first kernel.
     unsigned* tickets = F(st_cnt);
     if (tickets != nullptr) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();   // every wave's partial stores drained; `part` no longer read
+      if (t < BN) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the storing wave drains
+      __syncthreads();   // partial stores drained; `part` no longer read
       int* last = reinterpret_cast<int*>(part);
       if (t == 0) {
         const unsigned ticket = __hip_atomic_fetch_add(tickets + b * ntiles + nt, 1u, __ATOMIC_RELAXED,
@@ -497,10 +556,10 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args) {
       if (last[0]) {
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // (no instruction: keeps the
                                                                  // loads below the ticket)
-        // two passes over the partials (sc1 loads, 16 tiles in flight per thread):
-        //   mean = sum n_i mean_i / n,   M2 = sum (M2_i + n_i (mean_i - mean)^2)   in double
-        // (no per-merge division, unlike a pairwise Chan merge); NG tile-interleaved groups
-        // per column, added in group order through LDS
+        // one pass over the partials (sc1 loads, 16 tiles in flight per thread), shifted by
+        // tile 0's mean c:  S1 = sum n_i (mean_i - c),  S2 = sum M2_i + n_i (mean_i - c)^2,
+        // mean = c + S1 / n,  M2 = S2 - S1^2 / n  (double; no per-merge division, unlike a
+        // pairwise Chan merge).  NG tile-interleaved groups per column, added in group order.
         static_assert(EPI != EPI_STATS || T::NT % BN == 0, "finalize groups");
         constexpr int NG = T::NT / BN;
         const int col = t % BN, grp = t / BN;
@@ -510,22 +569,8 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args) {
           return __hip_atomic_load(sp + (int64_t)ti * 2 * N + half * N, __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
         };
-        double s0 = 0.0, s1 = 0.0;
-        for (int t0 = grp; t0 < mtiles; t0 += 16 * NG) {
-          float mv[16];
-#pragma unroll
-          for (int u = 0; u < 16; ++u) mv[u] = ld(min(t0 + u * NG, mtiles - 1), 0);
-#pragma unroll
-          for (int u = 0; u < 16; ++u) {
-            const int ti = t0 + u * NG;
-            if (ti < mtiles) s0 += (double)min(BM, M - ti * BM) * (double)mv[u];
-          }
-        }
-        red[grp * BN + col] = s0;
-        __syncthreads();
-        for (int g = 0; g < NG; ++g) s1 += red[g * BN + col];
-        const double gmean = s1 / (double)M;
-        s0 = 0.0;
+        const double c0 = (double)ld(0, 0);
+        double s1 = 0.0, s2 = 0.0;
         for (int t0 = grp; t0 < mtiles; t0 += 16 * NG) {
           float mv[16], qv[16];
 #pragma unroll
@@ -537,17 +582,26 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args) {
 #pragma unroll
           for (int u = 0; u < 16; ++u) {
             const int ti = t0 + u * NG;
-            const double d = (double)mv[u] - gmean;
-            if (ti < mtiles) s0 += (double)qv[u] + (double)min(BM, M - ti * BM) * d * d;
+            const double nb = (double)min(BM, M - ti * BM), d = (double)mv[u] - c0;
+            if (ti < mtiles) {
+              s1 += nb * d;
+              s2 += (double)qv[u] + nb * d * d;
+            }
           }
         }
-        red[(NG + grp) * BN + col] = s0;
+        red[grp * BN + col] = s1;
+        red[(NG + grp) * BN + col] = s2;
         __syncthreads();
         if (grp == 0 && n0 + col < N) {
-          double m2 = 0.0;
-          for (int g = 0; g < NG; ++g) m2 += red[(NG + g) * BN + col];
-          F(st_mean)[(int64_t)b * N + n0 + col] = (float)gmean;
-          F(st_rstd)[(int64_t)b * N + n0 + col] = (float)(1.0 / sqrt(m2 / (double)M + 1e-5));
+          double S1 = 0.0, S2 = 0.0;
+          for (int g = 0; g < NG; ++g) {
+            S1 += red[g * BN + col];
+            S2 += red[(NG + g) * BN + col];
+          }
+          const double n = (double)M;
+          F(st_mean)[(int64_t)b * N + n0 + col] = (float)(c0 + S1 / n);
+          F(st_rstd)[(int64_t)b * N + n0 + col] =
+              (float)(1.0 / sqrt((S2 - S1 * S1 / n) / n + 1e-5));
         }
       }
     }
@@ -607,11 +661,11 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args) {
 #undef F
 }
 
-template <int EPI, int PRO, class T, bool BF>
+template <int EPI, int PRO, class T, int PM>
 __global__ __launch_bounds__(T::NT) __attribute__((amdgpu_waves_per_eu(3)))
 void gemm_kernel(GemmArgs args) {
   stamp_begin(args.stamp);
-  gemm_body<EPI, PRO, T, BF>(args);
+  gemm_body<EPI, PRO, T, PM>(args);
   stamp_end(args.stamp);
 }
 
@@ -620,9 +674,9 @@ using T32x128 = Tile<32, 128, 1, 4, 32>;
 using T64x32K2 = Tile<64, 32, 2, 4, 64>;
 
 
-template <int EPI, int PRO, class T, bool BF>
+template <int EPI, int PRO, class T, int PM>
 void launch_one(GemmArgs& args, int grid, hipStream_t stream) {
-  hipLaunchKernelGGL((gemm_kernel<EPI, PRO, T, BF>), dim3(grid), dim3(T::NT), 0, stream, args);
+  hipLaunchKernelGGL((gemm_kernel<EPI, PRO, T, PM>), dim3(grid), dim3(T::NT), 0, stream, args);
 }
 
 struct TileDims {
@@ -667,7 +721,7 @@ GemmProb gemm_prob(const float* A, int lda, const float* W, int ldw, const float
 }
 
 int gemm_launch(int epi, int pro, int tile, GemmArgs& args, hipStream_t stream, int kind,
-                bool bf16) {
+                int pm) {
   const TileDims td = tile_dims(tile);
   OP_REQUIRE(td.bm > 0, "gemm: unknown tile %d", tile);
   int grid = 0;
@@ -692,27 +746,33 @@ int gemm_launch(int epi, int pro, int tile, GemmArgs& args, hipStream_t stream, 
   }
   if (grid == 0) return ONEPOSE_OK;
   args.stamp = nullptr;
-#define CASE(E, PR, TI, T, BF)                           \
-  if (epi == E && pro == PR && tile == TI && bf16 == BF) { \
+#define CASE(E, PR, TI, T, PMV)                          \
+  if (epi == E && pro == PR && tile == TI && pm == PMV) { \
     prof_pre(kind, stream);                              \
     args.stamp = prof_stamp_slot(kind);                  \
-    launch_one<E, PR, T, BF>(args, grid, stream);        \
+    launch_one<E, PR, T, PMV>(args, grid, stream);       \
     prof_post(kind, stream);                             \
     OP_LAUNCHED();                                       \
     return ONEPOSE_OK;                                   \
   }
-  CASE(EPI_QKV, PRO_PLAIN, TILE_32x128, T32x128, false)
-  CASE(EPI_STATS, PRO_HEADZ, TILE_64x64, T64x64, false)
-  CASE(EPI_RESID, PRO_NORM_RELU, TILE_64x64, T64x64, false)
-  CASE(EPI_RESID, PRO_NORM_RELU, TILE_64x32K2, T64x32K2, false)
-  CASE(EPI_SCORE, PRO_PLAIN, TILE_64x64, T64x64, false)
-  CASE(EPI_BIAS, PRO_PLAIN, TILE_64x64, T64x64, false)
+  CASE(EPI_QKV, PRO_PLAIN, TILE_32x128, T32x128, PM_F32)
+  CASE(EPI_STATS, PRO_HEADZ, TILE_64x64, T64x64, PM_F32)
+  CASE(EPI_RESID, PRO_NORM_RELU, TILE_64x64, T64x64, PM_F32)
+  CASE(EPI_RESID, PRO_NORM_RELU, TILE_64x32K2, T64x32K2, PM_F32)
+  CASE(EPI_SCORE, PRO_PLAIN, TILE_64x64, T64x64, PM_F32)
+  CASE(EPI_BIAS, PRO_PLAIN, TILE_64x64, T64x64, PM_F32)
   // bf16-MFMA attention layers (precision mode ONEPOSE_PREC_BF16_ATTN)
-  CASE(EPI_QKV, PRO_PLAIN, TILE_32x128, T32x128, true)
-  CASE(EPI_STATS, PRO_HEADZ, TILE_64x64, T64x64, true)
-  CASE(EPI_RESID, PRO_NORM_RELU, TILE_64x64, T64x64, true)
+  CASE(EPI_QKV, PRO_PLAIN, TILE_32x128, T32x128, PM_BF16)
+  CASE(EPI_STATS, PRO_HEADZ, TILE_64x64, T64x64, PM_BF16)
+  CASE(EPI_RESID, PRO_NORM_RELU, TILE_64x64, T64x64, PM_BF16)
+  // fp32 by exact 3-way bf16 split (precision mode ONEPOSE_PREC_FP32_SPLIT)
+  CASE(EPI_QKV, PRO_PLAIN, TILE_32x128, T32x128, PM_SPLIT3)
+  CASE(EPI_STATS, PRO_HEADZ, TILE_64x64, T64x64, PM_SPLIT3)
+  CASE(EPI_RESID, PRO_NORM_RELU, TILE_64x64, T64x64, PM_SPLIT3)
+  CASE(EPI_SCORE, PRO_PLAIN, TILE_64x64, T64x64, PM_SPLIT3)
+  CASE(EPI_BIAS, PRO_PLAIN, TILE_64x64, T64x64, PM_SPLIT3)
 #undef CASE
-  set_error("gemm: unsupported epilogue/prologue/tile/bf16 %d/%d/%d/%d", epi, pro, tile, (int)bf16);
+  set_error("gemm: unsupported epilogue/prologue/tile/mode %d/%d/%d/%d", epi, pro, tile, pm);
   return ONEPOSE_ERR_INVALID;
 }
 

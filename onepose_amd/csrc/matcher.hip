@@ -91,12 +91,12 @@ StampAcc* prof_stamp_slot(int kind) {
 void prof_pre(int kind, hipStream_t s) {
   if (g_prof.device) return;
   if (!((g_prof.mask >> kind) & 1ull) || 2 * g_prof.n + 1 >= (int)g_prof.ev.size()) return;
-  hipEventRecord(g_prof.ev[2 * g_prof.n], s);
+  (void)hipEventRecord(g_prof.ev[2 * g_prof.n], s);
 }
 void prof_post(int kind, hipStream_t s) {
   if (g_prof.device) return;
   if (!((g_prof.mask >> kind) & 1ull) || 2 * g_prof.n + 1 >= (int)g_prof.ev.size()) return;
-  hipEventRecord(g_prof.ev[2 * g_prof.n + 1], s);
+  (void)hipEventRecord(g_prof.ev[2 * g_prof.n + 1], s);
   g_prof.kinds[g_prof.n] = kind;
   ++g_prof.n;
 }
@@ -118,16 +118,17 @@ constexpr int kGatLayers = 4;
 //   C   [512][256] = mlp.0.weight[:, 256:] @ merge.weight, columns head-major (h*64+q)
 //   b1f [512]      = mlp.0.bias + mlp.0.weight[:, 256:] @ merge.bias
 //   W2 [256][512], b2 [256]
+//   CT [4][64][512]: CT[h][q][o] = C[o][h*64+q]  (the fold's operand, o contiguous)
 constexpr int64_t kApWqkv = 768 * 256, kApBqkv = 768;
 constexpr int64_t kApW1a = 512 * 256, kApC = 512 * 256, kApB1 = 512, kApW2 = 256 * 512,
-                  kApB2 = 256;
-constexpr int64_t kApFloats = kApWqkv + kApBqkv + kApW1a + kApC + kApB1 + kApW2 + kApB2;
+                  kApB2 = 256, kApCT = 512 * 256;
+constexpr int64_t kApFloats = kApWqkv + kApBqkv + kApW1a + kApC + kApB1 + kApW2 + kApB2 + kApCT;
 constexpr int64_t kGatFloats = 512;
 constexpr int64_t kFinalFloats = 256 * 256 + 256;
 constexpr int64_t kPackedFloats = kApLayers * kApFloats + kGatLayers * kGatFloats + kFinalFloats;
 
 struct ApW {
-  const float *wqkv, *bqkv, *w1a, *c, *b1, *w2, *b2;
+  const float *wqkv, *bqkv, *w1a, *c, *b1, *w2, *b2, *ct;
 };
 ApW ap_weights(const float* base, int ap) {
   const float* p = base + (int64_t)ap * kApFloats;
@@ -138,7 +139,8 @@ ApW ap_weights(const float* base, int ap) {
   w.c = p; p += kApC;
   w.b1 = p; p += kApB1;
   w.w2 = p; p += kApW2;
-  w.b2 = p;
+  w.b2 = p; p += kApB2;
+  w.ct = p;
   return w;
 }
 const float* gat_weights(const float* base, int g) {
@@ -339,6 +341,104 @@ __global__ __launch_bounds__(256) void m_fold_kernel(FoldArgs args, int batch) {
   float* out = P.mf + (int64_t)b * 512 * 256 + (ot * 64 + wm * 32) * 256 + h * 64 + wn * 32 + l32;
 #pragma unroll
   for (int i = 0; i < 16; ++i) out[((i & 3) + 8 * (i >> 2) + 4 * half) * 256] = acc[i];
+}
+
+// kv_reduce and m_fold in one launch (whole frames): a workgroup that has reduced KV_h rows
+// d0..d0+3 of one source also owns Mf columns h*64 + d0..d0+3 of the side attending to it,
+// since  Mf[o][h*64+d] = sum_q C[o][h*64+q] KV_h[d][q]  reads only those rows.  16 waves:
+//   chunk sum   wave w sums chunks w, w+16, ... (8 loads in flight), the 16 wave sums are
+//               added in wave order through LDS;
+//   fold        thread (q quarter qq, o pair) takes 16 q of CT[h][q][o] (the per-head
+//               transpose of C, coalesced over o, loaded before the chunk sum so its latency
+//               overlaps it) times KV rows d0..d0+3; the four q quarters are added in order.
+// Workgroup 64 of each (source, sample) is sum phi(k) (chunk sum only).
+struct KvFoldArgs {
+  KvProb p[2];     // chunk partials of source slot 0 / 1
+  float* mf[2];    // [B][512][256] Mf of the side that attends to slot 0 / 1
+  const float* ct; // [4][64][512]  C transposed per head (packed weights)
+};
+typedef float f2v __attribute__((ext_vector_type(2)));
+__global__ __launch_bounds__(1024) void kv_fold_kernel(KvFoldArgs args, float* kv, float* ksum,
+                                                       int batch) {
+  constexpr int per = (16384 + 256) / 4;   // float4 outputs per (source, sample) = 4160
+  constexpr int groups = per / 64;         // 65 workgroups per (source, sample)
+  __shared__ float4 red[16][64];           // wave sums; then KV rows; then fold partials
+  __shared__ f2v fpart[3][4][256];         // fold partials of q quarters 1..3
+  const int g = blockIdx.x % groups, bs = blockIdx.x / groups;
+  const int b = bs % batch, src = bs / batch;
+  const KvProb& P = src ? args.p[1] : args.p[0];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int e4 = g * 64 + lane;
+  const int h = (g >> 4) & 3, d0 = (g & 15) * 4;
+  const int op = t & 255, qq = t >> 8;
+  f2v cv[16];
+  if (g < 64) {
+    const float* ct = args.ct + (h * 64 + qq * 16) * 512 + 2 * op;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) cv[i] = *reinterpret_cast<const f2v*>(ct + i * 512);
+  }
+  const float4* p;
+  int64_t stride;
+  if (e4 < 4096) {
+    p = reinterpret_cast<const float4*>(P.part + (int64_t)b * P.chunks * 16384) + e4;
+    stride = 4096;
+  } else {
+    p = reinterpret_cast<const float4*>(P.kspart + (int64_t)b * P.chunks * 256) + (e4 - 4096);
+    stride = 64;
+  }
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int c0 = w; c0 < P.chunks; c0 += 128) {
+    float4 v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = p[(int64_t)min(c0 + 16 * j, P.chunks - 1) * stride];
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (c0 + 16 * j < P.chunks) {
+        acc.x += v[j].x; acc.y += v[j].y; acc.z += v[j].z; acc.w += v[j].w;
+      }
+  }
+  red[w][lane] = acc;
+  __syncthreads();
+  if (w == 0) {
+    float4 s = red[0][lane];
+#pragma unroll
+    for (int j = 1; j < 16; ++j) { s.x += red[j][lane].x; s.y += red[j][lane].y; s.z += red[j][lane].z; s.w += red[j][lane].w; }
+    if (e4 < 4096)
+      reinterpret_cast<float4*>(kv + ((int64_t)src * batch + b) * 16384)[e4] = s;
+    else
+      reinterpret_cast<float4*>(ksum + ((int64_t)src * batch + b) * 256)[e4 - 4096] = s;
+    red[0][lane] = s;   // KV rows d0..d0+3: red[0][16 j + q/4] = KV_h[d0 + j][q .. q+3]
+  }
+  if (g == 64) return;
+  __syncthreads();
+  const float* kvr = reinterpret_cast<const float*>(&red[0][0]) + qq * 16;
+  f2v y[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    y[j] = (f2v)(0.f);
+#pragma unroll
+    for (int i = 0; i < 16; i += 4) {
+      const float4 k = *reinterpret_cast<const float4*>(kvr + j * 64 + i);   // LDS broadcast
+      y[j] = __builtin_elementwise_fma(cv[i], (f2v)(k.x), y[j]);
+      y[j] = __builtin_elementwise_fma(cv[i + 1], (f2v)(k.y), y[j]);
+      y[j] = __builtin_elementwise_fma(cv[i + 2], (f2v)(k.z), y[j]);
+      y[j] = __builtin_elementwise_fma(cv[i + 3], (f2v)(k.w), y[j]);
+    }
+  }
+  if (qq > 0)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) fpart[qq - 1][j][op] = y[j];
+  __syncthreads();
+  if (qq == 0) {
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) y[j] += fpart[r][j][op];
+    float* mf = (src ? args.mf[1] : args.mf[0]) + (int64_t)b * 512 * 256 + (2 * op) * 256 +
+                h * 64 + d0;
+    *reinterpret_cast<float4*>(mf) = make_float4(y[0].x, y[1].x, y[2].x, y[3].x);
+    *reinterpret_cast<float4*>(mf + 256) = make_float4(y[0].y, y[1].y, y[2].y, y[3].y);
+  }
 }
 
 // InstanceNorm1d statistics (GATs_SuperGlue.py:145; biased variance, eps 1e-5): per-64-row-tile
@@ -979,6 +1079,9 @@ int onepose_matcher_pack(const float* const* tensors, int n_tensors, void* packe
     }
     memcpy(w2, m3w, kApW2 * sizeof(float));
     memcpy(b2, m3b, kApB2 * sizeof(float));
+    float* ct = b2 + kApB2;
+    for (int o = 0; o < 512; ++o)
+      for (int cp = 0; cp < 256; ++cp) ct[(int64_t)cp * 512 + o] = cw[(int64_t)o * 256 + cp];
     ++ap;
   }
   float* fin = out + kApLayers * kApFloats + kGatLayers * kGatFloats;
@@ -1043,6 +1146,14 @@ int shard_exchange(const ShardCtx& sh, size_t bytes, hipStream_t st) {
   return ONEPOSE_OK;
 }
 
+bool valid_precision(int p) {
+  return p == ONEPOSE_PREC_FP32 || p == ONEPOSE_PREC_BF16_ATTN || p == ONEPOSE_PREC_FP32_SPLIT;
+}
+int attention_pm(int precision) {
+  return precision == ONEPOSE_PREC_BF16_ATTN ? PM_BF16
+         : precision == ONEPOSE_PREC_FP32_SPLIT ? PM_SPLIT3 : PM_F32;
+}
+
 // One side of an attention layer: its input state (x_bs 0 = shared by the batch: the object
 // cache), where the residual output goes, its per-layer scratch, and which slot's KV it
 // attends to.  Slot i of kv / ksum / mf / mean / rstd belongs to side i of the launch.
@@ -1061,7 +1172,7 @@ struct Side {
 // reductions), so a side gives the same bits alone or grouped.  Sharded runs have two
 // sides, slot 1 being the 3D shard.
 int attention_layer(const ApW& w, const Side* sd, int nside, int B, const Plan& p,
-                    unsigned* cnt, hipStream_t st, bool bf, const ShardCtx* sh) {
+                    unsigned* cnt, hipStream_t st, int pm, const ShardCtx* sh) {
   int rc;
   {  // 1. [q | k_h v_h ...]: phi(q) stored, per-chunk KV / ksum partials
     GemmArgs a;
@@ -1075,10 +1186,22 @@ int attention_layer(const ApW& w, const Side* sd, int nside, int B, const Plan& 
       a.p[i].kspart = s.kspart;
       a.p[i].y_bs = (int64_t)s.n * 256;
     }
-    if ((rc = gemm_launch(EPI_QKV, PRO_PLAIN, kTileKV, a, st, K_QKV_GEMM, bf)) != ONEPOSE_OK)
+    if ((rc = gemm_launch(EPI_QKV, PRO_PLAIN, kTileKV, a, st, K_QKV_GEMM, pm)) != ONEPOSE_OK)
       return rc;
   }
-  {  // 2. KV[slot], ksum[slot]
+  if (!sh) {  // 2+3. KV[slot], ksum[slot] and the folded message weights, one launch
+    KvFoldArgs ka;
+    ka.ct = w.ct;
+    ka.mf[0] = ka.mf[1] = nullptr;
+    for (int i = 0; i < nside; ++i) {
+      ka.p[i] = {sd[i].kvpart, sd[i].kspart, ceil_div(sd[i].n, gemm_tile_rows(kTileKV))};
+      ka.mf[sd[i].src] = p.mf + (size_t)i * B * 512 * 256;
+    }
+    for (int i = 0; i < nside; ++i)
+      OP_REQUIRE(ka.mf[i] != nullptr, "attention layer: source slot %d has no reader", i);
+    OP_LAUNCH(K_KV_REDUCE, st, kv_fold_kernel, dim3(nside * B * 65), dim3(1024), 0, st, ka, p.kv,
+              p.ksum, B);
+  } else {  // sharded: the 3D source's KV is summed over the ranks before the fold
     KvArgs kva;
     for (int i = 0; i < nside; ++i)
       kva.p[i] = {sd[i].kvpart, sd[i].kspart, ceil_div(sd[i].n, gemm_tile_rows(kTileKV))};
@@ -1096,8 +1219,7 @@ int attention_layer(const ApW& w, const Side* sd, int nside, int B, const Plan& 
       OP_LAUNCH(K_KV_REDUCE, st, shard_sum_kernel, dim3((unsigned)ceil_div((int)nks, 256)),
                 dim3(256), 0, st, rv, sh->world, nkv + nks, nkv, nks, p.ksum + nks);
     }
-  }
-  {  // 3. folded message weights per side
+    // 3. folded message weights per side
     FoldArgs fa;
     fa.c = w.c;
     for (int i = 0; i < nside; ++i)
@@ -1127,7 +1249,7 @@ int attention_layer(const ApW& w, const Side* sd, int nside, int B, const Plan& 
       a.p[i].ksum_bs = 256;
       a.p[i].ns = sd[s.src].len;
     }
-    if ((rc = gemm_launch(EPI_STATS, PRO_HEADZ, kTileMLP1, a, st, K_MLP1, bf)) != ONEPOSE_OK)
+    if ((rc = gemm_launch(EPI_STATS, PRO_HEADZ, kTileMLP1, a, st, K_MLP1, pm)) != ONEPOSE_OK)
       return rc;
   }
   // 5. InstanceNorm statistics: finalized inside MLP conv 1 by each column block's last
@@ -1161,8 +1283,8 @@ int attention_layer(const ApW& w, const Side* sd, int nside, int B, const Plan& 
       a.p[i].pro_rstd = p.rstd + (size_t)i * B * 512;
       a.p[i].pro_bs = 512;
     }
-    if ((rc = gemm_launch(EPI_RESID, PRO_NORM_RELU, bf ? kTileMLP2 : kTileMLP2F32, a, st, K_MLP2,
-                          bf)) != ONEPOSE_OK)
+    if ((rc = gemm_launch(EPI_RESID, PRO_NORM_RELU, pm == PM_F32 ? kTileMLP2F32 : kTileMLP2, a,
+                          st, K_MLP2, pm)) != ONEPOSE_OK)
       return rc;
   }
   return ONEPOSE_OK;
@@ -1179,7 +1301,8 @@ int match_impl(const void* packed_weights, const float* desc2d, int64_t desc2d_b
                const ShardCtx* sh = nullptr, const float* obj_cache = nullptr) {
   const bool with_conf = conf != nullptr;
   const int n3g = sh ? sh->n3_total : n3;   // the 3D side's full length (softmax / attention)
-  const bool bf = precision == ONEPOSE_PREC_BF16_ATTN;   // attention-layer GEMMs on bf16 MFMA
+  const int pm = attention_pm(precision);   // attention-layer GEMM operand mode
+  const int pm_out = precision == ONEPOSE_PREC_FP32_SPLIT ? PM_SPLIT3 : PM_F32;   // final, score
   const float* wbase = static_cast<const float*>(packed_weights);
   const int B = batch;
   float* S = with_conf ? conf : p.s;
@@ -1229,7 +1352,7 @@ int match_impl(const void* packed_weights, const float* desc2d, int64_t desc2d_b
              (float)n3g, kind == 1 ? 1 : 0};
     const int nside = cached3 ? 1 : 2;
     int rc = attention_layer(w, sd, nside, B, p, p.cnt + (size_t)(ap - 1) * 2 * B * kCntPerSide,
-                             st, bf, sh);
+                             st, pm, sh);
     if (rc != ONEPOSE_OK) return rc;
     x2r = p.x2[c2 ^ 1];
     c2 ^= 1;
@@ -1247,7 +1370,8 @@ int match_impl(const void* packed_weights, const float* desc2d, int64_t desc2d_b
     a.nprob = 2;
     a.p[0] = gemm_prob(x2r, 256, fw, 256, fw + 65536, p.f2, 256, n1, 256, 256, B);
     a.p[1] = gemm_prob(x3r, 256, fw, 256, fw + 65536, p.f3, 256, n3, 256, 256, B);
-    if ((rc = gemm_launch(EPI_BIAS, PRO_PLAIN, kTileFinal, a, st, K_FINAL)) != ONEPOSE_OK) return rc;
+    if ((rc = gemm_launch(EPI_BIAS, PRO_PLAIN, kTileFinal, a, st, K_FINAL, pm_out)) != ONEPOSE_OK)
+      return rc;
     const int rows = B * (n1 + n3);
     OP_LAUNCH(K_L2NORM, st, l2norm_kernel, dim3(ceil_div(rows, 4)), dim3(256), 0, st, p.f2, B * n1,
                        p.f3, B * n3);
@@ -1260,7 +1384,8 @@ int match_impl(const void* packed_weights, const float* desc2d, int64_t desc2d_b
     a.p[0].scale = scale_factor;
     a.p[0].rowstat = p.rowpart;
     a.p[0].colstat = p.colpart;
-    if ((rc = gemm_launch(EPI_SCORE, PRO_PLAIN, TILE_64x64, a, st, K_SCORE)) != ONEPOSE_OK) return rc;
+    if ((rc = gemm_launch(EPI_SCORE, PRO_PLAIN, TILE_64x64, a, st, K_SCORE, pm_out)) != ONEPOSE_OK)
+      return rc;
   }
   {
     const int64_t total = (int64_t)B * (n1 + n3);
@@ -1337,7 +1462,7 @@ int object_prepare_impl(const void* packed_weights, const float* desc3d, const f
   const Side s3 = {p.x3[1], (int64_t)n3 * 256, cache, p.phiq3, p.kvpart3, p.kspart3, p.y13,
                    p.stats3, n3, (float)n3, 0};
   return attention_layer(ap_weights(wbase, 0), &s3, 1, 1, p, p.cnt, st,
-                         precision == ONEPOSE_PREC_BF16_ATTN, nullptr);
+                         attention_pm(precision), nullptr);
 }
 
 int check_match_args(const void* packed_weights, const float* desc2d, const float* desc3d,
@@ -1388,7 +1513,7 @@ int onepose_match_ex(const void* packed_weights, const float* desc2d, int64_t de
                      int64_t* matches0, int64_t* matches1, float* mscores0, float* mscores1,
                      float* conf, void* workspace, size_t workspace_bytes, void* stream_) {
   clear_error();
-  OP_REQUIRE(precision == ONEPOSE_PREC_FP32 || precision == ONEPOSE_PREC_BF16_ATTN,
+  OP_REQUIRE(valid_precision(precision),
              "match: precision %d", precision);
   int rc = check_match_args(packed_weights, desc2d, desc3d, leaves, batch, n1, n3, num_leaf,
                             scale_factor, matches0, matches1, mscores0, mscores1, workspace);
@@ -1431,7 +1556,7 @@ int onepose_match_prepared_ex(const void* packed_weights, const float* desc2d,
                               int64_t* matches1, float* mscores0, float* mscores1, float* conf,
                               void* workspace, size_t workspace_bytes, void* stream_) {
   clear_error();
-  OP_REQUIRE(precision == ONEPOSE_PREC_FP32 || precision == ONEPOSE_PREC_BF16_ATTN,
+  OP_REQUIRE(valid_precision(precision),
              "match: precision %d", precision);
   int rc = check_match_args(packed_weights, desc2d, desc3d, leaves_prepared, batch, n1, n3,
                             num_leaf, scale_factor, matches0, matches1, mscores0, mscores1,
@@ -1479,7 +1604,7 @@ int onepose_object_prepare(const void* packed_weights, const float* desc3d,
                            float* cache, void* workspace, size_t workspace_bytes, void* stream_) {
   clear_error();
   OP_REQUIRE(packed_weights && desc3d && leaves_prepared && cache, "object_prepare: null pointer");
-  OP_REQUIRE(precision == ONEPOSE_PREC_FP32 || precision == ONEPOSE_PREC_BF16_ATTN,
+  OP_REQUIRE(valid_precision(precision),
              "object_prepare: precision %d", precision);
   OP_REQUIRE(n3 >= 1 && num_leaf >= 1 && num_leaf <= 16, "object_prepare: n3=%d num_leaf=%d", n3,
              num_leaf);
@@ -1501,7 +1626,7 @@ int onepose_match_cached(const void* packed_weights, const float* desc2d, int64_
                          int64_t* matches0, int64_t* matches1, float* mscores0, float* mscores1,
                          float* conf, void* workspace, size_t workspace_bytes, void* stream_) {
   clear_error();
-  OP_REQUIRE(precision == ONEPOSE_PREC_FP32 || precision == ONEPOSE_PREC_BF16_ATTN,
+  OP_REQUIRE(valid_precision(precision),
              "match_cached: precision %d", precision);
   int rc = check_match_args(packed_weights, desc2d, object_cache, leaves_prepared, batch, n1, n3,
                             num_leaf, scale_factor, matches0, matches1, mscores0, mscores1,
@@ -1553,7 +1678,7 @@ int onepose_match_sharded(const void* packed_weights, const float* desc2d, int64
                           int64_t* matches1, float* mscores0, float* mscores1, float* conf_shard,
                           void* workspace, size_t workspace_bytes, void* stream_) {
   clear_error();
-  OP_REQUIRE(precision == ONEPOSE_PREC_FP32 || precision == ONEPOSE_PREC_BF16_ATTN,
+  OP_REQUIRE(valid_precision(precision),
              "match_sharded: precision %d", precision);
   OP_REQUIRE(world >= 1 && rank >= 0 && rank < world, "match_sharded: rank %d of %d", rank, world);
   OP_REQUIRE(xchg_send && xchg_recv && allgather, "match_sharded: null exchange buffer/callback");

@@ -101,7 +101,8 @@ class AttentionalGNN(nn.Module):
         self.names = list(layer_names)
 
 
-PRECISIONS = {"fp32": 0, "bf16": 1}   # ONEPOSE_PREC_FP32 / ONEPOSE_PREC_BF16_ATTN
+# ONEPOSE_PREC_FP32 / ONEPOSE_PREC_BF16_ATTN / ONEPOSE_PREC_FP32_SPLIT (include/onepose_hip.h)
+PRECISIONS = {"fp32": 0, "bf16": 1, "fp32_split": 2}
 
 
 class GATsSuperGlue(nn.Module):

@@ -59,7 +59,7 @@ def _pack(sd):
     return buf
 
 
-AP_FLOATS = 768 * 256 + 768 + 512 * 256 + 512 * 256 + 512 + 256 * 512 + 256
+AP_FLOATS = 768 * 256 + 768 + 512 * 256 + 512 * 256 + 512 + 256 * 512 + 256 + 512 * 256
 
 
 def test_pack_layout():
@@ -81,6 +81,8 @@ def test_pack_layout():
     cw = take(512 * 256).reshape(512, 256)
     b1 = take(512)
     w2 = take(256 * 512).reshape(256, 512)
+    take(256)
+    ct = take(512 * 256).reshape(256, 512)   # [h*64+q][o]
     q_w = sd["gnn.layers.1.attn.proj.0.weight"][:, :, 0]
     k_w = sd["gnn.layers.1.attn.proj.1.weight"][:, :, 0]
     v_w = sd["gnn.layers.1.attn.proj.2.weight"][:, :, 0]
@@ -100,6 +102,7 @@ def test_pack_layout():
     b1f = sd["gnn.layers.1.mlp.0.bias"] + m0[:, 256:] @ sd["gnn.layers.1.attn.merge.bias"]
     np.testing.assert_allclose(b1, b1f, rtol=1e-5, atol=1e-6)
     np.testing.assert_array_equal(w2, sd["gnn.layers.1.mlp.3.weight"][:, :, 0])
+    np.testing.assert_array_equal(ct, cw.T)
     # GAT fold: wa = W @ a (layer 0)
     gat0 = buf[8 * AP_FLOATS:8 * AP_FLOATS + 512]
     W, a = sd["gnn.layers.0.W"].astype(np.float64), sd["gnn.layers.0.a"][:, 0].astype(np.float64)

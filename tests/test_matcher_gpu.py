@@ -20,8 +20,9 @@ MARGIN = 1e-4
 ATOL = 2e-5
 
 
-def run_matcher(sd, data, device, expand=False):
-    m = matcher.from_state_dict(sd).to(device)
+def run_matcher(sd, data, device, expand=False, precision="fp32"):
+    m = matcher.from_state_dict(sd, {**synthetic.DEFAULT_HPARAMS,
+                                     "attention_precision": precision}).to(device)
     t = {k: torch.from_numpy(v).to(device) for k, v in data.items()}
     if expand:   # the per-object tensors shared across the batch (stride 0)
         for k in ("descriptors3d_db", "descriptors2d_db", "keypoints3d"):
@@ -48,15 +49,16 @@ def margins(g):
     return row_margin, col_margin
 
 
+@pytest.mark.parametrize("precision", ["fp32", "fp32_split"])
 @pytest.mark.parametrize("name", ["matcher_c1_wc", "matcher_c1_rand", "matcher_b2",
                                   "matcher_ragged", "matcher_c2_idx"])
-def test_matcher_matches_reference_fixture(name, device):
+def test_matcher_matches_reference_fixture(name, precision, device):
     g = golden(name)
     n1, n3, L, B, seed, wc = [int(g[k]) for k in ("n1", "n3", "num_leaf", "batch", "seed",
                                                    "well_conditioned")]
     sd = synthetic.make_state_dict(seed, well_conditioned=bool(wc))
     data, _, _ = synthetic.make_matcher_inputs(n1, n3, L, seed=seed, batch=B)
-    pred, conf = run_matcher(sd, data, device)
+    pred, conf = run_matcher(sd, data, device, precision=precision)
     rm, cm = margins(g)
     check_indices(pred["matches0"], g["matches0"], rm, "matches0")
     check_indices(pred["matches1"], g["matches1"], cm, "matches1")
@@ -69,12 +71,13 @@ def test_matcher_matches_reference_fixture(name, device):
     assert pred["matches0"].dtype == np.int64 and pred["matches1"].dtype == np.int64
 
 
-def test_matcher_vs_oracle_batch_shared_object(device):
+@pytest.mark.parametrize("precision", ["fp32", "fp32_split"])
+def test_matcher_vs_oracle_batch_shared_object(precision, device):
     """Batch of 3 frames against one object passed as stride-0 (expanded) tensors."""
     from oracle import matcher_np as M
     sd = synthetic.make_state_dict(5)
     data, _, _ = synthetic.make_matcher_inputs(200, 330, 6, seed=5, batch=3)
-    pred, conf = run_matcher(sd, data, device, expand=True)
+    pred, conf = run_matcher(sd, data, device, expand=True, precision=precision)
     opred, oconf = M.forward(sd, data)
     np.testing.assert_allclose(conf, oconf, atol=ATOL)
     top = -np.sort(-oconf[0], axis=1)[:, :2]
@@ -84,13 +87,38 @@ def test_matcher_vs_oracle_batch_shared_object(device):
     assert (pred["matches0"] > -1).sum() > 20
 
 
-def test_matcher_deterministic(device):
+@pytest.mark.parametrize("precision", ["fp32", "fp32_split"])
+def test_matcher_deterministic(precision, device):
     sd = synthetic.make_state_dict(6)
     data, _, _ = synthetic.make_matcher_inputs(256, 512, 8, seed=6)
-    a = run_matcher(sd, data, device)
-    b = run_matcher(sd, data, device)
+    a = run_matcher(sd, data, device, precision=precision)
+    b = run_matcher(sd, data, device, precision=precision)
     np.testing.assert_array_equal(a[1], b[1])
     np.testing.assert_array_equal(a[0]["matches0"], b[0]["matches0"])
+
+
+@pytest.mark.parametrize("n1,n3,L,seed", [(256, 512, 8, 0), (1024, 4096, 8, 1)])
+def test_split_precision_is_fp32_accurate(n1, n3, L, seed, device):
+    """ONEPOSE_PREC_FP32_SPLIT (every GEMM on three bf16 pieces per operand, six products)
+    against the exact fp32-MFMA path, both measured from the float32 numpy oracle: the split's
+    conf error is of the same size as the fp32 path's (summation-order noise), far below
+    the bf16-rounded mode's, and its correspondences equal the fp32 path's."""
+    from oracle import matcher_np as M
+    sd = synthetic.make_state_dict(seed)
+    data, _, _ = synthetic.make_matcher_inputs(n1, n3, L, seed=seed)
+    opred, oconf = M.forward(sd, data)
+    err = {}
+    preds = {}
+    for prec in ("fp32", "fp32_split", "bf16"):
+        preds[prec], conf = run_matcher(sd, data, device, precision=prec)
+        err[prec] = float(np.abs(conf - oconf).max())
+    print("max |conf - oracle|:", err)
+    assert err["fp32_split"] <= 2.0 * err["fp32"] + 1e-6
+    assert err["fp32_split"] * 20 < err["bf16"]
+    top = -np.sort(-oconf[0], axis=1)[:, :2]
+    rm = np.minimum(top[:, 0] - top[:, 1], np.abs(opred["matching_scores0"] - 0.2))
+    check_indices(preds["fp32_split"]["matches0"], opred["matches0"], rm, "matches0")
+    assert (preds["fp32_split"]["matches0"] > -1).sum() > 20
 
 
 def test_matcher_full_size_properties(device):
@@ -179,7 +207,8 @@ def test_bf16_attention_mode_tracks_fp32(n1, n3, device):
 
 
 @pytest.mark.parametrize("n1,n3,L,B,prec", [(200, 777, 8, 1, 0), (1024, 4096, 8, 2, 0),
-                                             (128, 256, 12, 1, 0), (1024, 4096, 8, 1, 1)])
+                                             (128, 256, 12, 1, 0), (1024, 4096, 8, 1, 1),
+                                             (1024, 4096, 8, 1, 2)])
 def test_object_cache_is_bit_identical(device, n1, n3, L, B, prec):
     """onepose_object_prepare + onepose_match_cached (GAT 0 and the 3D half of self-attention
     1 run once per object) vs onepose_match_prepared_ex on the same object: every output

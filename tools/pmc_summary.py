@@ -15,10 +15,10 @@ GEMM_KIND = {(1, 0): "qkv_gemm", (2, 2): "mlp1_gemm", (3, 1): "mlp2_gemm", (0, 0
 
 
 def kind_of(name):
-    m = re.search(r"gemm_(?:f32_)?kernel<(\d+), (\d+), [^<]*Tile<[^>]*>(?:, (true|false))?", name)
-    if m:
+    m = re.search(r"gemm_(?:f32_)?kernel<(\d+), (\d+), [^<]*Tile<[^>]*>(?:, (true|false|\d))?", name)
+    if m:   # operand mode: bool (older builds) or GemmPm 0 / 1 (bf16) / 2 (split3)
         k = GEMM_KIND.get((int(m.group(1)), int(m.group(2))), name)
-        return k + ("_bf16" if m.group(3) == "true" else "")
+        return k + {"true": "_bf16", "1": "_bf16", "2": "_split3"}.get(m.group(3) or "", "")
     m = re.search(r"onepose::(?:\(anonymous namespace\)::)?(\w+?)(?:<|\(|$)", name)
     return m.group(1) if m else name
 
