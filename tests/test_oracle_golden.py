@@ -93,3 +93,20 @@ def test_object_leaves_match_reference():
         np.testing.assert_array_equal(a_s.numpy(), g[f"{tag}_avg_scores"])
         np.testing.assert_array_equal(leaves.numpy(), g[f"{tag}_leaves"])
         np.testing.assert_array_equal(l_s.numpy(), g[f"{tag}_leaf_scores"])
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_torch_cpu_restatement_matches_reference(name):
+    """oracle/matcher_torch.py (the PyTorch-CPU path bench.py's cpu_baseline times) against
+    the reference's own outputs."""
+    from oracle import matcher_torch as MT
+    g = golden(name)
+    sd, data, _ = regen(g)
+    pred, conf = MT.forward(MT.to_torch(sd), data)
+    np.testing.assert_array_equal(pred["matches0"], g["matches0"])
+    np.testing.assert_array_equal(pred["matches1"], g["matches1"])
+    np.testing.assert_allclose(pred["matching_scores0"], g["matching_scores0"], atol=1e-5)
+    np.testing.assert_allclose(pred["matching_scores1"], g["matching_scores1"], atol=1e-5)
+    if "conf" in g:
+        np.testing.assert_allclose(conf, g["conf"], atol=1e-5)
+    np.testing.assert_allclose(conf.sum(axis=2), g["conf_row_sum"], rtol=1e-4, atol=1e-5)

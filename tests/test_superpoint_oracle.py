@@ -72,3 +72,22 @@ def test_simple_nms_keeps_plateau_and_isolated_maxima():
     out = O.simple_nms(s, 2)
     assert out[5, 5] == np.float32(0.9) and out[5, 7] == 0
     assert out[12, 12] == np.float32(0.3) and out[12, 13] == np.float32(0.3)
+
+
+@pytest.mark.parametrize("tag", sorted(CASES))
+def test_torch_cpu_restatement_matches_reference(tag):
+    """oracle/superpoint_torch.py (the PyTorch-CPU detector bench.py's e2e cpu_baseline
+    times) against the reference's outputs: score map, and the keypoint set (torch.topk's
+    order among equal scores is unspecified) with its scores and descriptors."""
+    from oracle import superpoint_torch as ST
+    sd, img, max_kp, g = case(tag)
+    kp, sc, desc, smap = ST.forward(ST.to_torch(sd), img, nms_radius=3, keypoint_threshold=0.005,
+                                    remove_borders=4, max_keypoints=max_kp)
+    np.testing.assert_allclose(smap, g[f"{tag}_score_map"], rtol=1e-4, atol=1e-6)
+    ref = g[f"{tag}_keypoints"]
+    assert len(kp) == len(ref)
+    key = lambda k: np.lexsort((k[:, 0], k[:, 1]))   # noqa: E731
+    o, r = key(kp), key(ref)
+    np.testing.assert_array_equal(kp[o], ref[r])
+    np.testing.assert_allclose(sc[o], g[f"{tag}_scores"][r], rtol=1e-4)
+    np.testing.assert_allclose(desc[:, o], g[f"{tag}_descriptors"][:, r], atol=2e-5)

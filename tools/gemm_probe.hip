@@ -7,6 +7,7 @@
 //   hipcc -O3 --offload-arch=gfx950 -std=c++17 -DONEPOSE_GEMM_PROBE_NOLOAD tools/gemm_probe.hip -o tools/gemm_probe_noload
 #include "../onepose_amd/csrc/gemm.hip"
 #include <cstdarg>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 namespace onepose {
@@ -46,6 +47,52 @@ float run(float* A, float* W, float* Y, float* bias, int M0, int M1, int N, int 
   return ms * 1e3f / iters;
 }
 
+// Clock sampler: one workgroup spins ~40 us reading the shader-clock counter (s_memtime) and
+// the 100 MHz real-time counter; their ratio is the core clock of the CU it lands on.
+__global__ void clock_sampler(double* out, int i) {
+  if (threadIdx.x != 0) return;
+  const unsigned long long r0 = __builtin_amdgcn_s_memrealtime(), c0 = __builtin_amdgcn_s_memtime();
+  unsigned long long r1 = r0, c1 = c0;
+  while (r1 - r0 < 4000) {
+    r1 = __builtin_amdgcn_s_memrealtime();
+    c1 = __builtin_amdgcn_s_memtime();
+  }
+  out[i] = (double)(c1 - c0) / (double)(r1 - r0) * 0.1;   // GHz
+}
+
+template <class T, int PM>
+void clock_under_load(float* A, float* W, float* Y, float* bias) {
+  GemmArgs a;
+  memset(&a, 0, sizeof(a));
+  a.nprob = 2;
+  const int Ms[2] = {1024, 4096};
+  int grid = 0;
+  for (int i = 0; i < 2; ++i) {
+    GemmProb& p = a.p[i];
+    p = gemm_prob(A, 512, W, 512, bias, Y, 512, Ms[i], 512, 512, 1);
+    p.mtiles = (Ms[i] + T::BM - 1) / T::BM;
+    p.ntiles = (512 + T::BN - 1) / T::BN;
+    p.tiles = p.mtiles * p.ntiles;
+    grid += p.tiles;
+  }
+  double* d;
+  (void)hipMalloc(&d, 64 * sizeof(double));
+  hipStream_t s1, s2;
+  (void)hipStreamCreateWithFlags(&s1, hipStreamNonBlocking);
+  (void)hipStreamCreateWithFlags(&s2, hipStreamNonBlocking);
+  clock_sampler<<<1, 64, 0, s2>>>(d, 0);   // idle
+  (void)hipStreamSynchronize(s2);
+  for (int it = 0; it < 400; ++it) launch_one<EPI_BIAS, PRO_PLAIN, T, PM>(a, grid, s1);
+  for (int i = 1; i < 16; ++i) clock_sampler<<<1, 64, 0, s2>>>(d, i);
+  (void)hipDeviceSynchronize();
+  double h[16];
+  (void)hipMemcpy(h, d, sizeof(h), hipMemcpyDeviceToHost);
+  printf("%-7s clock idle %.3f GHz; under back-to-back mlp1 launches:", PM ? "split3" : "fp32", h[0]);
+  for (int i = 1; i < 16; ++i) printf(" %.2f", h[i]);
+  printf("\n");
+  (void)hipFree(d);
+}
+
 template <class T>
 void probe(const char* name, float* A, float* W, float* Y, float* bias) {
   const int M1s[3] = {3072, 4096, 7168};   // + 1024 tokens: config-2 mlp1 is M1 = 4096
@@ -78,6 +125,11 @@ int main() {
 #else
   printf("in-loop global loads on\n");
 #endif
+  if (getenv("PROBE_CLOCK")) {
+    clock_under_load<Tile<64, 64, 1, 4, 32>, PM_F32>(A, W, Y, bias);
+    clock_under_load<Tile<64, 64, 1, 4, 32>, PM_SPLIT3>(A, W, Y, bias);
+    return 0;
+  }
   probe<Tile<64, 64, 1, 4, 32>>("64x64 4w (production)", A, W, Y, bias);
   probe<Tile<64, 64, 2, 4, 64>>("64x64 4w K2 FN2 bks64", A, W, Y, bias);
   probe<Tile<64, 64, 1, 2, 32>>("64x64 2w FN2", A, W, Y, bias);
