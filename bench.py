@@ -190,6 +190,8 @@ def main():
     ap.add_argument("--eager", action="store_true",
                     help="launch every kernel from the host each step instead of replaying "
                          "captured HIP graphs")
+    ap.add_argument("--slots", type=int, default=0,
+                    help="frame buffer slots (default: match streams + 1)")
     ap.add_argument("--precision", choices=["fp32", "bf16", "fp32_split"], default="fp32",
                     help="matcher attention-layer GEMMs: fp32 MFMA (the reference's numerics, "
                          "default) or bf16 MFMA with fp32 accumulation (BASELINE config 5)")
@@ -238,7 +240,7 @@ def main():
         images = np.stack([synthetic.superpoint_image(S, S, rank * 1000 + i) for i in range(B)])
     pipe = FramePipeline(m, data["keypoints3d"][0], data["descriptors3d_db"][0],
                          data["descriptors2d_db"][0], B, n1, dev, scale=1000.0,
-                         slots=max(2, args.match_streams + 1), detector=detector,
+                         slots=args.slots or max(2, args.match_streams + 1), detector=detector,
                          image_hw=(args.image_size, args.image_size),
                          object_cache=not args.no_object_cache)
     cached = pipe.object_cache is not None

@@ -40,6 +40,8 @@ namespace onepose {
 // GEMM tile per layer GEMM (gemm.h; measured per shape on config 2).
 constexpr int kTileKV = TILE_32x128, kTileMLP1 = TILE_64x64,
               kTileMLP2 = TILE_64x64, kTileMLP2F32 = TILE_64x32K2, kTileFinal = TILE_64x64;
+constexpr int kFusedFoldMaxBatch = 4;   // kv_fold up to this batch, kv_reduce + m_fold above
+constexpr int kMlp2WideTiles = 1024;    // fp32 mlp2: 64x64 tiles from this many (4 per CU)
 
 // ------------------------------------------------------------------------------------
 // errors
@@ -1189,7 +1191,11 @@ int attention_layer(const ApW& w, const Side* sd, int nside, int B, const Plan& 
     if ((rc = gemm_launch(EPI_QKV, PRO_PLAIN, kTileKV, a, st, K_QKV_GEMM, pm)) != ONEPOSE_OK)
       return rc;
   }
-  if (!sh) {  // 2+3. KV[slot], ksum[slot] and the folded message weights, one launch
+  // kv_fold re-reads the whole 128 KB C_h panel per workgroup (64 of them per side and
+  // sample): one launch instead of two pays at small batches; at B = 32 the separate MFMA
+  // m_fold (16 KB of C per workgroup) is cheaper (config 3: 1.68 vs 2.02 ms per step).
+  const bool fused_fold = !sh && B <= kFusedFoldMaxBatch;
+  if (fused_fold) {  // 2+3. KV[slot], ksum[slot] and the folded message weights, one launch
     KvFoldArgs ka;
     ka.ct = w.ct;
     ka.mf[0] = ka.mf[1] = nullptr;
@@ -1201,7 +1207,8 @@ int attention_layer(const ApW& w, const Side* sd, int nside, int B, const Plan& 
       OP_REQUIRE(ka.mf[i] != nullptr, "attention layer: source slot %d has no reader", i);
     OP_LAUNCH(K_KV_REDUCE, st, kv_fold_kernel, dim3(nside * B * 65), dim3(1024), 0, st, ka, p.kv,
               p.ksum, B);
-  } else {  // sharded: the 3D source's KV is summed over the ranks before the fold
+  } else {  // separate reduce and fold; sharded: the 3D source's KV is summed over the ranks
+            // before the fold
     KvArgs kva;
     for (int i = 0; i < nside; ++i)
       kva.p[i] = {sd[i].kvpart, sd[i].kspart, ceil_div(sd[i].n, gemm_tile_rows(kTileKV))};
@@ -1283,7 +1290,13 @@ int attention_layer(const ApW& w, const Side* sd, int nside, int B, const Plan& 
       a.p[i].pro_rstd = p.rstd + (size_t)i * B * 512;
       a.p[i].pro_bs = 512;
     }
-    if ((rc = gemm_launch(EPI_RESID, PRO_NORM_RELU, pm == PM_F32 ? kTileMLP2F32 : kTileMLP2, a,
+    // fp32: the 64x32 K-split tile doubles the workgroup count where 64x64 tiles would leave
+    // CUs idle (config 2: 320 -> 640 tiles, 23.2 -> 19.7 us); with >= 4 tiles per CU anyway
+    // (batched configs) 64x64 moves less data per FLOP (config 3: 9.5 vs 12.3 ms per step)
+    int t64 = 0;
+    for (int i = 0; i < nside; ++i) t64 += ceil_div(sd[i].n, 64) * 4 * B;
+    const int mlp2_tile = pm == PM_F32 && t64 < kMlp2WideTiles ? kTileMLP2F32 : kTileMLP2;
+    if ((rc = gemm_launch(EPI_RESID, PRO_NORM_RELU, mlp2_tile, a,
                           st, K_MLP2, pm)) != ONEPOSE_OK)
       return rc;
   }
