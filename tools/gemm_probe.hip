@@ -130,6 +130,18 @@ int main() {
     clock_under_load<Tile<64, 64, 1, 4, 32>, PM_SPLIT3>(A, W, Y, bias);
     return 0;
   }
+  {   // the production tile at 1 / 2 / 2.5 (config 2) / 3 / 4 tiles per CU
+    using T = Tile<64, 64, 1, 4, 32>;
+    const int M1s[5] = {1024, 3072, 4096, 5120, 7168};
+    for (int pmi = 0; pmi < 2; ++pmi)
+      for (int mi = 0; mi < 5; ++mi) {
+        const int m1 = M1s[mi], tiles = (1024 / 64 + m1 / 64) * 8;
+        const float us = pmi == 0 ? run<T, PM_F32>(A, W, Y, bias, 1024, m1, 512, 512, 50)
+                                  : run<T, PM_SPLIT3>(A, W, Y, bias, 1024, m1, 512, 512, 50);
+        printf("64x64 %-7s tiles %5d  %8.2f us  %6.1f TF/s (fp32-equivalent)\n",
+               pmi ? "split3" : "fp32", tiles, us, 2.0 * (1024 + m1) * 512 * 512 / us * 1e-6);
+      }
+  }
   probe<Tile<64, 64, 1, 4, 32>>("64x64 4w (production)", A, W, Y, bias);
   probe<Tile<64, 64, 2, 4, 64>>("64x64 4w K2 FN2 bks64", A, W, Y, bias);
   probe<Tile<64, 64, 1, 2, 32>>("64x64 2w FN2", A, W, Y, bias);
