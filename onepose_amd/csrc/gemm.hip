@@ -20,6 +20,14 @@
 
 #include <cstring>
 
+// Pins the pipeline's phase order (tools/gemm_probe.hip compiles it out to compare with the
+// compiler's own schedule: ONEPOSE_GEMM_PROBE_NO_SCHED).
+#ifdef ONEPOSE_GEMM_PROBE_NO_SCHED
+#define ONEPOSE_SCHED_BARRIER() ((void)0)
+#else
+#define ONEPOSE_SCHED_BARRIER() __builtin_amdgcn_sched_barrier(0)
+#endif
+
 namespace onepose {
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
@@ -373,18 +381,18 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args) {
     load_stage<PRO, T>(c, m0, n0, min(kt + 2, nk - 1) * T::BKS, spare);
 #endif
     mfma_kk(tg, cur, 0);
-    __builtin_amdgcn_sched_barrier(0);
+    ONEPOSE_SCHED_BARRIER();
     float* na = lds + ((kt + 1) & 1) * STAGE;
     store_stage<PRO, T, PM>(na, next);                // (unused after the last step)
-    __builtin_amdgcn_sched_barrier(0);
+    ONEPOSE_SCHED_BARRIER();
 #pragma unroll
     for (int kk = 1; kk < KKW - 1; ++kk) mfma_kk(tg, cur, kk);
     __syncthreads();
     read_frag(na, nxt);                               // (unused after the last step)
     zdot(na, kt + 1);
-    __builtin_amdgcn_sched_barrier(0);
+    ONEPOSE_SCHED_BARRIER();
     mfma_kk(tg, cur, KKW - 1);
-    __builtin_amdgcn_sched_barrier(0);
+    ONEPOSE_SCHED_BARRIER();
   };
   if (PRO != PRO_HEADZ) {
     for (int kt = 0; kt < nk; kt += 2) {   // nk is even (checked at launch)
