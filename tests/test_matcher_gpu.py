@@ -256,3 +256,20 @@ def test_object_cache_is_bit_identical(device, n1, n3, L, B, prec):
         np.testing.assert_array_equal(outs[0][k], outs[1][k], err_msg=k)
     if n1 == 1024 and prec == 0:
         assert (outs[1]["m0"] > -1).sum() > 100
+
+
+@pytest.mark.parametrize("n1,n3,L", [(1, 1, 1), (1, 7, 2), (3, 5, 8), (65, 1, 8), (33, 97, 16)])
+def test_matcher_tiny_and_odd_shapes(n1, n3, L, device):
+    """Single-token sides (InstanceNorm over one row: variance 0), one partial chunk, tile
+    edges at 33 / 65 / 97 rows and L = 1 / 16: conf and indices vs the numpy oracle."""
+    from oracle import matcher_np as M
+    sd = synthetic.make_state_dict(9)
+    data, _, _ = synthetic.make_matcher_inputs(n1, n3, L, seed=9)
+    pred, conf = run_matcher(sd, data, device)
+    opred, oconf = M.forward(sd, data)
+    assert np.isfinite(conf).all()
+    np.testing.assert_allclose(conf, oconf, atol=ATOL)
+    top = -np.sort(-oconf[0], axis=1)[:, :2] if n3 > 1 else np.stack([oconf[0, :, 0], 0 * oconf[0, :, 0]], 1)
+    rm = np.minimum(top[:, 0] - top[:, 1], np.abs(opred["matching_scores0"] - 0.2))
+    check_indices(pred["matches0"], opred["matches0"], rm, "matches0")
+    np.testing.assert_allclose(pred["matching_scores0"], opred["matching_scores0"], atol=ATOL)
