@@ -171,8 +171,8 @@ def cpu_baseline(sd, data, frames, obj, seconds=15.0, detector_image=None):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=500)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--batch", type=int, default=1, help="frames per GPU per step")
     ap.add_argument("--n1", type=int, default=1024)
     ap.add_argument("--n3", type=int, default=4096)
@@ -260,6 +260,7 @@ def main():
     for k, t in zip(kinds, ms):
         per_kind.setdefault(names[k], []).append(float(t))
     total = {k: sum(v) / 3.0 for k, v in per_kind.items()}
+    mean_launch = {k: sum(v) / len(v) for k, v in per_kind.items()}
     # the dominant kernel is timed by device stamps, which the token GEMMs record
     dominant = max((k for k in total if kernel_work(k, B, n1, n3, L, cached) and k in STAMPED),
                    key=lambda k: total[k])
@@ -335,6 +336,7 @@ def main():
     n_dom = int(launches[dom_id])
     assert n_dom > 0 and tot_ms[dom_id] > 0, "dominant-kernel timing missing"
     dom_ms = float(tot_ms[dom_id] / n_dom)
+    alone_ms = float(mean_launch[dominant])
     elapsed = D.max_over_ranks(elapsed, dev)   # the slowest rank's clock
 
     stage_ms = None
@@ -393,7 +395,13 @@ def main():
             "traffic_source": traffic_src, "kernel": dominant,
             "avg_launch_us": round(dom_ms * 1e3, 2),
             "launches_timed": n_dom, "flop_per_launch": work,
-            "timing": "device clock, first workgroup start to last workgroup end"}
+            "timing": "device clock, first workgroup start to last workgroup end",
+            # context: the same kernel when nothing else runs (serial profile pass before the
+            # timed region, HIP events); inside the timed region a launch shares the chip with
+            # the other match stream's kernels
+            "alone": {"avg_launch_us": round(alone_ms * 1e3, 2),
+                      "frac": round(work / (alone_ms * 1e-3) / 1e12 / peak, 4),
+                      "timing": "serial profile pass (3 steps), HIP events per launch"}}
 
     # SURVEY.md §8d "fraction = F * frames/s / peak" for the whole frame's contractions
     ff = frame_flops(n1, n3, L, cached)
