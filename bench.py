@@ -190,6 +190,9 @@ def main():
     ap.add_argument("--eager", action="store_true",
                     help="launch every kernel from the host each step instead of replaying "
                          "captured HIP graphs")
+    ap.add_argument("--no-stamps", action="store_true",
+                    help="diagnostic: no device stamps in the timed region (roofline then "
+                         "reports the serial profile pass)")
     ap.add_argument("--slots", type=int, default=0,
                     help="frame buffer slots (default: match streams + 1)")
     ap.add_argument("--precision", choices=["fp32", "bf16", "fp32_split"], default="fp32",
@@ -275,6 +278,8 @@ def main():
     # argument); begin_device again below re-zeroes the same accumulators
     sp_id = names.index("sp_conv")
     stamp_mask = (1 << dom_id) | ((1 << sp_id) if args.e2e else 0)
+    if args.no_stamps:   # diagnostic: what device stamping costs the timed region
+        stamp_mask = 0
     _lib.check(lib.onepose_profile_begin_device(stamp_mask), "profile_begin_device")
     stage_graphs = pipe.capture_stages(torch.cuda.graph_pool_handle()) if graphs_on else None
     step_graph = pipe.capture(0) if graphs_on and not overlap else None
@@ -333,10 +338,13 @@ def main():
     launches, tot_ms = np.zeros(nk, np.int64), np.zeros(nk, np.float64)
     _lib.check(lib.onepose_profile_end_device(launches.ctypes.data, tot_ms.ctypes.data, nk),
                "profile_end_device")
-    n_dom = int(launches[dom_id])
-    assert n_dom > 0 and tot_ms[dom_id] > 0, "dominant-kernel timing missing"
-    dom_ms = float(tot_ms[dom_id] / n_dom)
     alone_ms = float(mean_launch[dominant])
+    n_dom = int(launches[dom_id])
+    if args.no_stamps:
+        n_dom, dom_ms = 0, alone_ms
+    else:
+        assert n_dom > 0 and tot_ms[dom_id] > 0, "dominant-kernel timing missing"
+        dom_ms = float(tot_ms[dom_id] / n_dom)
     elapsed = D.max_over_ranks(elapsed, dev)   # the slowest rank's clock
 
     stage_ms = None

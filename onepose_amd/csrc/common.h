@@ -49,36 +49,72 @@ enum KernelKind {
 };
 void prof_pre(int kind, hipStream_t s);
 void prof_post(int kind, hipStream_t s);
-// Device-stamp accumulator of one kernel kind (onepose_profile_begin_device).
+// Device-stamp accumulator of one launch site (graph node or eager launch) of a kernel kind
+// (onepose_profile_begin_device).  Workgroups are spread over kStampShards counters and
+// records by linear block id, so no word sees more than 1/16 of a launch's atomics (one
+// word absorbs only ~88 atomics per us).  Per workgroup: thread 0 takes a ticket from its
+// shard at the start (a returning atomic whose latency hides behind the kernel's first
+// loads); at the end each wave counts itself in an LDS word, and the workgroup's last wave
+// books launch e = ticket / (the shard's workgroups per launch) with two non-returning
+// atomics: rec[e][shard] = (max of ~start, max end); the host takes min start / max end over
+// the shards.  No barrier and no exposed round trip at the end: the earlier scheme (barrier +
+// a returning atomic per workgroup on one word) cost the bench 3.5% (1456 vs 1509 frames/s).
+constexpr int kStampShards = 16;
+constexpr int kStampRecs = 256;   // launches per site recorded after arming (later ones dropped)
+struct StampRec {
+  unsigned long long nstart, end;   // ~min start, max end (0 = unused)
+};
 struct StampAcc {
-  unsigned long long start;      // min over the running launch's workgroups (~0 when armed)
-  unsigned long long total;      // sum of finished launches' durations, clock ticks
-  unsigned long long launches;   // finished launches
-  unsigned int arrived;          // workgroups of the running launch that have finished
-  unsigned int pad;
+  unsigned long long issued[kStampShards];   // workgroups started per shard since arming
+  unsigned int overflow;                      // launches past kStampRecs (dropped)
+  unsigned int pad[3];
+  StampRec rec[kStampRecs][kStampShards];
+};
+struct StampTick {
+  unsigned long long t0, tick;
+};
+struct StampLds {   // per workgroup, in LDS
+  unsigned long long t0, tick;
+  unsigned int arrived, pad;
 };
 // Accumulator for the next launch of `kind`, or null when stamping is off for it.
 StampAcc* prof_stamp_slot(int kind);
 
-__device__ __forceinline__ void stamp_begin(StampAcc* s) {
-  if (s != nullptr && threadIdx.x == 0) atomicMin(&s->start, (unsigned long long)wall_clock64());
+__device__ __forceinline__ unsigned int stamp_block_id() {
+  return blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
 }
-// Every thread of the workgroup calls this at the kernel's end (s is launch-uniform).  The
-// workgroup that arrives last reads the clock after its arrival, so no earlier workgroup
-// ended later; it books the launch and re-arms the slot.  No fence: an agent-scope release
-// would write back the XCD's L2 (microseconds) and the timing needs no data hand-off.
-__device__ __forceinline__ void stamp_end(StampAcc* s) {
-  if (s == nullptr) return;
-  __syncthreads();
-  if (threadIdx.x != 0) return;
-  const unsigned int blocks = gridDim.x * gridDim.y * gridDim.z;
-  if (atomicAdd(&s->arrived, 1u) == blocks - 1) {
-    const unsigned long long e = (unsigned long long)wall_clock64();
-    const unsigned long long b = atomicExch(&s->start, ~0ull);
-    atomicAdd(&s->total, e - b);
-    atomicAdd(&s->launches, 1ull);
-    atomicExch(&s->arrived, 0u);
+// Called by every thread at the kernel's start (s is launch-uniform).  The kernel must pass a
+// workgroup barrier before any wave reaches stamp_end (thread 0 zeroes the arrival word).
+__device__ __forceinline__ StampTick stamp_begin(StampAcc* s, StampLds* l) {
+  StampTick k{0ull, 0ull};
+  if (s != nullptr && threadIdx.x == 0) {
+    l->arrived = 0u;
+    k.t0 = (unsigned long long)wall_clock64();
+    k.tick = atomicAdd(&s->issued[stamp_block_id() % kStampShards], 1ull);
   }
+  return k;
+}
+// Called at the end by every wave of the workgroup.
+__device__ __forceinline__ void stamp_end(StampAcc* s, const StampTick& k, StampLds* l) {
+  if (s == nullptr || (threadIdx.x & 63) != 0) return;
+  if (threadIdx.x == 0) {   // wave 0 hands its ticket over before it counts itself
+    l->t0 = k.t0;
+    l->tick = k.tick;
+  }
+  const unsigned int nw = (blockDim.x * blockDim.y * blockDim.z + 63) / 64;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  if (atomicAdd(&l->arrived, 1u) != nw - 1) return;   // not the workgroup's last wave
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  const unsigned long long end = (unsigned long long)wall_clock64();
+  const unsigned int blocks = gridDim.x * gridDim.y * gridDim.z, j = stamp_block_id() % kStampShards;
+  const unsigned int per = blocks / kStampShards + (j < blocks % kStampShards ? 1u : 0u);
+  const unsigned long long e = l->tick / per;
+  if (e >= (unsigned long long)kStampRecs) {
+    atomicAdd(&s->overflow, 1u);
+    return;
+  }
+  atomicMax(&s->rec[e][j].nstart, ~l->t0);
+  atomicMax(&s->rec[e][j].end, end);
 }
 
 // hipLaunchKernelGGL bracketed by the profiling hook, then a launch-error check

@@ -68,14 +68,17 @@ struct Prof {
   std::vector<hipEvent_t> ev;
   std::vector<int> kinds;
   int n = 0;
-  StampAcc* acc = nullptr;   // device, kStampPool per kind
+  StampAcc* acc[K_NUM_KINDS] = {};   // device, kStampPool sites, allocated per stamped kind
   int next[K_NUM_KINDS] = {};   // round-robin pool cursor per kind
 };
 // Each launch (or graph node captured while stamping) gets its own accumulator from the
 // kind's pool, so launches of one kind that run concurrently (several match streams)
 // never share one; a graph node keeps its accumulator across replays, which of the same
 // graph are serialised.
-constexpr int kStampPool = 256;
+// Launch sites per kind: a graph node keeps its site; eager launches cycle through the pool,
+// and 120 is a multiple of the per-frame launch counts (8 mlp1, 12 SuperPoint convs), so a
+// site always sees the same grid (the ticket -> launch arithmetic divides by its wave count).
+constexpr int kStampPool = 120;
 Prof g_prof;
 const char* kKindNames[K_NUM_KINDS] = {
     "transpose_in", "gat", "qkv_gemm", "kv_reduce", "m_fold", "mlp1_gemm",
@@ -85,9 +88,10 @@ const char* kKindNames[K_NUM_KINDS] = {
 }  // namespace
 
 StampAcc* prof_stamp_slot(int kind) {
-  if (!g_prof.device || !((g_prof.mask >> kind) & 1ull)) return nullptr;
+  if (!g_prof.device || !((g_prof.mask >> kind) & 1ull) || g_prof.acc[kind] == nullptr)
+    return nullptr;
   const int i = g_prof.next[kind]++ % kStampPool;
-  return g_prof.acc + (size_t)kind * kStampPool + i;
+  return g_prof.acc[kind] + i;
 }
 
 void prof_pre(int kind, hipStream_t s) {
@@ -927,11 +931,16 @@ int onepose_profile_begin(uint64_t kind_mask, int capacity) {
 
 int onepose_profile_begin_device(uint64_t kind_mask) {
   clear_error();
-  const size_t n_acc = (size_t)K_NUM_KINDS * kStampPool;
-  if (g_prof.acc == nullptr) OP_HIP(hipMalloc(&g_prof.acc, sizeof(StampAcc) * n_acc));
-  std::vector<StampAcc> init(n_acc);
-  for (auto& a : init) a = StampAcc{~0ull, 0ull, 0ull, 0u, 0u};
-  OP_HIP(hipMemcpy(g_prof.acc, init.data(), sizeof(StampAcc) * n_acc, hipMemcpyHostToDevice));
+  // per stamped kind: allocated once (graph nodes keep their sites' addresses), zeroed on
+  // every call (all zero = armed)
+  OP_HIP(hipDeviceSynchronize());
+  for (int k = 0; k < K_NUM_KINDS; ++k) {
+    if (!((kind_mask >> k) & 1ull)) continue;
+    if (g_prof.acc[k] == nullptr)
+      OP_HIP(hipMalloc(&g_prof.acc[k], sizeof(StampAcc) * kStampPool));
+    OP_HIP(hipMemset(g_prof.acc[k], 0, sizeof(StampAcc) * kStampPool));
+  }
+  OP_HIP(hipDeviceSynchronize());
   g_prof.n = 0;
   g_prof.mask = kind_mask;
   g_prof.device = true;
@@ -942,25 +951,37 @@ int onepose_profile_end_device(int64_t* launches, double* total_ms, int n_kinds)
   clear_error();
   OP_REQUIRE(g_prof.device, "profile_end_device: device stamping not active");
   g_prof.device = false;
+  const uint64_t mask = g_prof.mask;
   g_prof.mask = 0;
   OP_HIP(hipDeviceSynchronize());
-  std::vector<StampAcc> pool((size_t)K_NUM_KINDS * kStampPool);
-  OP_HIP(hipMemcpy(pool.data(), g_prof.acc, sizeof(StampAcc) * pool.size(),
-                   hipMemcpyDeviceToHost));
-  std::vector<StampAcc> a(K_NUM_KINDS, StampAcc{0ull, 0ull, 0ull, 0u, 0u});
-  for (int k = 0; k < K_NUM_KINDS; ++k)
-    for (int i = 0; i < kStampPool; ++i) {
-      a[k].total += pool[(size_t)k * kStampPool + i].total;
-      a[k].launches += pool[(size_t)k * kStampPool + i].launches;
-    }
+  std::vector<unsigned long long> tot(K_NUM_KINDS, 0ull), cnt(K_NUM_KINDS, 0ull);
+  std::vector<StampAcc> pool(kStampPool);
+  for (int k = 0; k < K_NUM_KINDS; ++k) {
+    if (!((mask >> k) & 1ull) || g_prof.acc[k] == nullptr) continue;
+    OP_HIP(hipMemcpy(pool.data(), g_prof.acc[k], sizeof(StampAcc) * kStampPool,
+                     hipMemcpyDeviceToHost));
+    for (const StampAcc& s : pool)   // launches past kStampRecs per site (s.overflow) dropped
+      for (int e = 0; e < kStampRecs; ++e) {
+        unsigned long long st = ~0ull, en = 0ull;
+        for (int j = 0; j < kStampShards; ++j) {
+          const StampRec& r = s.rec[e][j];
+          if (r.end == 0) continue;
+          st = std::min(st, ~r.nstart);
+          en = std::max(en, r.end);
+        }
+        if (en == 0) continue;
+        tot[k] += en > st ? en - st : 0ull;
+        ++cnt[k];
+      }
+  }
   int dev = 0, khz = 0;
   OP_HIP(hipGetDevice(&dev));
   OP_HIP(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev));
   OP_REQUIRE(khz > 0, "profile: wall clock rate unavailable");
   for (int k = 0; k < n_kinds; ++k) {
     const bool ok = k < K_NUM_KINDS;
-    if (launches) launches[k] = ok ? (int64_t)a[k].launches : 0;
-    if (total_ms) total_ms[k] = ok ? (double)a[k].total / khz : 0.0;
+    if (launches) launches[k] = ok ? (int64_t)cnt[k] : 0;
+    if (total_ms) total_ms[k] = ok ? (double)tot[k] / khz : 0.0;
   }
   return ONEPOSE_OK;
 }

@@ -112,7 +112,8 @@ __global__ __launch_bounds__(TL::NT) void conv_kernel(ConvArgs a) {
   constexpr int NKG = NK / TL::KS;   // stages per K-group
   static_assert(NK % TL::KS == 0 && NKG >= 2, "stages must split evenly over the K-groups");
   __shared__ __attribute__((aligned(16))) float lds[TL::KS * 2 * TL::STAGE];
-  stamp_begin(a.stamp);
+  __shared__ StampLds sl;
+  const StampTick tk = stamp_begin(a.stamp, &sl);
   const int b = blockIdx.y;
   const int mt = blockIdx.x / a.ntiles, nt = blockIdx.x - mt * a.ntiles;
   const int n0 = nt * BN;
@@ -256,7 +257,7 @@ __global__ __launch_bounds__(TL::NT) void conv_kernel(ConvArgs a) {
         }
       }
     }
-    stamp_end(a.stamp);
+    stamp_end(a.stamp, tk, &sl);
     return;
   }
   // CE_SOFTMAX: BM cells x 65 logits -> softmax over 65, drop the dustbin, pixel shuffle
@@ -294,7 +295,7 @@ __global__ __launch_bounds__(TL::NT) void conv_kernel(ConvArgs a) {
       }
     }
   }
-  stamp_end(a.stamp);
+  stamp_end(a.stamp, tk, &sl);
 }
 
 // conv1a (1 -> 64, 3x3, pad 1) + ReLU, direct: 16 threads per pixel, 4 output channels each,
