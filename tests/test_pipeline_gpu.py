@@ -145,3 +145,46 @@ def test_detector_pipeline_from_images():
     torch.cuda.synchronize()
     for s in pipe.slots:
         _assert_same(ref, _outputs(s))
+
+
+@pytest.mark.gpu
+def test_device_stamps_count_and_time_graph_launches(setup):
+    """bench.py's roofline timing (onepose_profile_begin_device): every MLP-conv-1 launch of a
+    replayed graph is booked once, and the stamped average (first wave start to last wave end)
+    agrees with HIP-event timing of the same launches run eagerly."""
+    import ctypes
+    from onepose_amd import _lib
+    lib = _lib.load()
+    pipe, batches = setup
+    pipe.set_frames(*batches[0])
+    names = [lib.onepose_profile_kind_name(i).decode() for i in range(64)
+             if lib.onepose_profile_kind_name(i)]
+    k = names.index("mlp1_gemm")
+    # eager HIP-event reference
+    _lib.check(lib.onepose_profile_begin(1 << k, 256), "profile_begin")
+    for _ in range(4):
+        pipe.enqueue(0)
+    kinds = np.zeros(256, np.int32)
+    ms = np.zeros(256, np.float32)
+    cnt = np.zeros(1, np.int32)
+    _lib.check(lib.onepose_profile_end(kinds.ctypes.data, ms.ctypes.data, 256, cnt.ctypes.data),
+               "profile_end")
+    per_frame = int(cnt[0]) // 4
+    assert per_frame == 8
+    ev_ms = float(ms[:cnt[0]].mean())
+    # stamped graph replays
+    _lib.check(lib.onepose_profile_begin_device(1 << k), "profile_begin_device")
+    g = pipe.capture(0)
+    _lib.check(lib.onepose_profile_begin_device(1 << k), "profile_begin_device")   # re-arm
+    reps = 20
+    for _ in range(reps):
+        g.replay()
+    torch.cuda.synchronize()
+    n = len(names)
+    launches = np.zeros(n, np.int64)
+    tot = np.zeros(n, np.float64)
+    _lib.check(lib.onepose_profile_end_device(launches.ctypes.data, tot.ctypes.data, n),
+               "profile_end_device")
+    assert launches[k] == reps * per_frame
+    st_ms = tot[k] / launches[k]
+    assert 0.5 * ev_ms < st_ms < 1.5 * ev_ms, (st_ms, ev_ms)
