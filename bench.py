@@ -190,6 +190,9 @@ def main():
     ap.add_argument("--eager", action="store_true",
                     help="launch every kernel from the host each step instead of replaying "
                          "captured HIP graphs")
+    ap.add_argument("--stage-marks", action="store_true",
+                    help="diagnostic: per-step timing events in the timed region -> stage_ms "
+                         "(they cost ~0.5%% of the frame rate, so they are off by default)")
     ap.add_argument("--no-stamps", action="store_true",
                     help="diagnostic: no device stamps in the timed region (roofline then "
                          "reports the serial profile pass)")
@@ -298,7 +301,8 @@ def main():
                 step_events.append(ev)
             return out
         if overlap:
-            pipe.run_stream(k, graphs=stage_graphs, marks=marks if record else None,
+            pipe.run_stream(k, graphs=stage_graphs,
+                            marks=marks if record and args.stage_marks else None,
                             match_streams=args.match_streams)
             return pipe.slots[(k - 1) % len(pipe.slots)]
         for _ in range(k):
