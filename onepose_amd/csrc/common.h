@@ -83,15 +83,24 @@ StampAcc* prof_stamp_slot(int kind);
 __device__ __forceinline__ unsigned int stamp_block_id() {
   return blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
 }
-// Called by every thread at the kernel's start (s is launch-uniform).  The kernel must pass a
+// stamp_start at the kernel's start, stamp_ticket anywhere before the first early return
+// (stamp_begin = both).  Called by every thread (s is launch-uniform).  The kernel must pass a
 // workgroup barrier before any wave reaches stamp_end (thread 0 zeroes the arrival word).
-__device__ __forceinline__ StampTick stamp_begin(StampAcc* s, StampLds* l) {
+__device__ __forceinline__ StampTick stamp_start(StampAcc* s, StampLds* l) {
   StampTick k{0ull, 0ull};
   if (s != nullptr && threadIdx.x == 0) {
     l->arrived = 0u;
     k.t0 = (unsigned long long)wall_clock64();
-    k.tick = atomicAdd(&s->issued[stamp_block_id() % kStampShards], 1ull);
   }
+  return k;
+}
+__device__ __forceinline__ void stamp_ticket(StampAcc* s, StampTick& k) {
+  if (s != nullptr && threadIdx.x == 0)
+    k.tick = atomicAdd(&s->issued[stamp_block_id() % kStampShards], 1ull);
+}
+__device__ __forceinline__ StampTick stamp_begin(StampAcc* s, StampLds* l) {
+  StampTick k = stamp_start(s, l);
+  stamp_ticket(s, k);
   return k;
 }
 // Called at the end by every wave of the workgroup.

@@ -370,9 +370,7 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
 
   load_stage<PRO, T>(c, m0, n0, 0, s0);
   load_stage<PRO, T>(c, m0, n0, T::BKS, s1);
-  // profiling ticket behind the prologue loads: waiting for those (in-order vmcnt) does not
-  // wait for the atomic, whose value is used only at the end
-  tk = stamp_begin(args.stamp, sl);
+  tk = stamp_start(args.stamp, sl);
   store_stage<PRO, T, PM>(lds, s0);
   __syncthreads();
   read_frag(lds, f0);
@@ -426,6 +424,9 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
     }
   }
   __syncthreads();   // every wave done with the LDS stages before they are reused below
+  // profiling ticket after the K loop: no in-loop wait (vmcnt counts in order) includes the
+  // atomic; its value is needed only at the end
+  stamp_ticket(args.stamp, tk);
 
   // ---- k-slice reduction: slices 1..KS-1 add into slice 0 in order (deterministic) ----
   if (T::KS > 1) {
