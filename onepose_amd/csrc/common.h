@@ -52,9 +52,10 @@ void prof_post(int kind, hipStream_t s);
 // Device-stamp accumulator of one launch site (graph node or eager launch) of a kernel kind
 // (onepose_profile_begin_device).  Workgroups are spread over kStampShards counters and
 // records by linear block id, so no word sees more than 1/16 of a launch's atomics (one
-// word absorbs only ~88 atomics per us).  Per workgroup: thread 0 takes a ticket from its
-// shard at the start (a returning atomic whose latency hides behind the kernel's first
-// loads); at the end each wave counts itself in an LDS word, and the workgroup's last wave
+// word absorbs only ~88 atomics per us).  Per workgroup: thread 0 reads the clock at the start
+// and takes a ticket from its shard (a returning atomic, issued where no wait includes it: the
+// GEMMs take it after the K loop, which cut their stamp cost from ~1.1% to ~0.4% of the bench
+// frame rate); at the end each wave counts itself in an LDS word, and the workgroup's last wave
 // books launch e = ticket / (the shard's workgroups per launch) with two non-returning
 // atomics: rec[e][shard] = (max of ~start, max end); the host takes min start / max end over
 // the shards.  No barrier and no exposed round trip at the end: the earlier scheme (barrier +
