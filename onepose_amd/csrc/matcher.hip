@@ -755,24 +755,26 @@ __global__ __launch_bounds__(256) void conf_kernel(float* S, int n1, int n3,
       for (int j = 0; j < 4; ++j) v[i][j] = cok[j] ? ps[col[j]] : 0.f;
     }
   }
-  unsigned long long cbest[4] = {0ull, 0ull, 0ull, 0ull};
+  // Running winners as (conf bits + 1, index): conf >= 0 (or NaN), so 32-bit unsigned order of
+  // the bits is pack_best's order, and a strict > over ascending indices keeps the first one
+  // (0 = none yet; bits + 1 does not wrap for any conf the kernel can produce).
+  unsigned cbu[4] = {0u, 0u, 0u, 0u};
+  int cbi[4] = {0, 0, 0, 0};
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     const int n = tiler * 32 + wave * 8 + i;
     if (n >= n1) break;   // wave-uniform
     const float rmx = rowmax[(int64_t)b * n1 + n];
     const float rinv = 1.0f / rowsum[(int64_t)b * n1 + n];
-    unsigned long long key = 0ull;
+    unsigned ru = 0u;
+    int ri = 0;
     float c[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       c[j] = (expf(v[i][j] - cmx[j]) * cinv[j]) * (expf(v[i][j] - rmx) * rinv);
-      if (cok[j]) {
-        const unsigned long long rk = pack_best(c[j], col[j] + col_offset);
-        key = rk > key ? rk : key;
-        const unsigned long long ck = pack_best(c[j], n);
-        cbest[j] = ck > cbest[j] ? ck : cbest[j];
-      }
+      const unsigned u = __float_as_uint(c[j]) + 1u;
+      if (cok[j] && u > ru) { ru = u; ri = col[j]; }
+      if (cok[j] && u > cbu[j]) { cbu[j] = u; cbi[j] = n; }
     }
     if (write_conf) {
       float* ps = Sb + (int64_t)n * n3;
@@ -784,6 +786,7 @@ __global__ __launch_bounds__(256) void conf_kernel(float* S, int n1, int n3,
           if (cok[j]) ps[col[j]] = c[j];
       }
     }
+    unsigned long long key = ru ? pack_best(__uint_as_float(ru - 1u), ri + col_offset) : 0ull;
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) {
       const unsigned long long other = shfl_xor_u64(key, o);
@@ -792,7 +795,9 @@ __global__ __launch_bounds__(256) void conf_kernel(float* S, int n1, int n3,
     if (lane == 0 && key != 0ull) atomicMax(rowbest + (int64_t)b * n1 + n, key);
   }
 #pragma unroll
-  for (int j = 0; j < 4; ++j) cb[wave][VEC ? lane * 4 + j : lane + 64 * j] = cbest[j];
+  for (int j = 0; j < 4; ++j)
+    cb[wave][VEC ? lane * 4 + j : lane + 64 * j] =
+        cbu[j] ? pack_best(__uint_as_float(cbu[j] - 1u), cbi[j]) : 0ull;
   __syncthreads();
   {
     const int cc = threadIdx.x, cg = tilec * 256 + cc;

@@ -14,7 +14,7 @@ f = glob.glob(f"gpurun_out/var_{v}/**/*kernel_stats.csv", recursive=True)[0]
 out = []
 for r in csv.DictReader(open(f)):
     n = r["Name"]
-    if any(k in n for k in ("kv_fold", "gat_kernel", "gemm_kernel<1", "conf_kernel", "l2norm", "pose_error")):
+    if any(k in n for k in ("kv_fold", "gat_kernel", "gemm_kernel<1", "conf_kernel", "softmax_reduce", "mutual", "l2norm", "pose_error")):
         out.append(f"{n.split('(')[0][-22:]} {float(r['AverageNs'])/1e3:.2f}")
 print(v, "|", "; ".join(out))
 PY
