@@ -685,6 +685,7 @@ void gemm_kernel(GemmArgs args) {
 using T64x64 = Tile<64, 64, 1, 4, 32>;
 using T32x128 = Tile<32, 128, 1, 4, 32>;
 using T64x32K2 = Tile<64, 32, 2, 4, 64>;
+using T64x128 = Tile<64, 128, 1, 4, 32>;
 
 
 template <int EPI, int PRO, class T, int PM>
@@ -700,6 +701,7 @@ TileDims tile_dims(int tile) {
     case TILE_64x64: return {64, 64, 32};
     case TILE_32x128: return {32, 128, 32};
     case TILE_64x32K2: return {64, 32, 64};
+    case TILE_64x128: return {64, 128, 32};
 
     default: return {0, 0, 0};
   }
@@ -769,6 +771,7 @@ int gemm_launch(int epi, int pro, int tile, GemmArgs& args, hipStream_t stream, 
     return ONEPOSE_OK;                                   \
   }
   CASE(EPI_QKV, PRO_PLAIN, TILE_32x128, T32x128, PM_F32)
+  CASE(EPI_QKV, PRO_PLAIN, TILE_64x128, T64x128, PM_F32)
   CASE(EPI_STATS, PRO_HEADZ, TILE_64x64, T64x64, PM_F32)
   CASE(EPI_RESID, PRO_NORM_RELU, TILE_64x64, T64x64, PM_F32)
   CASE(EPI_RESID, PRO_NORM_RELU, TILE_64x32K2, T64x32K2, PM_F32)

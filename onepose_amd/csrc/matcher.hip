@@ -42,6 +42,7 @@ constexpr int kTileKV = TILE_32x128, kTileMLP1 = TILE_64x64,
               kTileMLP2 = TILE_64x64, kTileMLP2F32 = TILE_64x32K2, kTileFinal = TILE_64x64;
 constexpr int kFusedFoldMaxBatch = 4;   // kv_fold up to this batch, kv_reduce + m_fold above
 constexpr int kMlp2WideTiles = 1024;    // fp32 mlp2: 64x64 tiles from this many (4 per CU)
+constexpr int kQkvWideTiles = 1024;     // fp32 qkv: 64x128 tiles from this many (4 per CU)
 
 // ------------------------------------------------------------------------------------
 // errors
@@ -1202,6 +1203,16 @@ struct Side {
 int attention_layer(const ApW& w, const Side* sd, int nside, int B, const Plan& p,
                     unsigned* cnt, hipStream_t st, int pm, const ShardCtx* sh) {
   int rc;
+  // QKV tile: 32 rows, or 64 in fp32 once there are >= 4 64-row tiles per CU (the short K = 256
+  // loop then amortises over twice the rows; at config 2 the frame rate is the same either way).
+  // The tile's rows are also the KV chunk length the fold sums over.
+  int qkv_tile = kTileKV;
+  {
+    int64_t t64 = 0;
+    for (int i = 0; i < nside; ++i) t64 += (int64_t)B * ceil_div(sd[i].n, 64) * 6;
+    if (pm == PM_F32 && t64 >= kQkvWideTiles) qkv_tile = TILE_64x128;
+  }
+  const int kv_rows = gemm_tile_rows(qkv_tile);
   {  // 1. [q | k_h v_h ...]: phi(q) stored, per-chunk KV / ksum partials
     GemmArgs a;
     a.nprob = nside;
@@ -1214,7 +1225,7 @@ int attention_layer(const ApW& w, const Side* sd, int nside, int B, const Plan& 
       a.p[i].kspart = s.kspart;
       a.p[i].y_bs = (int64_t)s.n * 256;
     }
-    if ((rc = gemm_launch(EPI_QKV, PRO_PLAIN, kTileKV, a, st, K_QKV_GEMM, pm)) != ONEPOSE_OK)
+    if ((rc = gemm_launch(EPI_QKV, PRO_PLAIN, qkv_tile, a, st, K_QKV_GEMM, pm)) != ONEPOSE_OK)
       return rc;
   }
   // kv_fold re-reads the whole 128 KB C_h panel per workgroup (64 of them per side and
@@ -1226,7 +1237,7 @@ int attention_layer(const ApW& w, const Side* sd, int nside, int B, const Plan& 
     ka.ct = w.ct;
     ka.mf[0] = ka.mf[1] = nullptr;
     for (int i = 0; i < nside; ++i) {
-      ka.p[i] = {sd[i].kvpart, sd[i].kspart, ceil_div(sd[i].n, gemm_tile_rows(kTileKV))};
+      ka.p[i] = {sd[i].kvpart, sd[i].kspart, ceil_div(sd[i].n, kv_rows)};
       ka.mf[sd[i].src] = p.mf + (size_t)i * B * 512 * 256;
     }
     for (int i = 0; i < nside; ++i)
@@ -1237,7 +1248,7 @@ int attention_layer(const ApW& w, const Side* sd, int nside, int B, const Plan& 
             // before the fold
     KvArgs kva;
     for (int i = 0; i < nside; ++i)
-      kva.p[i] = {sd[i].kvpart, sd[i].kspart, ceil_div(sd[i].n, gemm_tile_rows(kTileKV))};
+      kva.p[i] = {sd[i].kvpart, sd[i].kspart, ceil_div(sd[i].n, kv_rows)};
     OP_LAUNCH(K_KV_REDUCE, st, kv_reduce_kernel, dim3(nside * B * 65), dim3(256), 0, st, kva,
               p.kv, p.ksum, B);
     if (sh) {   // the 3D side's KV / sum phi(k) over every rank's points

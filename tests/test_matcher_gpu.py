@@ -141,6 +141,23 @@ def test_matcher_full_size_properties(device):
     np.testing.assert_array_equal(conf[0].argmax(axis=1)[valid], m0[valid])
 
 
+def test_wide_qkv_tile_batch_matches_single_frames(device):
+    """At >= 1024 64-row QKV tiles (kQkvWideTiles) fp32 runs the 64x128 QKV tile with 64-row
+    KV chunks; each frame of such a batch must agree with the same frame run alone (32-row
+    tile, pinned to the oracle above) up to the KV chunk-sum order."""
+    sd = synthetic.make_state_dict(11)
+    B = 3   # 3 x (16 + 64) 64-row tiles x 6 = 1440 >= 1024; alone 480
+    data, _, _ = synthetic.make_matcher_inputs(1024, 4096, 4, seed=11, batch=B)
+    pred, conf = run_matcher(sd, data, device, expand=True)
+    for b in range(B):
+        one = {k: v[b:b + 1] for k, v in data.items()}
+        p1, c1 = run_matcher(sd, one, device)
+        np.testing.assert_allclose(conf[b], c1[0], rtol=0, atol=ATOL)
+        if b == 0:   # pred holds sample 0's correspondences, as the reference returns them
+            assert (pred["matches0"] == p1["matches0"]).mean() > 0.998
+            assert (pred["matches0"] > -1).sum() > 100
+
+
 @pytest.mark.parametrize("n1,n3,L", [(200, 777, 8), (96, 300, 3), (128, 256, 12)])
 def test_prepared_leaves_path_is_identical(device, n1, n3, L):
     """onepose_match_prepared on leaves transposed once by onepose_prepare_leaves gives the

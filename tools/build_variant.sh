@@ -12,5 +12,5 @@ for s in onepose_amd/csrc/*.hip; do
   objs="$objs $o"
 done
 wait
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC $objs -o tools/ab/lib_$name.so
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC $objs -o tools/ab/lib_$name.so && rm -rf $out
 echo tools/ab/lib_$name.so
