@@ -88,6 +88,7 @@ enum GemmTile {
   TILE_64x32K2 = 2, // mlp2 fp32 (RESID + NORM): 64 x 32 outputs, K split over two wave pairs
                     //   (N = 256 gives 2x the 64x64 tile count: 640 tiles at config 2)
   TILE_64x128 = 3,  // qkv fp32 at large batches: 2 accumulators per wave, 64-row KV chunks
+  TILE_128x128 = 4, // qkv fp32 at larger batches: 4 accumulators per wave, 128-row KV chunks
 };
 // (STATS + HEADZ also compile for 64x32 / 2 waves and for 64x64 / 8 waves with K split in
 // two and 64-deep stages, one head per stage; both measured slower than 64x64 for mlp1 in the

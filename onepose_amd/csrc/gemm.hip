@@ -686,6 +686,7 @@ using T64x64 = Tile<64, 64, 1, 4, 32>;
 using T32x128 = Tile<32, 128, 1, 4, 32>;
 using T64x32K2 = Tile<64, 32, 2, 4, 64>;
 using T64x128 = Tile<64, 128, 1, 4, 32>;
+using T128x128 = Tile<128, 128, 1, 4, 32>;
 
 
 template <int EPI, int PRO, class T, int PM>
@@ -702,6 +703,7 @@ TileDims tile_dims(int tile) {
     case TILE_32x128: return {32, 128, 32};
     case TILE_64x32K2: return {64, 32, 64};
     case TILE_64x128: return {64, 128, 32};
+    case TILE_128x128: return {128, 128, 32};
 
     default: return {0, 0, 0};
   }
@@ -772,6 +774,7 @@ int gemm_launch(int epi, int pro, int tile, GemmArgs& args, hipStream_t stream, 
   }
   CASE(EPI_QKV, PRO_PLAIN, TILE_32x128, T32x128, PM_F32)
   CASE(EPI_QKV, PRO_PLAIN, TILE_64x128, T64x128, PM_F32)
+  CASE(EPI_QKV, PRO_PLAIN, TILE_128x128, T128x128, PM_F32)
   CASE(EPI_STATS, PRO_HEADZ, TILE_64x64, T64x64, PM_F32)
   CASE(EPI_RESID, PRO_NORM_RELU, TILE_64x64, T64x64, PM_F32)
   CASE(EPI_RESID, PRO_NORM_RELU, TILE_64x32K2, T64x32K2, PM_F32)

@@ -43,6 +43,7 @@ constexpr int kTileKV = TILE_32x128, kTileMLP1 = TILE_64x64,
 constexpr int kFusedFoldMaxBatch = 4;   // kv_fold up to this batch, kv_reduce + m_fold above
 constexpr int kMlp2WideTiles = 1024;    // fp32 mlp2: 64x64 tiles from this many (4 per CU)
 constexpr int kQkvWideTiles = 1024;     // fp32 qkv: 64x128 tiles from this many (4 per CU)
+constexpr int kQkvWiderTiles = 4096;    // fp32 qkv: 128x128 tiles from this many 64-row tiles
 
 // ------------------------------------------------------------------------------------
 // errors
@@ -1203,14 +1204,16 @@ struct Side {
 int attention_layer(const ApW& w, const Side* sd, int nside, int B, const Plan& p,
                     unsigned* cnt, hipStream_t st, int pm, const ShardCtx* sh) {
   int rc;
-  // QKV tile: 32 rows, or 64 in fp32 once there are >= 4 64-row tiles per CU (the short K = 256
-  // loop then amortises over twice the rows; at config 2 the frame rate is the same either way).
-  // The tile's rows are also the KV chunk length the fold sums over.
+  // QKV tile: 32 rows; in fp32, 64 rows from 4 64-row tiles per CU and 128 rows from 16. The
+  // tile's rows are the KV chunk length, so wider tiles cut the KV partials the chunk sum reads
+  // (B = 32, config 3: 570 MB per launch at 64 rows); at config 2 (480 tiles) the 32-row tile
+  // keeps the launch spread over the CUs.
   int qkv_tile = kTileKV;
   {
     int64_t t64 = 0;
     for (int i = 0; i < nside; ++i) t64 += (int64_t)B * ceil_div(sd[i].n, 64) * 6;
     if (pm == PM_F32 && t64 >= kQkvWideTiles) qkv_tile = TILE_64x128;
+    if (pm == PM_F32 && t64 >= kQkvWiderTiles) qkv_tile = TILE_128x128;
   }
   const int kv_rows = gemm_tile_rows(qkv_tile);
   {  // 1. [q | k_h v_h ...]: phi(q) stored, per-chunk KV / ksum partials

@@ -141,15 +141,16 @@ def test_matcher_full_size_properties(device):
     np.testing.assert_array_equal(conf[0].argmax(axis=1)[valid], m0[valid])
 
 
-def test_wide_qkv_tile_batch_matches_single_frames(device):
-    """At >= 1024 64-row QKV tiles (kQkvWideTiles) fp32 runs the 64x128 QKV tile with 64-row
-    KV chunks; each frame of such a batch must agree with the same frame run alone (32-row
-    tile, pinned to the oracle above) up to the KV chunk-sum order."""
+@pytest.mark.parametrize("B", [3, 16])
+def test_wide_qkv_tile_batch_matches_single_frames(B, device):
+    """From 1024 / 4096 64-row QKV tiles (kQkvWideTiles / kQkvWiderTiles) fp32 runs the 64x128 /
+    128x128 QKV tile with 64- / 128-row KV chunks: B = 3 gives 3 x (16 + 64) x 6 = 1440 tiles,
+    B = 16 gives 7680 (alone: 480).  Each frame of such a batch must agree with the same frame
+    run alone (32-row tile, pinned to the oracle above) up to the KV chunk-sum order."""
     sd = synthetic.make_state_dict(11)
-    B = 3   # 3 x (16 + 64) 64-row tiles x 6 = 1440 >= 1024; alone 480
     data, _, _ = synthetic.make_matcher_inputs(1024, 4096, 4, seed=11, batch=B)
     pred, conf = run_matcher(sd, data, device, expand=True)
-    for b in range(B):
+    for b in sorted({0, B // 2, B - 1}):
         one = {k: v[b:b + 1] for k, v in data.items()}
         p1, c1 = run_matcher(sd, one, device)
         np.testing.assert_allclose(conf[b], c1[0], rtol=0, atol=ATOL)
