@@ -42,8 +42,8 @@ constexpr int kTileKV = TILE_32x128, kTileMLP1 = TILE_64x64,
               kTileMLP2 = TILE_64x64, kTileMLP2F32 = TILE_64x32K2, kTileFinal = TILE_64x64;
 constexpr int kFusedFoldMaxBatch = 4;   // kv_fold up to this batch, kv_reduce + m_fold above
 constexpr int kMlp2WideTiles = 1024;    // fp32 mlp2: 64x64 tiles from this many (4 per CU)
-constexpr int kQkvWideTiles = 1024;     // fp32 qkv: 64x128 tiles from this many (4 per CU)
-constexpr int kQkvWiderTiles = 4096;    // fp32 qkv: 128x128 tiles from this many 64-row tiles
+constexpr int kQkvWideTiles = 256;      // fp32 qkv: 64x128 tiles from this many 64-row tiles
+constexpr int kQkvWiderTiles = 4096;    //   of the 3D side; 128x128 from this many (qkv_tile_for)
 
 // ------------------------------------------------------------------------------------
 // errors
@@ -861,12 +861,24 @@ struct Plan {
   float *rowpart, *colpart, *rowmax, *rowsum, *colmax, *colsum;
   unsigned long long *rowbest, *colbest;
   float* leaves_pm;   // point-major copy of the leaves (onepose_match only)
+  int qkv_tile;       // fp32 QKV tile (qkv_tile_for)
   size_t bytes;
 };
+
+// fp32 QKV tile: 32 rows; 64 rows from 256 64-row tiles of the 3D side (config 2: 384; QKV
+// 14% faster alone, +0.3% frames/s) and 128 rows from 4096 (config 3/4 at B = 32).  The tile's
+// rows are the KV chunk length, so wider tiles also cut the KV partials the chunk sum reads
+// (config 3: 570 MB per launch at 64 rows).  A function of n3 alone up to B = 4, so the object
+// prefix (onepose_object_prepare, B = 1) and cached / uncached forwards pick the same tile.
+int qkv_tile_for(int n3, int B) {
+  const int64_t t64 = (int64_t)ceil_div(n3, 64) * 6 * (B > kFusedFoldMaxBatch ? B : 1);
+  return t64 >= kQkvWiderTiles ? TILE_128x128 : t64 >= kQkvWideTiles ? TILE_64x128 : kTileKV;
+}
 
 Plan make_plan(void* ws, int B, int n1, int n3, int L, bool with_conf) {
   Carve c(ws);
   Plan p;
+  p.qkv_tile = qkv_tile_for(n3, B);
   const size_t t2 = (size_t)B * n1, t3 = (size_t)B * n3;
   for (int i = 0; i < 2; ++i) {
     p.x2[i] = c.take<float>(t2 * 256);
@@ -1204,17 +1216,8 @@ struct Side {
 int attention_layer(const ApW& w, const Side* sd, int nside, int B, const Plan& p,
                     unsigned* cnt, hipStream_t st, int pm, const ShardCtx* sh) {
   int rc;
-  // QKV tile: 32 rows; in fp32, 64 rows from 4 64-row tiles per CU and 128 rows from 16. The
-  // tile's rows are the KV chunk length, so wider tiles cut the KV partials the chunk sum reads
-  // (B = 32, config 3: 570 MB per launch at 64 rows); at config 2 (480 tiles) the 32-row tile
-  // keeps the launch spread over the CUs.
-  int qkv_tile = kTileKV;
-  {
-    int64_t t64 = 0;
-    for (int i = 0; i < nside; ++i) t64 += (int64_t)B * ceil_div(sd[i].n, 64) * 6;
-    if (pm == PM_F32 && t64 >= kQkvWideTiles) qkv_tile = TILE_64x128;
-    if (pm == PM_F32 && t64 >= kQkvWiderTiles) qkv_tile = TILE_128x128;
-  }
+  // QKV tile (fp32): chosen per forward in make_plan, the same for every layer and side.
+  const int qkv_tile = pm == PM_F32 ? p.qkv_tile : kTileKV;
   const int kv_rows = gemm_tile_rows(qkv_tile);
   {  // 1. [q | k_h v_h ...]: phi(q) stored, per-chunk KV / ksum partials
     GemmArgs a;

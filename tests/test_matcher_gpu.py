@@ -143,10 +143,11 @@ def test_matcher_full_size_properties(device):
 
 @pytest.mark.parametrize("B", [3, 16])
 def test_wide_qkv_tile_batch_matches_single_frames(B, device):
-    """From 1024 / 4096 64-row QKV tiles (kQkvWideTiles / kQkvWiderTiles) fp32 runs the 64x128 /
-    128x128 QKV tile with 64- / 128-row KV chunks: B = 3 gives 3 x (16 + 64) x 6 = 1440 tiles,
-    B = 16 gives 7680 (alone: 480).  Each frame of such a batch must agree with the same frame
-    run alone (32-row tile, pinned to the oracle above) up to the KV chunk-sum order."""
+    """From 256 / 4096 64-row QKV tiles of the 3D side (qkv_tile_for; x B above B = 4) fp32
+    runs the 64x128 / 128x128 QKV tile with 64- / 128-row KV chunks: B = 3 gives 3 x 64 x 6 =
+    1152 tiles (64 rows, as alone: 384), B = 16 gives 6144 (128 rows).  Each frame of the batch
+    must agree with the same frame run alone up to the KV chunk-sum order; the 64-row path at
+    this size is pinned to the reference fixture matcher_c2_idx."""
     sd = synthetic.make_state_dict(11)
     data, _, _ = synthetic.make_matcher_inputs(1024, 4096, 4, seed=11, batch=B)
     pred, conf = run_matcher(sd, data, device, expand=True)
