@@ -861,15 +861,13 @@ struct Plan {
   float *rowpart, *colpart, *rowmax, *rowsum, *colmax, *colsum;
   unsigned long long *rowbest, *colbest;
   float* leaves_pm;   // point-major copy of the leaves (onepose_match only)
-  int qkv_tile;       // fp32 QKV tile (qkv_tile_for)
   size_t bytes;
 };
 
 // fp32 QKV tile: 32 rows; 64 rows from 256 64-row tiles of the 3D side (config 2: 384; QKV
 // 14% faster alone, +0.3% frames/s) and 128 rows from 4096 (config 3/4 at B = 32).  The tile's
 // rows are the KV chunk length, so wider tiles also cut the KV partials the chunk sum reads
-// (config 3: 570 MB per launch at 64 rows).  A function of n3 alone up to B = 4, so the object
-// prefix (onepose_object_prepare, B = 1) and cached / uncached forwards pick the same tile.
+// (config 3: 570 MB per launch at 64 rows).
 int qkv_tile_for(int n3, int B) {
   const int64_t t64 = (int64_t)ceil_div(n3, 64) * 6 * (B > kFusedFoldMaxBatch ? B : 1);
   return t64 >= kQkvWiderTiles ? TILE_128x128 : t64 >= kQkvWideTiles ? TILE_64x128 : kTileKV;
@@ -878,7 +876,6 @@ int qkv_tile_for(int n3, int B) {
 Plan make_plan(void* ws, int B, int n1, int n3, int L, bool with_conf) {
   Carve c(ws);
   Plan p;
-  p.qkv_tile = qkv_tile_for(n3, B);
   const size_t t2 = (size_t)B * n1, t3 = (size_t)B * n3;
   for (int i = 0; i < 2; ++i) {
     p.x2[i] = c.take<float>(t2 * 256);
@@ -1207,17 +1204,50 @@ struct Side {
   int n;        // tokens (this rank's)
   float len;    // the side's full length as an attention source (Ns, v / Ns)
   int src;      // slot of the side this one attends to
+  int ntile;    // token count the tile choices use (n; a sharded 3D side: the largest shard,
+                // so that every rank picks the same tiles and rounds alike)
 };
+
+// Per-launch choices of one attention layer that change the summation order.  A side's bits
+// depend on them (and on nothing else about the launch), so launches whose results must agree
+// bit for bit -- the object prefix and the uncached forward's layer 1, every rank of a sharded
+// frame -- are given the same choices (layer_tiles over the same sides, batch and qkv_n3).
+struct LayerTiles {
+  int qkv;          // QKV GEMM tile (its rows are the KV chunk length)
+  bool fused_fold;  // kv_fold (one launch) vs kv_reduce + m_fold
+  int mlp2;         // MLP conv 2 tile
+};
+
+LayerTiles layer_tiles(int qkv_n3, const Side* sd, int nside, int B, int pm, bool sharded) {
+  LayerTiles t;
+  t.qkv = pm == PM_F32 ? qkv_tile_for(qkv_n3, B) : kTileKV;
+  // kv_fold re-reads the whole 128 KB C_h panel per workgroup (64 of them per side and
+  // sample): one launch instead of two pays at small batches; at B = 32 the separate MFMA
+  // m_fold (16 KB of C per workgroup) is cheaper (config 3: 1.68 vs 2.02 ms per step).
+  // Sharded: the 3D source's KV is summed over the ranks between the two.
+  t.fused_fold = !sharded && B <= kFusedFoldMaxBatch;
+  // fp32: the 64x32 K-split tile doubles the workgroup count where 64x64 tiles would leave
+  // CUs idle (config 2: 320 -> 640 tiles, 23.2 -> 19.7 us); with >= 4 tiles per CU anyway
+  // (batched configs) 64x64 moves less data per FLOP (config 3: 9.5 vs 12.3 ms per step)
+  int64_t t64 = 0;
+  for (int i = 0; i < nside; ++i) t64 += (int64_t)ceil_div(sd[i].ntile, 64) * 4 * B;
+  t.mlp2 = pm == PM_F32 && t64 < kMlp2WideTiles ? kTileMLP2F32 : kTileMLP2;
+  return t;
+}
+
+bool same_tiles(const LayerTiles& a, const LayerTiles& b) {
+  return a.qkv == b.qkv && a.fused_fold == b.fused_fold && a.mlp2 == b.mlp2;
+}
 
 // AttentionPropagation (GATs_SuperGlue.py:123-132) for 1 or 2 sides in grouped launches.
 // Each side's arithmetic is independent of the others' (per-problem tiles, per-slot
 // reductions), so a side gives the same bits alone or grouped.  Sharded runs have two
 // sides, slot 1 being the 3D shard.
 int attention_layer(const ApW& w, const Side* sd, int nside, int B, const Plan& p,
-                    unsigned* cnt, hipStream_t st, int pm, const ShardCtx* sh) {
+                    unsigned* cnt, hipStream_t st, int pm, const ShardCtx* sh,
+                    const LayerTiles& tl) {
   int rc;
-  // QKV tile (fp32): chosen per forward in make_plan, the same for every layer and side.
-  const int qkv_tile = pm == PM_F32 ? p.qkv_tile : kTileKV;
+  const int qkv_tile = tl.qkv;
   const int kv_rows = gemm_tile_rows(qkv_tile);
   {  // 1. [q | k_h v_h ...]: phi(q) stored, per-chunk KV / ksum partials
     GemmArgs a;
@@ -1234,11 +1264,7 @@ int attention_layer(const ApW& w, const Side* sd, int nside, int B, const Plan& 
     if ((rc = gemm_launch(EPI_QKV, PRO_PLAIN, qkv_tile, a, st, K_QKV_GEMM, pm)) != ONEPOSE_OK)
       return rc;
   }
-  // kv_fold re-reads the whole 128 KB C_h panel per workgroup (64 of them per side and
-  // sample): one launch instead of two pays at small batches; at B = 32 the separate MFMA
-  // m_fold (16 KB of C per workgroup) is cheaper (config 3: 1.68 vs 2.02 ms per step).
-  const bool fused_fold = !sh && B <= kFusedFoldMaxBatch;
-  if (fused_fold) {  // 2+3. KV[slot], ksum[slot] and the folded message weights, one launch
+  if (tl.fused_fold) {  // 2+3. KV[slot], ksum[slot] and the folded message weights, one launch
     KvFoldArgs ka;
     ka.ct = w.ct;
     ka.mf[0] = ka.mf[1] = nullptr;
@@ -1333,13 +1359,7 @@ int attention_layer(const ApW& w, const Side* sd, int nside, int B, const Plan& 
       a.p[i].pro_rstd = p.rstd + (size_t)i * B * 512;
       a.p[i].pro_bs = 512;
     }
-    // fp32: the 64x32 K-split tile doubles the workgroup count where 64x64 tiles would leave
-    // CUs idle (config 2: 320 -> 640 tiles, 23.2 -> 19.7 us); with >= 4 tiles per CU anyway
-    // (batched configs) 64x64 moves less data per FLOP (config 3: 9.5 vs 12.3 ms per step)
-    int t64 = 0;
-    for (int i = 0; i < nside; ++i) t64 += ceil_div(sd[i].n, 64) * 4 * B;
-    const int mlp2_tile = pm == PM_F32 && t64 < kMlp2WideTiles ? kTileMLP2F32 : kTileMLP2;
-    if ((rc = gemm_launch(EPI_RESID, PRO_NORM_RELU, mlp2_tile, a,
+    if ((rc = gemm_launch(EPI_RESID, PRO_NORM_RELU, tl.mlp2, a,
                           st, K_MLP2, pm)) != ONEPOSE_OK)
       return rc;
   }
@@ -1403,12 +1423,36 @@ int match_impl(const void* packed_weights, const float* desc2d, int64_t desc2d_b
     // self: each side attends to itself; cross: 2D <-> 3D
     Side sd[2];
     sd[0] = {x2r, (int64_t)n1 * 256, p.x2[c2 ^ 1], p.phiq2, p.kvpart2, p.kspart2, p.y12,
-             p.stats2, n1, (float)n1, kind == 1 ? 0 : 1};
+             p.stats2, n1, (float)n1, kind == 1 ? 0 : 1, n1};
     sd[1] = {x3r, x3bs, p.x3[c3 ^ 1], p.phiq3, p.kvpart3, p.kspart3, p.y13, p.stats3, n3,
-             (float)n3g, kind == 1 ? 1 : 0};
-    const int nside = cached3 ? 1 : 2;
-    int rc = attention_layer(w, sd, nside, B, p, p.cnt + (size_t)(ap - 1) * 2 * B * kCntPerSide,
-                             st, pm, sh);
+             (float)n3g, kind == 1 ? 1 : 0, sh ? sh->max_shard : n3};
+    const int qkv_n3 = sh ? sh->max_shard : n3;
+    unsigned* lcnt = p.cnt + (size_t)(ap - 1) * 2 * B * kCntPerSide;
+    int rc;
+    if (cached3) {   // self-attention 1, 2D half (the 3D half is in the object cache)
+      rc = attention_layer(w, sd, 1, B, p, lcnt, st, pm, sh, layer_tiles(qkv_n3, sd, 1, B, pm, sh));
+    } else {
+      const LayerTiles tg = layer_tiles(qkv_n3, sd, 2, B, pm, sh);
+      bool split = false;
+      LayerTiles t3{}, t2{};
+      Side s3 = sd[1];
+      s3.src = 0;
+      if (ap == 1 && !sh) {
+        // Uncached self-attention 1 gives the bits of the cached forward: its 3D half with the
+        // object prefix's choices (onepose_object_prepare: that side alone, B = 1 -- each
+        // sample's arithmetic does not depend on the launch's batch), its 2D half with the
+        // cached forward's.  Where those equal the grouped choices one launch does both.
+        t3 = layer_tiles(n3, &s3, 1, 1, pm, false);
+        t2 = layer_tiles(n3, sd, 1, B, pm, false);
+        split = !same_tiles(t3, tg) || !same_tiles(t2, tg);
+      }
+      if (split) {
+        rc = attention_layer(w, &s3, 1, B, p, lcnt + (size_t)B * kCntPerSide, st, pm, nullptr, t3);
+        if (rc == ONEPOSE_OK) rc = attention_layer(w, sd, 1, B, p, lcnt, st, pm, nullptr, t2);
+      } else {
+        rc = attention_layer(w, sd, 2, B, p, lcnt, st, pm, sh, tg);
+      }
+    }
     if (rc != ONEPOSE_OK) return rc;
     x2r = p.x2[c2 ^ 1];
     c2 ^= 1;
@@ -1516,9 +1560,10 @@ int object_prepare_impl(const void* packed_weights, const float* desc3d, const f
     OP_LAUNCH(K_GAT, st, gat_kernel<16>, ggrid, dim3(256), 0, st, p.x3[0], leaves_pm, (int64_t)0,
               gat_weights(wbase, 0), p.x3[1], n3, num_leaf, 1);
   const Side s3 = {p.x3[1], (int64_t)n3 * 256, cache, p.phiq3, p.kvpart3, p.kspart3, p.y13,
-                   p.stats3, n3, (float)n3, 0};
-  return attention_layer(ap_weights(wbase, 0), &s3, 1, 1, p, p.cnt, st,
-                         attention_pm(precision), nullptr);
+                   p.stats3, n3, (float)n3, 0, n3};
+  const int pm = attention_pm(precision);
+  return attention_layer(ap_weights(wbase, 0), &s3, 1, 1, p, p.cnt, st, pm, nullptr,
+                         layer_tiles(n3, &s3, 1, 1, pm, false));
 }
 
 int check_match_args(const void* packed_weights, const float* desc2d, const float* desc3d,

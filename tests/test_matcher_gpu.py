@@ -227,11 +227,15 @@ def test_bf16_attention_mode_tracks_fp32(n1, n3, device):
 
 @pytest.mark.parametrize("n1,n3,L,B,prec", [(200, 777, 8, 1, 0), (1024, 4096, 8, 2, 0),
                                              (128, 256, 12, 1, 0), (1024, 4096, 8, 1, 1),
-                                             (1024, 4096, 8, 1, 2)])
+                                             (1024, 4096, 8, 1, 2), (1024, 4096, 8, 4, 0),
+                                             (512, 2048, 8, 8, 0), (256, 1024, 8, 32, 0)])
 def test_object_cache_is_bit_identical(device, n1, n3, L, B, prec):
     """onepose_object_prepare + onepose_match_cached (GAT 0 and the 3D half of self-attention
     1 run once per object) vs onepose_match_prepared_ex on the same object: every output
-    bit-equal, for a ragged cloud, a batch sharing the object, the L=12 GAT and bf16 mode."""
+    bit-equal, for a ragged cloud, a batch sharing the object, the L=12 GAT and bf16 mode.
+    B = 4 / 8 / 32 reach the batch-dependent choices (layer_tiles: the 64x64 MLP-conv-2 tile,
+    kv_reduce + m_fold instead of kv_fold, the 64-row QKV tile at n3 = 1024), where the
+    uncached forward runs self-attention 1's halves with the prefix's / cached choices."""
     from onepose_amd import _lib
     lib = _lib.load()
     sd = synthetic.make_state_dict(0)
@@ -277,10 +281,13 @@ def test_object_cache_is_bit_identical(device, n1, n3, L, B, prec):
         assert (outs[1]["m0"] > -1).sum() > 100
 
 
-@pytest.mark.parametrize("n1,n3,L", [(1, 1, 1), (1, 7, 2), (3, 5, 8), (65, 1, 8), (33, 97, 16)])
+@pytest.mark.parametrize("n1,n3,L", [(1, 1, 1), (1, 7, 2), (3, 5, 8), (65, 1, 8), (33, 97, 16),
+                                      (1000, 3001, 8)])
 def test_matcher_tiny_and_odd_shapes(n1, n3, L, device):
     """Single-token sides (InstanceNorm over one row: variance 0), one partial chunk, tile
-    edges at 33 / 65 / 97 rows and L = 1 / 16: conf and indices vs the numpy oracle."""
+    edges at 33 / 65 / 97 rows and L = 1 / 16: conf and indices vs the numpy oracle.
+    1000 x 3001 takes the 64x128 QKV tile (47 x 6 = 282 >= 256 64-row tiles) with a partial
+    last KV chunk on both sides."""
     from oracle import matcher_np as M
     sd = synthetic.make_state_dict(9)
     data, _, _ = synthetic.make_matcher_inputs(n1, n3, L, seed=9)

@@ -2,7 +2,9 @@
 holding a contiguous shard of the object's 3D points, exchange the per-layer partials through
 the all-gather callback; every rank must end with the whole frame's matches, equal to the
 single-process GPU matcher on the unsplit frame (indices exactly except on low-margin rows,
-scores to 2e-5) -- and equal to each other bitwise."""
+scores to 2e-5) -- and equal to each other bitwise.  n3 = 5377 over 2 ranks gives shards of
+2689 / 2688 points, either side of the 64-row QKV tile's threshold (43 x 6 = 258 vs 252 tiles):
+every rank takes its tiles from the largest shard so the replicated 2D state rounds alike."""
 import os
 import socket
 
@@ -58,7 +60,7 @@ def _worker(rank, world, port, out_dir, n1, n3, seed, precision):
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("world,n1,n3", [(2, 256, 1024), (3, 200, 1023)])
+@pytest.mark.parametrize("world,n1,n3", [(2, 256, 1024), (3, 200, 1023), (2, 512, 5377)])
 def test_sharded_frame_equals_whole_frame(tmp_path, world, n1, n3):
     mp.start_processes(_worker, args=(world, _free_port(), str(tmp_path), n1, n3, 7, "fp32"),
                        nprocs=world, join=True, start_method="spawn")
