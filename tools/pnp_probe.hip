@@ -16,6 +16,8 @@ StampAcc* prof_stamp_slot(int) { return nullptr; }
 }
 int main(int argc, char** argv) {
   const int n = argc > 1 ? atoi(argv[1]) : 700;
+  const double outl = argc > 2 ? atof(argv[2]) : 0.0;   // fraction of gross outliers
+  std::uniform_real_distribution<float> U01(0.f, 1.f), UI(0.f, 512.f);
   std::mt19937 rng(3);
   std::uniform_real_distribution<float> U(-100.f, 100.f);
   std::normal_distribution<float> N(0.f, 0.5f);
@@ -28,6 +30,10 @@ int main(int argc, char** argv) {
     for (int r = 0; r < 3; ++r) X[r] = R[3 * r] * p3[3 * i] + R[3 * r + 1] * p3[3 * i + 1] + R[3 * r + 2] * p3[3 * i + 2] + t[r];
     p2[2 * i] = (float)(600 * X[0] / X[2] + 256) + N(rng);
     p2[2 * i + 1] = (float)(600 * X[1] / X[2] + 256) + N(rng);
+    if (U01(rng) < outl) {
+      p2[2 * i] = UI(rng);
+      p2[2 * i + 1] = UI(rng);
+    }
   }
   float *d2, *d3; double *dK, *pose; int *cnt, *nin, *st; uint8_t* mask; void* ws;
   hipMalloc(&d2, 8 * n); hipMalloc(&d3, 12 * n); hipMalloc(&dK, 72); hipMalloc(&pose, 96);
