@@ -173,6 +173,11 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=500)
     ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--settle-steps", type=int, default=60,
+                    help="at least this many steps of the timed schedule run back to back "
+                         "right before the timed region, the W warm-up steps last (the GPU "
+                         "reaches its loaded clock within ~40 ms of sustained work: a 20-step "
+                         "region after 5 warm-ups reads ~6%% below one after 50, DESIGN.md 4b)")
     ap.add_argument("--batch", type=int, default=1, help="frames per GPU per step")
     ap.add_argument("--n1", type=int, default=1024)
     ap.add_argument("--n3", type=int, default=4096)
@@ -323,9 +328,13 @@ def main():
     # can take tens of ms) stay out of the timed region
     D.gather_frames(result_rows(run_steps(max(2, len(pipe.slots)))), world * B)
     torch.cuda.synchronize()
-    # W warm-up steps of the timed schedule, immediately before the timed region: the GPU
-    # leaves its idle power state within them (after >= 20 ms idle a 20-step region reads
-    # ~8% slow for its first milliseconds, tools/short_probe.py)
+    # settle + W warm-up steps of the timed schedule, back to back and immediately before the
+    # timed region: the GPU leaves its idle power state within them (after >= 20 ms idle a
+    # 20-step region reads ~8% slow for its first milliseconds, tools/short_probe.py; after
+    # only 5 busy steps still ~6%, tools/gpu_s20.sh)
+    settle = max(0, args.settle_steps - args.warmup)
+    if settle > 0:   # untimed, same schedule: the GPU's clock / power state settles
+        run_steps(settle)
     if args.warmup > 0:
         run_steps(args.warmup)
     # the dominant kernel's launches are timed on the device (first workgroup start -> last
@@ -440,7 +449,7 @@ def main():
                   if cached else "; every layer run per frame")
         out = {
             "metric": METRIC, "value": round(value, 2), "unit": "frames/s", "n_gpus": world,
-            "steps": args.steps, "warmup": args.warmup,
+            "steps": args.steps, "warmup": args.warmup, "settle_steps": settle,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None,
             "dtype": "fp32" if args.precision == "fp32" else "bf16 attention GEMMs, fp32 rest",

@@ -1462,6 +1462,7 @@ __global__ __launch_bounds__(kThreads) void pnp_ransac_kernel(
     return;
   }
 
+  PNP_PHASE(8);
   while (!sh.done) {
     if (t == 0) {  // getSubset x 64, in iteration order
       unsigned long long s = sh.rng;
@@ -1481,6 +1482,7 @@ __global__ __launch_bounds__(kThreads) void pnp_ransac_kernel(
       sh.rng = s;
     }
     __syncthreads();
+    PNP_PHASE(9);
     if (wave == 0) {  // one EPnP model per lane
       double rvec[3], tvec[3];
       epnp5(sh.subset[lane], p2, p3, K4, rvec, tvec, sh.hh + lane, kRound);
@@ -1494,6 +1496,7 @@ __global__ __launch_bounds__(kThreads) void pnp_ransac_kernel(
       sh.count[lane] = 0;
     }
     __syncthreads();
+    PNP_PHASE(10);
     // inlier counts: wave w takes hypotheses w, w+4, ...; lanes sweep the points
     for (int h = wave; h < kRound; h += 4) {
       int c = 0;
@@ -1505,6 +1508,7 @@ __global__ __launch_bounds__(kThreads) void pnp_ransac_kernel(
       if (lane == 0) sh.count[h] = c;
     }
     __syncthreads();
+    PNP_PHASE(11);
     if (t == 0) {  // OpenCV's acceptance rule, in iteration order
       int iter = sh.iter, niters = sh.niters, best = sh.max_good;
       for (int h = 0; h < kRound && iter < niters; ++h, ++iter) {
@@ -1525,6 +1529,7 @@ __global__ __launch_bounds__(kThreads) void pnp_ransac_kernel(
     }
     __syncthreads();
   }
+  PNP_PHASE(12);
 
   int nin;
   if (n == kModelPoints) {
@@ -1567,6 +1572,7 @@ __global__ __launch_bounds__(kThreads) void pnp_ransac_kernel(
     n_inliers[b] = nin;
     status[b] = 0;
   }
+  PNP_PHASE(13);
 }
 
 // EPnP on the RANSAC inliers (solvePnPRansac's final solvePnP call), then

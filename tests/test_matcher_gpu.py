@@ -41,6 +41,23 @@ def check_indices(got, ref, margin, what):
     assert bad.sum() <= max(1, 0.002 * bad.size), f"{what}: {int(bad.sum())} low-margin flips"
 
 
+def check_scores(got, ref, conf0, own_top2, other_top2, rows, what):
+    """Matching scores within ATOL, except where the mutual check flipped (one side is 0) and
+    a top-1 - top-2 conf margin below MARGIN explains it: the row's (column's) own, so its
+    best index may differ, or that of its best index on the other axis, so the mutual pick
+    may.  There the fp32 summation order legitimately decides.  `conf0` is the [n1, n3]
+    conf; `own_top2` / `other_top2` the top-2 conf values of this / the other axis, [2, n]."""
+    bad = np.abs(got - ref) > ATOL
+    if not bad.any():
+        return
+    best = conf0.argmax(axis=1 if rows else 0)
+    low = ((other_top2[0] - other_top2[1])[best] < MARGIN) | (own_top2[0] - own_top2[1] < MARGIN)
+    unexplained = bad & ~(((got == 0) | (ref == 0)) & low)
+    assert not unexplained.any(), f"{what}: {int(unexplained.sum())} score mismatches at " \
+                                  f"{np.nonzero(unexplained)[0][:10]}"
+    assert bad.sum() <= max(1, 0.002 * bad.size), f"{what}: {int(bad.sum())} mutual flips"
+
+
 def margins(g):
     top = g["row_top2"][0]
     row_margin = np.minimum(top[:, 0] - top[:, 1], np.abs(g["matching_scores0"] - 0.2))
@@ -62,8 +79,11 @@ def test_matcher_matches_reference_fixture(name, precision, device):
     rm, cm = margins(g)
     check_indices(pred["matches0"], g["matches0"], rm, "matches0")
     check_indices(pred["matches1"], g["matches1"], cm, "matches1")
-    np.testing.assert_allclose(pred["matching_scores0"], g["matching_scores0"], atol=ATOL)
-    np.testing.assert_allclose(pred["matching_scores1"], g["matching_scores1"], atol=ATOL)
+    rt, ct = g["row_top2"][0].T, g["col_top2"][0]
+    check_scores(pred["matching_scores0"], g["matching_scores0"], conf[0], rt, ct, True,
+                 "matching_scores0")
+    check_scores(pred["matching_scores1"], g["matching_scores1"], conf[0], ct, rt, False,
+                 "matching_scores1")
     if "conf" in g:
         np.testing.assert_allclose(conf, g["conf"], atol=ATOL)
     np.testing.assert_allclose(conf.sum(axis=2), g["conf_row_sum"], rtol=1e-4, atol=1e-4)
@@ -298,4 +318,6 @@ def test_matcher_tiny_and_odd_shapes(n1, n3, L, device):
     top = -np.sort(-oconf[0], axis=1)[:, :2] if n3 > 1 else np.stack([oconf[0, :, 0], 0 * oconf[0, :, 0]], 1)
     rm = np.minimum(top[:, 0] - top[:, 1], np.abs(opred["matching_scores0"] - 0.2))
     check_indices(pred["matches0"], opred["matches0"], rm, "matches0")
-    np.testing.assert_allclose(pred["matching_scores0"], opred["matching_scores0"], atol=ATOL)
+    ctop = -np.sort(-oconf[0], axis=0)[:2] if n1 > 1 else np.stack([oconf[0][0], 0 * oconf[0][0]])
+    check_scores(pred["matching_scores0"], opred["matching_scores0"], conf[0], top.T, ctop, True,
+                 "matching_scores0")

@@ -52,6 +52,9 @@ int main(int argc, char** argv) {
     printf("n=%d inliers=%d ransac+refit %.1f us | refit phases (us): MtM %.1f  blocksum78 %.1f  eig+L %.1f  3x(betas,GN,R,err) %.1f  total %.1f\n",
            n, ni, ms * 1e3, (ph[1] - ph[0]) / 100.0, (ph[2] - ph[1]) / 100.0, (ph[3] - ph[2]) / 100.0,
            (ph[4] - ph[3]) / 100.0, (ph[5] - ph[0]) / 100.0);
+    printf("  ransac phases (us, last round): load %.1f  subsets %.1f  epnp5 x64 %.1f  count %.1f  accept %.1f  mask %.1f\n",
+           (ph[8] - 0) * 0.0, (ph[9] - ph[8]) / 100.0, (ph[10] - ph[9]) / 100.0, (ph[11] - ph[10]) / 100.0,
+           (ph[12] - ph[11]) / 100.0, (ph[13] - ph[12]) / 100.0);
   }
   return 0;
 }
