@@ -22,6 +22,28 @@ namespace {
 constexpr int kModelPoints = 5;
 constexpr int kRound = 64;
 constexpr int kThreads = 256;
+// cv::RNG (multiply-with-carry): state' = (state & 0xffffffff) * kMwcA + (state >> 32)
+constexpr unsigned long long kMwcA = 4164903690ull;
+constexpr unsigned long long kMwcM = kMwcA * 4294967296ull - 1ull;   // < 2^64
+constexpr int kRngPrefix = 8, kRngPos = kRngPrefix + 6 * 64;   // draws generated per round
+
+// A^(6 l) mod kMwcM, l = 0..63 (compile time)
+constexpr unsigned long long mwc_mulmod_c(unsigned long long a, unsigned long long b) {
+  return (unsigned long long)((unsigned __int128)a * b % kMwcM);
+}
+struct MwcJumps {
+  unsigned long long v[64];
+  constexpr MwcJumps() : v() {
+    unsigned long long a6 = 1ull;
+    for (int i = 0; i < 6; ++i) a6 = mwc_mulmod_c(a6, kMwcA);
+    unsigned long long x = 1ull;
+    for (int l = 0; l < 64; ++l) {
+      v[l] = x;
+      x = mwc_mulmod_c(x, a6);
+    }
+  }
+};
+__constant__ const MwcJumps kMwcJumps = MwcJumps();
 
 // ---------------------------------------------------------------------------------------
 // small dense linear algebra, double
@@ -677,12 +699,25 @@ __device__ __forceinline__ void rodrigues_v2m(const double* r, double* R) {
 }
 
 // ---------------------------------------------------------------------------------------
-// 5-point EPnP, one lane (RANSAC kernel): epnp::compute_pose with n = 5.  The points are
-// read from the workgroup's LDS copy through `sub` whenever needed (volatile reads), so they
-// do not occupy registers across the eigen-solve.
+// 5-point EPnP (RANSAC kernel): epnp::compute_pose with n = 5, one hypothesis per lane, in
+// two stages so that the workgroup's waves share the work:
+//   epnp5_eig     (wave 0, lane h)      control points, M^T M, its four smallest eigenvectors,
+//                                       handed over in LDS (HypState, lane h's column);
+//   epnp5_approx  (wave w = 1..3)       approximation `w` (betas, Gauss-Newton, R, t, mean
+//                                       reprojection error) for every hypothesis -- the three
+//                                       run concurrently instead of one after another;
+// then the smallest error picks the model, as compute_pose's sequential comparison does.
+// Each piece is the arithmetic of the one-lane version, so the models are the same.  The
+// points are read from the workgroup's LDS copy through `sub` whenever needed (volatile
+// reads), so they do not occupy registers across the eigen-solve.
 // ---------------------------------------------------------------------------------------
-__device__ __forceinline__ void epnp5(const volatile int* sub, const volatile float* p2, const volatile float* p3,
-                      const double* K4, double* rvec, double* tvec, double* hh, int hs) {
+// Per-hypothesis state between the stages, SoA rows of kRound doubles (element h = lane h):
+// it overlays eig12_small4's per-lane Householder scratch (Shared::hh), dead by then.
+constexpr int kHsVs = 0, kHsRho = 48, kHsCw0 = 54, kHsCi = 57, kHsRows = 66;
+
+__device__ __forceinline__ void epnp5_eig(const volatile int* sub, const volatile float* p2,
+                                          const volatile float* p3, const double* K4, double* hh,
+                                          int hs) {
   constexpr int n = kModelPoints;
   const double fu = K4[0], fv = K4[1], uc = K4[2], vc = K4[3];
   auto PW = [&](int i, int j) { return (double)p3[3 * sub[i] + j]; };
@@ -754,77 +789,94 @@ __device__ __forceinline__ void epnp5(const volatile int* sub, const volatile fl
   }
   double ev4[4][12];
   eig12_small4<28>(mtm, ev4, hh, hs);
-  const double* ut = &ev4[0][0];
+  // hand over (the Householder scratch is dead: eig12_small4 has back-transformed)
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int k = 0; k < 12; ++k) hh[(kHsVs + 12 * i + k) * hs] = ev4[i][k];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) hh[(kHsRho + i) * hs] = rho[i];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) hh[(kHsCw0 + i) * hs] = cw0[i];
+#pragma unroll
+  for (int i = 0; i < 9; ++i) hh[(kHsCi + i) * hs] = ci[i];
+}
+
+// Approximation `which` (1..3) of compute_pose for the hypothesis whose state is at hh
+// (stride hs): R, t and the mean reprojection error over its five points.
+__device__ __forceinline__ void epnp5_approx(int which, const volatile int* sub,
+                                             const volatile float* p2, const volatile float* p3,
+                                             const double* K4, const double* hh, int hs,
+                                             double* R, double* t, double* err_out) {
+  constexpr int n = kModelPoints;
+  const double fu = K4[0], fv = K4[1], uc = K4[2], vc = K4[3];
+  auto PW = [&](int i, int j) { return (double)p3[3 * sub[i] + j]; };
+  auto US = [&](int i, int j) { return (double)p2[2 * sub[i] + j]; };
+  double ut[48], rho[6], cw0[3], ci[9];
+#pragma unroll
+  for (int i = 0; i < 48; ++i) ut[i] = hh[(kHsVs + i) * hs];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) rho[i] = hh[(kHsRho + i) * hs];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) cw0[i] = hh[(kHsCw0 + i) * hs];
+#pragma unroll
+  for (int i = 0; i < 9; ++i) ci[i] = hh[(kHsCi + i) * hs];
   double L[60];
   compute_L_6x10(ut, L);
-  double bestR[9], bestT[3], bestErr = 0.0;
-  for (int which = 1; which <= 3; ++which) {
-    double betas[4], ccs[4][3], pcs[n * 3];
-    betas_approx(which, L, rho, betas);
-    gauss_newton(L, rho, betas);
-    ccs_from_betas(ut, betas, ccs);
+  double betas[4], ccs[4][3], pcs[n * 3];
+  betas_approx(which, L, rho, betas);
+  gauss_newton(L, rho, betas);
+  ccs_from_betas(ut, betas, ccs);
 #pragma unroll
-    for (int i = 0; i < n; ++i) {
-      double a[4];
+  for (int i = 0; i < n; ++i) {
+    double a[4];
 #pragma unroll
-      for (int j = 0; j < 3; ++j)
-        a[1 + j] = ci[3 * j] * (PW(i, 0) - cw0[0]) + ci[3 * j + 1] * (PW(i, 1) - cw0[1]) +
-                   ci[3 * j + 2] * (PW(i, 2) - cw0[2]);
-      a[0] = 1.0 - a[1] - a[2] - a[3];
+    for (int j = 0; j < 3; ++j)
+      a[1 + j] = ci[3 * j] * (PW(i, 0) - cw0[0]) + ci[3 * j + 1] * (PW(i, 1) - cw0[1]) +
+                 ci[3 * j + 2] * (PW(i, 2) - cw0[2]);
+    a[0] = 1.0 - a[1] - a[2] - a[3];
 #pragma unroll
-      for (int j = 0; j < 3; ++j)
-        pcs[3 * i + j] = a[0] * ccs[0][j] + a[1] * ccs[1][j] + a[2] * ccs[2][j] + a[3] * ccs[3][j];
-    }
-    if (pcs[2] < 0.0) {
+    for (int j = 0; j < 3; ++j)
+      pcs[3 * i + j] = a[0] * ccs[0][j] + a[1] * ccs[1][j] + a[2] * ccs[2][j] + a[3] * ccs[3][j];
+  }
+  if (pcs[2] < 0.0) {
 #pragma unroll
-      for (int i = 0; i < 3 * n; ++i) pcs[i] = -pcs[i];
-    }
-    double pc0[3] = {0, 0, 0}, pw0[3] = {0, 0, 0};
+    for (int i = 0; i < 3 * n; ++i) pcs[i] = -pcs[i];
+  }
+  double pc0[3] = {0, 0, 0}, pw0[3] = {0, 0, 0};
 #pragma unroll
-    for (int i = 0; i < n; ++i)
-#pragma unroll
-      for (int j = 0; j < 3; ++j) {
-        pc0[j] += pcs[3 * i + j];
-        pw0[j] += PW(i, j);
-      }
+  for (int i = 0; i < n; ++i)
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
-      pc0[j] /= n;
-      pw0[j] /= n;
+      pc0[j] += pcs[3 * i + j];
+      pw0[j] += PW(i, j);
     }
-    double abt[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll
-    for (int i = 0; i < n; ++i)
-#pragma unroll
-      for (int j = 0; j < 3; ++j)
-#pragma unroll
-        for (int k = 0; k < 3; ++k) abt[3 * j + k] += (pcs[3 * i + j] - pc0[j]) * (PW(i, k) - pw0[k]);
-    double R[9], t[3];
-    finish_R(abt, R);
-#pragma unroll
-    for (int j = 0; j < 3; ++j) t[j] = pc0[j] - dot3(R + 3 * j, pw0);
-    double err = 0.0;
-#pragma unroll
-    for (int i = 0; i < n; ++i) {
-      const double pw[3] = {PW(i, 0), PW(i, 1), PW(i, 2)};
-      const double Xc = dot3(R, pw) + t[0], Yc = dot3(R + 3, pw) + t[1];
-      const double iz = 1.0 / (dot3(R + 6, pw) + t[2]);
-      const double ue = uc + fu * Xc * iz, ve = vc + fv * Yc * iz;
-      const double du = US(i, 0) - ue, dv = US(i, 1) - ve;
-      err += sqrt(du * du + dv * dv);
-    }
-    err /= n;
-    if (which == 1 || err < bestErr) {
-      bestErr = err;
-#pragma unroll
-      for (int i = 0; i < 9; ++i) bestR[i] = R[i];
-#pragma unroll
-      for (int i = 0; i < 3; ++i) bestT[i] = t[i];
-    }
+  for (int j = 0; j < 3; ++j) {
+    pc0[j] /= n;
+    pw0[j] /= n;
   }
-  rodrigues_m2v(bestR, rvec);
+  double abt[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll
-  for (int i = 0; i < 3; ++i) tvec[i] = bestT[i];
+  for (int i = 0; i < n; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+#pragma unroll
+      for (int k = 0; k < 3; ++k) abt[3 * j + k] += (pcs[3 * i + j] - pc0[j]) * (PW(i, k) - pw0[k]);
+  finish_R(abt, R);
+#pragma unroll
+  for (int j = 0; j < 3; ++j) t[j] = pc0[j] - dot3(R + 3 * j, pw0);
+  double err = 0.0;
+#pragma unroll
+  for (int i = 0; i < n; ++i) {
+    const double pw[3] = {PW(i, 0), PW(i, 1), PW(i, 2)};
+    const double Xc = dot3(R, pw) + t[0], Yc = dot3(R + 3, pw) + t[1];
+    const double iz = 1.0 / (dot3(R + 6, pw) + t[2]);
+    const double ue = uc + fu * Xc * iz, ve = vc + fv * Yc * iz;
+    const double du = US(i, 0) - ue, dv = US(i, 1) - ve;
+    err += sqrt(du * du + dv * dv);
+  }
+  *err_out = err / n;
 }
 
 // RANSACUpdateNumIters (ptsetreg.cpp)
@@ -879,13 +931,21 @@ __device__ __forceinline__ void block_sum(double* vals, double* scratch /* [4][C
 }
 
 struct Shared {
-  double hh[65 * kRound];   // per-lane Householder scratch of eig12_small4
+  double hh[kHsRows * kRound];   // per-lane Householder scratch of eig12_small4 (65 rows),
+                                 // then the hypotheses' HypState rows (epnp5_eig -> epnp5_approx)
+  double herr[4][kRound];         // mean reprojection error of approximation w (1..3)
   // RANSAC round
   int subset[kRound][kModelPoints];
   double hypR[kRound][9];
   double hypT[kRound][3];
   double hypRvec[kRound][3];
   int count[kRound];
+  // RNG positions of a round, generated in parallel: state after each draw, draw % n
+  unsigned long long rst[kRngPos];
+  int rii[kRngPos];
+  short rend[kRngPos], rstart[kRound];
+  unsigned long long rz;
+  int rk, rP, rdealt, rpos;
   // control
   int iter, niters, max_good, done, p3p;
   double bestRvec[3], bestT[3];
@@ -900,34 +960,35 @@ struct Shared {
   double ccs[4][3];
   double sol_R[4][9], sol_t[4][3], sol_err[4];
   double flip;
+  double wccs[3][4][3], wflip[3];   // per approximation wave (refit, n >= 6)
+  double S40[40];                    // M^T M's distinct sums (refit, n >= 6)
+  int ord[4];
   int wave_cnt[4];
   int n_inl;
   // refit eigensolver (jacobi12_block)
-  double jA[144], jV[144], jc[6], js[6], jscale;
+  double jA[144], jV[144], jc[6], js[6];
   int jp[6], jq[6], jrot[12];
 };
 
-// Eigenvectors of the four smallest eigenvalues of the symmetric 12x12 M^T M (packed lower
-// triangle `acc`, identical on every thread), ascending -> ev4 (thread 0), for the EPnP
-// refit.  Cyclic Jacobi in parallel rounds: the circle method pairs the 12 indices into 6
-// disjoint (p, q) per round, 11 rounds per sweep; a round computes the 6 rotations, then
-// applies them to A's columns and V's columns, then to A's rows.  Workgroup-collective (every
-// thread calls it); ~15 us against ~160 us for one thread's eig12_small4.  EPnP's result does
-// not depend on the eigenvectors' signs, and any accurate eigensolver gives the oracle's
-// vectors up to sign when the eigenvalues are separated.
-__device__ void jacobi12_block(Shared& sh, const double* acc, double (&ev4)[4][12]) {
+// Eigenvectors of the four smallest eigenvalues of the symmetric 12x12 M^T M (in sh.jA),
+// ascending -> sh.vs (48 doubles), for the EPnP refit.  Cyclic Jacobi in parallel rounds:
+// the circle method pairs the 12 indices into 6 disjoint (p, q) per round, 11 rounds per
+// sweep; a round computes the 6 rotations, then applies them to A's columns and V's columns,
+// then to A's rows.  Workgroup-collective (every thread calls it).  EPnP's result does not
+// depend on the eigenvectors' signs, and any accurate eigensolver gives the oracle's vectors
+// up to sign when the eigenvalues are separated.  (A one-barrier variant -- each thread
+// computing its A' = J^T A J entry from the previous A, six threads the next round's
+// rotations from the entries they need -- measured 2.3x slower: the rotation chain grew.)
+__device__ void jacobi12_block(Shared& sh) {
   const int t = threadIdx.x;
   for (int i = t; i < 144; i += kThreads) {
     const int r = i / 12, c = i - r * 12;
-    sh.jA[i] = r >= c ? acc[LI(r, c)] : acc[LI(c, r)];
     sh.jV[i] = r == c ? 1.0 : 0.0;
   }
   if (t < 12) sh.jrot[t] = 0;
-  if (t == 0) {   // trace: the scale of "converged" off-diagonals (M^T M is PSD)
-    double tr = 0.0;
-    for (int i = 0; i < 12; ++i) tr += fabs(acc[LI(i, i)]);
-    sh.jscale = tr;
-  }
+  double tr = 0.0;   // trace: the scale of "converged" off-diagonals (M^T M is PSD)
+  for (int i = 0; i < 12; ++i) tr += fabs(sh.jA[i * 13]);
+  const double thr = 1e-22 * tr;
   __syncthreads();
   for (int sweep = 0; sweep < 12; ++sweep) {
     for (int round = 0; round < 11; ++round) {
@@ -941,7 +1002,7 @@ __device__ void jacobi12_block(Shared& sh, const double* acc, double (&ev4)[4][1
         }
         const double apq = sh.jA[p * 12 + q];
         double c = 1.0, sn = 0.0;
-        if (fabs(apq) > 1e-22 * sh.jscale) sh.jrot[sweep] = 1;   // not yet converged
+        if (fabs(apq) > thr) sh.jrot[sweep] = 1;   // not yet converged
         if (apq != 0.0) {
           const double theta = (sh.jA[q * 12 + q] - sh.jA[p * 12 + p]) / (2.0 * apq);
           const double tt = (theta >= 0.0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
@@ -976,19 +1037,22 @@ __device__ void jacobi12_block(Shared& sh, const double* acc, double (&ev4)[4][1
     }
     if (!sh.jrot[sweep]) break;   // a sweep without a rotation: converged (uniform)
   }
+  const double* A = sh.jA;
+  const double* V = sh.jV;
   if (t == 0) {   // the four smallest eigenvalues, ascending (ties by index)
     int order[12];
     for (int i = 0; i < 12; ++i) order[i] = i;
     for (int i = 0; i < 4; ++i)
       for (int j = i + 1; j < 12; ++j)
-        if (sh.jA[order[j] * 13] < sh.jA[order[i] * 13]) {
+        if (A[order[j] * 13] < A[order[i] * 13]) {
           const int x = order[i];
           order[i] = order[j];
           order[j] = x;
         }
-    for (int i = 0; i < 4; ++i)
-      for (int k = 0; k < 12; ++k) ev4[i][k] = sh.jV[k * 12 + order[i]];
+    for (int i = 0; i < 4; ++i) sh.ord[i] = order[i];
   }
+  __syncthreads();
+  if (t < 48) sh.vs[t] = V[(t % 12) * 12 + sh.ord[t / 12]];
 }
 
 // Canonical basis of the 4-dimensional EPnP null space of exactly 4 correspondences (M is
@@ -1123,87 +1187,174 @@ __device__ __forceinline__ void epnp_refit(Shared& sh, const float* p2, const fl
     for (int k = 0; k < 3; ++k) a[1 + k] = sh.ci[3 * k] * d0 + sh.ci[3 * k + 1] * d1 + sh.ci[3 * k + 2] * d2;
     a[0] = 1.0 - a[1] - a[2] - a[3];
   };
-  // M^T M (upper triangle, 78 entries)
-  double acc[78];
+  const int lane = t & 63, wave = t >> 6;
+  if (n >= 6) {
+    // M^T M from its 40 distinct sums: with r1 = [a_k fu, 0, a_k (uc - u)] and
+    // r2 = [0, a_k fv, a_k (vc - v)], entry (3k+i, 3l+j) is G_ij summed with a_k a_l:
+    //   (0,0) fu^2 S,  (1,1) fv^2 S,  (0,2) fu Su,  (1,2) fv Sv,  (2,2) Sw,  (0,1) 0,
+    // S / Su / Sv / Sw = sum a_k a_l x {1, uc - u, vc - v, (uc - u)^2 + (vc - v)^2}, k <= l.
+    // Wave 0 accumulates (lane = point stride), then a transposed reduction through LDS.
+    if (wave == 0) {
+      double S[40];
 #pragma unroll
-  for (int i = 0; i < 78; ++i) acc[i] = 0.0;
-  for (int i = t; i < n; i += kThreads) {
-    const int j = idx[i];
-    double as[4];
-    alphas(j, as);
-    const double u = (double)p2[2 * j], v = (double)p2[2 * j + 1];
-    double r1[12], r2[12];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      r1[3 * k] = as[k] * fu;
-      r1[3 * k + 1] = 0.0;
-      r1[3 * k + 2] = as[k] * (uc - u);
-      r2[3 * k] = 0.0;
-      r2[3 * k + 1] = as[k] * fv;
-      r2[3 * k + 2] = as[k] * (vc - v);
-    }
-#pragma unroll
-    for (int a = 0; a < 12; ++a)
-#pragma unroll
-      for (int b = 0; b <= a; ++b) acc[LI(a, b)] += r1[a] * r1[b] + r2[a] * r2[b];
-  }
-  PNP_PHASE(1);
-  block_sum<78>(acc, sh.red);
-  PNP_PHASE(2);
-  // n >= 6: parallel Jacobi.  n = 5 (M 10 x 12: a 2-dimensional null space whose basis the
-  // refit's result depends on, as OpenCV's does on its SVD) keeps the per-lane solver the
-  // RANSAC hypotheses use; n = 4 takes null4_basis.
-  double ev4[4][12];
-  if (n >= 6) jacobi12_block(sh, acc, ev4);   // workgroup-collective; thread 0 holds ev4
-  if (t == 0) {
-    if (n == 4) {   // canonical null-space basis (null4_basis), no eigensolver
-      double M[8][12];
-      for (int i = 0; i < 4; ++i) {
+      for (int e = 0; e < 40; ++e) S[e] = 0.0;
+      for (int i = lane; i < n; i += 64) {
+        const int j = idx[i];
         double as[4];
-        alphas(idx[i], as);
-        const double u = (double)p2[2 * idx[i]], v = (double)p2[2 * idx[i] + 1];
-        for (int k = 0; k < 4; ++k) {
-          M[2 * i][3 * k] = as[k] * fu;
-          M[2 * i][3 * k + 1] = 0.0;
-          M[2 * i][3 * k + 2] = as[k] * (uc - u);
-          M[2 * i + 1][3 * k] = 0.0;
-          M[2 * i + 1][3 * k + 1] = as[k] * fv;
-          M[2 * i + 1][3 * k + 2] = as[k] * (vc - v);
-        }
+        alphas(j, as);
+        const double du = uc - (double)p2[2 * j], dv = vc - (double)p2[2 * j + 1];
+        const double dw = du * du + dv * dv;
+        int q = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+#pragma unroll
+          for (int l = k; l < 4; ++l, ++q) {
+            const double aa = as[k] * as[l];
+            S[4 * q] += aa;
+            S[4 * q + 1] += aa * du;
+            S[4 * q + 2] += aa * dv;
+            S[4 * q + 3] += aa * dw;
+          }
       }
-      null4_basis(M, ev4);
-    } else if (n == 5) {
-      eig12_small4<100>(acc, ev4, sh.hh, 1);
+      double* red = sh.hh;   // [40][64], free in this kernel
+#pragma unroll
+      for (int e = 0; e < 40; ++e) red[e * 64 + lane] = S[e];
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      if (lane < 40) {
+        double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+        for (int l = 0; l < 64; l += 4) {
+          a0 += red[lane * 64 + l];
+          a1 += red[lane * 64 + l + 1];
+          a2 += red[lane * 64 + l + 2];
+          a3 += red[lane * 64 + l + 3];
+        }
+        sh.S40[lane] = (a0 + a1) + (a2 + a3);
+      }
     }
-    for (int i = 0; i < 48; ++i) sh.vs[i] = (&ev4[0][0])[i];
-    compute_L_6x10(sh.vs, sh.L);
-    compute_rho(sh.cws, sh.rho);
+    __syncthreads();
+    PNP_PHASE(1);
+    for (int i = t; i < 144; i += kThreads) {
+      const int r = i / 12, c = i - r * 12;
+      const int k = r / 3, ii = r - 3 * k, l = c / 3, jj = c - 3 * l;
+      const int lo = k < l ? k : l, hi = k < l ? l : k;
+      const int q = lo * 4 - lo * (lo - 1) / 2 + (hi - lo);   // pair index of (lo, hi), k <= l
+      const int a = ii < jj ? ii : jj, b = ii < jj ? jj : ii;
+      const double* Sq = sh.S40 + 4 * q;
+      double v = 0.0;
+      if (a == 0 && b == 0) v = fu * fu * Sq[0];
+      else if (a == 1 && b == 1) v = fv * fv * Sq[0];
+      else if (a == 0 && b == 2) v = fu * Sq[1];
+      else if (a == 1 && b == 2) v = fv * Sq[2];
+      else if (a == 2 && b == 2) v = Sq[3];
+      sh.jA[i] = v;
+    }
+    __syncthreads();
+    PNP_PHASE(2);
+    jacobi12_block(sh);   // workgroup-collective -> sh.vs
+    __syncthreads();
+    if (t < 60) {   // compute_L_6x10, one entry per thread
+      constexpr int pa[6] = {0, 0, 0, 1, 1, 2}, pb[6] = {1, 2, 3, 2, 3, 3};
+      constexpr int cp[10] = {0, 0, 1, 0, 1, 2, 0, 1, 2, 3}, cq[10] = {0, 1, 1, 2, 2, 2, 3, 3, 3, 3};
+      const int i = t / 10, c = t - 10 * i;
+      const double* vp = sh.vs + 12 * cp[c];
+      const double* vq = sh.vs + 12 * cq[c];
+      double dp[3], dq[3];
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        dp[k] = vp[3 * pa[i] + k] - vp[3 * pb[i] + k];
+        dq[k] = vq[3 * pa[i] + k] - vq[3 * pb[i] + k];
+      }
+      const double d = dot3(dp, dq);
+      sh.L[t] = cp[c] == cq[c] ? d : 2.0 * d;
+    } else if (t == 64) {
+      compute_rho(sh.cws, sh.rho);
+    }
+  } else {
+    // n = 4 / 5: M^T M per thread, summed over the workgroup (the arithmetic the oracle's
+    // test scenes pin for these rank-deficient cases), then thread 0's basis
+    double acc[78];
+#pragma unroll
+    for (int i = 0; i < 78; ++i) acc[i] = 0.0;
+    for (int i = t; i < n; i += kThreads) {
+      const int j = idx[i];
+      double as[4];
+      alphas(j, as);
+      const double u = (double)p2[2 * j], v = (double)p2[2 * j + 1];
+      double r1[12], r2[12];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        r1[3 * k] = as[k] * fu;
+        r1[3 * k + 1] = 0.0;
+        r1[3 * k + 2] = as[k] * (uc - u);
+        r2[3 * k] = 0.0;
+        r2[3 * k + 1] = as[k] * fv;
+        r2[3 * k + 2] = as[k] * (vc - v);
+      }
+#pragma unroll
+      for (int a = 0; a < 12; ++a)
+#pragma unroll
+        for (int b = 0; b <= a; ++b) acc[LI(a, b)] += r1[a] * r1[b] + r2[a] * r2[b];
+    }
+    block_sum<78>(acc, sh.red);
+    if (t == 0) {
+      double ev4[4][12];
+      if (n == 4) {   // canonical null-space basis (null4_basis), no eigensolver
+        double M[8][12];
+        for (int i = 0; i < 4; ++i) {
+          double as[4];
+          alphas(idx[i], as);
+          const double u = (double)p2[2 * idx[i]], v = (double)p2[2 * idx[i] + 1];
+          for (int k = 0; k < 4; ++k) {
+            M[2 * i][3 * k] = as[k] * fu;
+            M[2 * i][3 * k + 1] = 0.0;
+            M[2 * i][3 * k + 2] = as[k] * (uc - u);
+            M[2 * i + 1][3 * k] = 0.0;
+            M[2 * i + 1][3 * k + 1] = as[k] * fv;
+            M[2 * i + 1][3 * k + 2] = as[k] * (vc - v);
+          }
+        }
+        null4_basis(M, ev4);
+      } else {
+        eig12_small4<100>(acc, ev4, sh.hh, 1);
+      }
+      for (int i = 0; i < 48; ++i) sh.vs[i] = (&ev4[0][0])[i];
+      compute_L_6x10(sh.vs, sh.L);
+      compute_rho(sh.cws, sh.rho);
+    }
   }
   __syncthreads();
   PNP_PHASE(3);
-  for (int which = 1; which <= 3; ++which) {
-    if (t == 0) {
+  // compute_pose's three approximations, one per wave (waves 0..2), each reducing over the
+  // points with wave-level sums; wave 3 waits
+  if (wave < 3) {
+    const int which = wave + 1;
+    double(*ccs)[3] = sh.wccs[wave];
+    if (lane == 0) {
       double betas[4];
       betas_approx(which, sh.L, sh.rho, betas);
       gauss_newton(sh.L, sh.rho, betas);
-      ccs_from_betas(sh.vs, betas, sh.ccs);
+      ccs_from_betas(sh.vs, betas, ccs);
       // solve_for_sign looks at the first point's camera-frame depth
       double a[4];
       alphas(idx[0], a);
-      const double z0 = a[0] * sh.ccs[0][2] + a[1] * sh.ccs[1][2] + a[2] * sh.ccs[2][2] + a[3] * sh.ccs[3][2];
-      sh.flip = z0 < 0.0 ? -1.0 : 1.0;
+      const double z0 = a[0] * ccs[0][2] + a[1] * ccs[1][2] + a[2] * ccs[2][2] + a[3] * ccs[3][2];
+      sh.wflip[wave] = z0 < 0.0 ? -1.0 : 1.0;
     }
-    __syncthreads();
-    const double fl = sh.flip;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const double fl = sh.wflip[wave];
     auto pc_of = [&](int j, double* pc) {
       double a[4];
       alphas(j, a);
 #pragma unroll
       for (int k = 0; k < 3; ++k)
-        pc[k] = fl * (a[0] * sh.ccs[0][k] + a[1] * sh.ccs[1][k] + a[2] * sh.ccs[2][k] + a[3] * sh.ccs[3][k]);
+        pc[k] = fl * (a[0] * ccs[0][k] + a[1] * ccs[1][k] + a[2] * ccs[2][k] + a[3] * ccs[3][k]);
     };
     double s6[6] = {0, 0, 0, 0, 0, 0};
-    for (int i = t; i < n; i += kThreads) {
+    for (int i = lane; i < n; i += 64) {
       const int j = idx[i];
       double pc[3];
       pc_of(j, pc);
@@ -1214,10 +1365,11 @@ __device__ __forceinline__ void epnp_refit(Shared& sh, const float* p2, const fl
       s6[4] += (double)p3[3 * j + 1];
       s6[5] += (double)p3[3 * j + 2];
     }
-    block_sum<6>(s6, sh.red);
+#pragma unroll
+    for (int k = 0; k < 6; ++k) s6[k] = wave_sum_d(s6[k]);
     const double pc0[3] = {s6[0] / n, s6[1] / n, s6[2] / n}, pw0[3] = {s6[3] / n, s6[4] / n, s6[5] / n};
     double abt[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-    for (int i = t; i < n; i += kThreads) {
+    for (int i = lane; i < n; i += 64) {
       const int j = idx[i];
       double pc[3];
       pc_of(j, pc);
@@ -1228,31 +1380,30 @@ __device__ __forceinline__ void epnp_refit(Shared& sh, const float* p2, const fl
 #pragma unroll
         for (int b = 0; b < 3; ++b) abt[3 * a + b] += (pc[a] - pc0[a]) * pw[b];
     }
-    block_sum<9>(abt, sh.red);
-    if (t == 0) {
-      double* R = sh.sol_R[which];
-      finish_R(abt, R);
-      for (int j = 0; j < 3; ++j) sh.sol_t[which][j] = pc0[j] - dot3(R + 3 * j, pw0);
+#pragma unroll
+    for (int k = 0; k < 9; ++k) abt[k] = wave_sum_d(abt[k]);
+    double R[9], tt[3];
+    finish_R(abt, R);   // every lane (identical inputs): no hand-over needed
+#pragma unroll
+    for (int j = 0; j < 3; ++j) tt[j] = pc0[j] - dot3(R + 3 * j, pw0);
+    double err = 0.0;
+    for (int i = lane; i < n; i += 64) {
+      const int j = idx[i];
+      const double pw[3] = {(double)p3[3 * j], (double)p3[3 * j + 1], (double)p3[3 * j + 2]};
+      const double Xc = dot3(R, pw) + tt[0], Yc = dot3(R + 3, pw) + tt[1];
+      const double iz = 1.0 / (dot3(R + 6, pw) + tt[2]);
+      const double ue = uc + fu * Xc * iz, ve = vc + fv * Yc * iz;
+      const double du = (double)p2[2 * j] - ue, dv = (double)p2[2 * j + 1] - ve;
+      err += sqrt(du * du + dv * dv);
     }
-    __syncthreads();
-    double err[1] = {0.0};
-    {
-      const double* R = sh.sol_R[which];
-      const double* tt = sh.sol_t[which];
-      for (int i = t; i < n; i += kThreads) {
-        const int j = idx[i];
-        const double pw[3] = {(double)p3[3 * j], (double)p3[3 * j + 1], (double)p3[3 * j + 2]};
-        const double Xc = dot3(R, pw) + tt[0], Yc = dot3(R + 3, pw) + tt[1];
-        const double iz = 1.0 / (dot3(R + 6, pw) + tt[2]);
-        const double ue = uc + fu * Xc * iz, ve = vc + fv * Yc * iz;
-        const double du = (double)p2[2 * j] - ue, dv = (double)p2[2 * j + 1] - ve;
-        err[0] += sqrt(du * du + dv * dv);
-      }
+    err = wave_sum_d(err);
+    if (lane == 0) {
+      for (int k = 0; k < 9; ++k) sh.sol_R[which][k] = R[k];
+      for (int k = 0; k < 3; ++k) sh.sol_t[which][k] = tt[k];
+      sh.sol_err[which] = err / n;
     }
-    block_sum<1>(err, sh.red);
-    if (t == 0) sh.sol_err[which] = err[0] / n;
-    __syncthreads();
   }
+  __syncthreads();
   PNP_PHASE(4);
   int N = 1;
   if (sh.sol_err[2] < sh.sol_err[1]) N = 2;
@@ -1398,6 +1549,22 @@ __device__ __forceinline__ unsigned rng_next(unsigned long long& s) {
   return (unsigned)s;
 }
 
+// cv::RNG is a lag-1 multiply-with-carry generator: for a state z = c * 2^32 + x below
+// m = A * 2^32 - 1, the next state A x + c equals A z mod m (A 2^32 = 1 mod m), so the state
+// k draws ahead is A^k z mod m -- lane l of a wave starts its 6 draws at A^(6 l) z.
+__device__ __forceinline__ unsigned long long mwc_mulmod(unsigned long long a,
+                                                         unsigned long long b) {
+  // a b mod m for a, b < m: fold the high word with 2^64 = r (mod m), r = (2^32 - A) 2^32 + 1
+  constexpr unsigned long long r = ((4294967296ull - kMwcA) << 32) | 1ull;
+  unsigned long long lo = a * b, hi = __umul64hi(a, b);
+  while (hi != 0ull) {
+    const unsigned long long l2 = hi * r, h2 = __umul64hi(hi, r);
+    lo += l2;
+    hi = h2 + (lo < l2 ? 1ull : 0ull);
+  }
+  return lo >= kMwcM ? lo - kMwcM : lo;
+}
+
 __global__ __launch_bounds__(kThreads) void pnp_ransac_kernel(
     const float* __restrict__ pts2d, const float* __restrict__ pts3d, const int* __restrict__ counts,
     int max_points, const double* __restrict__ Kmat, int64_t K_bs, double scale, float reproj,
@@ -1464,70 +1631,174 @@ __global__ __launch_bounds__(kThreads) void pnp_ransac_kernel(
 
   PNP_PHASE(8);
   while (!sh.done) {
-    if (t == 0) {  // getSubset x 64, in iteration order
-      unsigned long long s = sh.rng;
-      for (int h = 0; h < kRound; ++h) {
-        for (int i = 0; i < kModelPoints;) {
-          int ii, j;
-          for (;;) {
-            ii = (int)(rng_next(s) % (unsigned)n);
-            for (j = 0; j < i; ++j)
-              if (ii == sh.subset[h][j]) break;
-            if (j == i) break;
-          }
-          sh.subset[h][i] = ii;
-          ++i;
+    // getSubset x 64, in iteration order.  The round's draws are generated in parallel by
+    // jump-ahead (see mwc_mulmod; states at or above m -- the first draws from
+    // RNG((uint64)-1) -- are stepped by lane 0 first).  A subset takes draws until it has 5
+    // distinct indices, so the subset starting at draw s ends at a draw e(s) that depends on
+    // the draws alone: every thread evaluates e(s) for its positions, thread 0 chains
+    // s_{h+1} = e(s_h), and lane h deals subset h from s_h.  A chain that runs past the
+    // generated draws continues sequentially (rng_next) from that subset on.
+    if (wave == 0) {
+      if (lane == 0) {
+        unsigned long long z = sh.rng;
+        int k = 0;
+        while (z >= kMwcM && k < kRngPrefix) {
+          const unsigned v = rng_next(z);
+          sh.rst[k] = z;
+          sh.rii[k] = (int)(v % (unsigned)n);
+          ++k;
+        }
+        sh.rk = k;
+        sh.rz = z;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      const int k = sh.rk;
+      const unsigned long long z0 = sh.rz;
+      if (z0 < kMwcM) {
+        unsigned long long z = mwc_mulmod(z0, kMwcJumps.v[lane]);
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+          const unsigned v = rng_next(z);
+          sh.rst[k + 6 * lane + i] = z;
+          sh.rii[k + 6 * lane + i] = (int)(v % (unsigned)n);
         }
       }
-      sh.rng = s;
+      if (lane == 0) sh.rP = z0 < kMwcM ? k + 6 * 64 : k;
+    }
+    __syncthreads();
+    {
+      const int P = sh.rP;
+      // the 5 distinct draws from position s: their positions' end (one past the 5th) or -1
+      auto deal = [&](int s0, int* out) __attribute__((always_inline)) {
+        int c0 = -1, c1 = -1, c2 = -1, c3 = -1, got = 0, q = s0;
+        while (got < kModelPoints && q < P) {
+          const int v = sh.rii[q++];
+          if (v == c0 || v == c1 || v == c2 || v == c3) continue;
+          if (out) out[got] = v;
+          if (got == 0) c0 = v;
+          else if (got == 1) c1 = v;
+          else if (got == 2) c2 = v;
+          else if (got == 3) c3 = v;
+          ++got;
+        }
+        return got == kModelPoints ? q : -1;
+      };
+      for (int q = t; q < P; q += kThreads) sh.rend[q] = (short)deal(q, nullptr);
+      __syncthreads();
+      if (t == 0) {   // the chain of subset starts
+        int q = 0, h = 0;
+        for (; h < kRound && q >= 0 && q < P; ++h) {
+          sh.rstart[h] = (short)q;
+          q = sh.rend[q];
+        }
+        sh.rdealt = q < 0 ? h - 1 : h;   // subsets with all 5 draws among the generated ones
+        sh.rpos = q;
+      }
+      __syncthreads();
+      const int dealt = sh.rdealt;
+      if (t < dealt) deal(sh.rstart[t], sh.subset[t]);
+      if (t == 0) {
+        unsigned long long st;
+        if (dealt == kRound) {   // the state after the last draw dealt
+          st = sh.rst[sh.rpos - 1];
+        } else {   // sequential from subset `dealt`, at its start draw
+          const int q0 = dealt > 0 ? sh.rend[sh.rstart[dealt - 1]] : 0;
+          st = q0 > 0 ? sh.rst[q0 - 1] : sh.rng;
+          int pos = q0;
+          for (int h = dealt; h < kRound; ++h) {
+            for (int i = 0; i < kModelPoints;) {
+              int ii, j;
+              for (;;) {
+                if (pos < P) {
+                  st = sh.rst[pos];
+                  ii = sh.rii[pos];
+                } else {
+                  ii = (int)(rng_next(st) % (unsigned)n);
+                }
+                ++pos;
+                for (j = 0; j < i; ++j)
+                  if (ii == sh.subset[h][j]) break;
+                if (j == i) break;
+              }
+              sh.subset[h][i] = ii;
+              ++i;
+            }
+          }
+        }
+        sh.rng = st;
+      }
     }
     __syncthreads();
     PNP_PHASE(9);
-    if (wave == 0) {  // one EPnP model per lane
-      double rvec[3], tvec[3];
-      epnp5(sh.subset[lane], p2, p3, K4, rvec, tvec, sh.hh + lane, kRound);
-      double R[9];
-      rodrigues_v2m(rvec, R);
-      for (int i = 0; i < 9; ++i) sh.hypR[lane][i] = R[i];
-      for (int i = 0; i < 3; ++i) {
-        sh.hypT[lane][i] = tvec[i];
-        sh.hypRvec[lane][i] = rvec[i];
-      }
+    // one EPnP model per hypothesis: wave 0 the eigenvectors (lane h = hypothesis h), then
+    // waves 1..3 one approximation each for every hypothesis; the smallest mean error wins
+    // (ties to the earlier approximation, as compute_pose's sequential comparison)
+    if (wave == 0) {
+      epnp5_eig(sh.subset[lane], p2, p3, K4, sh.hh + lane, kRound);
       sh.count[lane] = 0;
     }
     __syncthreads();
-    PNP_PHASE(10);
-    // inlier counts: wave w takes hypotheses w, w+4, ...; lanes sweep the points
-    for (int h = wave; h < kRound; h += 4) {
-      int c = 0;
-      for (int i = lane; i < n; i += 64)
-        c += reproj_err2(sh.hypR[h], sh.hypT[h], K4, p3[3 * i], p3[3 * i + 1], p3[3 * i + 2],
-                         p2[2 * i], p2[2 * i + 1]) <= thr;
-#pragma unroll
-      for (int o = 32; o >= 1; o >>= 1) c += __shfl_xor(c, o, 64);
-      if (lane == 0) sh.count[h] = c;
+    double Rw[9], tw[3];
+    if (wave > 0) {
+      epnp5_approx(wave, sh.subset[lane], p2, p3, K4, sh.hh + lane, kRound, Rw, tw,
+                   &sh.herr[wave][lane]);
     }
     __syncthreads();
-    PNP_PHASE(11);
-    if (t == 0) {  // OpenCV's acceptance rule, in iteration order
-      int iter = sh.iter, niters = sh.niters, best = sh.max_good;
-      for (int h = 0; h < kRound && iter < niters; ++h, ++iter) {
-        const int good = sh.count[h];
-        if (good > max(best, kModelPoints - 1)) {
-          best = good;
-          for (int i = 0; i < 3; ++i) {
-            sh.bestRvec[i] = sh.hypRvec[h][i];
-            sh.bestT[i] = sh.hypT[h][i];
-          }
-          niters = update_num_iters(confidence, (double)(n - good) / n, kModelPoints, niters);
+    if (wave > 0) {
+      int best = 1;
+      if (sh.herr[2][lane] < sh.herr[best][lane]) best = 2;
+      if (sh.herr[3][lane] < sh.herr[best][lane]) best = 3;
+      if (best == wave) {   // Rodrigues(R) -> rvec -> R, as solvePnP hands the model over
+        double rvec[3], R[9];
+        rodrigues_m2v(Rw, rvec);
+        rodrigues_v2m(rvec, R);
+        for (int i = 0; i < 9; ++i) sh.hypR[lane][i] = R[i];
+        for (int i = 0; i < 3; ++i) {
+          sh.hypT[lane][i] = tw[i];
+          sh.hypRvec[lane][i] = rvec[i];
         }
       }
-      sh.iter = iter;
-      sh.niters = niters;
-      sh.max_good = best;
-      sh.done = iter >= niters;
     }
     __syncthreads();
+    PNP_PHASE(10);
+    // inlier counts and OpenCV's acceptance rule, 16 iterations at a time: iterations past
+    // the stopping point are neither counted nor accepted (wave w counts w, w + 4, ...;
+    // lanes sweep the points)
+    for (int hb = 0; hb < kRound; hb += 16) {
+      for (int h = hb + wave; h < hb + 16; h += 4) {
+        int c = 0;
+        for (int i = lane; i < n; i += 64)
+          c += reproj_err2(sh.hypR[h], sh.hypT[h], K4, p3[3 * i], p3[3 * i + 1], p3[3 * i + 2],
+                           p2[2 * i], p2[2 * i + 1]) <= thr;
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) c += __shfl_xor(c, o, 64);
+        if (lane == 0) sh.count[h] = c;
+      }
+      __syncthreads();
+      PNP_PHASE(11);
+      if (t == 0) {  // in iteration order
+        int iter = sh.iter, niters = sh.niters, best = sh.max_good;
+        for (int h = hb; h < hb + 16 && iter < niters; ++h, ++iter) {
+          const int good = sh.count[h];
+          if (good > max(best, kModelPoints - 1)) {
+            best = good;
+            for (int i = 0; i < 3; ++i) {
+              sh.bestRvec[i] = sh.hypRvec[h][i];
+              sh.bestT[i] = sh.hypT[h][i];
+            }
+            niters = update_num_iters(confidence, (double)(n - good) / n, kModelPoints, niters);
+          }
+        }
+        sh.iter = iter;
+        sh.niters = niters;
+        sh.max_good = best;
+        sh.done = iter >= niters;
+      }
+      __syncthreads();
+      if (sh.done) break;
+    }
   }
   PNP_PHASE(12);
 

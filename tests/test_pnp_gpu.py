@@ -72,6 +72,27 @@ def test_ransac_matches_oracle(outliers, device):
         assert np.abs(pose[b, :, 3] - gt[:, 3]).max() < 0.01
 
 
+def test_ransac_small_sets_and_many_rounds(device):
+    """The round's cv::RNG draws are generated in parallel by jump-ahead and dealt out by one
+    lane: small point sets redraw duplicates often (n = 6..16 runs past the generated draws
+    into the sequential fallback), and 50-70% outliers keep RANSAC going for several
+    64-iteration rounds (jump-ahead from a mid-stream state).  Same model as the oracle."""
+    cases = [(6, 0.0), (7, 0.3), (9, 0.3), (12, 0.4), (16, 0.5), (60, 0.6), (300, 0.7),
+             (500, 0.5)]
+    scenes = [scene(300 + i, n, f) for i, (n, f) in enumerate(cases)]
+    pose, mask, nin, status = run_gpu(scenes, device)
+    for b, (p2, p3, K, gt, inl) in enumerate(scenes):
+        st, opose, omask, onin, iters = O.pnp_ransac(p2, p3, K, scale=1000.0)
+        n = p2.shape[0]
+        assert status[b] == st, b
+        assert nin[b] == onin, b
+        np.testing.assert_array_equal(mask[b, :n], omask)
+        if st == 0:
+            assert rot_angle(pose[b, :, :3], opose[:, :3]) < 1e-6
+            assert np.abs(pose[b, :, 3] - opose[:, 3]).max() < 1e-6
+    assert O.pnp_ransac(*scenes[-2][:3], scale=1000.0)[4] > 64   # several rounds
+
+
 def test_ransac_edge_counts(device):
     s5 = scene(7, 5, 0.0)
     s4 = scene(8, 4, 0.0)

@@ -49,7 +49,7 @@ int main(int argc, char** argv) {
     float ms; hipEventElapsedTime(&ms, e0, e1);
     unsigned long long ph[16]; hipMemcpyFromSymbol(ph, HIP_SYMBOL(g_pnp_phase), sizeof(ph));
     int ni; hipMemcpy(&ni, nin, 4, hipMemcpyDeviceToHost);
-    printf("n=%d inliers=%d ransac+refit %.1f us | refit phases (us): MtM %.1f  blocksum78 %.1f  eig+L %.1f  3x(betas,GN,R,err) %.1f  total %.1f\n",
+    printf("n=%d inliers=%d ransac+refit %.1f us | refit phases (us): MtM+reduce %.1f  assemble %.1f  eig+L %.1f  approx %.1f  total %.1f\n",
            n, ni, ms * 1e3, (ph[1] - ph[0]) / 100.0, (ph[2] - ph[1]) / 100.0, (ph[3] - ph[2]) / 100.0,
            (ph[4] - ph[3]) / 100.0, (ph[5] - ph[0]) / 100.0);
     printf("  ransac phases (us, last round): load %.1f  subsets %.1f  epnp5 x64 %.1f  count %.1f  accept %.1f  mask %.1f\n",
