@@ -126,3 +126,24 @@ def test_pose_error_semantics():
     pr[2, 3] += 0.02
     r, t = O.pose_error(pr, gt)
     assert abs(t - 2.0) < 1e-9 and r < 1e-4
+
+
+def test_mwc_jump_ahead_identity():
+    """cv::RNG's multiply-with-carry step s' = (s mod 2^32) * A + (s >> 32) is, for states
+    below m = A * 2^32 - 1, multiplication by A mod m -- the identity the GPU RANSAC uses to
+    generate a round's draws in parallel (lane l starts at A^(6 l) z mod m).  RNG((uint64)-1)
+    starts above m: the first two draws are stepped one by one (pnp.hip kRngPrefix)."""
+    A = 4164903690
+    m = A * 2**32 - 1
+
+    def step(s):
+        return (s & 0xFFFFFFFF) * A + (s >> 32)
+
+    z, seq = 2**64 - 1, []
+    for _ in range(800):
+        z = step(z)
+        seq.append(z)
+    first = next(i for i, v in enumerate(seq) if v < m)
+    assert first == 1 and all(v < m for v in seq[first:])
+    for k in (1, 5, 6, 64, 384, 700):
+        assert seq[first + k] == pow(A, k, m) * seq[first] % m
