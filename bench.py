@@ -213,6 +213,9 @@ def main():
                     help="start each step from images: SuperPoint (max_keypoints = n1, nms 3, "
                          "threshold 0.005) on the GPU produces the query keypoints/descriptors")
     ap.add_argument("--image-size", type=int, default=512)
+    ap.add_argument("--unfused-pose", action="store_true",
+                    help="pose stage as select + RANSAC-EPnP + errors (4 launches) instead of "
+                         "onepose_pose_stage (2)")
     ap.add_argument("--diag-repeats", type=int, default=0,
                     help="diagnostic: after the timed region, time it again this many times "
                          "and report those ms/step too (value always comes from the first)")
@@ -254,6 +257,7 @@ def main():
                          slots=args.slots or max(2, args.match_streams + 1), detector=detector,
                          image_hw=(args.image_size, args.image_size),
                          object_cache=not args.no_object_cache)
+    pipe.fused_pose = not args.unfused_pose
     cached = pipe.object_cache is not None
     pipe.set_frames(data["descriptors2d_query"], data["keypoints2d"],
                     np.stack([f.K for f in frames]), np.stack([f.pose_gt for f in frames]))

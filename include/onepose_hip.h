@@ -267,6 +267,25 @@ int onepose_pose_errors(const double* pose_pred, const double* pose_gt, int64_t 
                         void* stream);
 
 /* ------------------------------------------------------------------------------------ *
+ * The whole per-frame pose stage in two launches  --  inference.py:147-160 (mkpts selection,
+ * ransac_PnP, evaluator.evaluate): onepose_select_correspondences fused into the RANSAC
+ * kernel (which compacts the matches straight into its LDS copy of the points) and
+ * onepose_pose_errors fused into the refit kernel.  Same results as the three calls, with
+ * max_points = n1 (pts2d [batch, n1, 2], pts3d [batch, n1, 3], inlier_mask [batch, n1]).
+ * scale multiplies kpts3d (select) and divides the translation (ransac_PnP), as inference.py
+ * uses one scale for both.  pose_gt null: no error outputs (R_err_deg / t_err_cm / cmd may
+ * be null).  Workspace: onepose_pnp_workspace_bytes(batch, n1, max_iters).
+ * ------------------------------------------------------------------------------------ */
+int onepose_pose_stage(const int64_t* matches0, const float* kpts2d, int64_t kpts2d_bstride,
+                       const float* kpts3d, int64_t kpts3d_bstride, int batch, int n1, int n3,
+                       double scale, const double* K, int64_t K_bstride, float reproj_error,
+                       int max_iters, double confidence, const double* pose_gt,
+                       int64_t gt_bstride, float* pts2d, float* pts3d, int* counts,
+                       double* pose34, uint8_t* inlier_mask, int* n_inliers, int* status,
+                       double* R_err_deg, double* t_err_cm, uint8_t* cmd, void* workspace,
+                       size_t workspace_bytes, void* stream);
+
+/* ------------------------------------------------------------------------------------ *
  * SuperPoint keypoint detector + descriptor -- replaces SuperPoint.forward
  * (src/models/extractors/SuperPoint/superpoint.py:170-224; the model extract_features.py:
  * 27-40 builds, nms_radius 3, keypoint_threshold 0.005, remove_borders 4, max_keypoints

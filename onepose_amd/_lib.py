@@ -79,6 +79,11 @@ PROTOTYPES = {
                                    c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
     "onepose_pose_errors": (c_int, [c_void_p, c_void_p, c_int64, c_int, c_void_p, c_void_p,
                                     c_void_p, c_void_p]),
+    "onepose_pose_stage": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_int64, c_int, c_int,
+                                   c_int, c_double, c_void_p, c_int64, c_float, c_int, c_double,
+                                   c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p,
+                                   c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                   c_void_p, c_size_t, c_void_p]),
     "onepose_superpoint_num_tensors": (c_int, []),
     "onepose_superpoint_tensor_name": (c_char_p, [c_int]),
     "onepose_superpoint_packed_bytes": (c_size_t, []),

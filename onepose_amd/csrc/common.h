@@ -168,6 +168,25 @@ __device__ __forceinline__ float wave_max(float v) {
 // F.elu as ATen computes it (x > 0 ? x : exp(x) - 1), GATs.py:102 / GATs_SuperGlue.py:90-91
 __device__ __forceinline__ float elu1(float x) { return x > 0.f ? x : (expf(x) - 1.0f); }
 
+// query_pose_error / Evaluator for one frame: t_err = |t_p - t_gt| * 100, R_err =
+// deg(acos((tr(R_p R_gt^T) - 1) / 2)) with the trace clamped to <= 3 only (as the reference
+// does; NaN -> 3 too), cm/deg flags at 1 / 3 / 5.  P, G: 3x4 row-major.
+__device__ __forceinline__ void pose_error_one(const double* P, const double* G, double* rerr,
+                                               double* terr, uint8_t* cmd3) {
+  const double dx = P[3] - G[3], dy = P[7] - G[7], dz = P[11] - G[11];
+  const double t = sqrt(dx * dx + dy * dy + dz * dz) * 100.0;
+  double tr = 0.0;
+  for (int i = 0; i < 3; ++i)
+    for (int k = 0; k < 3; ++k) tr += P[i * 4 + k] * G[i * 4 + k];
+  if (!(tr <= 3.0)) tr = 3.0;
+  const double ang = acos((tr - 1.0) / 2.0) * (180.0 / M_PI);
+  *rerr = ang;
+  *terr = t;
+  cmd3[0] = (t < 1.0 && ang < 1.0) ? 1 : 0;
+  cmd3[1] = (t < 3.0 && ang < 3.0) ? 1 : 0;
+  cmd3[2] = (t < 5.0 && ang < 5.0) ? 1 : 0;
+}
+
 // Chan et al. pairwise merge of (count, mean, M2) statistics (InstanceNorm moments).
 __device__ __forceinline__ void chan_merge(double& n, double& mean, double& m2, double nb,
                                            double mb, double m2b) {

@@ -127,27 +127,13 @@ __global__ __launch_bounds__(1024) void select_kernel(const int64_t* __restrict_
   if (t == 0) counts[b] = base_s;
 }
 
-// query_pose_error / Evaluator: t_err = |t_p - t_gt| * 100, R_err = deg(acos((tr(R_p R_gt^T) - 1) / 2))
-// with the trace clamped to <= 3 only (as the reference does).
+// query_pose_error / Evaluator (pose_error_one, common.h), one thread per frame.
 __global__ void pose_error_kernel(const double* __restrict__ pred, const double* __restrict__ gt,
                                   int64_t gt_bs, int batch, double* rerr, double* terr,
                                   uint8_t* cmd) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= batch) return;
-  const double* P = pred + (int64_t)b * 12;
-  const double* G = gt + b * gt_bs;
-  const double dx = P[3] - G[3], dy = P[7] - G[7], dz = P[11] - G[11];
-  const double t = sqrt(dx * dx + dy * dy + dz * dz) * 100.0;
-  double tr = 0.0;
-  for (int i = 0; i < 3; ++i)
-    for (int k = 0; k < 3; ++k) tr += P[i * 4 + k] * G[i * 4 + k];
-  if (!(tr <= 3.0)) tr = 3.0;   // `trace if trace <= 3 else 3` (NaN -> 3 too)
-  const double ang = acos((tr - 1.0) / 2.0) * (180.0 / M_PI);
-  rerr[b] = ang;
-  terr[b] = t;
-  cmd[b * 3 + 0] = (t < 1.0 && ang < 1.0) ? 1 : 0;
-  cmd[b * 3 + 1] = (t < 3.0 && ang < 3.0) ? 1 : 0;
-  cmd[b * 3 + 2] = (t < 5.0 && ang < 5.0) ? 1 : 0;
+  pose_error_one(pred + (int64_t)b * 12, gt + b * gt_bs, rerr + b, terr + b, cmd + b * 3);
 }
 
 }  // namespace onepose

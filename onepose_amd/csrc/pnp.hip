@@ -1565,18 +1565,73 @@ __device__ __forceinline__ unsigned long long mwc_mulmod(unsigned long long a,
   return lo >= kMwcM ? lo - kMwcM : lo;
 }
 
+// Correspondence selection fused into the RANSAC kernel (onepose_pose_stage): the frame's
+// valid matches compacted in ascending 2D-index order (select_kernel's rule) straight into
+// the LDS point copy, and into pts2d / pts3d / counts for the refit and the caller.
+struct SelArgs {
+  const int64_t* matches0;   // null: the points are given (onepose_pnp_ransac)
+  const float* kp2;
+  int64_t kp2_bs;
+  const float* kp3;
+  int64_t kp3_bs;
+  int n1, n3;
+  double scale3d;
+};
+
 __global__ __launch_bounds__(kThreads) void pnp_ransac_kernel(
     const float* __restrict__ pts2d, const float* __restrict__ pts3d, const int* __restrict__ counts,
     int max_points, const double* __restrict__ Kmat, int64_t K_bs, double scale, float reproj,
     int max_iters, double confidence, double* __restrict__ pose34, uint8_t* __restrict__ mask_out,
-    int* __restrict__ n_inliers, int* __restrict__ status, int* __restrict__ idx_ws) {
+    int* __restrict__ n_inliers, int* __restrict__ status, int* __restrict__ idx_ws, SelArgs sel,
+    float* __restrict__ sel_p2, float* __restrict__ sel_p3, int* __restrict__ sel_counts) {
   extern __shared__ __attribute__((aligned(16))) unsigned char dyn[];
   Shared& sh = *reinterpret_cast<Shared*>(dyn);
   float* p2 = reinterpret_cast<float*>(dyn + ((sizeof(Shared) + 15) / 16) * 16);
   float* p3 = p2 + 2 * max_points;
   const int b = blockIdx.x;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  const int n = min(counts[b], max_points);
+  int n;
+  if (sel.matches0 != nullptr) {   // select: compact the valid matches (block-wide scan)
+    const int64_t* m = sel.matches0 + (int64_t)b * sel.n1;
+    const float* k2 = sel.kp2 + b * sel.kp2_bs;
+    const float* k3 = sel.kp3 + b * sel.kp3_bs;
+    float* o2 = sel_p2 + (int64_t)b * max_points * 2;
+    float* o3 = sel_p3 + (int64_t)b * max_points * 3;
+    int base = 0;
+    for (int start = 0; start < sel.n1; start += kThreads) {
+      const int i = start + t;
+      const int64_t j = (i < sel.n1) ? m[i] : -1;
+      const bool valid = j > -1 && j < sel.n3;
+      const unsigned long long bal = __ballot(valid);
+      if (lane == 0) sh.wave_cnt[wave] = __popcll(bal);
+      __syncthreads();
+      int off = base;
+      for (int w2 = 0; w2 < wave; ++w2) off += sh.wave_cnt[w2];
+      if (valid) {
+        const int q = off + __popcll(bal & ((1ull << lane) - 1ull));
+        const float u = k2[(int64_t)i * 2], v = k2[(int64_t)i * 2 + 1];
+        const float X = (float)((double)k3[j * 3] * sel.scale3d);
+        const float Y = (float)((double)k3[j * 3 + 1] * sel.scale3d);
+        const float Z = (float)((double)k3[j * 3 + 2] * sel.scale3d);
+        p2[2 * q] = u;
+        p2[2 * q + 1] = v;
+        p3[3 * q] = X;
+        p3[3 * q + 1] = Y;
+        p3[3 * q + 2] = Z;
+        o2[2 * q] = u;
+        o2[2 * q + 1] = v;
+        o3[3 * q] = X;
+        o3[3 * q + 1] = Y;
+        o3[3 * q + 2] = Z;
+      }
+      base += sh.wave_cnt[0] + sh.wave_cnt[1] + sh.wave_cnt[2] + sh.wave_cnt[3];
+      __syncthreads();
+    }
+    n = base;
+    if (t == 0) sel_counts[b] = n;
+  } else {
+    n = min(counts[b], max_points);
+  }
   const double* K = Kmat + b * K_bs;
   const double K4[4] = {K[0], K[4], K[2], K[5]};
   uint8_t* mask = mask_out + (int64_t)b * max_points;
@@ -1595,12 +1650,14 @@ __global__ __launch_bounds__(kThreads) void pnp_ransac_kernel(
     identity(1);
     return;
   }
-  for (int i = t; i < n; i += kThreads) {
-    p2[2 * i] = pts2d[((int64_t)b * max_points + i) * 2];
-    p2[2 * i + 1] = pts2d[((int64_t)b * max_points + i) * 2 + 1];
-    p3[3 * i] = pts3d[((int64_t)b * max_points + i) * 3];
-    p3[3 * i + 1] = pts3d[((int64_t)b * max_points + i) * 3 + 1];
-    p3[3 * i + 2] = pts3d[((int64_t)b * max_points + i) * 3 + 2];
+  if (sel.matches0 == nullptr) {
+    for (int i = t; i < n; i += kThreads) {
+      p2[2 * i] = pts2d[((int64_t)b * max_points + i) * 2];
+      p2[2 * i + 1] = pts2d[((int64_t)b * max_points + i) * 2 + 1];
+      p3[3 * i] = pts3d[((int64_t)b * max_points + i) * 3];
+      p3[3 * i + 1] = pts3d[((int64_t)b * max_points + i) * 3 + 1];
+      p3[3 * i + 2] = pts3d[((int64_t)b * max_points + i) * 3 + 2];
+    }
   }
   const float thr = (float)((double)reproj * (double)reproj);
   if (t == 0) {
@@ -1852,11 +1909,21 @@ __global__ __launch_bounds__(kThreads) void pnp_refit_kernel(
     const float* __restrict__ pts2d, const float* __restrict__ pts3d, int max_points,
     const double* __restrict__ Kmat, int64_t K_bs, double scale, double* __restrict__ pose34,
     const int* __restrict__ n_inliers, const int* __restrict__ status,
-    const int* __restrict__ idx_ws) {
+    const int* __restrict__ idx_ws, const double* __restrict__ pose_gt, int64_t gt_bs,
+    double* __restrict__ rerr, double* __restrict__ terr, uint8_t* __restrict__ cmd) {
   __shared__ Shared sh;
   const int b = blockIdx.x;
-  if (status[b] != 0) return;
   const int t = threadIdx.x;
+  double* pose = pose34 + (int64_t)b * 12;
+  // pose_gt (onepose_pose_stage): query_pose_error of the frame's final pose, fused
+  auto errors = [&]() {
+    if (pose_gt != nullptr && t == 0)
+      pose_error_one(pose, pose_gt + b * gt_bs, rerr + b, terr + b, cmd + b * 3);
+  };
+  if (status[b] != 0) {   // identity pose (written by the RANSAC kernel)
+    errors();
+    return;
+  }
   const int nin = n_inliers[b];
   const double* K = Kmat + b * K_bs;
   const double K4[4] = {K[0], K[4], K[2], K[5]};
@@ -1869,12 +1936,12 @@ __global__ __launch_bounds__(kThreads) void pnp_refit_kernel(
   rodrigues_m2v(Rf, rv);
   rodrigues_v2m(rv, Rr);
   if (t == 0) {
-    double* pose = pose34 + (int64_t)b * 12;
     for (int i = 0; i < 3; ++i) {
       for (int j = 0; j < 3; ++j) pose[i * 4 + j] = Rr[i * 3 + j];
       pose[i * 4 + 3] = tf[i] / scale;
     }
   }
+  errors();
 }
 
 }  // namespace
@@ -1916,12 +1983,58 @@ int onepose_pnp_ransac(const float* pts2d, const float* pts3d, const int* counts
     attr_set = true;
   }
   hipStream_t st = static_cast<hipStream_t>(stream);
+  SelArgs none{};
   OP_LAUNCH(K_PNP, st, pnp_ransac_kernel, dim3(batch), dim3(kThreads), lds, st, pts2d, pts3d,
             counts, max_points, K, K_bstride, scale, reproj_error, max_iters, confidence, pose34,
-            inlier_mask, n_inliers, status, static_cast<int*>(workspace));
+            inlier_mask, n_inliers, status, static_cast<int*>(workspace), none, nullptr, nullptr,
+            nullptr);
   OP_LAUNCH(K_PNP_REFIT, st, pnp_refit_kernel, dim3(batch), dim3(kThreads), 0, st, pts2d, pts3d,
             max_points, K, K_bstride, scale, pose34, n_inliers, status,
-            static_cast<const int*>(workspace));
+            static_cast<const int*>(workspace), nullptr, (int64_t)0, nullptr, nullptr, nullptr);
+  return ONEPOSE_OK;
+}
+
+int onepose_pose_stage(const int64_t* matches0, const float* kpts2d, int64_t kpts2d_bstride,
+                       const float* kpts3d, int64_t kpts3d_bstride, int batch, int n1, int n3,
+                       double scale, const double* K, int64_t K_bstride, float reproj_error,
+                       int max_iters, double confidence, const double* pose_gt,
+                       int64_t gt_bstride, float* pts2d, float* pts3d, int* counts,
+                       double* pose34, uint8_t* inlier_mask, int* n_inliers, int* status,
+                       double* R_err_deg, double* t_err_cm, uint8_t* cmd, void* workspace,
+                       size_t workspace_bytes, void* stream) {
+  clear_error();
+  OP_REQUIRE(matches0 && kpts2d && kpts3d && K && pts2d && pts3d && counts && pose34 &&
+                 inlier_mask && n_inliers && status,
+             "pose_stage: null pointer");
+  OP_REQUIRE(!pose_gt || (R_err_deg && t_err_cm && cmd), "pose_stage: null error output");
+  OP_REQUIRE(batch >= 1 && n1 >= 1 && n1 <= 8192 && n3 >= 1, "pose_stage: batch=%d n1=%d n3=%d",
+             batch, n1, n3);
+  OP_REQUIRE(confidence > 0 && confidence < 1, "pose_stage: confidence %f not in (0,1)",
+             confidence);
+  OP_REQUIRE(scale != 0.0, "pose_stage: scale 0");
+  const int max_points = n1;
+  const size_t need = onepose_pnp_workspace_bytes(batch, max_points, max_iters);
+  if (!workspace || workspace_bytes < need) {
+    set_error("pose_stage: workspace %zu < %zu bytes", workspace_bytes, need);
+    return ONEPOSE_ERR_WORKSPACE;
+  }
+  const size_t lds = ((sizeof(Shared) + 15) / 16) * 16 + (size_t)max_points * 5 * sizeof(float);
+  OP_REQUIRE(lds <= 160 * 1024, "pose_stage: n1=%d needs %zu B of LDS", n1, lds);
+  static bool attr_set = false;
+  if (!attr_set) {
+    OP_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(pnp_ransac_kernel),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    attr_set = true;
+  }
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const SelArgs sel{matches0, kpts2d, kpts2d_bstride, kpts3d, kpts3d_bstride, n1, n3, scale};
+  OP_LAUNCH(K_PNP, st, pnp_ransac_kernel, dim3(batch), dim3(kThreads), lds, st, nullptr, nullptr,
+            nullptr, max_points, K, K_bstride, scale, reproj_error, max_iters, confidence, pose34,
+            inlier_mask, n_inliers, status, static_cast<int*>(workspace), sel, pts2d, pts3d,
+            counts);
+  OP_LAUNCH(K_PNP_REFIT, st, pnp_refit_kernel, dim3(batch), dim3(kThreads), 0, st, pts2d, pts3d,
+            max_points, K, K_bstride, scale, pose34, n_inliers, status,
+            static_cast<const int*>(workspace), pose_gt, gt_bstride, R_err_deg, t_err_cm, cmd);
   return ONEPOSE_OK;
 }
 

@@ -190,11 +190,26 @@ class FramePipeline:
             o.mscores1.data_ptr(), _lib.ptr(o.conf), o.ws_match.data_ptr(),
             o.ws_match_bytes, s), "onepose_match_prepared")
 
-    def enqueue_pose(self, slot: int = 0):
+    fused_pose = True   # enqueue_pose's default: onepose_pose_stage (two launches)
+
+    def enqueue_pose(self, slot: int = 0, fused: bool | None = None):
+        """Selection -> RANSAC-EPnP -> cm/deg errors for the slot's frames: two launches
+        (onepose_pose_stage), or the three separate entry points (fused=False)."""
+        fused = self.fused_pose if fused is None else fused
         o = self.slots[slot]
         s = _lib.stream_ptr(self.device)
         lib = self.lib
         _, kpts2d = self._inputs(o)
+        if fused:
+            _lib.check(lib.onepose_pose_stage(
+                o.matches0.data_ptr(), kpts2d.data_ptr(), self.n1 * 2, self.kp3.data_ptr(), 0,
+                self.B, self.n1, self.n3, self.scale, self.K.data_ptr(), 9, self.reproj,
+                self.iters, self.conf_level, self.pose_gt.data_ptr(), 12, o.pts2d.data_ptr(),
+                o.pts3d.data_ptr(), o.counts.data_ptr(), o.pose.data_ptr(),
+                o.inlier_mask.data_ptr(), o.n_inliers.data_ptr(), o.status.data_ptr(),
+                o.R_err.data_ptr(), o.t_err.data_ptr(), o.cmd.data_ptr(), o.ws_pnp.data_ptr(),
+                o.ws_pnp_bytes, s), "pose_stage")
+            return
         _lib.check(lib.onepose_select_correspondences(
             o.matches0.data_ptr(), kpts2d.data_ptr(), self.n1 * 2, self.kp3.data_ptr(), 0,
             self.B, self.n1, self.n3, self.scale, o.pts2d.data_ptr(), o.pts3d.data_ptr(),

@@ -61,6 +61,35 @@ def test_graph_replay_matches_eager(setup):
 
 
 @pytest.mark.gpu
+def test_fused_pose_stage_matches_separate_calls(setup):
+    """onepose_pose_stage (selection in the RANSAC kernel, errors in the refit kernel) gives
+    the bits of onepose_select_correspondences + onepose_pnp_ransac + onepose_pose_errors."""
+    pipe, batches = setup
+    for bt in batches:
+        pipe.set_frames(*bt)
+        pipe.enqueue_front(0)
+        pipe.enqueue_pose(0, fused=False)
+        torch.cuda.synchronize()
+        sep = _outputs(pipe.slots[0])
+        sep.update(pts2d=pipe.slots[0].pts2d.cpu().numpy().copy(),
+                   pts3d=pipe.slots[0].pts3d.cpu().numpy().copy(),
+                   counts=pipe.slots[0].counts.cpu().numpy().copy())
+        for k in ("pose", "inlier_mask", "R_err", "t_err", "cmd", "n_inliers", "counts"):
+            getattr(pipe.slots[0], k).zero_()
+        pipe.enqueue_pose(0, fused=True)
+        torch.cuda.synchronize()
+        fused = _outputs(pipe.slots[0])
+        o = pipe.slots[0]
+        for b in range(B):
+            c = int(sep["counts"][b])
+            assert int(o.counts[b]) == c
+            np.testing.assert_array_equal(o.pts2d[b, :c].cpu().numpy(), sep["pts2d"][b, :c])
+            np.testing.assert_array_equal(o.pts3d[b, :c].cpu().numpy(), sep["pts3d"][b, :c])
+        _assert_same(sep_core := {k: sep[k] for k in fused}, fused)
+        assert sep_core["status"].tolist() == [0] * B
+
+
+@pytest.mark.gpu
 def test_stream_schedule_matches_eager(setup):
     pipe, batches = setup
     pipe.set_frames(*batches[1])
