@@ -46,11 +46,23 @@ def superpoint_conv_flops(h, w):
     return sum(2 * (h // d) * (w // d) * co * ci * k * k for d, ci, co, k in layers)
 
 
-def frame_flops(n1, n3, L, cached):
+def cross_cached(cached, B):
+    """Whether the object cache also holds cross-attention 1's frame-independent 3D half
+    (the 3D side's q / k / v projections, KV and the x range of its MLP conv 1): the cached
+    forward uses it at batches <= 4 (matcher.hip, kFusedFoldMaxBatch)."""
+    return cached and B <= 4
+
+
+def frame_flops(n1, n3, L, cached, B=1):
     """algorithmic MFMA FLOPs per frame, F, or F_dep when the object-only
-    prefix (GAT 0 + the 3D half of self-attention 1) is cached per object."""
+    prefix (GAT 0 + the 3D half of self-attention 1) is cached per object.  With cross-
+    attention 1's 3D half cached too (cross_cached), half of that layer's per-3D-token work
+    (q, k, v projections 10 C^2, KV 2 C dh, W1a x 4 C^2 = 688,128 FLOP) is not per frame."""
     f = 11141120 * (n1 + n3) + 512 * n1 * n3 + 2048 * (L + 2) * n3
-    return f - 1376256 * n3 - 512 * (L + 2) * n3 if cached else f
+    if not cached:
+        return f
+    f -= 1376256 * n3 + 512 * (L + 2) * n3
+    return f - 688128 * n3 if cross_cached(cached, B) else f
 
 
 def kernel_work(kind, B, n1, n3, L, cached=False):
@@ -59,10 +71,13 @@ def kernel_work(kind, B, n1, n3, L, cached=False):
     object cache, one of a frame's 8 launches of each attention GEMM has the 2D side only, so
     the figure is the frame's work of that kind / 8 (the average launch)."""
     T = B * (n1 + n3) - (B * n3 / 8 if cached else 0)
+    xc = cross_cached(cached, B)   # cross-attention 1: the 3D side's QKV and W1a x cached
+    Tq = T - (B * n3 / 8 if xc else 0)
+    T1 = T - (B * n3 / 16 if xc else 0)   # half of that layer's 3D MLP-conv-1 K range
     C = 256
     table = {
-        "qkv_gemm": (2 * 3 * C * C * T, "flop", "mfma"),      # [q | k v] = Wqkv x
-        "mlp1_gemm": (2 * 2 * C * 2 * C * T, "flop", "mfma"),   # [W1a | Mf] [x ; QZ]
+        "qkv_gemm": (2 * 3 * C * C * Tq, "flop", "mfma"),      # [q | k v] = Wqkv x
+        "mlp1_gemm": (2 * 2 * C * 2 * C * T1, "flop", "mfma"),   # [W1a | Mf] [x ; QZ]
         "mlp2_gemm": (2 * 2 * C * C * T, "flop", "mfma"),
         "final_gemm": (2 * C * C * T, "flop", "mfma"),
         "score_gemm": (2 * C * n1 * n3 * B, "flop", "mfma"),
@@ -435,9 +450,11 @@ def main():
                       "timing": "serial profile pass (3 steps), HIP events per launch"}}
 
     # SURVEY.md §8d "fraction = F * frames/s / peak" for the whole frame's contractions
-    ff = frame_flops(n1, n3, L, cached)
-    frame_roof = {"flop_per_frame": ff, "formula": "F_dep (object prefix cached)" if cached
-                  else "F", "achieved_tflops": round(ff * value / 1e12, 2),
+    ff = frame_flops(n1, n3, L, cached, B)
+    formula = ("F_dep - 688128 n3 (object prefix and cross-attention 1's 3D half cached)"
+               if cross_cached(cached, B) else "F_dep (object prefix cached)" if cached else "F")
+    frame_roof = {"flop_per_frame": ff, "formula": formula,
+                  "achieved_tflops": round(ff * value / 1e12, 2),
                   "peak": peak, "frac": round(ff * value / 1e12 / peak, 4)}
 
     cfg_name = {(1024, 4096): "config 2", (1024, 16384): "config 3",

@@ -148,7 +148,9 @@ int onepose_match_prepared(const void* packed_weights,
  * depend on the object alone: GAT layer 0 (GATs.py:62-123, the 3D descriptors and their
  * leaves) and the 3D half of self-attention 1 (GATs_SuperGlue.py:67-85 -- the 3D side attends
  * only to itself there).  onepose_object_prepare runs them once per object and leaves the
- * 3D state entering layer 2 in `cache` ([n3][256] fp32, onepose_object_cache_bytes);
+ * 3D state entering layer 2 in `cache` ([n3][256] fp32), followed by the leaf logits
+ * leaf_j . (W a)_lo of GAT layers 1-3 ([3][n3][16] fp32; GATs.py:113, constant per object since
+ * the leaves never change, GATs_SuperGlue.py:70-72) -- onepose_object_cache_bytes in all;
  * onepose_match_cached then runs every frame from there.  Its results are bit-identical to
  * onepose_match_prepared_ex's on the same object (the same kernels and tiles produce the
  * cached state), provided the cache was prepared with the same `precision`.

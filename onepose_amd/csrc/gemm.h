@@ -23,6 +23,8 @@ enum GemmEpi {
   EPI_STATS = 2,   // y = acc + bias, plus per-tile (mean, M2) of every column  (InstanceNorm)
   EPI_RESID = 3,   // y = R + (acc + bias)                                     (desc += delta)
   EPI_SCORE = 4,   // y = acc / scale, plus per-tile row/col (max, sum exp)     (dual softmax)
+  EPI_ACC = 5,     // the raw accumulators in register order, Y[b][tile][wave][FN][16][64]
+                   //   (tile = mt * ntiles + nt): a PRO_HEADZ launch's acc0
 };
 enum GemmPro {
   PRO_PLAIN = 0,
@@ -65,6 +67,10 @@ struct GemmProb {
   float* kspart;       // EPI_QKV: [batch][mtiles][256]
   const float* ksum;   // PRO_HEADZ: [batch][256] sum phi(k) of the attention source
   int64_t ksum_bs;
+  const float* acc0;   // PRO_HEADZ: the accumulators after the K range [0, ksplit), as an
+  int64_t acc0_bs;     //   EPI_ACC launch of the same tile over that range stored them (the same
+                       //   MFMA sequence, so the same bits); that range is then skipped.  Null:
+                       //   start from zero.
   float scale;         // EPI_SCORE divisor (scale_factor)
   float vdiv;          // EPI_QKV: v divisor (source length)
   float ns;            // PRO_HEADZ: source length (v_length)

@@ -368,12 +368,24 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
       }
   };
 
-  load_stage<PRO, T>(c, m0, n0, 0, s0);
-  load_stage<PRO, T>(c, m0, n0, T::BKS, s1);
+  // PRO_HEADZ with acc0: the x range's accumulators were computed before (EPI_ACC, the same
+  // MFMA sequence); start from them at stage xs (even, so it sits in LDS buffer 0 like stage 0)
+  const float* acc0 = PRO == PRO_HEADZ ? F(acc0) : nullptr;
+  const int kt0 = acc0 != nullptr ? xs : 0;
+  if (acc0 != nullptr) {
+    const float* a0p = acc0 + b * F(acc0_bs) + ((int64_t)(mt * ntiles + nt) * T::NW + wave) * FN * 1024 + lane;
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[j][i] = a0p[j * 1024 + i * 64];
+  }
+  load_stage<PRO, T>(c, m0, n0, kt0 * T::BKS, s0);
+  load_stage<PRO, T>(c, m0, n0, (kt0 + 1) * T::BKS, s1);
   tk = stamp_start(args.stamp, sl);
   store_stage<PRO, T, PM>(lds, s0);
   __syncthreads();
   read_frag(lds, f0);
+  zdot(lds, kt0);   // the first phi(q) stage's Z partials when the x range is skipped
 
   auto step = [&](int kt, Stage<T>& next, Stage<T>& spare, const Frag& cur, Frag& nxt,
                   floatx16 (&tg)[FN]) __attribute__((always_inline)) {
@@ -401,7 +413,7 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
       step(kt + 1, s0, s1, f1, f0, acc);
     }
   } else {
-    for (int kt = 0; kt < xs; kt += 2) {   // x part
+    for (int kt = kt0; kt < xs; kt += 2) {   // x part
       step(kt, s1, s0, f0, f1, acc);
       step(kt + 1, s0, s1, f1, f0, acc);
     }
@@ -462,6 +474,16 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
   constexpr bool kStage = EPI == EPI_STATS || EPI == EPI_SCORE || EPI == EPI_QKV;
   const bool q_tile = EPI == EPI_QKV && n0 < 256;   // phi(q) columns: stored, no reduction
 
+  if (EPI == EPI_ACC) {   // raw accumulators in register order (a later PRO_HEADZ's acc0)
+    if (ks == 0) {
+      float* yp = Y + ((int64_t)(mt * ntiles + nt) * T::NW + wave) * FN * 1024 + lane;
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) yp[j * 1024 + i * 64] = acc[j][i];
+    }
+    return;
+  }
   if (ks == 0) {
     float res[FN][16];
     if (EPI == EPI_RESID) {   // all residual loads issued before the first store
@@ -780,6 +802,9 @@ int gemm_launch(int epi, int pro, int tile, GemmArgs& args, hipStream_t stream, 
   CASE(EPI_RESID, PRO_NORM_RELU, TILE_64x32K2, T64x32K2, PM_F32)
   CASE(EPI_SCORE, PRO_PLAIN, TILE_64x64, T64x64, PM_F32)
   CASE(EPI_BIAS, PRO_PLAIN, TILE_64x64, T64x64, PM_F32)
+  CASE(EPI_ACC, PRO_PLAIN, TILE_64x64, T64x64, PM_F32)
+  CASE(EPI_ACC, PRO_PLAIN, TILE_64x64, T64x64, PM_BF16)
+  CASE(EPI_ACC, PRO_PLAIN, TILE_64x64, T64x64, PM_SPLIT3)
   // bf16-MFMA attention layers (precision mode ONEPOSE_PREC_BF16_ATTN)
   CASE(EPI_QKV, PRO_PLAIN, TILE_32x128, T32x128, PM_BF16)
   CASE(EPI_STATS, PRO_HEADZ, TILE_64x64, T64x64, PM_BF16)

@@ -449,6 +449,87 @@ __global__ __launch_bounds__(1024) void kv_fold_kernel(KvFoldArgs args, float* k
   }
 }
 
+// kv_fold on 256-thread workgroups of at most 80 VGPRs per lane, so that one fits on a CU next
+// to three MLP-conv-1 workgroups (143 VGPRs) of the other frame in flight: the 1024-thread
+// form (16 waves of 84 VGPRs, 40 KB LDS) waits for a CU to drain.  The chunk sum is
+// kv_reduce's (wave w sums chunks w, w+4, ... in order, the four wave sums added in wave
+// order), so KV / ksum equal kv_reduce's bit for bit; the fold is kv_fold's (q quarters
+// accumulated in q order, then added in quarter order), now all four quarters in one thread.
+__global__ __launch_bounds__(256) void kv_fold256_kernel(KvFoldArgs args, float* kv, float* ksum,
+                                                         int batch) {
+  constexpr int per = (16384 + 256) / 4;   // float4 outputs per (source, sample) = 4160
+  constexpr int groups = per / 64;         // 65 workgroups per (source, sample)
+  __shared__ float4 red[4][64];            // wave sums; then KV rows d0..d0+3
+  const int g = blockIdx.x % groups, bs = blockIdx.x / groups;
+  const int b = bs % batch, src = bs / batch;
+  const KvProb& P = src ? args.p[1] : args.p[0];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int e4 = g * 64 + lane;
+  const int h = (g >> 4) & 3, d0 = (g & 15) * 4;
+  const float4* p;
+  int64_t stride;
+  if (e4 < 4096) {
+    p = reinterpret_cast<const float4*>(P.part + (int64_t)b * P.chunks * 16384) + e4;
+    stride = 4096;
+  } else {
+    p = reinterpret_cast<const float4*>(P.kspart + (int64_t)b * P.chunks * 256) + (e4 - 4096);
+    stride = 64;
+  }
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  int c = w;
+  for (; c + 28 < P.chunks; c += 32) {
+    float4 v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = p[(int64_t)(c + 4 * j) * stride];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { acc.x += v[j].x; acc.y += v[j].y; acc.z += v[j].z; acc.w += v[j].w; }
+  }
+  for (; c < P.chunks; c += 4) {
+    const float4 v = p[(int64_t)c * stride];
+    acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+  }
+  red[w][lane] = acc;
+  __syncthreads();
+  if (w == 0) {
+    float4 s = red[0][lane];
+#pragma unroll
+    for (int j = 1; j < 4; ++j) { s.x += red[j][lane].x; s.y += red[j][lane].y; s.z += red[j][lane].z; s.w += red[j][lane].w; }
+    if (e4 < 4096)
+      reinterpret_cast<float4*>(kv + ((int64_t)src * batch + b) * 16384)[e4] = s;
+    else
+      reinterpret_cast<float4*>(ksum + ((int64_t)src * batch + b) * 256)[e4 - 4096] = s;
+    red[0][lane] = s;   // KV rows d0..d0+3: red[0][16 j + q/4] = KV_h[d0 + j][q .. q+3]
+  }
+  if (g == 64) return;
+  __syncthreads();
+  const int op = t;   // Mf rows 2 op, 2 op + 1
+  const float* kvr = reinterpret_cast<const float*>(&red[0][0]);
+  const float* ct = args.ct + (h * 64) * 512 + 2 * op;
+  f2v y[4];
+#pragma unroll
+  for (int qq = 0; qq < 4; ++qq) {
+    f2v cv[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) cv[i] = *reinterpret_cast<const f2v*>(ct + (qq * 16 + i) * 512);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      f2v yq = (f2v)(0.f);
+#pragma unroll
+      for (int i = 0; i < 16; i += 4) {
+        const float4 k = *reinterpret_cast<const float4*>(kvr + j * 64 + qq * 16 + i);
+        yq = __builtin_elementwise_fma(cv[i], (f2v)(k.x), yq);
+        yq = __builtin_elementwise_fma(cv[i + 1], (f2v)(k.y), yq);
+        yq = __builtin_elementwise_fma(cv[i + 2], (f2v)(k.z), yq);
+        yq = __builtin_elementwise_fma(cv[i + 3], (f2v)(k.w), yq);
+      }
+      y[j] = qq == 0 ? yq : y[j] + yq;
+    }
+  }
+  float* mf = (src ? args.mf[1] : args.mf[0]) + (int64_t)b * 512 * 256 + (2 * op) * 256 + h * 64 + d0;
+  *reinterpret_cast<float4*>(mf) = make_float4(y[0].x, y[1].x, y[2].x, y[3].x);
+  *reinterpret_cast<float4*>(mf + 256) = make_float4(y[0].y, y[1].y, y[2].y, y[3].y);
+}
+
 // InstanceNorm1d statistics (GATs_SuperGlue.py:145; biased variance, eps 1e-5): per-64-row-tile
 // (mean, M2) partials from MLP conv 1, Chan-merged (double) in tile order by the last tile of
 // each column block inside that launch (gemm.hip, EPI_STATS with st_cnt).
@@ -577,17 +658,60 @@ __global__ __launch_bounds__(256) void colbest_assemble_kernel(const unsigned lo
 // One wave per 3D point over point-major leaves [n3][L][256]: each leaf row is one 1 KB
 // coalesced load (a float4 per lane), the L+1 logits are wave reductions, softmax and ELU run
 // in registers -- no LDS, every leaf byte crosses HBM once per layer.
+//
+// The leaf logits s2_j = leaf_j.wa_lo depend on the object alone (the leaves never change
+// across layers, GATs_SuperGlue.py:70-72).  onepose_object_prepare stores them for GAT layers
+// 1-3 (gat_logits_kernel, kLogitStride per point); a cached forward's GAT then reduces only
+// s3.  Both kernels form a logit with gat_dot + gat_wave_sum, so a stored logit has the bits
+// the in-kernel one would have.
+constexpr int kLogitStride = 16;   // stored leaf logits per point (num_leaf <= 16)
+
+__device__ __forceinline__ float gat_dot(float4 a, float4 w) {
+  return fmaf(a.w, w.w, fmaf(a.z, w.z, fmaf(a.y, w.y, a.x * w.x)));
+}
+
+template <int MAXL>
+__global__ __launch_bounds__(256) void gat_logits_kernel(const float* __restrict__ leaves_pm,
+                                                         const float* __restrict__ wa1,
+                                                         float* __restrict__ out, int n3, int L) {
+  // wa1: GAT layer 1's packed vectors; layers 2 and 3 follow at +kGatFloats (512) each.
+  // out[(g - 1)][p][kLogitStride]
+  const int p = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (p >= n3) return;
+  const int lane = threadIdx.x & 63;
+  const float* lp = leaves_pm + (int64_t)p * L * kDim;
+  float4 lf[MAXL];
+#pragma unroll
+  for (int j = 0; j < MAXL; ++j)
+    if (j < L) lf[j] = reinterpret_cast<const float4*>(lp + j * kDim)[lane];
+  for (int g = 0; g < 3; ++g) {
+    const float4 wl = reinterpret_cast<const float4*>(wa1 + g * 512)[lane];
+    float d[MAXL];
+#pragma unroll
+    for (int j = 0; j < MAXL; ++j) d[j] = (j < L) ? gat_dot(lf[j], wl) : 0.f;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1)
+#pragma unroll
+      for (int j = 0; j < MAXL; ++j) d[j] += __shfl_xor(d[j], o, 64);
+    float v = 0.f;
+#pragma unroll
+    for (int j = 0; j < MAXL; ++j) v = lane == j ? d[j] : v;
+    if (lane < L) out[((int64_t)g * n3 + p) * kLogitStride + lane] = v;
+  }
+}
+
+// slog: the stored leaf logits of this layer ([n3][kLogitStride], shared by the batch) or null.
 template <int MAXL>
 __global__ __launch_bounds__(256) void gat_kernel(const float* __restrict__ x3,
                                                   const float* __restrict__ leaves_pm,
                                                   int64_t leaves_bs, const float* __restrict__ wa,
+                                                  const float* __restrict__ slog,
                                                   float* __restrict__ y3, int n3, int L,
                                                   int batch) {
   const int gw = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int b = gw / n3, p = gw - b * n3;
   if (b >= batch) return;
   const int lane = threadIdx.x & 63;
-  const float4 wl = reinterpret_cast<const float4*>(wa)[lane];
   const float4 wh = reinterpret_cast<const float4*>(wa + 256)[lane];
   const float4 h = reinterpret_cast<const float4*>(x3 + ((int64_t)b * n3 + p) * kDim)[lane];
   const float* lp = leaves_pm + b * leaves_bs + (int64_t)p * L * kDim;
@@ -596,14 +720,24 @@ __global__ __launch_bounds__(256) void gat_kernel(const float* __restrict__ x3,
   for (int j = 0; j < MAXL; ++j)
     if (j < L) lf[j] = reinterpret_cast<const float4*>(lp + j * kDim)[lane];
   float d[MAXL + 1];
-  d[0] = h.x * wh.x + h.y * wh.y + h.z * wh.z + h.w * wh.w;
+  d[0] = gat_dot(h, wh);
+  if (slog != nullptr) {
+    // wave-uniform point: the logits come in through scalar loads
+    const int pu = __builtin_amdgcn_readfirstlane(p);
+    const float* sl = slog + (int64_t)pu * kLogitStride;
 #pragma unroll
-  for (int j = 0; j < MAXL; ++j)
-    d[j + 1] = (j < L) ? lf[j].x * wl.x + lf[j].y * wl.y + lf[j].z * wl.z + lf[j].w * wl.w : 0.f;
+    for (int j = 0; j < MAXL; ++j) d[j + 1] = (j < L) ? sl[j] : 0.f;
 #pragma unroll
-  for (int o = 32; o >= 1; o >>= 1)
+    for (int o = 32; o >= 1; o >>= 1) d[0] += __shfl_xor(d[0], o, 64);
+  } else {
+    const float4 wl = reinterpret_cast<const float4*>(wa)[lane];
 #pragma unroll
-    for (int j = 0; j <= MAXL; ++j) d[j] += __shfl_xor(d[j], o, 64);
+    for (int j = 0; j < MAXL; ++j) d[j + 1] = (j < L) ? gat_dot(lf[j], wl) : 0.f;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1)
+#pragma unroll
+      for (int j = 0; j <= MAXL; ++j) d[j] += __shfl_xor(d[j], o, 64);
+  }
   const float s3 = d[0];
   float e[MAXL + 1];
   float mx = -INFINITY;
@@ -1239,20 +1373,59 @@ bool same_tiles(const LayerTiles& a, const LayerTiles& b) {
   return a.qkv == b.qkv && a.fused_fold == b.fused_fold && a.mlp2 == b.mlp2;
 }
 
+// Object cache layout (floats; onepose_object_cache_bytes): the 3D state entering layer 2,
+// GAT layers 1-3's leaf logits, then cross-attention 1's frame-independent 3D half (SideCache).
+struct ObjLayout {
+  int64_t logits, phiq, acc, ksum, mf, total;
+};
+ObjLayout obj_layout(int n3) {
+  ObjLayout L;
+  L.logits = (int64_t)n3 * 256;
+  L.phiq = L.logits + (int64_t)3 * n3 * kLogitStride;
+  L.acc = L.phiq + (int64_t)n3 * 256;
+  L.ksum = L.acc + (int64_t)ceil_div(n3, 64) * 64 * 512;   // TILE_64x64 tiles of N = 512
+  L.mf = L.ksum + 256;
+  L.total = L.mf + 512 * 256;
+  return L;
+}
+
+// Cross-attention 1's frame-independent half (object cache, onepose_object_prepare): the 3D
+// side enters layer 2 with the cached state, so its q projection (phi(q)), its k / v as the 2D
+// side's source (sum phi(k), and the 2D side's folded weights Mf = C KV_3D) and the x range of
+// its MLP conv 1 (W1a x, as raw accumulators) are the same for every frame.
+struct SideCache {
+  const float* phiq;   // [n3][256]  phi(q) of the 3D side
+  const float* acc;    // MLP conv 1 accumulators over K [0, 256) (EPI_ACC layout, TILE_64x64)
+  const float* ksum;   // [256]      sum phi(k) of the 3D side
+  const float* mf;     // [512][256] the 2D side's Mf
+};
+
+void launch_kv_fold(const KvFoldArgs& ka, int nslot, int B, float* kv, float* ksum, hipStream_t st) {
+#ifdef KVF_WG1024
+  hipLaunchKernelGGL(kv_fold_kernel, dim3(nslot * B * 65), dim3(1024), 0, st, ka, kv, ksum, B);
+#else
+  hipLaunchKernelGGL(kv_fold256_kernel, dim3(nslot * B * 65), dim3(256), 0, st, ka, kv, ksum, B);
+#endif
+}
+
 // AttentionPropagation (GATs_SuperGlue.py:123-132) for 1 or 2 sides in grouped launches.
 // Each side's arithmetic is independent of the others' (per-problem tiles, per-slot
 // reductions), so a side gives the same bits alone or grouped.  Sharded runs have two
-// sides, slot 1 being the 3D shard.
+// sides, slot 1 being the 3D shard.  xc (cross-attention 1 of a cached forward, sides 2D / 3D):
+// the 3D side's frame-independent half comes from the object cache -- QKV and the KV fold run
+// for the 2D side only, MLP conv 1 starts the 3D side from its cached accumulators.
 int attention_layer(const ApW& w, const Side* sd, int nside, int B, const Plan& p,
                     unsigned* cnt, hipStream_t st, int pm, const ShardCtx* sh,
-                    const LayerTiles& tl) {
+                    const LayerTiles& tl, const SideCache* xc = nullptr) {
   int rc;
   const int qkv_tile = tl.qkv;
   const int kv_rows = gemm_tile_rows(qkv_tile);
+  OP_REQUIRE(!xc || (nside == 2 && tl.fused_fold && !sh), "attention layer: cached cross half");
+  const int nsrc = xc ? 1 : nside;   // sides whose QKV and KV fold run here
   {  // 1. [q | k_h v_h ...]: phi(q) stored, per-chunk KV / ksum partials
     GemmArgs a;
-    a.nprob = nside;
-    for (int i = 0; i < nside; ++i) {
+    a.nprob = nsrc;
+    for (int i = 0; i < nsrc; ++i) {
       const Side& s = sd[i];
       a.p[i] = gemm_prob(s.x, 256, w.wqkv, 256, w.bqkv, s.phiq, 256, s.n, 768, 256, B);
       a.p[i].a0_bs = s.x_bs;
@@ -1269,13 +1442,15 @@ int attention_layer(const ApW& w, const Side* sd, int nside, int B, const Plan& 
     ka.ct = w.ct;
     ka.mf[0] = ka.mf[1] = nullptr;
     for (int i = 0; i < nside; ++i) {
-      ka.p[i] = {sd[i].kvpart, sd[i].kspart, ceil_div(sd[i].n, kv_rows)};
+      if (i < nsrc) ka.p[i] = {sd[i].kvpart, sd[i].kspart, ceil_div(sd[i].n, kv_rows)};
       ka.mf[sd[i].src] = p.mf + (size_t)i * B * 512 * 256;
     }
-    for (int i = 0; i < nside; ++i)
+    for (int i = 0; i < nsrc; ++i)
       OP_REQUIRE(ka.mf[i] != nullptr, "attention layer: source slot %d has no reader", i);
-    OP_LAUNCH(K_KV_REDUCE, st, kv_fold_kernel, dim3(nside * B * 65), dim3(1024), 0, st, ka, p.kv,
-              p.ksum, B);
+    prof_pre(K_KV_REDUCE, st);
+    launch_kv_fold(ka, nsrc, B, p.kv, p.ksum, st);
+    prof_post(K_KV_REDUCE, st);
+    OP_LAUNCHED();
   } else {  // separate reduce and fold; sharded: the 3D source's KV is summed over the ranks
             // before the fold
     KvArgs kva;
@@ -1324,6 +1499,16 @@ int attention_layer(const ApW& w, const Side* sd, int nside, int B, const Plan& 
       a.p[i].ksum = p.ksum + (size_t)s.src * B * 256;
       a.p[i].ksum_bs = 256;
       a.p[i].ns = sd[s.src].len;
+    }
+    if (xc) {   // the object's halves: shared by the batch (batch stride 0)
+      a.p[0].W1 = xc->mf;
+      a.p[0].w1_bs = 0;
+      a.p[0].ksum = xc->ksum;
+      a.p[0].ksum_bs = 0;
+      a.p[1].A1 = xc->phiq;
+      a.p[1].a1_bs = 0;
+      a.p[1].acc0 = xc->acc;
+      a.p[1].acc0_bs = 0;
     }
     if ((rc = gemm_launch(EPI_STATS, PRO_HEADZ, kTileMLP1, a, st, K_MLP1, pm)) != ONEPOSE_OK)
       return rc;
@@ -1407,12 +1592,17 @@ int match_impl(const void* packed_weights, const float* desc2d, int64_t desc2d_b
     if (kind == 0) {
       if (!cached3) {
         const dim3 ggrid(ceil_div(B * n3, 4));
+        // the object's stored leaf logits (one object for the whole batch: leaves stride 0)
+        const float* slog = obj_cache && leaves_bstride == 0 && gat >= 1
+                                ? obj_cache + (int64_t)n3 * 256 +
+                                      (int64_t)(gat - 1) * n3 * kLogitStride
+                                : nullptr;
         if (num_leaf <= 8)
           OP_LAUNCH(K_GAT, st, gat_kernel<8>, ggrid, dim3(256), 0, st, x3r, leaves,
-                    leaves_bstride, gat_weights(wbase, gat), p.x3[c3 ^ 1], n3, num_leaf, B);
+                    leaves_bstride, gat_weights(wbase, gat), slog, p.x3[c3 ^ 1], n3, num_leaf, B);
         else
           OP_LAUNCH(K_GAT, st, gat_kernel<16>, ggrid, dim3(256), 0, st, x3r, leaves,
-                    leaves_bstride, gat_weights(wbase, gat), p.x3[c3 ^ 1], n3, num_leaf, B);
+                    leaves_bstride, gat_weights(wbase, gat), slog, p.x3[c3 ^ 1], n3, num_leaf, B);
         x3r = p.x3[c3 ^ 1];
         c3 ^= 1;
       }
@@ -1431,6 +1621,14 @@ int match_impl(const void* packed_weights, const float* desc2d, int64_t desc2d_b
     int rc;
     if (cached3) {   // self-attention 1, 2D half (the 3D half is in the object cache)
       rc = attention_layer(w, sd, 1, B, p, lcnt, st, pm, sh, layer_tiles(qkv_n3, sd, 1, B, pm, sh));
+    } else if (obj_cache && layer == 2 && B <= kFusedFoldMaxBatch && !sh) {
+      // cross-attention 1: the 3D side's frame-independent half from the object cache (at
+      // these batches the grouped choices equal the object prefix's B = 1 ones)
+      const ObjLayout L = obj_layout(n3);
+      const SideCache xc = {obj_cache + L.phiq, obj_cache + L.acc, obj_cache + L.ksum,
+                            obj_cache + L.mf};
+      rc = attention_layer(w, sd, 2, B, p, lcnt, st, pm, nullptr,
+                           layer_tiles(qkv_n3, sd, 2, B, pm, false), &xc);
     } else {
       const LayerTiles tg = layer_tiles(qkv_n3, sd, 2, B, pm, sh);
       bool split = false;
@@ -1553,17 +1751,63 @@ int object_prepare_impl(const void* packed_weights, const float* desc3d, const f
     OP_LAUNCH(K_TRANSPOSE, st, transpose_in_kernel, dim3(ta.p[0].tiles), dim3(256), 0, st, ta, 1);
   }
   const dim3 ggrid(ceil_div(n3, 4));
-  if (num_leaf <= 8)
+  const float* nolog = nullptr;
+  float* slog = cache + (int64_t)n3 * 256;   // leaf logits of GAT layers 1-3
+  if (num_leaf <= 8) {
     OP_LAUNCH(K_GAT, st, gat_kernel<8>, ggrid, dim3(256), 0, st, p.x3[0], leaves_pm, (int64_t)0,
-              gat_weights(wbase, 0), p.x3[1], n3, num_leaf, 1);
-  else
+              gat_weights(wbase, 0), nolog, p.x3[1], n3, num_leaf, 1);
+    OP_LAUNCH(K_GAT, st, gat_logits_kernel<8>, ggrid, dim3(256), 0, st, leaves_pm,
+              gat_weights(wbase, 1), slog, n3, num_leaf);
+  } else {
     OP_LAUNCH(K_GAT, st, gat_kernel<16>, ggrid, dim3(256), 0, st, p.x3[0], leaves_pm, (int64_t)0,
-              gat_weights(wbase, 0), p.x3[1], n3, num_leaf, 1);
+              gat_weights(wbase, 0), nolog, p.x3[1], n3, num_leaf, 1);
+    OP_LAUNCH(K_GAT, st, gat_logits_kernel<16>, ggrid, dim3(256), 0, st, leaves_pm,
+              gat_weights(wbase, 1), slog, n3, num_leaf);
+  }
   const Side s3 = {p.x3[1], (int64_t)n3 * 256, cache, p.phiq3, p.kvpart3, p.kspart3, p.y13,
                    p.stats3, n3, (float)n3, 0, n3};
   const int pm = attention_pm(precision);
-  return attention_layer(ap_weights(wbase, 0), &s3, 1, 1, p, p.cnt, st, pm, nullptr,
-                         layer_tiles(n3, &s3, 1, 1, pm, false));
+  int rc = attention_layer(ap_weights(wbase, 0), &s3, 1, 1, p, p.cnt, st, pm, nullptr,
+                           layer_tiles(n3, &s3, 1, 1, pm, false));
+  if (rc != ONEPOSE_OK) return rc;
+
+  // Cross-attention 1 (layer 2), the 3D side's frame-independent half, with the choices a
+  // cached forward's layer 2 makes (batch <= kFusedFoldMaxBatch: QKV tile from n3 alone, one
+  // kv_fold launch), so that its bits are the ones the uncached forward computes in place.
+  const ObjLayout L = obj_layout(n3);
+  const ApW w = ap_weights(wbase, 1);
+  const Side x3 = {cache, 0, nullptr, cache + L.phiq, p.kvpart3, p.kspart3, nullptr, nullptr, n3,
+                   (float)n3, 0, n3};
+  const LayerTiles tl = layer_tiles(n3, &x3, 1, 1, pm, false);
+  {  // phi(q) into the cache; KV / sum phi(k) chunk partials
+    GemmArgs a;
+    a.nprob = 1;
+    a.p[0] = gemm_prob(cache, 256, w.wqkv, 256, w.bqkv, cache + L.phiq, 256, n3, 768, 256, 1);
+    a.p[0].vdiv = (float)n3;
+    a.p[0].kvpart = p.kvpart3;
+    a.p[0].kspart = p.kspart3;
+    if ((rc = gemm_launch(EPI_QKV, PRO_PLAIN, tl.qkv, a, st, K_QKV_GEMM, pm)) != ONEPOSE_OK)
+      return rc;
+  }
+  {  // sum phi(k) into the cache, and the 2D side's Mf = C KV_3D
+    KvFoldArgs ka;
+    ka.ct = w.ct;
+    ka.p[0] = {p.kvpart3, p.kspart3, ceil_div(n3, gemm_tile_rows(tl.qkv))};
+    ka.mf[0] = cache + L.mf;
+    ka.mf[1] = nullptr;
+    prof_pre(K_KV_REDUCE, st);
+    launch_kv_fold(ka, 1, 1, p.kv, cache + L.ksum, st);
+    prof_post(K_KV_REDUCE, st);
+    OP_LAUNCHED();
+  }
+  {  // MLP conv 1's x range: W1a x3 as raw accumulators of the TILE_64x64 MFMA sequence
+    GemmArgs a;
+    a.nprob = 1;
+    a.p[0] = gemm_prob(cache, 256, w.w1a, 256, nullptr, cache + L.acc, 512, n3, 512, 256, 1);
+    if ((rc = gemm_launch(EPI_ACC, PRO_PLAIN, kTileMLP1, a, st, K_MLP1, pm)) != ONEPOSE_OK)
+      return rc;
+  }
+  return ONEPOSE_OK;
 }
 
 int check_match_args(const void* packed_weights, const float* desc2d, const float* desc3d,
@@ -1691,7 +1935,7 @@ int onepose_match_prepared(const void* packed_weights, const float* desc2d,
 
 size_t onepose_object_cache_bytes(int n3) {
   if (n3 <= 0) return 0;
-  return (size_t)n3 * 256 * sizeof(float);
+  return (size_t)obj_layout(n3).total * sizeof(float);
 }
 
 size_t onepose_object_prepare_workspace_bytes(int n3, int num_leaf) {

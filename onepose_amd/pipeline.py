@@ -99,7 +99,7 @@ class FramePipeline:
         # computed once: every frame starts from it (onepose_match_cached, bit-identical)
         self.object_cache = None
         if object_cache:
-            self.object_cache = torch.empty(self.n3 * 256, **f32)
+            self.object_cache = torch.empty(self.lib.onepose_object_cache_bytes(self.n3) // 4, **f32)
             wsb = self.lib.onepose_object_prepare_workspace_bytes(self.n3, self.L)
             ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
             _lib.check(self.lib.onepose_object_prepare(
