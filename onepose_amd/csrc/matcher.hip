@@ -847,16 +847,19 @@ __device__ __forceinline__ unsigned long long shfl_xor_u64(unsigned long long v,
 }
 
 // conf = softmax(S, dim=1) * softmax(S, dim=2) (GATs_SuperGlue.py:253) in place over S,
-// plus row/column max+argmax (:256) folded in through 64-bit atomicMax.  Workgroup = 32 rows
-// (2D) x 256 columns (3D); wave w owns rows 8w..8w+7, lane l owns 4 columns (16-byte loads
-// when n3 % 4 == 0), all loads issued before any use.  Row winners: in-wave reduction, one
-// atomic per row per workgroup; column winners: per thread over its rows, then over the four
-// waves in LDS, one atomic per column per workgroup.
+// plus row/column max+argmax (:256).  Workgroup = 32 rows (2D) x 256 columns (3D); wave w owns
+// rows 8w..8w+7, lane l owns 4 columns (16-byte loads when n3 % 4 == 0), all loads issued
+// before any use.  Row winners: in-wave reduction, then lane i stores row i's winner over the
+// workgroup's 256 columns to rowpart[b][row][column tile] (plain stores; the consumers take
+// the max over the ceil(n3 / 256) parts).  A 64-bit atomicMax per row and workgroup instead
+// cost ~3.5 of the kernel's 12.5 us alone (tools/conf_probe.hip: 16 workgroups meet at each
+// row's word).  Column winners: per thread over its rows, then over the four waves in LDS,
+// one atomicMax per column per workgroup (~0.5 us).
 template <bool VEC>
 __global__ __launch_bounds__(256) void conf_kernel(float* S, int n1, int n3,
                                                    const float* rowmax, const float* rowsum,
                                                    const float* colmax, const float* colsum,
-                                                   unsigned long long* rowbest,
+                                                   unsigned long long* rowpart,
                                                    unsigned long long* colbest, int write_conf,
                                                    int col_offset) {
   __shared__ unsigned long long cb[4][256];
@@ -896,6 +899,7 @@ __global__ __launch_bounds__(256) void conf_kernel(float* S, int n1, int n3,
   // (0 = none yet; bits + 1 does not wrap for any conf the kernel can produce).
   unsigned cbu[4] = {0u, 0u, 0u, 0u};
   int cbi[4] = {0, 0, 0, 0};
+  unsigned long long rkey = 0ull;   // lane i: row 8 wave + i's winner
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     const int n = tiler * 32 + wave * 8 + i;
@@ -928,7 +932,11 @@ __global__ __launch_bounds__(256) void conf_kernel(float* S, int n1, int n3,
       const unsigned long long other = shfl_xor_u64(key, o);
       key = other > key ? other : key;
     }
-    if (lane == 0 && key != 0ull) atomicMax(rowbest + (int64_t)b * n1 + n, key);
+    rkey = lane == i ? key : rkey;
+  }
+  {
+    const int n = tiler * 32 + wave * 8 + lane;
+    if (lane < 8 && n < n1) rowpart[((int64_t)b * n1 + n) * ct + tilec] = rkey;
   }
 #pragma unroll
   for (int j = 0; j < 4; ++j)
@@ -946,7 +954,26 @@ __global__ __launch_bounds__(256) void conf_kernel(float* S, int n1, int n3,
 }
 
 // Mutual nearest neighbour + threshold (GATs_SuperGlue.py:256-267).
+// A row's winner over all columns: the max of its conf_kernel parts (ct of them).
+__device__ __forceinline__ unsigned long long row_best(const unsigned long long* rowpart, int ct,
+                                                       int64_t row) {
+  const unsigned long long* q = rowpart + row * ct;
+  unsigned long long k = q[0];
+  for (int i = 1; i < ct; ++i) k = q[i] > k ? q[i] : k;
+  return k;
+}
+
+// rowbest[row] = max of the row's parts (the sharded path's exchange sends whole-row winners)
+__global__ __launch_bounds__(256) void rowbest_reduce_kernel(const unsigned long long* rowpart,
+                                                             int ct, int64_t rows,
+                                                             unsigned long long* rowbest) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < rows) rowbest[i] = row_best(rowpart, ct, i);
+}
+
+// rowpart != null: the row winners are conf_kernel's parts (ct per row); else rowbest.
 __global__ __launch_bounds__(256) void mutual_kernel(const unsigned long long* rowbest,
+                                                     const unsigned long long* rowpart, int ct,
                                                      const unsigned long long* colbest,
                                                      int batch, int n1, int n3, float thr,
                                                      int64_t* matches0, int64_t* matches1,
@@ -955,7 +982,7 @@ __global__ __launch_bounds__(256) void mutual_kernel(const unsigned long long* r
   const int64_t nr = (int64_t)batch * n1, nc = (int64_t)batch * n3;
   if (idx < nr) {
     const int b = (int)(idx / n1), n = (int)(idx - (int64_t)b * n1);
-    const unsigned long long p = rowbest[idx];
+    const unsigned long long p = rowpart ? row_best(rowpart, ct, idx) : rowbest[idx];
     const int i0 = min(max(best_index(p), 0), n3 - 1);
     const float v = best_value(p);
     const int i1 = best_index(colbest[(int64_t)b * n3 + i0]);
@@ -967,7 +994,8 @@ __global__ __launch_bounds__(256) void mutual_kernel(const unsigned long long* r
     const int64_t j = idx - nr;
     const int b = (int)(j / n3), m = (int)(j - (int64_t)b * n3);
     const int i1 = min(max(best_index(colbest[j]), 0), n1 - 1);
-    const unsigned long long p = rowbest[(int64_t)b * n1 + i1];
+    const int64_t r1 = (int64_t)b * n1 + i1;
+    const unsigned long long p = rowpart ? row_best(rowpart, ct, r1) : rowbest[r1];
     const bool mutual = best_index(p) == m;
     const float v = best_value(p);
     const float s = mutual ? v : 0.f;
@@ -994,6 +1022,7 @@ struct Plan {
   float *f2, *f3, *s;
   float *rowpart, *colpart, *rowmax, *rowsum, *colmax, *colsum;
   unsigned long long *rowbest, *colbest;
+  unsigned long long* rowwin;    // [B][n1][ceil(n3 / 256)] conf_kernel's row winners per column tile
   float* leaves_pm;   // point-major copy of the leaves (onepose_match only)
   size_t bytes;
 };
@@ -1044,6 +1073,7 @@ Plan make_plan(void* ws, int B, int n1, int n3, int L, bool with_conf) {
   p.colmax = c.take<float>(t3);
   p.colsum = c.take<float>(t3);
   p.rowbest = c.take<unsigned long long>(t2);
+  p.rowwin = c.take<unsigned long long>(t2 * (size_t)ceil_div(n3, 256));
   p.colbest = c.take<unsigned long long>(t3);
   p.leaves_pm = c.take<float>(t3 * L * 256);
   p.bytes = align_up(c.off, 256);
@@ -1703,13 +1733,17 @@ int match_impl(const void* packed_weights, const float* desc2d, int64_t desc2d_b
     const dim3 cgrid(ceil_div(n1, 32) * ceil_div(n3, 256), B);
     if (n3 % 4 == 0)
       OP_LAUNCH(K_CONF, st, conf_kernel<true>, cgrid, dim3(256), 0, st, S, n1, n3, p.rowmax,
-                p.rowsum, p.colmax, p.colsum, p.rowbest, p.colbest, with_conf ? 1 : 0, coff);
+                p.rowsum, p.colmax, p.colsum, p.rowwin, p.colbest, with_conf ? 1 : 0, coff);
     else
       OP_LAUNCH(K_CONF, st, conf_kernel<false>, cgrid, dim3(256), 0, st, S, n1, n3, p.rowmax,
-                p.rowsum, p.colmax, p.colsum, p.rowbest, p.colbest, with_conf ? 1 : 0, coff);
+                p.rowsum, p.colmax, p.colsum, p.rowwin, p.colbest, with_conf ? 1 : 0, coff);
     const unsigned long long* colbest = p.colbest;
+    const unsigned long long* rowwin = p.rowwin;
     if (sh) {   // row winners over all columns; every rank's column winners at global columns
-      OP_HIP(hipMemcpyAsync(sh->send, p.rowbest, nr * 8, hipMemcpyDeviceToDevice, st));
+      OP_LAUNCH(K_MUTUAL, st, rowbest_reduce_kernel, dim3((unsigned)((nr + 255) / 256)), dim3(256),
+                0, st, p.rowwin, ceil_div(n3, 256), nr,
+                reinterpret_cast<unsigned long long*>(sh->send));
+      rowwin = nullptr;
       if ((rc = shard_exchange(*sh, nr * 8, st)) != ONEPOSE_OK) return rc;
       OP_LAUNCH(K_MUTUAL, st, best_max_kernel, dim3((unsigned)((nr + 255) / 256)), dim3(256), 0, st,
                 reinterpret_cast<const unsigned long long*>(sh->recv), sh->world, nr, nr,
@@ -1727,7 +1761,8 @@ int match_impl(const void* packed_weights, const float* desc2d, int64_t desc2d_b
     }
     const int64_t tot_g = (int64_t)B * (n1 + n3g);
     OP_LAUNCH(K_MUTUAL, st, mutual_kernel, dim3((unsigned)((tot_g + 255) / 256)), dim3(256), 0, st,
-                       p.rowbest, colbest, B, n1, n3g, match_threshold, matches0, matches1,
+                       p.rowbest, rowwin, ceil_div(n3, 256), colbest, B, n1, n3g,
+                       match_threshold, matches0, matches1,
                        mscores0, mscores1);
   }
   return ONEPOSE_OK;
