@@ -8,7 +8,7 @@
 #include <random>
 #include <vector>
 
-enum { NO_ROW_ATOMIC = 1, NO_COL_ATOMIC = 2, NO_WRITE = 4, NO_EXP = 8, NO_LOAD = 16, ROW_BATCH = 32 };
+enum { NO_ROW_ATOMIC = 1, NO_COL_ATOMIC = 2, NO_WRITE = 4, NO_EXP = 8, NO_LOAD = 16, ROW_BATCH = 32, NT_LOAD = 64, NT_STORE = 128 };
 
 __device__ __forceinline__ unsigned long long pack_best(float v, int idx) {
   return ((unsigned long long)__float_as_uint(v) << 32) | (unsigned)(0xFFFFFFFFu - (unsigned)idx);
@@ -43,7 +43,9 @@ __global__ __launch_bounds__(256) void conf_v(float* S, int n1, int n3, const fl
     if (F & NO_LOAD) {
       v[i][0] = v[i][1] = v[i][2] = v[i][3] = (float)(n & 7) * 0.01f;
     } else {
-      const float4 q = *reinterpret_cast<const float4*>(S + (int64_t)n * n3 + col[0]);
+      typedef float fv4 __attribute__((ext_vector_type(4)));
+      const fv4* ap = reinterpret_cast<const fv4*>(S + (int64_t)n * n3 + col[0]);
+      const fv4 q = (F & NT_LOAD) ? __builtin_nontemporal_load(ap) : *ap;
       v[i][0] = q.x; v[i][1] = q.y; v[i][2] = q.z; v[i][3] = q.w;
     }
   }
@@ -67,8 +69,13 @@ __global__ __launch_bounds__(256) void conf_v(float* S, int n1, int n3, const fl
       if (u > ru) { ru = u; ri = col[j]; }
       if (u > cbu[j]) { cbu[j] = u; cbi[j] = n; }
     }
-    if (!(F & NO_WRITE))
-      *reinterpret_cast<float4*>(S + (int64_t)n * n3 + col[0]) = make_float4(c[0], c[1], c[2], c[3]);
+    if (!(F & NO_WRITE)) {
+      typedef float fv4 __attribute__((ext_vector_type(4)));
+      fv4* sp = reinterpret_cast<fv4*>(S + (int64_t)n * n3 + col[0]);
+      const fv4 o = {c[0], c[1], c[2], c[3]};
+      if (F & NT_STORE) __builtin_nontemporal_store(o, sp);
+      else *sp = o;
+    }
     unsigned long long key = ru ? pack_best(__uint_as_float(ru - 1u), ri) : 0ull;
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) {
@@ -142,6 +149,10 @@ int main() {
     run<0, 4>("as built, 16-row tiles", S, n1, n3, drm, drs, dcm, dcs, rb, cb);
     run<0, 16>("as built, 64-row tiles", S, n1, n3, drm, drs, dcm, dcs, rb, cb);
     run<NO_ROW_ATOMIC | NO_COL_ATOMIC, 8>("in place, no atomics", S, n1, n3, drm, drs, dcm, dcs, rb, cb);
+    run<NT_LOAD, 8>("nt loads", S, n1, n3, drm, drs, dcm, dcs, rb, cb);
+    run<NT_STORE, 8>("nt stores", S, n1, n3, drm, drs, dcm, dcs, rb, cb);
+    run<NT_LOAD | NT_STORE, 8>("nt loads + stores", S, n1, n3, drm, drs, dcm, dcs, rb, cb);
+    run<NO_ROW_ATOMIC | NT_LOAD | NT_STORE, 8>("nt, no row atomics", S, n1, n3, drm, drs, dcm, dcs, rb, cb);
     run<ROW_BATCH, 8>("row atomics batched", S, n1, n3, drm, drs, dcm, dcs, rb, cb);
     run<ROW_BATCH, 4>("row atomics batched", S, n1, n3, drm, drs, dcm, dcs, rb, cb);
     run<ROW_BATCH, 16>("row atomics batched", S, n1, n3, drm, drs, dcm, dcs, rb, cb);
