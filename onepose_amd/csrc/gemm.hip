@@ -576,9 +576,15 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
     // Every store and load of the handed-off partials is sc1, so neither an agent-scope
     // release (it would write back the XCD's L2, this tile's Y in it) nor an acquire (an L1
     // invalidate, ~1.7 us) is needed.  The counters are zeroed by the forward's first kernel.
+#ifdef ONEPOSE_GEMM_PROBE_NOFINAL   // (probe: partials only; stale mean / rstd)
+    unsigned* tickets = nullptr;
+#else
     unsigned* tickets = F(st_cnt);
+#endif
     if (tickets != nullptr) {
+#ifndef ONEPOSE_GEMM_PROBE_NODRAIN   // (probe: ticket without draining the partial stores)
       if (t < BN) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the storing wave drains
+#endif
       __syncthreads();   // partial stores drained; `part` no longer read
       int* last = reinterpret_cast<int*>(part);
       if (t == 0) {
@@ -587,7 +593,11 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
         last[0] = ticket == (unsigned)(mtiles - 1) ? 1 : 0;
       }
       __syncthreads();
+#ifdef ONEPOSE_GEMM_PROBE_NOREDUCE   // (probe: tickets taken, the last tile reduces nothing)
+      if (false) {
+#else
       if (last[0]) {
+#endif
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // (no instruction: keeps the
                                                                  // loads below the ticket)
         // one pass over the partials (sc1 loads, 16 tiles in flight per thread), shifted by
