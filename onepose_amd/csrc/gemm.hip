@@ -651,27 +651,39 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
     }
   }
   if (EPI == EPI_SCORE) {
+    // Per-tile softmax partials, (max, sum exp) of every row over the tile's columns and of
+    // every column over its rows.  Four threads per row (then per column) take 16 entries
+    // each; the quarters are combined by lane butterflies ((q0 + q1) + (q2 + q3), fixed
+    // order).  Reads of the staged tile are bank-conflict free both ways (pitch BN + 1).
+    static_assert(EPI != EPI_SCORE || (BM == 64 && BN == 64 && T::NT == 256), "score tile");
     const int cols = min(BN, N - n0);
-    if (t < BM) {
-      if (t < rows) {   // row partial over this tile's columns
-        float mx = -INFINITY;
-        for (int cc = 0; cc < cols; ++cc) mx = fmaxf(mx, tile[t * TP + cc]);
-        float s = 0.f;
-        for (int cc = 0; cc < cols; ++cc) s += expf(tile[t * TP + cc] - mx);
-        float* o = F(rowstat) + (((int64_t)b * M + m0 + t) * ntiles + nt) * 2;
-        o[0] = mx;
-        o[1] = s;
+    const int line = t >> 2, qtr = t & 3, lo = qtr * 16;
+    auto partial = [&](const float* base, int stride, int count) __attribute__((always_inline)) {
+      const int hi = min(lo + 16, count);
+      float mx = -INFINITY;
+      for (int i = lo; i < hi; ++i) mx = fmaxf(mx, base[i * stride]);
+      mx = fmaxf(mx, __shfl_xor(mx, 1, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 2, 64));
+      float s = 0.f;
+      for (int i = lo; i < hi; ++i) s += expf(base[i * stride] - mx);
+      s += __shfl_xor(s, 1, 64);
+      s += __shfl_xor(s, 2, 64);
+      return make_float2(mx, s);
+    };
+    {   // row `line` over this tile's columns
+      const float2 r = partial(tile + line * TP, 1, cols);
+      if (qtr == 0 && line < rows) {
+        float* o = F(rowstat) + (((int64_t)b * M + m0 + line) * ntiles + nt) * 2;
+        o[0] = r.x;
+        o[1] = r.y;
       }
-    } else if (t < BM + BN) {
-      const int cc = t - BM;
-      if (cc < cols) {   // column partial over this tile's rows
-        float mx = -INFINITY;
-        for (int rr = 0; rr < rows; ++rr) mx = fmaxf(mx, tile[rr * TP + cc]);
-        float s = 0.f;
-        for (int rr = 0; rr < rows; ++rr) s += expf(tile[rr * TP + cc] - mx);
-        float* o = F(colstat) + (((int64_t)b * N + n0 + cc) * mtiles + mt) * 2;
-        o[0] = mx;
-        o[1] = s;
+    }
+    {   // column `line` over this tile's rows
+      const float2 r = partial(tile + line, TP, rows);
+      if (qtr == 0 && line < cols) {
+        float* o = F(colstat) + (((int64_t)b * N + n0 + line) * mtiles + mt) * 2;
+        o[0] = r.x;
+        o[1] = r.y;
       }
     }
   }
