@@ -47,10 +47,10 @@ def superpoint_conv_flops(h, w):
 
 
 def cross_cached(cached, B):
-    """Whether the object cache also holds cross-attention 1's frame-independent 3D half
-    (the 3D side's q / k / v projections, KV and the x range of its MLP conv 1): the cached
-    forward uses it at batches <= 4 (matcher.hip, kFusedFoldMaxBatch)."""
-    return cached and B <= 4
+    """Whether the cached forward also takes cross-attention 1's frame-independent 3D half
+    (the 3D side's q / k / v projections, KV and the x range of its MLP conv 1) from the
+    object cache: at every batch (matcher.hip, side_tiles)."""
+    return cached
 
 
 def frame_flops(n1, n3, L, cached, B=1):

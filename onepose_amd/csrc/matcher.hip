@@ -1372,35 +1372,61 @@ struct Side {
                 // so that every rank picks the same tiles and rounds alike)
 };
 
-// Per-launch choices of one attention layer that change the summation order.  A side's bits
-// depend on them (and on nothing else about the launch), so launches whose results must agree
-// bit for bit -- the object prefix and the uncached forward's layer 1, every rank of a sharded
-// frame -- are given the same choices (layer_tiles over the same sides, batch and qkv_n3).
+// Choices of one attention layer that change a side's summation order: the QKV tile of the
+// side (its rows are the side's KV chunk length), kv_fold vs kv_reduce + m_fold for the side as
+// a source slot, and the MLP-conv-2 tile of the side.  A side's bits depend on these (and on
+// nothing else about the launches), so launches whose results must agree bit for bit get the
+// same choices: the object prefix (B = 1) and the 3D side of layers 1-2 in every forward; a
+// cached and an uncached forward's 2D side; every rank of a sharded frame.  attention_layer
+// groups the sides with equal choices into one launch per step.
 struct LayerTiles {
-  int qkv;          // QKV GEMM tile (its rows are the KV chunk length)
-  bool fused_fold;  // kv_fold (one launch) vs kv_reduce + m_fold
-  int mlp2;         // MLP conv 2 tile
+  int qkv[2];
+  bool fused_fold[2];   // indexed by source slot (= side index)
+  int mlp2[2];
 };
 
+int mlp2_tile_for(int64_t t64, int pm) {
+  // fp32: the 64x32 K-split tile doubles the workgroup count where 64x64 tiles would leave
+  // CUs idle (config 2: 320 -> 640 tiles, 23.2 -> 19.7 us); with >= 4 tiles per CU anyway
+  // (batched configs) 64x64 moves less data per FLOP (config 3: 9.5 vs 12.3 ms per step)
+  return pm == PM_F32 && t64 < kMlp2WideTiles ? kTileMLP2F32 : kTileMLP2;
+}
+
+// Every side the same choices, from the launch as a whole (layers 4-11, sharded frames).
 LayerTiles layer_tiles(int qkv_n3, const Side* sd, int nside, int B, int pm, bool sharded) {
   LayerTiles t;
-  t.qkv = pm == PM_F32 ? qkv_tile_for(qkv_n3, B) : kTileKV;
+  const int q = pm == PM_F32 ? qkv_tile_for(qkv_n3, B) : kTileKV;
   // kv_fold re-reads the whole 128 KB C_h panel per workgroup (64 of them per side and
   // sample): one launch instead of two pays at small batches; at B = 32 the separate MFMA
   // m_fold (16 KB of C per workgroup) is cheaper (config 3: 1.68 vs 2.02 ms per step).
   // Sharded: the 3D source's KV is summed over the ranks between the two.
-  t.fused_fold = !sharded && B <= kFusedFoldMaxBatch;
-  // fp32: the 64x32 K-split tile doubles the workgroup count where 64x64 tiles would leave
-  // CUs idle (config 2: 320 -> 640 tiles, 23.2 -> 19.7 us); with >= 4 tiles per CU anyway
-  // (batched configs) 64x64 moves less data per FLOP (config 3: 9.5 vs 12.3 ms per step)
+  const bool fused = !sharded && B <= kFusedFoldMaxBatch;
   int64_t t64 = 0;
   for (int i = 0; i < nside; ++i) t64 += (int64_t)ceil_div(sd[i].ntile, 64) * 4 * B;
-  t.mlp2 = pm == PM_F32 && t64 < kMlp2WideTiles ? kTileMLP2F32 : kTileMLP2;
+  const int m2 = mlp2_tile_for(t64, pm);
+  for (int i = 0; i < 2; ++i) {
+    t.qkv[i] = q;
+    t.fused_fold[i] = fused;
+    t.mlp2[i] = m2;
+  }
   return t;
 }
 
-bool same_tiles(const LayerTiles& a, const LayerTiles& b) {
-  return a.qkv == b.qkv && a.fused_fold == b.fused_fold && a.mlp2 == b.mlp2;
+// Layers 1-2 of a whole frame: each side by itself.  The 3D side takes the object prefix's
+// choices (B = 1, so the cache serves any batch), the 2D side those of its tokens alone (a
+// 2D-only launch of 1024 tokens gets 32-row QKV tiles: 192 workgroups instead of 96).  Cross-
+// attention 1 runs both sides' MLP conv 2 in one launch (its 3D half is per frame), so both
+// take the choice over both sides there.
+LayerTiles side_tiles(int n1, int n3, int B, int pm, bool cross) {
+  LayerTiles t;
+  t.qkv[0] = pm == PM_F32 ? qkv_tile_for(n1, B) : kTileKV;
+  t.qkv[1] = pm == PM_F32 ? qkv_tile_for(n3, 1) : kTileKV;
+  t.fused_fold[0] = B <= kFusedFoldMaxBatch;
+  t.fused_fold[1] = true;
+  const int64_t t2 = (int64_t)ceil_div(n1, 64) * 4 * B, t3 = (int64_t)ceil_div(n3, 64) * 4;
+  t.mlp2[0] = mlp2_tile_for(cross ? t2 + t3 * B : t2, pm);
+  t.mlp2[1] = cross ? t.mlp2[0] : mlp2_tile_for(t3, pm);
+  return t;
 }
 
 // Object cache layout (floats; onepose_object_cache_bytes): the 3D state entering layer 2,
@@ -1438,75 +1464,102 @@ void launch_kv_fold(const KvFoldArgs& ka, int nslot, int B, float* kv, float* ks
 #endif
 }
 
-// AttentionPropagation (GATs_SuperGlue.py:123-132) for 1 or 2 sides in grouped launches.
-// Each side's arithmetic is independent of the others' (per-problem tiles, per-slot
-// reductions), so a side gives the same bits alone or grouped.  Sharded runs have two
-// sides, slot 1 being the 3D shard.  xc (cross-attention 1 of a cached forward, sides 2D / 3D):
-// the 3D side's frame-independent half comes from the object cache -- QKV and the KV fold run
-// for the 2D side only, MLP conv 1 starts the 3D side from its cached accumulators.
+// AttentionPropagation (GATs_SuperGlue.py:123-132) for 1 or 2 sides, grouped into one launch
+// per step wherever the sides' choices (LayerTiles) agree.  Each side's arithmetic is
+// independent of the others' (per-problem tiles, per-slot reductions), so a side gives the
+// same bits alone or grouped.  Sharded runs have two sides, slot 1 being the 3D shard.
+// xc (cross-attention 1 of a cached forward, sides 2D / 3D): the 3D side's frame-independent
+// half comes from the object cache -- QKV and the KV fold run for the 2D side only, MLP conv 1
+// starts the 3D side from its cached accumulators.
 int attention_layer(const ApW& w, const Side* sd, int nside, int B, const Plan& p,
                     unsigned* cnt, hipStream_t st, int pm, const ShardCtx* sh,
                     const LayerTiles& tl, const SideCache* xc = nullptr) {
   int rc;
-  const int qkv_tile = tl.qkv;
-  const int kv_rows = gemm_tile_rows(qkv_tile);
-  OP_REQUIRE(!xc || (nside == 2 && tl.fused_fold && !sh), "attention layer: cached cross half");
+  OP_REQUIRE(!xc || (nside == 2 && !sh), "attention layer: cached cross half");
+  OP_REQUIRE(!sh || (!tl.fused_fold[0] && !tl.fused_fold[1] && tl.qkv[0] == tl.qkv[1]),
+             "attention layer: sharded choices");
   const int nsrc = xc ? 1 : nside;   // sides whose QKV and KV fold run here
-  {  // 1. [q | k_h v_h ...]: phi(q) stored, per-chunk KV / ksum partials
+  // sides [i0, i1) with equal choices form one launch
+  auto groups = [&](int n, auto same, auto body) -> int {
+    for (int i0 = 0; i0 < n;) {
+      int i1 = i0 + 1;
+      while (i1 < n && same(i0, i1)) ++i1;
+      const int r = body(i0, i1);
+      if (r != ONEPOSE_OK) return r;
+      i0 = i1;
+    }
+    return ONEPOSE_OK;
+  };
+  // 1. [q | k_h v_h ...]: phi(q) stored, per-chunk KV / ksum partials
+  rc = groups(nsrc, [&](int a, int b) { return tl.qkv[a] == tl.qkv[b]; }, [&](int i0, int i1) -> int {
     GemmArgs a;
-    a.nprob = nsrc;
-    for (int i = 0; i < nsrc; ++i) {
+    a.nprob = i1 - i0;
+    for (int i = i0; i < i1; ++i) {
       const Side& s = sd[i];
-      a.p[i] = gemm_prob(s.x, 256, w.wqkv, 256, w.bqkv, s.phiq, 256, s.n, 768, 256, B);
-      a.p[i].a0_bs = s.x_bs;
-      a.p[i].vdiv = s.len;
-      a.p[i].kvpart = s.kvpart;
-      a.p[i].kspart = s.kspart;
-      a.p[i].y_bs = (int64_t)s.n * 256;
+      GemmProb& g = a.p[i - i0];
+      g = gemm_prob(s.x, 256, w.wqkv, 256, w.bqkv, s.phiq, 256, s.n, 768, 256, B);
+      g.a0_bs = s.x_bs;
+      g.vdiv = s.len;
+      g.kvpart = s.kvpart;
+      g.kspart = s.kspart;
+      g.y_bs = (int64_t)s.n * 256;
     }
-    if ((rc = gemm_launch(EPI_QKV, PRO_PLAIN, qkv_tile, a, st, K_QKV_GEMM, pm)) != ONEPOSE_OK)
-      return rc;
-  }
-  if (tl.fused_fold) {  // 2+3. KV[slot], ksum[slot] and the folded message weights, one launch
-    KvFoldArgs ka;
-    ka.ct = w.ct;
-    ka.mf[0] = ka.mf[1] = nullptr;
-    for (int i = 0; i < nside; ++i) {
-      if (i < nsrc) ka.p[i] = {sd[i].kvpart, sd[i].kspart, ceil_div(sd[i].n, kv_rows)};
-      ka.mf[sd[i].src] = p.mf + (size_t)i * B * 512 * 256;
+    return gemm_launch(EPI_QKV, PRO_PLAIN, tl.qkv[i0], a, st, K_QKV_GEMM, pm);
+  });
+  if (rc != ONEPOSE_OK) return rc;
+  // 2+3. KV[slot], ksum[slot] and the folded message weights Mf of the side attending to the
+  // slot: kv_fold (one launch), or kv_reduce + m_fold (sharded: the 3D source's KV is summed
+  // over the ranks between the two).  A launch over slots [i0, i1) writes their KV / ksum at
+  // their own slot offsets.
+  int reader[2] = {-1, -1};   // the side attending to slot i
+  for (int i = 0; i < nside; ++i) reader[sd[i].src] = i;
+  for (int i = 0; i < nsrc; ++i)
+    OP_REQUIRE(reader[i] >= 0, "attention layer: source slot %d has no reader", i);
+  auto mf_of = [&](int side) { return p.mf + (size_t)side * B * 512 * 256; };
+  auto chunks = [&](int i) { return ceil_div(sd[i].n, gemm_tile_rows(tl.qkv[i])); };
+  rc = groups(nsrc, [&](int a, int b) { return tl.fused_fold[a] == tl.fused_fold[b]; },
+              [&](int i0, int i1) -> int {
+    float* kv = p.kv + (size_t)i0 * B * 16384;
+    float* ksum = p.ksum + (size_t)i0 * B * 256;
+    const int ns = i1 - i0;
+    if (tl.fused_fold[i0]) {
+      KvFoldArgs ka;
+      ka.ct = w.ct;
+      for (int i = i0; i < i1; ++i) {
+        ka.p[i - i0] = {sd[i].kvpart, sd[i].kspart, chunks(i)};
+        ka.mf[i - i0] = mf_of(reader[i]);
+      }
+      prof_pre(K_KV_REDUCE, st);
+      launch_kv_fold(ka, ns, B, kv, ksum, st);
+      prof_post(K_KV_REDUCE, st);
+      OP_LAUNCHED();
+      return (int)ONEPOSE_OK;
     }
-    for (int i = 0; i < nsrc; ++i)
-      OP_REQUIRE(ka.mf[i] != nullptr, "attention layer: source slot %d has no reader", i);
-    prof_pre(K_KV_REDUCE, st);
-    launch_kv_fold(ka, nsrc, B, p.kv, p.ksum, st);
-    prof_post(K_KV_REDUCE, st);
-    OP_LAUNCHED();
-  } else {  // separate reduce and fold; sharded: the 3D source's KV is summed over the ranks
-            // before the fold
     KvArgs kva;
-    for (int i = 0; i < nside; ++i)
-      kva.p[i] = {sd[i].kvpart, sd[i].kspart, ceil_div(sd[i].n, kv_rows)};
-    OP_LAUNCH(K_KV_REDUCE, st, kv_reduce_kernel, dim3(nside * B * 65), dim3(256), 0, st, kva,
-              p.kv, p.ksum, B);
-    if (sh) {   // the 3D side's KV / sum phi(k) over every rank's points
+    for (int i = i0; i < i1; ++i) kva.p[i - i0] = {sd[i].kvpart, sd[i].kspart, chunks(i)};
+    OP_LAUNCH(K_KV_REDUCE, st, kv_reduce_kernel, dim3(ns * B * 65), dim3(256), 0, st, kva, kv,
+              ksum, B);
+    if (sh && i1 == 2) {   // the 3D side's KV / sum phi(k) over every rank's points
       const int64_t nkv = (int64_t)B * 16384, nks = (int64_t)B * 256;
       OP_HIP(hipMemcpyAsync(sh->send, p.kv + nkv, nkv * 4, hipMemcpyDeviceToDevice, st));
       OP_HIP(hipMemcpyAsync(sh->send + nkv * 4, p.ksum + nks, nks * 4, hipMemcpyDeviceToDevice,
                             st));
-      if ((rc = shard_exchange(*sh, (nkv + nks) * 4, st)) != ONEPOSE_OK) return rc;
+      int r = shard_exchange(*sh, (nkv + nks) * 4, st);
+      if (r != ONEPOSE_OK) return r;
       const float* rv = reinterpret_cast<const float*>(sh->recv);
       OP_LAUNCH(K_KV_REDUCE, st, shard_sum_kernel, dim3((unsigned)ceil_div((int)nkv, 256)),
                 dim3(256), 0, st, rv, sh->world, nkv + nks, (int64_t)0, nkv, p.kv + nkv);
       OP_LAUNCH(K_KV_REDUCE, st, shard_sum_kernel, dim3((unsigned)ceil_div((int)nks, 256)),
                 dim3(256), 0, st, rv, sh->world, nkv + nks, nkv, nks, p.ksum + nks);
     }
-    // 3. folded message weights per side
-    FoldArgs fa;
+    FoldArgs fa;   // Mf of the sides attending to these slots
     fa.c = w.c;
-    for (int i = 0; i < nside; ++i)
-      fa.p[i] = {p.kv + (size_t)sd[i].src * B * 16384, p.mf + (size_t)i * B * 512 * 256};
-    OP_LAUNCH(K_MFOLD, st, m_fold_kernel, dim3(nside * B * 32), dim3(256), 0, st, fa, B);
-  }
+    for (int i = i0; i < i1; ++i)
+      fa.p[i - i0] = {p.kv + (size_t)i * B * 16384, mf_of(reader[i])};
+    OP_LAUNCH(K_MFOLD, st, m_fold_kernel, dim3(ns * B * 32), dim3(256), 0, st, fa, B);
+    return (int)ONEPOSE_OK;
+  });
+  if (rc != ONEPOSE_OK) return rc;
   {  // 4. MLP conv 1 on [x ; phi(q)] with [W1a | Mf], the phi(q) heads scaled by Z * Ns
      //    in-kernel (PRO_HEADZ), + InstanceNorm partials
     GemmArgs a;
@@ -1519,7 +1572,7 @@ int attention_layer(const ApW& w, const Side* sd, int nside, int B, const Plan& 
       a.p[i].lda1 = 256;
       a.p[i].a1_bs = (int64_t)s.n * 256;
       a.p[i].ksplit = 256;
-      a.p[i].W1 = p.mf + (size_t)i * B * 512 * 256;
+      a.p[i].W1 = mf_of(i);
       a.p[i].ldw1 = 256;
       a.p[i].w1_bs = 512 * 256;
       a.p[i].stats = s.stats;
@@ -1561,24 +1614,23 @@ int attention_layer(const ApW& w, const Side* sd, int nside, int B, const Plan& 
                 p.mean + (size_t)B * 512, p.rstd + (size_t)B * 512);
     }
   }
-  {  // 6. MLP conv 2 on ReLU(InstanceNorm(.)) + residual: desc + delta
+  // 6. MLP conv 2 on ReLU(InstanceNorm(.)) + residual: desc + delta
+  return groups(nside, [&](int a, int b) { return tl.mlp2[a] == tl.mlp2[b]; }, [&](int i0, int i1) -> int {
     GemmArgs a;
-    a.nprob = nside;
-    for (int i = 0; i < nside; ++i) {
+    a.nprob = i1 - i0;
+    for (int i = i0; i < i1; ++i) {
       const Side& s = sd[i];
-      a.p[i] = gemm_prob(s.y1, 512, w.w2, 512, w.b2, s.xo, 256, s.n, 256, 512, B);
-      a.p[i].R = s.x;
-      a.p[i].ldr = 256;
-      a.p[i].r_bs = s.x_bs;
-      a.p[i].pro_mean = p.mean + (size_t)i * B * 512;
-      a.p[i].pro_rstd = p.rstd + (size_t)i * B * 512;
-      a.p[i].pro_bs = 512;
+      GemmProb& g = a.p[i - i0];
+      g = gemm_prob(s.y1, 512, w.w2, 512, w.b2, s.xo, 256, s.n, 256, 512, B);
+      g.R = s.x;
+      g.ldr = 256;
+      g.r_bs = s.x_bs;
+      g.pro_mean = p.mean + (size_t)i * B * 512;
+      g.pro_rstd = p.rstd + (size_t)i * B * 512;
+      g.pro_bs = 512;
     }
-    if ((rc = gemm_launch(EPI_RESID, PRO_NORM_RELU, tl.mlp2, a,
-                          st, K_MLP2, pm)) != ONEPOSE_OK)
-      return rc;
-  }
-  return ONEPOSE_OK;
+    return gemm_launch(EPI_RESID, PRO_NORM_RELU, tl.mlp2[i0], a, st, K_MLP2, pm);
+  });
 }
 
 // The matcher forward on point-major leaves [*, n3*L, 256] (leaves_pm_bs elements per sample).
@@ -1648,38 +1700,22 @@ int match_impl(const void* packed_weights, const float* desc2d, int64_t desc2d_b
              (float)n3g, kind == 1 ? 1 : 0, sh ? sh->max_shard : n3};
     const int qkv_n3 = sh ? sh->max_shard : n3;
     unsigned* lcnt = p.cnt + (size_t)(ap - 1) * 2 * B * kCntPerSide;
+    // layers 1-2 of a whole frame: per-side choices (the 3D side's are the object prefix's,
+    // so cached and uncached forwards agree bit for bit at any batch); later layers and
+    // sharded frames: one set for the launch
+    const LayerTiles tl = !sh && ap <= 2 ? side_tiles(n1, n3, B, pm, kind == 2)
+                                         : layer_tiles(qkv_n3, sd, 2, B, pm, sh);
     int rc;
     if (cached3) {   // self-attention 1, 2D half (the 3D half is in the object cache)
-      rc = attention_layer(w, sd, 1, B, p, lcnt, st, pm, sh, layer_tiles(qkv_n3, sd, 1, B, pm, sh));
-    } else if (obj_cache && layer == 2 && B <= kFusedFoldMaxBatch && !sh) {
-      // cross-attention 1: the 3D side's frame-independent half from the object cache (at
-      // these batches the grouped choices equal the object prefix's B = 1 ones)
+      rc = attention_layer(w, sd, 1, B, p, lcnt, st, pm, sh, tl);
+    } else if (obj_cache && layer == 2 && !sh) {
+      // cross-attention 1: the 3D side's frame-independent half from the object cache
       const ObjLayout L = obj_layout(n3);
       const SideCache xc = {obj_cache + L.phiq, obj_cache + L.acc, obj_cache + L.ksum,
                             obj_cache + L.mf};
-      rc = attention_layer(w, sd, 2, B, p, lcnt, st, pm, nullptr,
-                           layer_tiles(qkv_n3, sd, 2, B, pm, false), &xc);
+      rc = attention_layer(w, sd, 2, B, p, lcnt, st, pm, nullptr, tl, &xc);
     } else {
-      const LayerTiles tg = layer_tiles(qkv_n3, sd, 2, B, pm, sh);
-      bool split = false;
-      LayerTiles t3{}, t2{};
-      Side s3 = sd[1];
-      s3.src = 0;
-      if (ap == 1 && !sh) {
-        // Uncached self-attention 1 gives the bits of the cached forward: its 3D half with the
-        // object prefix's choices (onepose_object_prepare: that side alone, B = 1 -- each
-        // sample's arithmetic does not depend on the launch's batch), its 2D half with the
-        // cached forward's.  Where those equal the grouped choices one launch does both.
-        t3 = layer_tiles(n3, &s3, 1, 1, pm, false);
-        t2 = layer_tiles(n3, sd, 1, B, pm, false);
-        split = !same_tiles(t3, tg) || !same_tiles(t2, tg);
-      }
-      if (split) {
-        rc = attention_layer(w, &s3, 1, B, p, lcnt + (size_t)B * kCntPerSide, st, pm, nullptr, t3);
-        if (rc == ONEPOSE_OK) rc = attention_layer(w, sd, 1, B, p, lcnt, st, pm, nullptr, t2);
-      } else {
-        rc = attention_layer(w, sd, 2, B, p, lcnt, st, pm, sh, tg);
-      }
+      rc = attention_layer(w, sd, 2, B, p, lcnt, st, pm, sh, tl);
     }
     if (rc != ONEPOSE_OK) return rc;
     x2r = p.x2[c2 ^ 1];
@@ -1813,7 +1849,7 @@ int object_prepare_impl(const void* packed_weights, const float* desc3d, const f
   const ApW w = ap_weights(wbase, 1);
   const Side x3 = {cache, 0, nullptr, cache + L.phiq, p.kvpart3, p.kspart3, nullptr, nullptr, n3,
                    (float)n3, 0, n3};
-  const LayerTiles tl = layer_tiles(n3, &x3, 1, 1, pm, false);
+  const LayerTiles tl = layer_tiles(n3, &x3, 1, 1, pm, false);   // = side_tiles' 3D choices
   {  // phi(q) into the cache; KV / sum phi(k) chunk partials
     GemmArgs a;
     a.nprob = 1;
@@ -1821,13 +1857,13 @@ int object_prepare_impl(const void* packed_weights, const float* desc3d, const f
     a.p[0].vdiv = (float)n3;
     a.p[0].kvpart = p.kvpart3;
     a.p[0].kspart = p.kspart3;
-    if ((rc = gemm_launch(EPI_QKV, PRO_PLAIN, tl.qkv, a, st, K_QKV_GEMM, pm)) != ONEPOSE_OK)
+    if ((rc = gemm_launch(EPI_QKV, PRO_PLAIN, tl.qkv[0], a, st, K_QKV_GEMM, pm)) != ONEPOSE_OK)
       return rc;
   }
   {  // sum phi(k) into the cache, and the 2D side's Mf = C KV_3D
     KvFoldArgs ka;
     ka.ct = w.ct;
-    ka.p[0] = {p.kvpart3, p.kspart3, ceil_div(n3, gemm_tile_rows(tl.qkv))};
+    ka.p[0] = {p.kvpart3, p.kspart3, ceil_div(n3, gemm_tile_rows(tl.qkv[0]))};
     ka.mf[0] = cache + L.mf;
     ka.mf[1] = nullptr;
     prof_pre(K_KV_REDUCE, st);
