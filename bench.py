@@ -49,7 +49,9 @@ def superpoint_conv_flops(h, w):
 def cross_cached(cached, B):
     """Whether the cached forward also takes cross-attention 1's frame-independent 3D half
     (the 3D side's q / k / v projections, KV and the x range of its MLP conv 1) from the
-    object cache: at every batch (matcher.hip, side_tiles)."""
+    object cache: at every batch since round 2's per-side layer choices (matcher.hip,
+    side_tiles); B is kept for the callers' symmetry with frame_flops."""
+    del B
     return cached
 
 

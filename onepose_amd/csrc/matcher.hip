@@ -366,92 +366,9 @@ struct KvFoldArgs {
   const float* ct; // [4][64][512]  C transposed per head (packed weights)
 };
 typedef float f2v __attribute__((ext_vector_type(2)));
-__global__ __launch_bounds__(1024) void kv_fold_kernel(KvFoldArgs args, float* kv, float* ksum,
-                                                       int batch) {
-  constexpr int per = (16384 + 256) / 4;   // float4 outputs per (source, sample) = 4160
-  constexpr int groups = per / 64;         // 65 workgroups per (source, sample)
-  __shared__ float4 red[16][64];           // wave sums; then KV rows; then fold partials
-  __shared__ f2v fpart[3][4][256];         // fold partials of q quarters 1..3
-  const int g = blockIdx.x % groups, bs = blockIdx.x / groups;
-  const int b = bs % batch, src = bs / batch;
-  const KvProb& P = src ? args.p[1] : args.p[0];
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  const int e4 = g * 64 + lane;
-  const int h = (g >> 4) & 3, d0 = (g & 15) * 4;
-  const int op = t & 255, qq = t >> 8;
-  f2v cv[16];
-  if (g < 64) {
-    const float* ct = args.ct + (h * 64 + qq * 16) * 512 + 2 * op;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) cv[i] = *reinterpret_cast<const f2v*>(ct + i * 512);
-  }
-  const float4* p;
-  int64_t stride;
-  if (e4 < 4096) {
-    p = reinterpret_cast<const float4*>(P.part + (int64_t)b * P.chunks * 16384) + e4;
-    stride = 4096;
-  } else {
-    p = reinterpret_cast<const float4*>(P.kspart + (int64_t)b * P.chunks * 256) + (e4 - 4096);
-    stride = 64;
-  }
-  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-  for (int c0 = w; c0 < P.chunks; c0 += 128) {
-    float4 v[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = p[(int64_t)min(c0 + 16 * j, P.chunks - 1) * stride];
-#pragma unroll
-    for (int j = 0; j < 8; ++j)
-      if (c0 + 16 * j < P.chunks) {
-        acc.x += v[j].x; acc.y += v[j].y; acc.z += v[j].z; acc.w += v[j].w;
-      }
-  }
-  red[w][lane] = acc;
-  __syncthreads();
-  if (w == 0) {
-    float4 s = red[0][lane];
-#pragma unroll
-    for (int j = 1; j < 16; ++j) { s.x += red[j][lane].x; s.y += red[j][lane].y; s.z += red[j][lane].z; s.w += red[j][lane].w; }
-    if (e4 < 4096)
-      reinterpret_cast<float4*>(kv + ((int64_t)src * batch + b) * 16384)[e4] = s;
-    else
-      reinterpret_cast<float4*>(ksum + ((int64_t)src * batch + b) * 256)[e4 - 4096] = s;
-    red[0][lane] = s;   // KV rows d0..d0+3: red[0][16 j + q/4] = KV_h[d0 + j][q .. q+3]
-  }
-  if (g == 64) return;
-  __syncthreads();
-  const float* kvr = reinterpret_cast<const float*>(&red[0][0]) + qq * 16;
-  f2v y[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    y[j] = (f2v)(0.f);
-#pragma unroll
-    for (int i = 0; i < 16; i += 4) {
-      const float4 k = *reinterpret_cast<const float4*>(kvr + j * 64 + i);   // LDS broadcast
-      y[j] = __builtin_elementwise_fma(cv[i], (f2v)(k.x), y[j]);
-      y[j] = __builtin_elementwise_fma(cv[i + 1], (f2v)(k.y), y[j]);
-      y[j] = __builtin_elementwise_fma(cv[i + 2], (f2v)(k.z), y[j]);
-      y[j] = __builtin_elementwise_fma(cv[i + 3], (f2v)(k.w), y[j]);
-    }
-  }
-  if (qq > 0)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) fpart[qq - 1][j][op] = y[j];
-  __syncthreads();
-  if (qq == 0) {
-#pragma unroll
-    for (int r = 0; r < 3; ++r)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) y[j] += fpart[r][j][op];
-    float* mf = (src ? args.mf[1] : args.mf[0]) + (int64_t)b * 512 * 256 + (2 * op) * 256 +
-                h * 64 + d0;
-    *reinterpret_cast<float4*>(mf) = make_float4(y[0].x, y[1].x, y[2].x, y[3].x);
-    *reinterpret_cast<float4*>(mf + 256) = make_float4(y[0].y, y[1].y, y[2].y, y[3].y);
-  }
-}
-
 // kv_fold on 256-thread workgroups of at most 80 VGPRs per lane, so that one fits on a CU next
-// to three MLP-conv-1 workgroups (143 VGPRs) of the other frame in flight: the 1024-thread
-// form (16 waves of 84 VGPRs, 40 KB LDS) waits for a CU to drain.  The chunk sum is
+// to three MLP-conv-1 workgroups (143 VGPRs) of the other frame in flight (a 1024-thread form,
+// 16 waves of 84 VGPRs and 40 KB LDS, measured the same in the frame).  The chunk sum is
 // kv_reduce's (wave w sums chunks w, w+4, ... in order, the four wave sums added in wave
 // order), so KV / ksum equal kv_reduce's bit for bit; the fold is kv_fold's (q quarters
 // accumulated in q order, then added in quarter order), now all four quarters in one thread.
@@ -1457,11 +1374,7 @@ struct SideCache {
 };
 
 void launch_kv_fold(const KvFoldArgs& ka, int nslot, int B, float* kv, float* ksum, hipStream_t st) {
-#ifdef KVF_WG1024
-  hipLaunchKernelGGL(kv_fold_kernel, dim3(nslot * B * 65), dim3(1024), 0, st, ka, kv, ksum, B);
-#else
   hipLaunchKernelGGL(kv_fold256_kernel, dim3(nslot * B * 65), dim3(256), 0, st, ka, kv, ksum, B);
-#endif
 }
 
 // AttentionPropagation (GATs_SuperGlue.py:123-132) for 1 or 2 sides, grouped into one launch
