@@ -353,19 +353,16 @@ __global__ __launch_bounds__(256) void m_fold_kernel(FoldArgs args, int batch) {
 
 // kv_reduce and m_fold in one launch (whole frames): a workgroup that has reduced KV_h rows
 // d0..d0+3 of one source also owns Mf columns h*64 + d0..d0+3 of the side attending to it,
-// since  Mf[o][h*64+d] = sum_q C[o][h*64+q] KV_h[d][q]  reads only those rows.  16 waves:
-//   chunk sum   wave w sums chunks w, w+16, ... (8 loads in flight), the 16 wave sums are
-//               added in wave order through LDS;
-//   fold        thread (q quarter qq, o pair) takes 16 q of CT[h][q][o] (the per-head
-//               transpose of C, coalesced over o, loaded before the chunk sum so its latency
-//               overlaps it) times KV rows d0..d0+3; the four q quarters are added in order.
-// Workgroup 64 of each (source, sample) is sum phi(k) (chunk sum only).
+// since  Mf[o][h*64+d] = sum_q C[o][h*64+q] KV_h[d][q]  reads only those rows; the fold reads
+// CT[h][q][o], the per-head transpose of C (coalesced over o).  Workgroup 64 of each (source,
+// sample) is sum phi(k) (chunk sum only).
 struct KvFoldArgs {
   KvProb p[2];     // chunk partials of source slot 0 / 1
   float* mf[2];    // [B][512][256] Mf of the side that attends to slot 0 / 1
   const float* ct; // [4][64][512]  C transposed per head (packed weights)
 };
 typedef float f2v __attribute__((ext_vector_type(2)));
+
 // kv_fold on 256-thread workgroups of at most 80 VGPRs per lane, so that one fits on a CU next
 // to three MLP-conv-1 workgroups (143 VGPRs) of the other frame in flight (a 1024-thread form,
 // 16 waves of 84 VGPRs and 40 KB LDS, measured the same in the frame).  The chunk sum is
