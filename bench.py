@@ -393,6 +393,10 @@ def main():
         pt = [b.elapsed_time(c) for _, b, c in marks]
         gap = [marks[i][1].elapsed_time(marks[i + 1][0]) for i in range(len(marks) - 1)]
         s2s = [marks[i][0].elapsed_time(marks[i + 1][0]) for i in range(len(marks) - 1)]
+        # idle time of a match stream between its consecutive frames (frame i and i + m run on
+        # the same stream; frame i + m waits for its buffer slot's previous pose stage)
+        m_ = args.match_streams
+        sgap = [marks[i][1].elapsed_time(marks[i + m_][0]) for i in range(len(marks) - m_)]
         stage_ms = {"gpu_region_ms": round(ev_begin.elapsed_time(ev_end), 3),
                     "lead_ms": round(ev_begin.elapsed_time(marks[0][0]), 3),
                     "tail_ms": round(marks[-1][2].elapsed_time(ev_end), 3),
@@ -402,7 +406,9 @@ def main():
                     "step_mean": round(float(np.mean(s2s)), 4) if s2s else None,
                     "matcher_max": round(float(np.max(mt)), 4),
                     "pose_mean": round(float(np.mean(pt)), 4),
-                    "pose_max": round(float(np.max(pt)), 4)}
+                    "pose_max": round(float(np.max(pt)), 4),
+                    "stream_gap_mean": round(float(np.mean(sgap)), 4) if sgap else None,
+                    "stream_gap_max": round(float(np.max(sgap)), 4) if sgap else None}
     diag = []
     if step_events:
         diag.append([round(a.elapsed_time(b), 3) for a, b in zip(step_events, step_events[1:])])
