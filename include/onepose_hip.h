@@ -150,8 +150,11 @@ int onepose_match_prepared(const void* packed_weights,
  * only to itself there).  onepose_object_prepare runs them once per object and leaves the
  * 3D state entering layer 2 in `cache` ([n3][256] fp32), followed by the leaf logits
  * leaf_j . (W a)_lo of GAT layers 1-3 ([3][n3][16] fp32; GATs.py:113, constant per object since
- * the leaves never change, GATs_SuperGlue.py:70-72) -- onepose_object_cache_bytes in all;
- * onepose_match_cached then runs every frame from there.  Its results are bit-identical to
+ * the leaves never change, GATs_SuperGlue.py:70-72) and by cross-attention 1's frame-
+ * independent 3D half (layer 2, GATs_SuperGlue.py:74-78: the 3D side's phi(q), sum phi(k), the
+ * 2D side's folded message weights and the W1a x half of its MLP conv 1) --
+ * onepose_object_cache_bytes in all (an opaque layout); onepose_match_cached then runs every
+ * frame from there.  Its results are bit-identical to
  * onepose_match_prepared_ex's on the same object (the same kernels and tiles produce the
  * cached state), provided the cache was prepared with the same `precision`.
  *   desc3d:          [256][n3] reference layout (descriptors3d_db of one object)
