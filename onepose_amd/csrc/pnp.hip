@@ -2028,6 +2028,9 @@ int onepose_pose_stage(const int64_t* matches0, const float* kpts2d, int64_t kpt
   }
   hipStream_t st = static_cast<hipStream_t>(stream);
   const SelArgs sel{matches0, kpts2d, kpts2d_bstride, kpts3d, kpts3d_bstride, n1, n3, scale};
+#ifdef ONEPOSE_PROBE_NOPOSE   // (probe: what the pose stage costs the matcher streams)
+  return ONEPOSE_OK;
+#endif
   OP_LAUNCH(K_PNP, st, pnp_ransac_kernel, dim3(batch), dim3(kThreads), lds, st, nullptr, nullptr,
             nullptr, max_points, K, K_bstride, scale, reproj_error, max_iters, confidence, pose34,
             inlier_mask, n_inliers, status, static_cast<int*>(workspace), sel, pts2d, pts3d,
