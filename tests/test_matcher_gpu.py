@@ -248,14 +248,18 @@ def test_bf16_attention_mode_tracks_fp32(n1, n3, device):
 @pytest.mark.parametrize("n1,n3,L,B,prec", [(200, 777, 8, 1, 0), (1024, 4096, 8, 2, 0),
                                              (128, 256, 12, 1, 0), (1024, 4096, 8, 1, 1),
                                              (1024, 4096, 8, 1, 2), (1024, 4096, 8, 4, 0),
-                                             (512, 2048, 8, 8, 0), (256, 1024, 8, 32, 0)])
+                                             (512, 2048, 8, 8, 0), (256, 1024, 8, 32, 0),
+                                             (1000, 3001, 8, 3, 0), (1000, 3001, 8, 6, 0)])
 def test_object_cache_is_bit_identical(device, n1, n3, L, B, prec):
     """onepose_object_prepare + onepose_match_cached (GAT 0 and the 3D half of self-attention
     1 run once per object) vs onepose_match_prepared_ex on the same object: every output
     bit-equal, for a ragged cloud, a batch sharing the object, the L=12 GAT and bf16 mode.
     B = 4 / 8 / 32 reach the batch-dependent choices (layer_tiles: the 64x64 MLP-conv-2 tile,
     kv_reduce + m_fold instead of kv_fold, the 64-row QKV tile at n3 = 1024), where the
-    uncached forward runs self-attention 1's halves with the prefix's / cached choices."""
+    uncached forward runs self-attention 1's halves with the prefix's / cached choices.
+    1000 x 3001 (B = 3 / 6): ragged sides with different per-side QKV tiles in layers 1-2 (2D
+    32-row, 3D 64-row chunks, both with a partial last chunk), and at B = 6 a 2D source slot
+    folded by kv_reduce + m_fold beside the 3D slot's kv_fold."""
     from onepose_amd import _lib
     lib = _lib.load()
     sd = synthetic.make_state_dict(0)
