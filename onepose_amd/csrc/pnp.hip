@@ -1588,6 +1588,9 @@ __global__ __launch_bounds__(kThreads) void pnp_ransac_kernel(
   Shared& sh = *reinterpret_cast<Shared*>(dyn);
   float* p2 = reinterpret_cast<float*>(dyn + ((sizeof(Shared) + 15) / 16) * 16);
   float* p3 = p2 + 2 * max_points;
+#ifdef ONEPOSE_PROBE_EMPTYPOSE   // (probe: launched with its resources, no work)
+  if (scale != 1.2345e-300) return;
+#endif
   const int b = blockIdx.x;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   int n;
@@ -1912,6 +1915,9 @@ __global__ __launch_bounds__(kThreads) void pnp_refit_kernel(
     const int* __restrict__ idx_ws, const double* __restrict__ pose_gt, int64_t gt_bs,
     double* __restrict__ rerr, double* __restrict__ terr, uint8_t* __restrict__ cmd) {
   __shared__ Shared sh;
+#ifdef ONEPOSE_PROBE_EMPTYPOSE
+  if (scale != 1.2345e-300) return;
+#endif
   const int b = blockIdx.x;
   const int t = threadIdx.x;
   double* pose = pose34 + (int64_t)b * 12;
