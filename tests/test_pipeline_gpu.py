@@ -217,3 +217,47 @@ def test_device_stamps_count_and_time_graph_launches(setup):
     assert launches[k] == reps * per_frame
     st_ms = tot[k] / launches[k]
     assert 0.5 * ev_ms < st_ms < 1.5 * ev_ms, (st_ms, ev_ms)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n1,n3,seed", [(256, 1024, 3), (1024, 4096, 4)])
+def test_pipeline_frame_matches_oracle(n1, n3, seed):
+    """The bench's per-frame path exactly as it runs there -- object cache (GAT 0, self-
+    attention 1's and cross-attention 1's 3D halves, GAT leaf logits), cached matcher, fused
+    selection + RANSAC-EPnP + cm/deg stage -- against the CPU oracle: the numpy matcher
+    (GATs_SuperGlue.py:203-278; indices exact except rows whose top-1 / top-2 or threshold
+    margin is below 1e-4) and the C restatement of solvePnPRansac(EPNP) + query_pose_error on
+    the pipeline's own correspondences (eval_utils.py:18-63; status and inliers exact, pose
+    within 1e-6, errors within 1e-6)."""
+    from oracle import matcher_np as M
+    from oracle import pnp_oracle as O
+    dev = torch.device("cuda", 0)
+    sd = synthetic.make_state_dict(0)
+    data, _, frames = synthetic.make_matcher_inputs(n1, n3, L, seed=seed, batch=1)
+    m = matcher.from_state_dict(sd)
+    pipe = FramePipeline(m, data["keypoints3d"][0], data["descriptors3d_db"][0],
+                         data["descriptors2d_db"][0], 1, n1, dev, scale=1000.0, slots=3)
+    assert pipe.object_cache is not None
+    pipe.set_frames(data["descriptors2d_query"], data["keypoints2d"], frames[0].K[None],
+                    frames[0].pose_gt[None])
+    pipe.enqueue(0)
+    torch.cuda.synchronize()
+    o = pipe.slots[0]
+    got = o.matches0.cpu().numpy()[0]
+    opred, oconf = M.forward(sd, data)
+    top = -np.sort(-oconf[0], axis=1)[:, :2]
+    margin = np.minimum(top[:, 0] - top[:, 1], np.abs(opred["matching_scores0"][0] - 0.2))
+    bad = got != opred["matches0"][0]
+    assert not (bad & (margin > 1e-4)).any(), np.nonzero(bad & (margin > 1e-4))[0][:10]
+    assert bad.sum() <= max(1, 0.002 * n1)
+    assert (got > -1).sum() > 0.3 * n1
+    n = int(o.counts.cpu()[0])
+    assert n == int((got > -1).sum())
+    st, pose, mask, nin, _ = O.pnp_ransac(o.pts2d.cpu().numpy()[0, :n], o.pts3d.cpu().numpy()[0, :n],
+                                          frames[0].K, scale=1000.0)
+    assert st == int(o.status.cpu()[0]) == 0
+    assert nin == int(o.n_inliers.cpu()[0])
+    np.testing.assert_allclose(o.pose.cpu().numpy()[0], pose, atol=1e-6)
+    r_err, t_err = O.pose_error(pose, frames[0].pose_gt)
+    np.testing.assert_allclose(o.R_err.cpu().numpy()[0], r_err, atol=1e-6)
+    np.testing.assert_allclose(o.t_err.cpu().numpy()[0], t_err, atol=1e-6)
