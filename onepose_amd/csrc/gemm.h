@@ -95,6 +95,8 @@ enum GemmTile {
                     //   (N = 256 gives 2x the 64x64 tile count: 640 tiles at config 2)
   TILE_64x128 = 3,  // qkv fp32 at large batches: 2 accumulators per wave, 64-row KV chunks
   TILE_128x128 = 4, // qkv fp32 at larger batches: 4 accumulators per wave, 128-row KV chunks
+  TILE_128x64W8 = 5, // score: 128 x 64 outputs on 8 waves of 32 x 32 (K = 256 is short: half
+                     //   the operand loads per FLOP of 64 x 64)
 };
 // (STATS + HEADZ also compile for 64x32 / 2 waves and for 64x64 / 8 waves with K split in
 // two and 64-deep stages, one head per stage; both measured slower than 64x64 for mlp1 in the

@@ -655,11 +655,15 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
     // every column over its rows.  Four threads per row (then per column) take 16 entries
     // each; the quarters are combined by lane butterflies ((q0 + q1) + (q2 + q3), fixed
     // order).  Reads of the staged tile are bank-conflict free both ways (pitch BN + 1).
-    static_assert(EPI != EPI_SCORE || (BM == 64 && BN == 64 && T::NT == 256), "score tile");
+    static_assert(EPI != EPI_SCORE || (T::NT >= 4 * BM && T::NT >= 4 * BN && BM % 16 == 0 &&
+                                       BN % 16 == 0 && BM <= 128 && BN <= 128), "score tile");
     const int cols = min(BN, N - n0);
-    const int line = t >> 2, qtr = t & 3, lo = qtr * 16;
-    auto partial = [&](const float* base, int stride, int count) __attribute__((always_inline)) {
-      const int hi = min(lo + 16, count);
+    const int line = t >> 2, qtr = t & 3;
+    // quarters of a row (column) of BN (BM) entries: 16 or 32 each
+    const int lo_r = qtr * (BN / 4), lo_c = qtr * (BM / 4);
+    auto partial = [&](const float* base, int stride, int count, int lo, int len)
+        __attribute__((always_inline)) {
+      const int hi = min(lo + len, count);
       float mx = -INFINITY;
       for (int i = lo; i < hi; ++i) mx = fmaxf(mx, base[i * stride]);
       mx = fmaxf(mx, __shfl_xor(mx, 1, 64));
@@ -670,16 +674,16 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
       s += __shfl_xor(s, 2, 64);
       return make_float2(mx, s);
     };
-    {   // row `line` over this tile's columns
-      const float2 r = partial(tile + line * TP, 1, cols);
+    if (line < BM) {   // row `line` over this tile's columns
+      const float2 r = partial(tile + line * TP, 1, cols, lo_r, BN / 4);
       if (qtr == 0 && line < rows) {
         float* o = F(rowstat) + (((int64_t)b * M + m0 + line) * ntiles + nt) * 2;
         o[0] = r.x;
         o[1] = r.y;
       }
     }
-    {   // column `line` over this tile's rows
-      const float2 r = partial(tile + line, TP, rows);
+    if (line < BN) {   // column `line` over this tile's rows
+      const float2 r = partial(tile + line, TP, rows, lo_c, BM / 4);
       if (qtr == 0 && line < cols) {
         float* o = F(colstat) + (((int64_t)b * N + n0 + line) * mtiles + mt) * 2;
         o[0] = r.x;
@@ -731,6 +735,7 @@ using T32x128 = Tile<32, 128, 1, 4, 32>;
 using T64x32K2 = Tile<64, 32, 2, 4, 64>;
 using T64x128 = Tile<64, 128, 1, 4, 32>;
 using T128x128 = Tile<128, 128, 1, 4, 32>;
+using T128x64W8 = Tile<128, 64, 1, 8, 32>;
 
 
 template <int EPI, int PRO, class T, int PM>
@@ -748,6 +753,7 @@ TileDims tile_dims(int tile) {
     case TILE_64x32K2: return {64, 32, 64};
     case TILE_64x128: return {64, 128, 32};
     case TILE_128x128: return {128, 128, 32};
+    case TILE_128x64W8: return {128, 64, 32};
 
     default: return {0, 0, 0};
   }
@@ -823,6 +829,7 @@ int gemm_launch(int epi, int pro, int tile, GemmArgs& args, hipStream_t stream, 
   CASE(EPI_RESID, PRO_NORM_RELU, TILE_64x64, T64x64, PM_F32)
   CASE(EPI_RESID, PRO_NORM_RELU, TILE_64x32K2, T64x32K2, PM_F32)
   CASE(EPI_SCORE, PRO_PLAIN, TILE_64x64, T64x64, PM_F32)
+  CASE(EPI_SCORE, PRO_PLAIN, TILE_128x64W8, T128x64W8, PM_F32)
   CASE(EPI_BIAS, PRO_PLAIN, TILE_64x64, T64x64, PM_F32)
   CASE(EPI_ACC, PRO_PLAIN, TILE_64x64, T64x64, PM_F32)
   CASE(EPI_ACC, PRO_PLAIN, TILE_64x64, T64x64, PM_BF16)

@@ -40,6 +40,11 @@ namespace onepose {
 // GEMM tile per layer GEMM (gemm.h; measured per shape on config 2).
 constexpr int kTileKV = TILE_32x128, kTileMLP1 = TILE_64x64,
               kTileMLP2 = TILE_64x64, kTileMLP2F32 = TILE_64x32K2, kTileFinal = TILE_64x64;
+#ifdef ONEPOSE_SCORE_TILE64   // A/B probe: the round-2 score tile
+constexpr int kTileScore = TILE_64x64, kScoreBM = 64;
+#else
+constexpr int kTileScore = TILE_128x64W8, kScoreBM = 128;
+#endif
 constexpr int kFusedFoldMaxBatch = 4;   // kv_fold up to this batch, kv_reduce + m_fold above
 constexpr int kMlp2WideTiles = 1024;    // fp32 mlp2: 64x64 tiles from this many (4 per CU)
 constexpr int kQkvWideTiles = 256;      // fp32 qkv: 64x128 tiles from this many 64-row tiles
@@ -1650,6 +1655,10 @@ int match_impl(const void* packed_weights, const float* desc2d, int64_t desc2d_b
     OP_LAUNCH(K_L2NORM, st, l2norm_kernel, dim3(ceil_div(rows, 4)), dim3(256), 0, st, p.f2, B * n1,
                        p.f3, B * n3);
   }
+  // score tile: 128 x 64 on 8 waves in fp32 (K = 256 is short; fewer operand loads per FLOP
+  // than 64 x 64), 64 x 64 in the split mode (its LDS images are three bf16 planes)
+  const int score_tile = pm_out == PM_F32 ? kTileScore : TILE_64x64;
+  const int score_mt = ceil_div(n1, pm_out == PM_F32 ? kScoreBM : 64);   // colpart per column
   {  // S = D2^T D3 / scale_factor with softmax partials
     GemmArgs a;
     a.nprob = 1;
@@ -1658,13 +1667,13 @@ int match_impl(const void* packed_weights, const float* desc2d, int64_t desc2d_b
     a.p[0].scale = scale_factor;
     a.p[0].rowstat = p.rowpart;
     a.p[0].colstat = p.colpart;
-    if ((rc = gemm_launch(EPI_SCORE, PRO_PLAIN, TILE_64x64, a, st, K_SCORE, pm_out)) != ONEPOSE_OK)
+    if ((rc = gemm_launch(EPI_SCORE, PRO_PLAIN, score_tile, a, st, K_SCORE, pm_out)) != ONEPOSE_OK)
       return rc;
   }
   {
     const int64_t total = (int64_t)B * (n1 + n3);
     OP_LAUNCH(K_SMX_REDUCE, st, softmax_reduce_kernel, dim3((unsigned)((total + 3) / 4)), dim3(256),
-                       0, st, p.rowpart, ch3, p.colpart, ch2, B, n1, n3, p.rowmax, p.rowsum,
+                       0, st, p.rowpart, ch3, p.colpart, score_mt, B, n1, n3, p.rowmax, p.rowsum,
                        p.colmax, p.colsum, p.rowbest, p.colbest);
     const int64_t nr = (int64_t)B * n1;
     if (sh) {   // row softmax over every rank's columns
