@@ -374,6 +374,9 @@ typedef float f2v __attribute__((ext_vector_type(2)));
 // kv_reduce's (wave w sums chunks w, w+4, ... in order, the four wave sums added in wave
 // order), so KV / ksum equal kv_reduce's bit for bit; the fold is kv_fold's (q quarters
 // accumulated in q order, then added in quarter order), now all four quarters in one thread.
+#ifndef KVF_DEPTH
+#define KVF_DEPTH 16
+#endif
 __global__ __launch_bounds__(256) void kv_fold256_kernel(KvFoldArgs args, float* kv, float* ksum,
                                                          int batch) {
   constexpr int per = (16384 + 256) / 4;   // float4 outputs per (source, sample) = 4160
@@ -385,28 +388,35 @@ __global__ __launch_bounds__(256) void kv_fold256_kernel(KvFoldArgs args, float*
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int e4 = g * 64 + lane;
   const int h = (g >> 4) & 3, d0 = (g & 15) * 4;
-  const float4* p;
-  int64_t stride;
-  if (e4 < 4096) {
-    p = reinterpret_cast<const float4*>(P.part + (int64_t)b * P.chunks * 16384) + e4;
-    stride = 4096;
-  } else {
-    p = reinterpret_cast<const float4*>(P.kspart + (int64_t)b * P.chunks * 256) + (e4 - 4096);
-    stride = 64;
-  }
+  // uniform base + 32-bit lane offsets: one VGPR per load address
+  const bool kvrow = g < 64;
+  const float4* base = kvrow
+      ? reinterpret_cast<const float4*>(P.part + (int64_t)b * P.chunks * 16384)
+      : reinterpret_cast<const float4*>(P.kspart + (int64_t)b * P.chunks * 256);
+  const int stride = kvrow ? 4096 : 64;
+  const int idx = kvrow ? e4 : e4 - 4096;
+  // Up to KVF_DEPTH chunk loads in flight per lane (config 2 at 16: one round for either
+  // side; the predicated-off slots add nothing, and the adds keep kv_reduce's order: chunk w,
+  // w + 4, ...)
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-  int c = w;
-  for (; c + 28 < P.chunks; c += 32) {
-    float4 v[8];
+  for (int c = w; c < P.chunks; c += 4 * KVF_DEPTH) {
+    float4 v[KVF_DEPTH];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = p[(int64_t)(c + 4 * j) * stride];
+    for (int j = 0; j < KVF_DEPTH; ++j)
+      v[j] = c + 4 * j < P.chunks ? base[idx + (c + 4 * j) * stride] : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) { acc.x += v[j].x; acc.y += v[j].y; acc.z += v[j].z; acc.w += v[j].w; }
+    for (int j = 0; j < KVF_DEPTH; ++j) { acc.x += v[j].x; acc.y += v[j].y; acc.z += v[j].z; acc.w += v[j].w; }
   }
-  for (; c < P.chunks; c += 4) {
-    const float4 v = p[(int64_t)c * stride];
-    acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+  // the fold's first quarter of C (independent of KV) is in flight across the reduction below
+  const int op = t;   // Mf rows 2 op, 2 op + 1
+  const float* ct = args.ct + (h * 64) * 512 + 2 * op;
+  f2v cv[16];
+#ifndef KVF_NO_PREFETCH
+  if (g != 64) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) cv[i] = *reinterpret_cast<const f2v*>(ct + i * 512);
   }
+#endif
   red[w][lane] = acc;
   __syncthreads();
   if (w == 0) {
@@ -421,15 +431,17 @@ __global__ __launch_bounds__(256) void kv_fold256_kernel(KvFoldArgs args, float*
   }
   if (g == 64) return;
   __syncthreads();
-  const int op = t;   // Mf rows 2 op, 2 op + 1
   const float* kvr = reinterpret_cast<const float*>(&red[0][0]);
-  const float* ct = args.ct + (h * 64) * 512 + 2 * op;
   f2v y[4];
 #pragma unroll
   for (int qq = 0; qq < 4; ++qq) {
-    f2v cv[16];
+#ifndef KVF_NO_PREFETCH
+    if (qq > 0)
+#endif
+    {
 #pragma unroll
-    for (int i = 0; i < 16; ++i) cv[i] = *reinterpret_cast<const f2v*>(ct + (qq * 16 + i) * 512);
+      for (int i = 0; i < 16; ++i) cv[i] = *reinterpret_cast<const f2v*>(ct + (qq * 16 + i) * 512);
+    }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       f2v yq = (f2v)(0.f);

@@ -16,6 +16,6 @@ for r in $(seq 1 ${ROUNDS:-3}); do
     if [ $v = cur ]; then lib=""; else lib=$PWD/tools/ab/lib_$v.so; fi
     ONEPOSE_LIB=$lib timeout -k 10 200 python bench.py --steps ${STEPS:-300} --warmup 10 \
       --no-cpu-baseline ${BENCH_ARGS:-} > gpurun_out/abm_$v.json 2> gpurun_out/abm_$v.err || exit $?
-    python -c "import json; d=json.loads(open('gpurun_out/abm_$v.json').read().strip().splitlines()[-1]); k=d['kernel_ms_per_step']; print('$v', d['value'], d['roofline']['kernel'], d['roofline']['avg_launch_us'], {x: k.get(x) for x in ('qkv_gemm','mlp1_gemm','mlp2_gemm','score_gemm','final_gemm','conf')})"
+    python -c "import json; d=json.loads(open('gpurun_out/abm_$v.json').read().strip().splitlines()[-1]); k=d['kernel_ms_per_step']; print('$v', d['value'], d['roofline']['kernel'], d['roofline']['avg_launch_us'], {x: k.get(x) for x in ('qkv_gemm','mlp1_gemm','mlp2_gemm','kv_reduce','score_gemm','conf')})"
   done
 done
