@@ -368,24 +368,38 @@ struct KvFoldArgs {
 };
 typedef float f2v __attribute__((ext_vector_type(2)));
 
-// kv_fold on 256-thread workgroups of at most 80 VGPRs per lane, so that one fits on a CU next
-// to three MLP-conv-1 workgroups (143 VGPRs) of the other frame in flight (a 1024-thread form,
-// 16 waves of 84 VGPRs and 40 KB LDS, measured the same in the frame).  The chunk sum is
-// kv_reduce's (wave w sums chunks w, w+4, ... in order, the four wave sums added in wave
-// order), so KV / ksum equal kv_reduce's bit for bit; the fold is kv_fold's (q quarters
-// accumulated in q order, then added in quarter order), now all four quarters in one thread.
+// kv_fold on 256-thread workgroups (88 VGPRs), small enough to share a CU with the other frame's
+// GEMM workgroups (a 1024-thread form, 16 waves and 40 KB LDS, measured the same in the frame).
+// The chunk sum is kv_reduce's (wave w sums chunks w, w+4, ... in order, the four wave sums
+// added in wave order), so KV / ksum equal kv_reduce's bit for bit.  The fold: KVF_OSPLIT
+// workgroups share a KV row block, each folding 512 / KVF_OSPLIT rows of Mf, so each reads that
+// share of C_h (a 512-row workgroup reads all 128 KB of it, 16 MB per launch at config 2, and
+// was the slower half of the kernel: 1625 -> 1627 frames/s, kv_fold 9.5 -> 8.7 us per launch
+// with launch overhead, `tools/ab_multi.sh`); q quarters accumulated in q order, then added in
+// quarter order.
 #ifndef KVF_DEPTH
 #define KVF_DEPTH 16
 #endif
+#ifndef KVF_OSPLIT   // Mf row blocks per KV row block (1: 512 rows, 2: 256 rows per workgroup)
+#define KVF_OSPLIT 2
+#endif
+#ifndef KVF_PROBE_NOSUM   // (probes: timing only, wrong results)
+#define KVF_PROBE_NOSUM 0
+#endif
+#ifndef KVF_PROBE_NOFOLD
+#define KVF_PROBE_NOFOLD 0
+#endif
 __global__ __launch_bounds__(256) void kv_fold256_kernel(KvFoldArgs args, float* kv, float* ksum,
                                                          int batch) {
-  constexpr int per = (16384 + 256) / 4;   // float4 outputs per (source, sample) = 4160
-  constexpr int groups = per / 64;         // 65 workgroups per (source, sample)
+  constexpr int OS = KVF_OSPLIT;
+  constexpr int groups = 64 * OS + 1;      // workgroups per (source, sample); the last: sum phi(k)
   __shared__ float4 red[4][64];            // wave sums; then KV rows d0..d0+3
-  const int g = blockIdx.x % groups, bs = blockIdx.x / groups;
+  const int gb = blockIdx.x % groups, bs = blockIdx.x / groups;
   const int b = bs % batch, src = bs / batch;
   const KvProb& P = src ? args.p[1] : args.p[0];
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const bool ks_wg = gb == 64 * OS;
+  const int g = ks_wg ? 64 : gb % 64, os = ks_wg ? 0 : gb / 64;   // KV row block, Mf row block
   const int e4 = g * 64 + lane;
   const int h = (g >> 4) & 3, d0 = (g & 15) * 4;
   // uniform base + 32-bit lane offsets: one VGPR per load address
@@ -403,42 +417,46 @@ __global__ __launch_bounds__(256) void kv_fold256_kernel(KvFoldArgs args, float*
     float4 v[KVF_DEPTH];
 #pragma unroll
     for (int j = 0; j < KVF_DEPTH; ++j)
-      v[j] = c + 4 * j < P.chunks ? base[idx + (c + 4 * j) * stride] : make_float4(0.f, 0.f, 0.f, 0.f);
+      v[j] = c + 4 * j < P.chunks && !KVF_PROBE_NOSUM ? base[idx + (c + 4 * j) * stride] : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
     for (int j = 0; j < KVF_DEPTH; ++j) { acc.x += v[j].x; acc.y += v[j].y; acc.z += v[j].z; acc.w += v[j].w; }
   }
   // the fold's first quarter of C (independent of KV) is in flight across the reduction below
+#if KVF_OSPLIT == 1
   const int op = t;   // Mf rows 2 op, 2 op + 1
   const float* ct = args.ct + (h * 64) * 512 + 2 * op;
   f2v cv[16];
-#ifndef KVF_NO_PREFETCH
+#else
+  const int o = os * 256 + t;   // Mf row o
+  const float* ct = args.ct + (h * 64) * 512 + o;
+  float cv[16];
+#endif
   if (g != 64) {
 #pragma unroll
-    for (int i = 0; i < 16; ++i) cv[i] = *reinterpret_cast<const f2v*>(ct + i * 512);
+    for (int i = 0; i < 16; ++i) cv[i] = *reinterpret_cast<const std::remove_reference_t<decltype(cv[0])>*>(ct + i * 512);
   }
-#endif
   red[w][lane] = acc;
   __syncthreads();
   if (w == 0) {
     float4 s = red[0][lane];
 #pragma unroll
     for (int j = 1; j < 4; ++j) { s.x += red[j][lane].x; s.y += red[j][lane].y; s.z += red[j][lane].z; s.w += red[j][lane].w; }
-    if (e4 < 4096)
-      reinterpret_cast<float4*>(kv + ((int64_t)src * batch + b) * 16384)[e4] = s;
-    else
-      reinterpret_cast<float4*>(ksum + ((int64_t)src * batch + b) * 256)[e4 - 4096] = s;
+    if (os == 0) {   // (every Mf row block sums the same KV rows)
+      if (e4 < 4096)
+        reinterpret_cast<float4*>(kv + ((int64_t)src * batch + b) * 16384)[e4] = s;
+      else
+        reinterpret_cast<float4*>(ksum + ((int64_t)src * batch + b) * 256)[e4 - 4096] = s;
+    }
     red[0][lane] = s;   // KV rows d0..d0+3: red[0][16 j + q/4] = KV_h[d0 + j][q .. q+3]
   }
-  if (g == 64) return;
+  if (g == 64 || KVF_PROBE_NOFOLD) return;
   __syncthreads();
   const float* kvr = reinterpret_cast<const float*>(&red[0][0]);
+#if KVF_OSPLIT == 1
   f2v y[4];
 #pragma unroll
   for (int qq = 0; qq < 4; ++qq) {
-#ifndef KVF_NO_PREFETCH
-    if (qq > 0)
-#endif
-    {
+    if (qq > 0) {
 #pragma unroll
       for (int i = 0; i < 16; ++i) cv[i] = *reinterpret_cast<const f2v*>(ct + (qq * 16 + i) * 512);
     }
@@ -459,6 +477,38 @@ __global__ __launch_bounds__(256) void kv_fold256_kernel(KvFoldArgs args, float*
   float* mf = (src ? args.mf[1] : args.mf[0]) + (int64_t)b * 512 * 256 + (2 * op) * 256 + h * 64 + d0;
   *reinterpret_cast<float4*>(mf) = make_float4(y[0].x, y[1].x, y[2].x, y[3].x);
   *reinterpret_cast<float4*>(mf + 256) = make_float4(y[0].y, y[1].y, y[2].y, y[3].y);
+#else
+  // one Mf row per thread, its four d as two packed pairs (d0, d0 + 1), (d0 + 2, d0 + 3); q
+  // quarters accumulated in q order, then added in quarter order
+  f2v y01, y23;
+#pragma unroll
+  for (int qq = 0; qq < 4; ++qq) {
+    if (qq > 0) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) cv[i] = ct[(qq * 16 + i) * 512];
+    }
+    f2v a01 = (f2v)(0.f), a23 = (f2v)(0.f);
+#pragma unroll
+    for (int i = 0; i < 16; i += 4) {
+      const float4 k0 = *reinterpret_cast<const float4*>(kvr + 0 * 64 + qq * 16 + i);
+      const float4 k1 = *reinterpret_cast<const float4*>(kvr + 1 * 64 + qq * 16 + i);
+      const float4 k2 = *reinterpret_cast<const float4*>(kvr + 2 * 64 + qq * 16 + i);
+      const float4 k3 = *reinterpret_cast<const float4*>(kvr + 3 * 64 + qq * 16 + i);
+      a01 = __builtin_elementwise_fma((f2v)(cv[i]), (f2v){k0.x, k1.x}, a01);
+      a23 = __builtin_elementwise_fma((f2v)(cv[i]), (f2v){k2.x, k3.x}, a23);
+      a01 = __builtin_elementwise_fma((f2v)(cv[i + 1]), (f2v){k0.y, k1.y}, a01);
+      a23 = __builtin_elementwise_fma((f2v)(cv[i + 1]), (f2v){k2.y, k3.y}, a23);
+      a01 = __builtin_elementwise_fma((f2v)(cv[i + 2]), (f2v){k0.z, k1.z}, a01);
+      a23 = __builtin_elementwise_fma((f2v)(cv[i + 2]), (f2v){k2.z, k3.z}, a23);
+      a01 = __builtin_elementwise_fma((f2v)(cv[i + 3]), (f2v){k0.w, k1.w}, a01);
+      a23 = __builtin_elementwise_fma((f2v)(cv[i + 3]), (f2v){k2.w, k3.w}, a23);
+    }
+    y01 = qq == 0 ? a01 : y01 + a01;
+    y23 = qq == 0 ? a23 : y23 + a23;
+  }
+  float* mf = (src ? args.mf[1] : args.mf[0]) + (int64_t)b * 512 * 256 + (int64_t)o * 256 + h * 64 + d0;
+  *reinterpret_cast<float4*>(mf) = make_float4(y01.x, y01.y, y23.x, y23.y);
+#endif
 }
 
 // InstanceNorm1d statistics (GATs_SuperGlue.py:145; biased variance, eps 1e-5): per-64-row-tile
@@ -1388,7 +1438,7 @@ struct SideCache {
 };
 
 void launch_kv_fold(const KvFoldArgs& ka, int nslot, int B, float* kv, float* ksum, hipStream_t st) {
-  hipLaunchKernelGGL(kv_fold256_kernel, dim3(nslot * B * 65), dim3(256), 0, st, ka, kv, ksum, B);
+  hipLaunchKernelGGL(kv_fold256_kernel, dim3(nslot * B * (64 * KVF_OSPLIT + 1)), dim3(256), 0, st, ka, kv, ksum, B);
 }
 
 // AttentionPropagation (GATs_SuperGlue.py:123-132) for 1 or 2 sides, grouped into one launch
