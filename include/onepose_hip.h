@@ -154,14 +154,22 @@ int onepose_match_prepared(const void* packed_weights,
  * independent 3D half (layer 2, GATs_SuperGlue.py:74-78: the 3D side's phi(q), sum phi(k), the
  * 2D side's folded message weights and the W1a x half of its MLP conv 1) --
  * onepose_object_cache_bytes in all (an opaque layout); onepose_match_cached then runs every
- * frame from there.  Its results are bit-identical to
- * onepose_match_prepared_ex's on the same object (the same kernels and tiles produce the
- * cached state), provided the cache was prepared with the same `precision`.
+ * frame from there.  With num_leaf <= 8 the cache also holds prefix tables of GAT layers 1-3
+ * (the leaves sorted by logit, exp-weighted prefix and suffix sums: [3][n3][16][256] fp32), and
+ * a cached frame's GAT layers 1-3 read two table rows per 3D point instead of its L leaves; they
+ * then differ from computing the layers from the leaves in rounding only.  With the tables off
+ * (onepose_set_gat_tables(0)) the results are bit-identical to onepose_match_prepared_ex's on the
+ * same object (the same kernels and tiles produce the cached state), provided the cache was
+ * prepared with the same `precision`.
  *   desc3d:          [256][n3] reference layout (descriptors3d_db of one object)
  *   leaves_prepared: [n3*L][256] point-major (onepose_prepare_leaves of the object)
  * The cache is shared by every sample of a batch (one object per call).
  * ------------------------------------------------------------------------------------ */
 size_t onepose_object_cache_bytes(int n3);
+/* Process-wide: whether onepose_match_cached's GAT layers 1-3 use the object's prefix tables
+ * (default 1) or the leaves.  Returns the previous setting.  (No reference counterpart: the
+ * reference has no object cache.) */
+int onepose_set_gat_tables(int enable);
 size_t onepose_object_prepare_workspace_bytes(int n3, int num_leaf);
 int onepose_object_prepare(const void* packed_weights, const float* desc3d,
                            const float* leaves_prepared, int n3, int num_leaf, int precision,

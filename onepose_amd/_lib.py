@@ -48,6 +48,7 @@ PROTOTYPES = {
                                           c_float, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                                           c_void_p, c_void_p, c_size_t, c_void_p]),
     "onepose_object_cache_bytes": (c_size_t, [c_int]),
+    "onepose_set_gat_tables": (c_int, [c_int]),
     "onepose_object_prepare_workspace_bytes": (c_size_t, [c_int, c_int]),
     "onepose_object_prepare": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
                                        c_void_p, c_void_p, c_size_t, c_void_p]),

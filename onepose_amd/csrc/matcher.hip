@@ -34,6 +34,7 @@
 #include "gemm.h"
 
 #include <algorithm>
+#include <atomic>
 
 namespace onepose {
 
@@ -44,6 +45,13 @@ constexpr int kTileKV = TILE_32x128, kTileMLP1 = TILE_64x64,
 constexpr int kTileScore = TILE_64x64, kScoreBM = 64;
 #else
 constexpr int kTileScore = TILE_128x64W8, kScoreBM = 128;
+#endif
+// The cached forward's GAT layers 1-3 from the object's prefix tables (gat_tab_kernel), or
+// from the leaves (gat_kernel, the uncached forward's kernel): onepose_set_gat_tables.
+#ifdef ONEPOSE_NO_GAT_TABLES
+std::atomic<bool> g_gat_tables{false};
+#else
+std::atomic<bool> g_gat_tables{true};
 #endif
 constexpr int kFusedFoldMaxBatch = 4;   // kv_fold up to this batch, kv_reduce + m_fold above
 constexpr int kMlp2WideTiles = 1024;    // fp32 mlp2: 64x64 tiles from this many (4 per CU)
@@ -752,6 +760,144 @@ __global__ __launch_bounds__(256) void gat_kernel(const float* __restrict__ x3,
       make_float4(elu1(acc.x), elu1(acc.y), elu1(acc.z), elu1(acc.w));
 }
 
+// GAT layers 1-3 of a cached forward from per-object prefix tables (onepose_object_prepare).
+// With the leaf logits s_(0) >= ... >= s_(L-1) sorted and c = s_(0), LeakyReLU splits the leaves
+// at the point's own logit s3: e_j = s3 + s_j where that is > 0 (a prefix of the sorted order,
+// k of them) and 0.2 (s3 + s_j) elsewhere, so
+//   sum_j exp(e_j - mx) leaf_j = exp(s3 + c - mx) A_k + exp(0.2 (s3 + c) - mx) B_k,
+//   A_k = sum_{i<k} exp(s_(i) - c) leaf_(i),   B_k = sum_{i>=k} exp(0.2 (s_(i) - c)) leaf_(i)
+// (both factors <= 1, so nothing overflows).  A frame then reads two table rows per point
+// instead of its L leaves (config 2: 16 instead of 42 MB per launch).  The sums differ from
+// the direct kernel's (gat_kernel) in rounding only.
+constexpr int kGatTabRows = 16;   // per point: A_1..A_L at 0..L-1, B_0..B_(L-1) at 8..8+L-1
+
+// Tables for the three frame-dependent GAT layers: slogs [3][n3][kLogitStride] (sorted leaf
+// logits, descending; equal logits by leaf index), tab [3][n3][kGatTabRows][256].
+__global__ __launch_bounds__(256) void gat_table_kernel(const float* __restrict__ leaves_pm,
+                                                        const float* __restrict__ wa1,
+                                                        float* __restrict__ slogs,
+                                                        float* __restrict__ tab, int n3, int L) {
+  constexpr int MAXL = 8;
+  const int p = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (p >= n3) return;
+  const int lane = threadIdx.x & 63;
+  const float* lp = leaves_pm + (int64_t)p * L * kDim;
+  float4 lf[MAXL];
+#pragma unroll
+  for (int j = 0; j < MAXL; ++j)
+    lf[j] = j < L ? reinterpret_cast<const float4*>(lp + j * kDim)[lane] : make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int g = 0; g < 3; ++g) {
+    const float4 wl = reinterpret_cast<const float4*>(wa1 + g * 512)[lane];
+    float d[MAXL];
+#pragma unroll
+    for (int j = 0; j < MAXL; ++j) d[j] = (j < L) ? gat_dot(lf[j], wl) : 0.f;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1)
+#pragma unroll
+      for (int j = 0; j < MAXL; ++j) d[j] += __shfl_xor(d[j], o, 64);
+    // rank of leaf j in descending order (ties by index), then the sorted logits / leaves
+    int rk[MAXL];
+#pragma unroll
+    for (int j = 0; j < MAXL; ++j) {
+      int r = 0;
+#pragma unroll
+      for (int i = 0; i < MAXL; ++i)
+        r += (i < L && i != j && (d[i] > d[j] || (d[i] == d[j] && i < j))) ? 1 : 0;
+      rk[j] = j < L ? r : MAXL;
+    }
+    float sv[MAXL];
+    float4 sl[MAXL];
+#pragma unroll
+    for (int r = 0; r < MAXL; ++r) {
+      float v = 0.f;
+      float4 f = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int j = 0; j < MAXL; ++j)
+        if (rk[j] == r) { v = d[j]; f = lf[j]; }
+      sv[r] = v;
+      sl[r] = f;
+    }
+    const float c = sv[0];
+    float* out = tab + (((int64_t)g * n3 + p) * kGatTabRows) * kDim;
+    float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int r = 0; r < MAXL; ++r) {
+      if (r >= L) break;
+      const float wp = expf(sv[r] - c);
+      a.x = fmaf(wp, sl[r].x, a.x); a.y = fmaf(wp, sl[r].y, a.y);
+      a.z = fmaf(wp, sl[r].z, a.z); a.w = fmaf(wp, sl[r].w, a.w);
+      reinterpret_cast<float4*>(out + r * kDim)[lane] = a;   // A_(r+1)
+    }
+    a = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int r = MAXL - 1; r >= 0; --r) {
+      if (r >= L) continue;
+      const float wn = expf(0.2f * (sv[r] - c));
+      a.x = fmaf(wn, sl[r].x, a.x); a.y = fmaf(wn, sl[r].y, a.y);
+      a.z = fmaf(wn, sl[r].z, a.z); a.w = fmaf(wn, sl[r].w, a.w);
+      reinterpret_cast<float4*>(out + (MAXL + r) * kDim)[lane] = a;   // B_r
+    }
+    float v = 0.f;
+#pragma unroll
+    for (int r = 0; r < MAXL; ++r) v = lane == r ? sv[r] : v;
+    if (lane < L) slogs[((int64_t)g * n3 + p) * kLogitStride + lane] = v;
+  }
+}
+
+// One GAT layer from the tables (slogs / tab of this layer, shared by the batch).
+__global__ __launch_bounds__(256) void gat_tab_kernel(const float* __restrict__ x3,
+                                                      const float* __restrict__ wa,
+                                                      const float* __restrict__ slogs,
+                                                      const float* __restrict__ tab,
+                                                      float* __restrict__ y3, int n3, int L,
+                                                      int batch) {
+  constexpr int MAXL = 8;
+  const int gw = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int b = gw / n3, p = gw - b * n3;
+  if (b >= batch) return;
+  const int lane = threadIdx.x & 63;
+  const float4 wh = reinterpret_cast<const float4*>(wa + 256)[lane];
+  const float4 h = reinterpret_cast<const float4*>(x3 + ((int64_t)b * n3 + p) * kDim)[lane];
+  float s3 = gat_dot(h, wh);
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) s3 += __shfl_xor(s3, o, 64);
+  const int pu = __builtin_amdgcn_readfirstlane(p);
+  const float* sp = slogs + (int64_t)pu * kLogitStride;
+  float sv[MAXL];
+#pragma unroll
+  for (int r = 0; r < MAXL; ++r) sv[r] = r < L ? sp[r] : 0.f;
+  const float c = sv[0];
+  float e0 = s3 + s3;
+  e0 = e0 > 0.f ? e0 : e0 * 0.2f;
+  const float v0 = s3 + c;
+  const float mx = fmaxf(e0, v0 > 0.f ? v0 : v0 * 0.2f);
+  int k = 0;
+#pragma unroll
+  for (int r = 0; r < MAXL; ++r) k += (r < L && s3 + sv[r] > 0.f) ? 1 : 0;
+  const float E0 = expf(e0 - mx), Fp = expf(v0 - mx), Fn = expf(0.2f * v0 - mx);
+  float sp_ = 0.f, sn = 0.f;
+#pragma unroll
+  for (int r = 0; r < MAXL; ++r) {
+    if (r >= L) break;
+    if (r < k) sp_ += expf(sv[r] - c);
+    else sn += expf(0.2f * (sv[r] - c));
+  }
+  const float sum = E0 + Fp * sp_ + Fn * sn;
+  const float* tp = tab + (int64_t)pu * kGatTabRows * kDim;
+  const float4 A = k > 0 ? reinterpret_cast<const float4*>(tp + (k - 1) * kDim)[lane]
+                         : make_float4(0.f, 0.f, 0.f, 0.f);
+  const float4 Bv = k < L ? reinterpret_cast<const float4*>(tp + (MAXL + k) * kDim)[lane]
+                          : make_float4(0.f, 0.f, 0.f, 0.f);
+  const float a0 = E0 / sum, ap = Fp / sum, an = Fn / sum;
+  float4 acc;
+  acc.x = fmaf(an, Bv.x, fmaf(ap, A.x, a0 * h.x));
+  acc.y = fmaf(an, Bv.y, fmaf(ap, A.y, a0 * h.y));
+  acc.z = fmaf(an, Bv.z, fmaf(ap, A.z, a0 * h.z));
+  acc.w = fmaf(an, Bv.w, fmaf(ap, A.w, a0 * h.w));
+  reinterpret_cast<float4*>(y3 + ((int64_t)b * n3 + p) * kDim)[lane] =
+      make_float4(elu1(acc.x), elu1(acc.y), elu1(acc.z), elu1(acc.w));
+}
+
 // F.normalize(x, p=2, dim=channels), one wave per token row (GATs_SuperGlue.py:245-246).
 __global__ __launch_bounds__(256) void l2norm_kernel(float* x2, int rows2, float* x3, int rows3) {
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -1411,9 +1557,10 @@ LayerTiles side_tiles(int n1, int n3, int B, int pm, bool cross) {
 }
 
 // Object cache layout (floats; onepose_object_cache_bytes): the 3D state entering layer 2,
-// GAT layers 1-3's leaf logits, then cross-attention 1's frame-independent 3D half (SideCache).
+// GAT layers 1-3's leaf logits, cross-attention 1's frame-independent 3D half (SideCache), then
+// GAT layers 1-3's prefix tables (gat_tab_kernel; built when num_leaf <= 8).
 struct ObjLayout {
-  int64_t logits, phiq, acc, ksum, mf, total;
+  int64_t logits, phiq, acc, ksum, mf, slogs, tab, total;
 };
 ObjLayout obj_layout(int n3) {
   ObjLayout L;
@@ -1422,7 +1569,9 @@ ObjLayout obj_layout(int n3) {
   L.acc = L.phiq + (int64_t)n3 * 256;
   L.ksum = L.acc + (int64_t)ceil_div(n3, 64) * 64 * 512;   // TILE_64x64 tiles of N = 512
   L.mf = L.ksum + 256;
-  L.total = L.mf + 512 * 256;
+  L.slogs = L.mf + 512 * 256;   // GAT layers 1-3 tables (num_leaf <= 8; gat_table_kernel)
+  L.tab = L.slogs + (int64_t)3 * n3 * kLogitStride;
+  L.total = L.tab + (int64_t)3 * n3 * kGatTabRows * 256;
   return L;
 }
 
@@ -1656,7 +1805,13 @@ int match_impl(const void* packed_weights, const float* desc2d, int64_t desc2d_b
                                 ? obj_cache + (int64_t)n3 * 256 +
                                       (int64_t)(gat - 1) * n3 * kLogitStride
                                 : nullptr;
-        if (num_leaf <= 8)
+        if (slog != nullptr && num_leaf <= 8 && g_gat_tables.load(std::memory_order_relaxed)) {
+          const ObjLayout OL = obj_layout(n3);
+          OP_LAUNCH(K_GAT, st, gat_tab_kernel, ggrid, dim3(256), 0, st, x3r, gat_weights(wbase, gat),
+                    obj_cache + OL.slogs + (int64_t)(gat - 1) * n3 * kLogitStride,
+                    obj_cache + OL.tab + (int64_t)(gat - 1) * n3 * kGatTabRows * 256,
+                    p.x3[c3 ^ 1], n3, num_leaf, B);
+        } else if (num_leaf <= 8)
           OP_LAUNCH(K_GAT, st, gat_kernel<8>, ggrid, dim3(256), 0, st, x3r, leaves,
                     leaves_bstride, gat_weights(wbase, gat), slog, p.x3[c3 ^ 1], n3, num_leaf, B);
         else
@@ -1810,6 +1965,9 @@ int object_prepare_impl(const void* packed_weights, const float* desc3d, const f
               gat_weights(wbase, 0), nolog, p.x3[1], n3, num_leaf, 1);
     OP_LAUNCH(K_GAT, st, gat_logits_kernel<8>, ggrid, dim3(256), 0, st, leaves_pm,
               gat_weights(wbase, 1), slog, n3, num_leaf);
+    const ObjLayout OL = obj_layout(n3);
+    OP_LAUNCH(K_GAT, st, gat_table_kernel, ggrid, dim3(256), 0, st, leaves_pm,
+              gat_weights(wbase, 1), cache + OL.slogs, cache + OL.tab, n3, num_leaf);
   } else {
     OP_LAUNCH(K_GAT, st, gat_kernel<16>, ggrid, dim3(256), 0, st, p.x3[0], leaves_pm, (int64_t)0,
               gat_weights(wbase, 0), nolog, p.x3[1], n3, num_leaf, 1);
@@ -1983,6 +2141,10 @@ int onepose_match_prepared(const void* packed_weights, const float* desc2d,
                                    scale_factor, match_threshold, ONEPOSE_PREC_FP32, matches0,
                                    matches1, mscores0, mscores1, conf, workspace, workspace_bytes,
                                    stream_);
+}
+
+int onepose_set_gat_tables(int enable) {
+  return onepose::g_gat_tables.exchange(enable != 0) ? 1 : 0;
 }
 
 size_t onepose_object_cache_bytes(int n3) {

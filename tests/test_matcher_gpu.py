@@ -259,11 +259,28 @@ def test_object_cache_is_bit_identical(device, n1, n3, L, B, prec):
     uncached forward runs self-attention 1's halves with the prefix's / cached choices.
     1000 x 3001 (B = 3 / 6): ragged sides with different per-side QKV tiles in layers 1-2 (2D
     32-row, 3D 64-row chunks, both with a partial last chunk), and at B = 6 a 2D source slot
-    folded by kv_reduce + m_fold beside the 3D slot's kv_fold."""
+    folded by kv_reduce + m_fold beside the 3D slot's kv_fold.  The cached forward's GAT
+    layers 1-3 read the leaves here (onepose_set_gat_tables(0)), as the uncached one does;
+    test_gat_tables_cached_forward covers the tables."""
     from onepose_amd import _lib
     lib = _lib.load()
-    sd = synthetic.make_state_dict(0)
-    data, _, _ = synthetic.make_matcher_inputs(n1, n3, L, seed=11, batch=B)
+    prev = lib.onepose_set_gat_tables(0)
+    try:
+        outs = cached_and_uncached(lib, device, n1, n3, L, B, prec, seed=11)
+    finally:
+        lib.onepose_set_gat_tables(prev)
+    for k in outs[0]:
+        np.testing.assert_array_equal(outs[0][k], outs[1][k], err_msg=k)
+    if n1 == 1024 and prec == 0:
+        assert (outs[1]["m0"] > -1).sum() > 100
+
+
+def cached_and_uncached(lib, device, n1, n3, L, B, prec, seed, sd_seed=0, modes=(False, True)):
+    """Outputs of onepose_match_prepared_ex (False) / onepose_object_prepare +
+    onepose_match_cached (True) on one object shared by the batch."""
+    from onepose_amd import _lib
+    sd = synthetic.make_state_dict(sd_seed)
+    data, _, _ = synthetic.make_matcher_inputs(n1, n3, L, seed=seed, batch=B)
     m = matcher.from_state_dict(sd)
     w = m.packed_weights(device)
     f32 = dict(dtype=torch.float32, device=device)
@@ -281,7 +298,7 @@ def test_object_cache_is_bit_identical(device, n1, n3, L, B, prec):
     ws_bytes = lib.onepose_match_workspace_bytes(B, n1, n3, L, 1)
     sf, thr = float(m.hparams["scale_factor"]), float(m.hparams["match_threshold"])
     outs = []
-    for cached in (False, True):
+    for cached in modes:
         o = dict(m0=torch.empty(B, n1, dtype=torch.int64, device=device),
                  m1=torch.empty(B, n3, dtype=torch.int64, device=device),
                  s0=torch.empty(B, n1, **f32), s1=torch.empty(B, n3, **f32),
@@ -299,10 +316,49 @@ def test_object_cache_is_bit_identical(device, n1, n3, L, B, prec):
         _lib.check(rc, "match")
         torch.cuda.synchronize()
         outs.append({k: v.cpu().numpy() for k, v in o.items()})
-    for k in outs[0]:
-        np.testing.assert_array_equal(outs[0][k], outs[1][k], err_msg=k)
-    if n1 == 1024 and prec == 0:
-        assert (outs[1]["m0"] > -1).sum() > 100
+    return outs
+
+
+@pytest.mark.parametrize("n1,n3,L,B", [(200, 777, 8, 1), (1000, 3001, 8, 1), (256, 1024, 4, 2),
+                                       (1024, 4096, 8, 2), (64, 96, 1, 1)])
+def test_gat_tables_cached_forward(device, n1, n3, L, B):
+    """The cached forward's GAT layers 1-3 from the object's prefix tables (sorted leaf logits,
+    exp-weighted prefix / suffix sums; num_leaf <= 8) vs the same forward reading the leaves
+    (onepose_set_gat_tables(0), bit-identical to the uncached forward): conf and scores within
+    ATOL, indices equal except low-margin rows; at B = 1 also vs the numpy oracle."""
+    from onepose_amd import _lib
+    lib = _lib.load()
+    assert lib.onepose_set_gat_tables(1) in (0, 1)
+    tab = cached_and_uncached(lib, device, n1, n3, L, B, 0, seed=5, modes=(True,))[0]
+    prev = lib.onepose_set_gat_tables(0)
+    try:
+        direct = cached_and_uncached(lib, device, n1, n3, L, B, 0, seed=5, modes=(True,))[0]
+    finally:
+        lib.onepose_set_gat_tables(prev)
+    assert np.isfinite(tab["conf"]).all()
+    np.testing.assert_allclose(tab["conf"], direct["conf"], atol=ATOL)
+    for b in range(B):
+        c = direct["conf"][b]
+        top = -np.sort(-c, axis=1)[:, :2] if n3 > 1 else np.stack([c[:, 0], 0 * c[:, 0]], 1)
+        ctop = -np.sort(-c, axis=0)[:2] if n1 > 1 else np.stack([c[0], 0 * c[0]])
+        rm = np.minimum(top[:, 0] - top[:, 1], np.abs(direct["s0"][b] - 0.2))
+        cm = np.minimum(ctop[0] - ctop[1], np.abs(direct["s1"][b] - 0.2))
+        check_indices(tab["m0"][b], direct["m0"][b], rm, "matches0")
+        check_indices(tab["m1"][b], direct["m1"][b], cm, "matches1")
+        check_scores(tab["s0"][b], direct["s0"][b], tab["conf"][b], top.T, ctop, True, "scores0")
+    if B == 1:
+        from oracle import matcher_np as M
+        sd = synthetic.make_state_dict(0)
+        data, _, _ = synthetic.make_matcher_inputs(n1, n3, L, seed=5, batch=1)
+        opred, oconf = M.forward(sd, data)
+        np.testing.assert_allclose(tab["conf"], oconf, atol=ATOL)
+        top = -np.sort(-oconf[0], axis=1)[:, :2]
+        ms0 = np.asarray(opred["matching_scores0"]).reshape(-1)
+        rm = np.minimum(top[:, 0] - top[:, 1], np.abs(ms0 - 0.2))
+        check_indices(tab["m0"][0], np.asarray(opred["matches0"]).reshape(-1), rm,
+                      "matches0 vs oracle")
+    if n1 >= 1000:
+        assert (tab["m0"] > -1).sum() > 100
 
 
 @pytest.mark.parametrize("n1,n3,L", [(1, 1, 1), (1, 7, 2), (3, 5, 8), (65, 1, 8), (33, 97, 16),
