@@ -95,8 +95,10 @@ class FramePipeline:
         _lib.check(self.lib.onepose_prepare_leaves(
             self.leaves.data_ptr(), 0, 1, self.n3, self.L, self.leaves_pm.data_ptr(),
             _lib.stream_ptr(dev)), "prepare_leaves")
-        # the object-only prefix of the forward (GAT 0 + the 3D half of self-attention 1),
-        # computed once: every frame starts from it (onepose_match_cached, bit-identical)
+        # the object-only prefix of the forward (GAT 0 + the 3D half of self-attention 1) and
+        # the GAT prefix tables, computed once: every frame starts from it (onepose_match_cached;
+        # bit-identical to the uncached forward with onepose_set_gat_tables(0), equal within
+        # rounding with the tables)
         self.object_cache = None
         if object_cache:
             self.object_cache = torch.empty(self.lib.onepose_object_cache_bytes(self.n3) // 4, **f32)
