@@ -319,20 +319,22 @@ def cached_and_uncached(lib, device, n1, n3, L, B, prec, seed, sd_seed=0, modes=
     return outs
 
 
-@pytest.mark.parametrize("n1,n3,L,B", [(200, 777, 8, 1), (1000, 3001, 8, 1), (256, 1024, 4, 2),
-                                       (1024, 4096, 8, 2), (64, 96, 1, 1)])
-def test_gat_tables_cached_forward(device, n1, n3, L, B):
+@pytest.mark.parametrize("n1,n3,L,B,prec", [(200, 777, 8, 1, 0), (1000, 3001, 8, 1, 0),
+                                            (256, 1024, 4, 2, 0), (1024, 4096, 8, 2, 0),
+                                            (64, 96, 1, 1, 0), (512, 2048, 8, 1, 2)])
+def test_gat_tables_cached_forward(device, n1, n3, L, B, prec):
     """The cached forward's GAT layers 1-3 from the object's prefix tables (sorted leaf logits,
     exp-weighted prefix / suffix sums; num_leaf <= 8) vs the same forward reading the leaves
     (onepose_set_gat_tables(0), bit-identical to the uncached forward): conf and scores within
-    ATOL, indices equal except low-margin rows; at B = 1 also vs the numpy oracle."""
+    ATOL, indices equal except low-margin rows; at B = 1 also vs the numpy oracle.  prec 2:
+    the fp32-by-3xbf16 split mode (fp32-accurate, same bar)."""
     from onepose_amd import _lib
     lib = _lib.load()
     assert lib.onepose_set_gat_tables(1) in (0, 1)
-    tab = cached_and_uncached(lib, device, n1, n3, L, B, 0, seed=5, modes=(True,))[0]
+    tab = cached_and_uncached(lib, device, n1, n3, L, B, prec, seed=5, modes=(True,))[0]
     prev = lib.onepose_set_gat_tables(0)
     try:
-        direct = cached_and_uncached(lib, device, n1, n3, L, B, 0, seed=5, modes=(True,))[0]
+        direct = cached_and_uncached(lib, device, n1, n3, L, B, prec, seed=5, modes=(True,))[0]
     finally:
         lib.onepose_set_gat_tables(prev)
     assert np.isfinite(tab["conf"]).all()
