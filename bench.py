@@ -59,7 +59,7 @@ def frame_flops(n1, n3, L, cached, B=1):
     """algorithmic MFMA FLOPs per frame, F, or F_dep when the object-only
     prefix (GAT 0 + the 3D half of self-attention 1) is cached per object.  With cross-
     attention 1's 3D half cached too (cross_cached), half of that layer's per-3D-token work
-    (q, k, v projections 10 C^2, KV 2 C dh, W1a x 4 C^2 = 688,128 FLOP) is not per frame."""
+    (q, k, v projections 6 C^2, KV 2 C dh, W1a x 4 C^2 = 688,128 FLOP) is not per frame."""
     f = 11141120 * (n1 + n3) + 512 * n1 * n3 + 2048 * (L + 2) * n3
     if not cached:
         return f

@@ -154,26 +154,33 @@ int onepose_match_prepared(const void* packed_weights,
  * independent 3D half (layer 2, GATs_SuperGlue.py:74-78: the 3D side's phi(q), sum phi(k), the
  * 2D side's folded message weights and the W1a x half of its MLP conv 1) --
  * onepose_object_cache_bytes in all (an opaque layout); onepose_match_cached then runs every
- * frame from there.  With num_leaf <= 8 the cache also holds prefix tables of GAT layers 1-3
- * (the leaves sorted by logit, exp-weighted prefix and suffix sums: [3][n3][16][256] fp32), and
- * a cached frame's GAT layers 1-3 read two table rows per 3D point instead of its L leaves; they
- * then differ from computing the layers from the leaves in rounding only.  With the tables off
- * (onepose_set_gat_tables(0)) the results are bit-identical to onepose_match_prepared_ex's on the
- * same object (the same kernels and tiles produce the cached state), provided the cache was
- * prepared with the same `precision`.
+ * frame from there.
+ *
+ * `flags` (ONEPOSE_OBJ_*) fix the cache's layout and contents at prepare time; pass the same
+ * value to onepose_object_cache_bytes and onepose_match_cached.  With ONEPOSE_OBJ_GAT_TABLES and
+ * num_leaf <= 8 the cache also holds prefix tables of GAT layers 1-3 (the leaves sorted by
+ * logit, exp-weighted prefix and suffix sums: [3][n3][2 num_leaf][256] fp32 plus [3][n3][16]
+ * sorted logits, i.e. 6 KB x num_leaf + 192 B per 3D point: 202 MB at n3 = 4096, L = 8), and a
+ * cached frame's GAT layers 1-3 read two table rows per 3D point instead of its L leaves; they
+ * then differ from computing the layers from the leaves in rounding only.  Without it (flags
+ * 0; the tables are never built for num_leaf > 8) the results are bit-identical to
+ * onepose_match_prepared_ex's on the same object (the same kernels and tiles produce the cached
+ * state), provided the cache was prepared with the same `precision`.  Without tables the cache
+ * is 4 KB + 192 B per 3D point (17.6 MB at n3 = 4096) plus a 0.5 MB fixed part.
  *   desc3d:          [256][n3] reference layout (descriptors3d_db of one object)
  *   leaves_prepared: [n3*L][256] point-major (onepose_prepare_leaves of the object)
- * The cache is shared by every sample of a batch (one object per call).
+ * The cache is shared by every sample of a batch (one object per call); it is read-only for
+ * onepose_match_cached, so any number of streams may use one cache concurrently.
  * ------------------------------------------------------------------------------------ */
-size_t onepose_object_cache_bytes(int n3);
-/* Process-wide: whether onepose_match_cached's GAT layers 1-3 use the object's prefix tables
- * (default 1) or the leaves.  Returns the previous setting.  (No reference counterpart: the
- * reference has no object cache.) */
-int onepose_set_gat_tables(int enable);
+enum {
+  ONEPOSE_OBJ_GAT_TABLES = 1    /* build / use the GAT prefix tables (num_leaf <= 8)          */
+};
+size_t onepose_object_cache_bytes(int n3, int num_leaf, int flags);
 size_t onepose_object_prepare_workspace_bytes(int n3, int num_leaf);
 int onepose_object_prepare(const void* packed_weights, const float* desc3d,
                            const float* leaves_prepared, int n3, int num_leaf, int precision,
-                           float* cache, void* workspace, size_t workspace_bytes, void* stream);
+                           int flags, float* cache, void* workspace, size_t workspace_bytes,
+                           void* stream);
 /* Workspace: onepose_match_workspace_bytes(batch, n1, n3, num_leaf, conf != NULL). */
 int onepose_match_cached(const void* packed_weights,
                          const float* desc2d, int64_t desc2d_bstride,
@@ -181,6 +188,7 @@ int onepose_match_cached(const void* packed_weights,
                          const float* leaves_prepared, int64_t prepared_bstride,
                          int batch, int n1, int n3, int num_leaf,
                          float scale_factor, float match_threshold, int precision,
+                         int object_flags,
                          int64_t* matches0, int64_t* matches1,
                          float* mscores0, float* mscores1, float* conf,
                          void* workspace, size_t workspace_bytes, void* stream);

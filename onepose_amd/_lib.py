@@ -20,6 +20,8 @@ c_void_p, c_char_p = ctypes.c_void_p, ctypes.c_char_p
 
 # onepose_allgather_fn: int (*)(size_t bytes_per_rank, void* stream, void* user)
 ALLGATHER_FN = ctypes.CFUNCTYPE(c_int, c_size_t, c_void_p, c_void_p)
+ABI_VERSION = 2
+OBJ_GAT_TABLES = 1   # ONEPOSE_OBJ_GAT_TABLES
 
 # name -> (restype, argtypes); mirrors include/onepose_hip.h
 PROTOTYPES = {
@@ -47,13 +49,12 @@ PROTOTYPES = {
                                           c_void_p, c_int64, c_int, c_int, c_int, c_int, c_float,
                                           c_float, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                                           c_void_p, c_void_p, c_size_t, c_void_p]),
-    "onepose_object_cache_bytes": (c_size_t, [c_int]),
-    "onepose_set_gat_tables": (c_int, [c_int]),
+    "onepose_object_cache_bytes": (c_size_t, [c_int, c_int, c_int]),
     "onepose_object_prepare_workspace_bytes": (c_size_t, [c_int, c_int]),
     "onepose_object_prepare": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
-                                       c_void_p, c_void_p, c_size_t, c_void_p]),
+                                       c_int, c_void_p, c_void_p, c_size_t, c_void_p]),
     "onepose_match_cached": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_int64,
-                                     c_int, c_int, c_int, c_int, c_float, c_float, c_int,
+                                     c_int, c_int, c_int, c_int, c_float, c_float, c_int, c_int,
                                      c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                      c_void_p, c_size_t, c_void_p]),
     "onepose_shard_range": (None, [c_int, c_int, c_int, ctypes.POINTER(c_int),
@@ -124,6 +125,9 @@ def load():
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args
+        if lib.onepose_abi_version() != ABI_VERSION:
+            raise OnePoseError(f"{LIB_PATH}: ABI version {lib.onepose_abi_version()}, "
+                               f"expected {ABI_VERSION}: rebuild with `python -m onepose_amd.build`")
         _lib = lib
     return _lib
 

@@ -20,13 +20,9 @@
 
 #include <cstring>
 
-// Pins the pipeline's phase order (tools/gemm_probe.hip compiles it out to compare with the
-// compiler's own schedule: ONEPOSE_GEMM_PROBE_NO_SCHED).
-#ifdef ONEPOSE_GEMM_PROBE_NO_SCHED
-#define ONEPOSE_SCHED_BARRIER() ((void)0)
-#else
+// Pins the pipeline's phase order (the compiler's own schedule measured within +-2%,
+// DESIGN.md §3d).
 #define ONEPOSE_SCHED_BARRIER() __builtin_amdgcn_sched_barrier(0)
-#endif
 
 namespace onepose {
 
@@ -390,9 +386,7 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
   auto step = [&](int kt, Stage<T>& next, Stage<T>& spare, const Frag& cur, Frag& nxt,
                   floatx16 (&tg)[FN]) __attribute__((always_inline)) {
     // unconditional: past the end the last stage is re-read into the spare set and ignored
-#ifndef ONEPOSE_GEMM_PROBE_NOLOAD   // (tools/gemm_probe.hip: the loop without its global loads)
     load_stage<PRO, T>(c, m0, n0, min(kt + 2, nk - 1) * T::BKS, spare);
-#endif
     mfma_kk(tg, cur, 0);
     ONEPOSE_SCHED_BARRIER();
     float* na = lds + ((kt + 1) & 1) * STAGE;
@@ -576,15 +570,9 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
     // Every store and load of the handed-off partials is sc1, so neither an agent-scope
     // release (it would write back the XCD's L2, this tile's Y in it) nor an acquire (an L1
     // invalidate, ~1.7 us) is needed.  The counters are zeroed by the forward's first kernel.
-#ifdef ONEPOSE_GEMM_PROBE_NOFINAL   // (probe: partials only; stale mean / rstd)
-    unsigned* tickets = nullptr;
-#else
     unsigned* tickets = F(st_cnt);
-#endif
     if (tickets != nullptr) {
-#ifndef ONEPOSE_GEMM_PROBE_NODRAIN   // (probe: ticket without draining the partial stores)
       if (t < BN) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the storing wave drains
-#endif
       __syncthreads();   // partial stores drained; `part` no longer read
       int* last = reinterpret_cast<int*>(part);
       if (t == 0) {
@@ -593,11 +581,7 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
         last[0] = ticket == (unsigned)(mtiles - 1) ? 1 : 0;
       }
       __syncthreads();
-#ifdef ONEPOSE_GEMM_PROBE_NOREDUCE   // (probe: tickets taken, the last tile reduces nothing)
-      if (false) {
-#else
       if (last[0]) {
-#endif
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // (no instruction: keeps the
                                                                  // loads below the ticket)
         // one pass over the partials (sc1 loads, 16 tiles in flight per thread), shifted by

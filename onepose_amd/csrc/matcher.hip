@@ -41,18 +41,7 @@ namespace onepose {
 // GEMM tile per layer GEMM (gemm.h; measured per shape on config 2).
 constexpr int kTileKV = TILE_32x128, kTileMLP1 = TILE_64x64,
               kTileMLP2 = TILE_64x64, kTileMLP2F32 = TILE_64x32K2, kTileFinal = TILE_64x64;
-#ifdef ONEPOSE_SCORE_TILE64   // A/B probe: the round-2 score tile
-constexpr int kTileScore = TILE_64x64, kScoreBM = 64;
-#else
 constexpr int kTileScore = TILE_128x64W8, kScoreBM = 128;
-#endif
-// The cached forward's GAT layers 1-3 from the object's prefix tables (gat_tab_kernel), or
-// from the leaves (gat_kernel, the uncached forward's kernel): onepose_set_gat_tables.
-#ifdef ONEPOSE_NO_GAT_TABLES
-std::atomic<bool> g_gat_tables{false};
-#else
-std::atomic<bool> g_gat_tables{true};
-#endif
 constexpr int kFusedFoldMaxBatch = 4;   // kv_fold up to this batch, kv_reduce + m_fold above
 constexpr int kMlp2WideTiles = 1024;    // fp32 mlp2: 64x64 tiles from this many (4 per CU)
 constexpr int kQkvWideTiles = 256;      // fp32 qkv: 64x128 tiles from this many 64-row tiles
@@ -385,18 +374,8 @@ typedef float f2v __attribute__((ext_vector_type(2)));
 // was the slower half of the kernel: 1625 -> 1627 frames/s, kv_fold 9.5 -> 8.7 us per launch
 // with launch overhead, `tools/ab_multi.sh`); q quarters accumulated in q order, then added in
 // quarter order.
-#ifndef KVF_DEPTH
-#define KVF_DEPTH 16
-#endif
-#ifndef KVF_OSPLIT   // Mf row blocks per KV row block (1: 512 rows, 2: 256 rows per workgroup)
-#define KVF_OSPLIT 2
-#endif
-#ifndef KVF_PROBE_NOSUM   // (probes: timing only, wrong results)
-#define KVF_PROBE_NOSUM 0
-#endif
-#ifndef KVF_PROBE_NOFOLD
-#define KVF_PROBE_NOFOLD 0
-#endif
+constexpr int KVF_DEPTH = 16;   // chunk loads in flight per lane
+constexpr int KVF_OSPLIT = 2;   // Mf row blocks per KV row block (256 Mf rows per workgroup)
 __global__ __launch_bounds__(256) void kv_fold256_kernel(KvFoldArgs args, float* kv, float* ksum,
                                                          int batch) {
   constexpr int OS = KVF_OSPLIT;
@@ -425,20 +404,14 @@ __global__ __launch_bounds__(256) void kv_fold256_kernel(KvFoldArgs args, float*
     float4 v[KVF_DEPTH];
 #pragma unroll
     for (int j = 0; j < KVF_DEPTH; ++j)
-      v[j] = c + 4 * j < P.chunks && !KVF_PROBE_NOSUM ? base[idx + (c + 4 * j) * stride] : make_float4(0.f, 0.f, 0.f, 0.f);
+      v[j] = c + 4 * j < P.chunks ? base[idx + (c + 4 * j) * stride] : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
     for (int j = 0; j < KVF_DEPTH; ++j) { acc.x += v[j].x; acc.y += v[j].y; acc.z += v[j].z; acc.w += v[j].w; }
   }
   // the fold's first quarter of C (independent of KV) is in flight across the reduction below
-#if KVF_OSPLIT == 1
-  const int op = t;   // Mf rows 2 op, 2 op + 1
-  const float* ct = args.ct + (h * 64) * 512 + 2 * op;
-  f2v cv[16];
-#else
   const int o = os * 256 + t;   // Mf row o
   const float* ct = args.ct + (h * 64) * 512 + o;
   float cv[16];
-#endif
   if (g != 64) {
 #pragma unroll
     for (int i = 0; i < 16; ++i) cv[i] = *reinterpret_cast<const std::remove_reference_t<decltype(cv[0])>*>(ct + i * 512);
@@ -457,35 +430,9 @@ __global__ __launch_bounds__(256) void kv_fold256_kernel(KvFoldArgs args, float*
     }
     red[0][lane] = s;   // KV rows d0..d0+3: red[0][16 j + q/4] = KV_h[d0 + j][q .. q+3]
   }
-  if (g == 64 || KVF_PROBE_NOFOLD) return;
+  if (g == 64) return;
   __syncthreads();
   const float* kvr = reinterpret_cast<const float*>(&red[0][0]);
-#if KVF_OSPLIT == 1
-  f2v y[4];
-#pragma unroll
-  for (int qq = 0; qq < 4; ++qq) {
-    if (qq > 0) {
-#pragma unroll
-      for (int i = 0; i < 16; ++i) cv[i] = *reinterpret_cast<const f2v*>(ct + (qq * 16 + i) * 512);
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      f2v yq = (f2v)(0.f);
-#pragma unroll
-      for (int i = 0; i < 16; i += 4) {
-        const float4 k = *reinterpret_cast<const float4*>(kvr + j * 64 + qq * 16 + i);
-        yq = __builtin_elementwise_fma(cv[i], (f2v)(k.x), yq);
-        yq = __builtin_elementwise_fma(cv[i + 1], (f2v)(k.y), yq);
-        yq = __builtin_elementwise_fma(cv[i + 2], (f2v)(k.z), yq);
-        yq = __builtin_elementwise_fma(cv[i + 3], (f2v)(k.w), yq);
-      }
-      y[j] = qq == 0 ? yq : y[j] + yq;
-    }
-  }
-  float* mf = (src ? args.mf[1] : args.mf[0]) + (int64_t)b * 512 * 256 + (2 * op) * 256 + h * 64 + d0;
-  *reinterpret_cast<float4*>(mf) = make_float4(y[0].x, y[1].x, y[2].x, y[3].x);
-  *reinterpret_cast<float4*>(mf + 256) = make_float4(y[0].y, y[1].y, y[2].y, y[3].y);
-#else
   // one Mf row per thread, its four d as two packed pairs (d0, d0 + 1), (d0 + 2, d0 + 3); q
   // quarters accumulated in q order, then added in quarter order
   f2v y01, y23;
@@ -516,7 +463,6 @@ __global__ __launch_bounds__(256) void kv_fold256_kernel(KvFoldArgs args, float*
   }
   float* mf = (src ? args.mf[1] : args.mf[0]) + (int64_t)b * 512 * 256 + (int64_t)o * 256 + h * 64 + d0;
   *reinterpret_cast<float4*>(mf) = make_float4(y01.x, y01.y, y23.x, y23.y);
-#endif
 }
 
 // InstanceNorm1d statistics (GATs_SuperGlue.py:145; biased variance, eps 1e-5): per-64-row-tile
@@ -769,10 +715,10 @@ __global__ __launch_bounds__(256) void gat_kernel(const float* __restrict__ x3,
 // (both factors <= 1, so nothing overflows).  A frame then reads two table rows per point
 // instead of its L leaves (config 2: 16 instead of 42 MB per launch).  The sums differ from
 // the direct kernel's (gat_kernel) in rounding only.
-constexpr int kGatTabRows = 16;   // per point: A_1..A_L at 0..L-1, B_0..B_(L-1) at 8..8+L-1
+// per point 2L rows: A_1..A_L at 0..L-1, B_0..B_(L-1) at L..2L-1
 
 // Tables for the three frame-dependent GAT layers: slogs [3][n3][kLogitStride] (sorted leaf
-// logits, descending; equal logits by leaf index), tab [3][n3][kGatTabRows][256].
+// logits, descending; equal logits by leaf index), tab [3][n3][2L][256].
 __global__ __launch_bounds__(256) void gat_table_kernel(const float* __restrict__ leaves_pm,
                                                         const float* __restrict__ wa1,
                                                         float* __restrict__ slogs,
@@ -818,7 +764,7 @@ __global__ __launch_bounds__(256) void gat_table_kernel(const float* __restrict_
       sl[r] = f;
     }
     const float c = sv[0];
-    float* out = tab + (((int64_t)g * n3 + p) * kGatTabRows) * kDim;
+    float* out = tab + (((int64_t)g * n3 + p) * 2 * L) * kDim;
     float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
     for (int r = 0; r < MAXL; ++r) {
@@ -835,7 +781,7 @@ __global__ __launch_bounds__(256) void gat_table_kernel(const float* __restrict_
       const float wn = expf(0.2f * (sv[r] - c));
       a.x = fmaf(wn, sl[r].x, a.x); a.y = fmaf(wn, sl[r].y, a.y);
       a.z = fmaf(wn, sl[r].z, a.z); a.w = fmaf(wn, sl[r].w, a.w);
-      reinterpret_cast<float4*>(out + (MAXL + r) * kDim)[lane] = a;   // B_r
+      reinterpret_cast<float4*>(out + (L + r) * kDim)[lane] = a;   // B_r
     }
     float v = 0.f;
 #pragma unroll
@@ -883,10 +829,10 @@ __global__ __launch_bounds__(256) void gat_tab_kernel(const float* __restrict__ 
     else sn += expf(0.2f * (sv[r] - c));
   }
   const float sum = E0 + Fp * sp_ + Fn * sn;
-  const float* tp = tab + (int64_t)pu * kGatTabRows * kDim;
+  const float* tp = tab + (int64_t)pu * 2 * L * kDim;
   const float4 A = k > 0 ? reinterpret_cast<const float4*>(tp + (k - 1) * kDim)[lane]
                          : make_float4(0.f, 0.f, 0.f, 0.f);
-  const float4 Bv = k < L ? reinterpret_cast<const float4*>(tp + (MAXL + k) * kDim)[lane]
+  const float4 Bv = k < L ? reinterpret_cast<const float4*>(tp + (L + k) * kDim)[lane]
                           : make_float4(0.f, 0.f, 0.f, 0.f);
   const float a0 = E0 / sum, ap = Fp / sum, an = Fn / sum;
   float4 acc;
@@ -1218,7 +1164,7 @@ using namespace onepose;
 extern "C" {
 
 const char* onepose_last_error(void) { return g_last_error.c_str(); }
-int onepose_abi_version(void) { return 1; }
+int onepose_abi_version(void) { return 2; }
 
 int onepose_profile_begin(uint64_t kind_mask, int capacity) {
   clear_error();
@@ -1557,21 +1503,27 @@ LayerTiles side_tiles(int n1, int n3, int B, int pm, bool cross) {
 }
 
 // Object cache layout (floats; onepose_object_cache_bytes): the 3D state entering layer 2,
-// GAT layers 1-3's leaf logits, cross-attention 1's frame-independent 3D half (SideCache), then
-// GAT layers 1-3's prefix tables (gat_tab_kernel; built when num_leaf <= 8).
+// GAT layers 1-3's leaf logits, cross-attention 1's frame-independent 3D half (SideCache), then,
+// with ONEPOSE_OBJ_GAT_TABLES and num_leaf <= 8, GAT layers 1-3's prefix tables (sorted logits
+// [3][n3][16] and [3][n3][2L][256] rows, gat_tab_kernel).
+bool obj_tables(int num_leaf, int flags) {
+  return (flags & ONEPOSE_OBJ_GAT_TABLES) != 0 && num_leaf <= 8;
+}
 struct ObjLayout {
   int64_t logits, phiq, acc, ksum, mf, slogs, tab, total;
+  bool tables;
 };
-ObjLayout obj_layout(int n3) {
+ObjLayout obj_layout(int n3, int num_leaf, int flags) {
   ObjLayout L;
+  L.tables = obj_tables(num_leaf, flags);
   L.logits = (int64_t)n3 * 256;
   L.phiq = L.logits + (int64_t)3 * n3 * kLogitStride;
   L.acc = L.phiq + (int64_t)n3 * 256;
   L.ksum = L.acc + (int64_t)ceil_div(n3, 64) * 64 * 512;   // TILE_64x64 tiles of N = 512
   L.mf = L.ksum + 256;
-  L.slogs = L.mf + 512 * 256;   // GAT layers 1-3 tables (num_leaf <= 8; gat_table_kernel)
-  L.tab = L.slogs + (int64_t)3 * n3 * kLogitStride;
-  L.total = L.tab + (int64_t)3 * n3 * kGatTabRows * 256;
+  L.slogs = L.mf + 512 * 256;
+  L.tab = L.slogs + (L.tables ? (int64_t)3 * n3 * kLogitStride : 0);
+  L.total = L.tab + (L.tables ? (int64_t)3 * n3 * 2 * num_leaf * 256 : 0);
   return L;
 }
 
@@ -1767,7 +1719,8 @@ int match_impl(const void* packed_weights, const float* desc2d, int64_t desc2d_b
                int64_t leaves_pm_bs, int batch, int n1, int n3, int num_leaf, float scale_factor,
                float match_threshold, int64_t* matches0, int64_t* matches1, float* mscores0,
                float* mscores1, float* conf, const Plan& p, hipStream_t st, int precision,
-               const ShardCtx* sh = nullptr, const float* obj_cache = nullptr) {
+               const ShardCtx* sh = nullptr, const float* obj_cache = nullptr,
+               int obj_flags = 0) {
   const bool with_conf = conf != nullptr;
   const int n3g = sh ? sh->n3_total : n3;   // the 3D side's full length (softmax / attention)
   const int pm = attention_pm(precision);   // attention-layer GEMM operand mode
@@ -1805,11 +1758,11 @@ int match_impl(const void* packed_weights, const float* desc2d, int64_t desc2d_b
                                 ? obj_cache + (int64_t)n3 * 256 +
                                       (int64_t)(gat - 1) * n3 * kLogitStride
                                 : nullptr;
-        if (slog != nullptr && num_leaf <= 8 && g_gat_tables.load(std::memory_order_relaxed)) {
-          const ObjLayout OL = obj_layout(n3);
+        const ObjLayout OL = obj_layout(n3, num_leaf, obj_flags);
+        if (slog != nullptr && OL.tables) {
           OP_LAUNCH(K_GAT, st, gat_tab_kernel, ggrid, dim3(256), 0, st, x3r, gat_weights(wbase, gat),
                     obj_cache + OL.slogs + (int64_t)(gat - 1) * n3 * kLogitStride,
-                    obj_cache + OL.tab + (int64_t)(gat - 1) * n3 * kGatTabRows * 256,
+                    obj_cache + OL.tab + (int64_t)(gat - 1) * n3 * 2 * num_leaf * 256,
                     p.x3[c3 ^ 1], n3, num_leaf, B);
         } else if (num_leaf <= 8)
           OP_LAUNCH(K_GAT, st, gat_kernel<8>, ggrid, dim3(256), 0, st, x3r, leaves,
@@ -1842,7 +1795,7 @@ int match_impl(const void* packed_weights, const float* desc2d, int64_t desc2d_b
       rc = attention_layer(w, sd, 1, B, p, lcnt, st, pm, sh, tl);
     } else if (obj_cache && layer == 2 && !sh) {
       // cross-attention 1: the 3D side's frame-independent half from the object cache
-      const ObjLayout L = obj_layout(n3);
+      const ObjLayout L = obj_layout(n3, num_leaf, obj_flags);
       const SideCache xc = {obj_cache + L.phiq, obj_cache + L.acc, obj_cache + L.ksum,
                             obj_cache + L.mf};
       rc = attention_layer(w, sd, 2, B, p, lcnt, st, pm, nullptr, tl, &xc);
@@ -1946,8 +1899,8 @@ int match_impl(const void* packed_weights, const float* desc2d, int64_t desc2d_b
 // The same kernels and tiles as the grouped forward, so the cached state is bit-identical
 // to what onepose_match computes in place.
 int object_prepare_impl(const void* packed_weights, const float* desc3d, const float* leaves_pm,
-                        int n3, int num_leaf, int precision, float* cache, const Plan& p,
-                        hipStream_t st) {
+                        int n3, int num_leaf, int precision, int flags, float* cache,
+                        const Plan& p, hipStream_t st) {
   const float* wbase = static_cast<const float*>(packed_weights);
   {
     TransArgs ta;
@@ -1965,9 +1918,10 @@ int object_prepare_impl(const void* packed_weights, const float* desc3d, const f
               gat_weights(wbase, 0), nolog, p.x3[1], n3, num_leaf, 1);
     OP_LAUNCH(K_GAT, st, gat_logits_kernel<8>, ggrid, dim3(256), 0, st, leaves_pm,
               gat_weights(wbase, 1), slog, n3, num_leaf);
-    const ObjLayout OL = obj_layout(n3);
-    OP_LAUNCH(K_GAT, st, gat_table_kernel, ggrid, dim3(256), 0, st, leaves_pm,
-              gat_weights(wbase, 1), cache + OL.slogs, cache + OL.tab, n3, num_leaf);
+    const ObjLayout OL = obj_layout(n3, num_leaf, flags);
+    if (OL.tables)
+      OP_LAUNCH(K_GAT, st, gat_table_kernel, ggrid, dim3(256), 0, st, leaves_pm,
+                gat_weights(wbase, 1), cache + OL.slogs, cache + OL.tab, n3, num_leaf);
   } else {
     OP_LAUNCH(K_GAT, st, gat_kernel<16>, ggrid, dim3(256), 0, st, p.x3[0], leaves_pm, (int64_t)0,
               gat_weights(wbase, 0), nolog, p.x3[1], n3, num_leaf, 1);
@@ -1984,7 +1938,7 @@ int object_prepare_impl(const void* packed_weights, const float* desc3d, const f
   // Cross-attention 1 (layer 2), the 3D side's frame-independent half, with the choices a
   // cached forward's layer 2 makes (batch <= kFusedFoldMaxBatch: QKV tile from n3 alone, one
   // kv_fold launch), so that its bits are the ones the uncached forward computes in place.
-  const ObjLayout L = obj_layout(n3);
+  const ObjLayout L = obj_layout(n3, num_leaf, flags);
   const ApW w = ap_weights(wbase, 1);
   const Side x3 = {cache, 0, nullptr, cache + L.phiq, p.kvpart3, p.kspart3, nullptr, nullptr, n3,
                    (float)n3, 0, n3};
@@ -2143,13 +2097,9 @@ int onepose_match_prepared(const void* packed_weights, const float* desc2d,
                                    stream_);
 }
 
-int onepose_set_gat_tables(int enable) {
-  return onepose::g_gat_tables.exchange(enable != 0) ? 1 : 0;
-}
-
-size_t onepose_object_cache_bytes(int n3) {
-  if (n3 <= 0) return 0;
-  return (size_t)obj_layout(n3).total * sizeof(float);
+size_t onepose_object_cache_bytes(int n3, int num_leaf, int flags) {
+  if (n3 <= 0 || num_leaf < 1 || num_leaf > 16) return 0;
+  return (size_t)obj_layout(n3, num_leaf, flags).total * sizeof(float);
 }
 
 size_t onepose_object_prepare_workspace_bytes(int n3, int num_leaf) {
@@ -2160,13 +2110,15 @@ size_t onepose_object_prepare_workspace_bytes(int n3, int num_leaf) {
 
 int onepose_object_prepare(const void* packed_weights, const float* desc3d,
                            const float* leaves_prepared, int n3, int num_leaf, int precision,
-                           float* cache, void* workspace, size_t workspace_bytes, void* stream_) {
+                           int flags, float* cache, void* workspace, size_t workspace_bytes,
+                           void* stream_) {
   clear_error();
   OP_REQUIRE(packed_weights && desc3d && leaves_prepared && cache, "object_prepare: null pointer");
   OP_REQUIRE(valid_precision(precision),
              "object_prepare: precision %d", precision);
   OP_REQUIRE(n3 >= 1 && num_leaf >= 1 && num_leaf <= 16, "object_prepare: n3=%d num_leaf=%d", n3,
              num_leaf);
+  OP_REQUIRE((flags & ~ONEPOSE_OBJ_GAT_TABLES) == 0, "object_prepare: flags %d", flags);
   OP_REQUIRE(workspace != nullptr, "object_prepare: null workspace");
   const size_t need = onepose_object_prepare_workspace_bytes(n3, num_leaf);
   if (workspace_bytes < need) {
@@ -2175,18 +2127,21 @@ int onepose_object_prepare(const void* packed_weights, const float* desc3d,
   }
   const Plan p = make_plan(workspace, 1, 1, n3, num_leaf, false);
   return object_prepare_impl(packed_weights, desc3d, leaves_prepared, n3, num_leaf, precision,
-                             cache, p, static_cast<hipStream_t>(stream_));
+                             flags, cache, p, static_cast<hipStream_t>(stream_));
 }
 
 int onepose_match_cached(const void* packed_weights, const float* desc2d, int64_t desc2d_bstride,
                          const float* object_cache, const float* leaves_prepared,
                          int64_t prepared_bstride, int batch, int n1, int n3, int num_leaf,
                          float scale_factor, float match_threshold, int precision,
-                         int64_t* matches0, int64_t* matches1, float* mscores0, float* mscores1,
-                         float* conf, void* workspace, size_t workspace_bytes, void* stream_) {
+                         int object_flags, int64_t* matches0, int64_t* matches1, float* mscores0,
+                         float* mscores1, float* conf, void* workspace, size_t workspace_bytes,
+                         void* stream_) {
   clear_error();
   OP_REQUIRE(valid_precision(precision),
              "match_cached: precision %d", precision);
+  OP_REQUIRE((object_flags & ~ONEPOSE_OBJ_GAT_TABLES) == 0, "match_cached: flags %d",
+             object_flags);
   int rc = check_match_args(packed_weights, desc2d, object_cache, leaves_prepared, batch, n1, n3,
                             num_leaf, scale_factor, matches0, matches1, mscores0, mscores1,
                             workspace);
@@ -2200,7 +2155,8 @@ int onepose_match_cached(const void* packed_weights, const float* desc2d, int64_
   return match_impl(packed_weights, desc2d, desc2d_bstride, object_cache, 0, leaves_prepared,
                     prepared_bstride, batch, n1, n3, num_leaf, scale_factor, match_threshold,
                     matches0, matches1, mscores0, mscores1, conf, p,
-                    static_cast<hipStream_t>(stream_), precision, nullptr, object_cache);
+                    static_cast<hipStream_t>(stream_), precision, nullptr, object_cache,
+                    object_flags);
 }
 
 void onepose_shard_range(int n3_total, int world, int rank, int* start, int* count) {

@@ -1125,18 +1125,6 @@ __device__ void null4_basis(const double (&M)[8][12], double (&v)[4][12]) {
 }
 
 // Workgroup-parallel EPnP over the points listed in idx[0..n) (epnp::compute_pose).
-#ifdef ONEPOSE_PNP_PHASES
-__device__ unsigned long long g_pnp_phase[16];
-#define PNP_PHASE(i) \
-  do {               \
-    __syncthreads(); \
-    if (threadIdx.x == 0 && blockIdx.x == 0) g_pnp_phase[i] = wall_clock64(); \
-  } while (0)
-#else
-#define PNP_PHASE(i) \
-  do {               \
-  } while (0)
-#endif
 
 __device__ __forceinline__ void epnp_refit(Shared& sh, const float* p2, const float* p3, const int* idx, int n,
                            const double* K4, double* R_out, double* t_out) {
@@ -1234,7 +1222,6 @@ __device__ __forceinline__ void epnp_refit(Shared& sh, const float* p2, const fl
       }
     }
     __syncthreads();
-    PNP_PHASE(1);
     for (int i = t; i < 144; i += kThreads) {
       const int r = i / 12, c = i - r * 12;
       const int k = r / 3, ii = r - 3 * k, l = c / 3, jj = c - 3 * l;
@@ -1251,7 +1238,6 @@ __device__ __forceinline__ void epnp_refit(Shared& sh, const float* p2, const fl
       sh.jA[i] = v;
     }
     __syncthreads();
-    PNP_PHASE(2);
     jacobi12_block(sh);   // workgroup-collective -> sh.vs
     __syncthreads();
     if (t < 60) {   // compute_L_6x10, one entry per thread
@@ -1325,7 +1311,6 @@ __device__ __forceinline__ void epnp_refit(Shared& sh, const float* p2, const fl
     }
   }
   __syncthreads();
-  PNP_PHASE(3);
   // compute_pose's three approximations, one per wave (waves 0..2), each reducing over the
   // points with wave-level sums; wave 3 waits
   if (wave < 3) {
@@ -1404,7 +1389,6 @@ __device__ __forceinline__ void epnp_refit(Shared& sh, const float* p2, const fl
     }
   }
   __syncthreads();
-  PNP_PHASE(4);
   int N = 1;
   if (sh.sol_err[2] < sh.sol_err[1]) N = 2;
   if (sh.sol_err[3] < sh.sol_err[N]) N = 3;
@@ -1588,9 +1572,6 @@ __global__ __launch_bounds__(kThreads) void pnp_ransac_kernel(
   Shared& sh = *reinterpret_cast<Shared*>(dyn);
   float* p2 = reinterpret_cast<float*>(dyn + ((sizeof(Shared) + 15) / 16) * 16);
   float* p3 = p2 + 2 * max_points;
-#ifdef ONEPOSE_PROBE_EMPTYPOSE   // (probe: launched with its resources, no work)
-  if (scale != 1.2345e-300) return;
-#endif
   const int b = blockIdx.x;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   int n;
@@ -1689,7 +1670,6 @@ __global__ __launch_bounds__(kThreads) void pnp_ransac_kernel(
     return;
   }
 
-  PNP_PHASE(8);
   while (!sh.done) {
     // getSubset x 64, in iteration order.  The round's draws are generated in parallel by
     // jump-ahead (see mwc_mulmod; states at or above m -- the first draws from
@@ -1791,7 +1771,6 @@ __global__ __launch_bounds__(kThreads) void pnp_ransac_kernel(
       }
     }
     __syncthreads();
-    PNP_PHASE(9);
     // one EPnP model per hypothesis: wave 0 the eigenvectors (lane h = hypothesis h), then
     // waves 1..3 one approximation each for every hypothesis; the smallest mean error wins
     // (ties to the earlier approximation, as compute_pose's sequential comparison)
@@ -1822,7 +1801,6 @@ __global__ __launch_bounds__(kThreads) void pnp_ransac_kernel(
       }
     }
     __syncthreads();
-    PNP_PHASE(10);
     // inlier counts and OpenCV's acceptance rule, 16 iterations at a time: iterations past
     // the stopping point are neither counted nor accepted (wave w counts w, w + 4, ...;
     // lanes sweep the points)
@@ -1837,7 +1815,6 @@ __global__ __launch_bounds__(kThreads) void pnp_ransac_kernel(
         if (lane == 0) sh.count[h] = c;
       }
       __syncthreads();
-      PNP_PHASE(11);
       if (t == 0) {  // in iteration order
         int iter = sh.iter, niters = sh.niters, best = sh.max_good;
         for (int h = hb; h < hb + 16 && iter < niters; ++h, ++iter) {
@@ -1860,7 +1837,6 @@ __global__ __launch_bounds__(kThreads) void pnp_ransac_kernel(
       if (sh.done) break;
     }
   }
-  PNP_PHASE(12);
 
   int nin;
   if (n == kModelPoints) {
@@ -1903,7 +1879,6 @@ __global__ __launch_bounds__(kThreads) void pnp_ransac_kernel(
     n_inliers[b] = nin;
     status[b] = 0;
   }
-  PNP_PHASE(13);
 }
 
 // EPnP on the RANSAC inliers (solvePnPRansac's final solvePnP call), then
@@ -1915,9 +1890,6 @@ __global__ __launch_bounds__(kThreads) void pnp_refit_kernel(
     const int* __restrict__ idx_ws, const double* __restrict__ pose_gt, int64_t gt_bs,
     double* __restrict__ rerr, double* __restrict__ terr, uint8_t* __restrict__ cmd) {
   __shared__ Shared sh;
-#ifdef ONEPOSE_PROBE_EMPTYPOSE
-  if (scale != 1.2345e-300) return;
-#endif
   const int b = blockIdx.x;
   const int t = threadIdx.x;
   double* pose = pose34 + (int64_t)b * 12;
@@ -1936,9 +1908,7 @@ __global__ __launch_bounds__(kThreads) void pnp_refit_kernel(
   const float* p2 = pts2d + (int64_t)b * max_points * 2;
   const float* p3 = pts3d + (int64_t)b * max_points * 3;
   double Rf[9], tf[3], rv[3], Rr[9];
-  PNP_PHASE(0);
   epnp_refit(sh, p2, p3, idx_ws + (int64_t)b * max_points, nin, K4, Rf, tf);
-  PNP_PHASE(5);
   rodrigues_m2v(Rf, rv);
   rodrigues_v2m(rv, Rr);
   if (t == 0) {
@@ -2034,9 +2004,6 @@ int onepose_pose_stage(const int64_t* matches0, const float* kpts2d, int64_t kpt
   }
   hipStream_t st = static_cast<hipStream_t>(stream);
   const SelArgs sel{matches0, kpts2d, kpts2d_bstride, kpts3d, kpts3d_bstride, n1, n3, scale};
-#ifdef ONEPOSE_PROBE_NOPOSE   // (probe: what the pose stage costs the matcher streams)
-  return ONEPOSE_OK;
-#endif
   OP_LAUNCH(K_PNP, st, pnp_ransac_kernel, dim3(batch), dim3(kThreads), lds, st, nullptr, nullptr,
             nullptr, max_points, K, K_bstride, scale, reproj_error, max_iters, confidence, pose34,
             inlier_mask, n_inliers, status, static_cast<int*>(workspace), sel, pts2d, pts3d,

@@ -116,10 +116,13 @@ def load_object_annotations(anno_dir, num_leaf=8, max_num_kp3d=None):
 
 
 def save_object_annotations(anno_dir, keypoints3d, clt_descriptors, clt_scores, idxs):
-    """Write the three files in the reference layout (``feature_process.py:191-194,357-363``)."""
+    """Write the three files in the reference layout (``feature_process.py:191-194,357-363``):
+    ``clt_descriptors`` [dim, sum(idxs)] as stored in ``anno_3d_collect.npz``.  The means are
+    taken over the point-major [sum(idxs), dim] copy the reference averages (``get_kpt_ann``'s
+    ``filter_descriptors``), so the summation order and the bits are the reference's."""
     os.makedirs(anno_dir, exist_ok=True)
     clt_descriptors = np.asarray(clt_descriptors)           # [dim, sum(idxs)]
-    avg_d = mean_descriptors(clt_descriptors.T, idxs)        # [N3, dim]
+    avg_d = mean_descriptors(np.ascontiguousarray(clt_descriptors.T), idxs)   # [N3, dim]
     avg_s = mean_scores(np.asarray(clt_scores), idxs)
     np.savez(os.path.join(anno_dir, "anno_3d_average.npz"), keypoints3d=keypoints3d,
              descriptors3d=avg_d.T, scores3d=avg_s)

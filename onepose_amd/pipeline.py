@@ -71,7 +71,8 @@ class FramePipeline:
     def __init__(self, matcher: GATsSuperGlue, keypoints3d, desc3d, leaves, batch: int, n1: int,
                  device, scale: float = 1000.0, reprojection_error: float = 5.0,
                  iterations_count: int = 10000, confidence: float = 0.99, with_conf=True,
-                 slots: int = 2, detector=None, image_hw=(512, 512), object_cache: bool = True):
+                 slots: int = 2, detector=None, image_hw=(512, 512), object_cache: bool = True,
+                 gat_tables: bool = True):
         self.lib = _lib.load()
         self.device = torch.device(device)
         self.B, self.n1 = int(batch), int(n1)
@@ -95,18 +96,21 @@ class FramePipeline:
         _lib.check(self.lib.onepose_prepare_leaves(
             self.leaves.data_ptr(), 0, 1, self.n3, self.L, self.leaves_pm.data_ptr(),
             _lib.stream_ptr(dev)), "prepare_leaves")
-        # the object-only prefix of the forward (GAT 0 + the 3D half of self-attention 1) and
-        # the GAT prefix tables, computed once: every frame starts from it (onepose_match_cached;
-        # bit-identical to the uncached forward with onepose_set_gat_tables(0), equal within
-        # rounding with the tables)
+        # the object-only prefix of the forward (GAT 0 + the 3D half of self-attention 1) and,
+        # with gat_tables, the GAT prefix tables, computed once: every frame starts from it
+        # (onepose_match_cached; bit-identical to the uncached forward without the tables,
+        # equal within rounding with them)
         self.object_cache = None
+        self.object_flags = _lib.OBJ_GAT_TABLES if gat_tables else 0
         if object_cache:
-            self.object_cache = torch.empty(self.lib.onepose_object_cache_bytes(self.n3) // 4, **f32)
+            nbytes = self.lib.onepose_object_cache_bytes(self.n3, self.L, self.object_flags)
+            self.object_cache = torch.empty(nbytes // 4, **f32)
             wsb = self.lib.onepose_object_prepare_workspace_bytes(self.n3, self.L)
             ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
             _lib.check(self.lib.onepose_object_prepare(
                 self.weights.data_ptr(), self.desc3d.data_ptr(), self.leaves_pm.data_ptr(),
-                self.n3, self.L, self.precision, self.object_cache.data_ptr(), ws.data_ptr(), wsb,
+                self.n3, self.L, self.precision, self.object_flags, self.object_cache.data_ptr(),
+                ws.data_ptr(), wsb,
                 _lib.stream_ptr(dev)), "object_prepare")
             torch.cuda.current_stream(dev).synchronize()
             del ws
@@ -180,7 +184,7 @@ class FramePipeline:
                 self.weights.data_ptr(), desc2d.data_ptr(), 256 * self.n1,
                 self.object_cache.data_ptr(), self.leaves_pm.data_ptr(), 0,
                 self.B, self.n1, self.n3, self.L, self.scale_factor, self.threshold,
-                self.precision, o.matches0.data_ptr(), o.matches1.data_ptr(),
+                self.precision, self.object_flags, o.matches0.data_ptr(), o.matches1.data_ptr(),
                 o.mscores0.data_ptr(), o.mscores1.data_ptr(), _lib.ptr(o.conf),
                 o.ws_match.data_ptr(), o.ws_match_bytes, s), "onepose_match_cached")
             return

@@ -81,10 +81,10 @@ class ShardedMatcher:
         try:
             send = self.send[:nbytes]
             recv = self.recv[:self.world * nbytes]
-            if self.world == 1:
-                recv.copy_(send)
-            elif self.backend == "nccl":
+            if self.backend == "nccl":   # RCCL, enqueued on the matcher's (current) stream
                 dist.all_gather_into_tensor(recv, send, group=self.group)
+            elif self.world == 1:
+                recv.copy_(send)
             else:   # gloo: host round trip, ordered by synchronising the matcher's stream
                 torch.cuda.current_stream(self.dev).synchronize()
                 cpu = send.cpu()

@@ -13,6 +13,9 @@ What is imported from the reference (read-only, nothing copied):
   * src.utils.data_utils.{pad_features3d_random, build_features3d_leaves} (numpy/torch; the
     module's unrelated top-level cv2 / loguru imports are satisfied by empty placeholder
     modules for the duration of the import only)
+  * src.sfm.postprocess.feature_process.{mean_descriptors, mean_scores, save_3d_anno} (numpy;
+    the module's top-level h5py import -- used only by functions not called here -- is
+    satisfied the same way)
 
 Inputs are regenerated from seeds by ``onepose_amd.synthetic`` (numpy RandomState), so
 each fixture stores only outputs plus SHA-256 digests of the inputs and weights.
@@ -106,6 +109,12 @@ def matcher_case(name, n1, n3, L, batch, seed, well_conditioned, full_conf, per_
     np.savez_compressed(os.path.join(HERE, f"{name}.npz"), **out)
     nm = int((pred["matches0"].numpy() > -1).sum())
     print(f"{name}: N1={n1} N3={n3} L={L} B={batch} matches={nm}")
+
+
+def matcher_c3_idx():
+    """BASELINE config 3's shape (1024 x 16384, L = 8): the index + score golden of one frame,
+    frame 0 of the batch tests/test_configs_gpu.py runs at B = 32."""
+    matcher_case("matcher_c3_idx", 1024, 16384, 8, 1, 8, True, False, False)
 
 
 def empty_case():
@@ -224,6 +233,49 @@ def object_case():
     np.savez_compressed(os.path.join(HERE, "object_leaves.npz"), **out)
 
 
+def anno3d_case():
+    """The 3D-annotation producer (feature_process.py:191-194, 297-317, 352-363): per-3D-point
+    means of the observation descriptors / scores and the three files inference.py:113-115 reads,
+    written by the reference's own save_3d_anno / np.save into a scratch directory and stored
+    here as arrays (float32 descriptors as count_features reads them from the h5 features file,
+    plus a float64 case)."""
+    import tempfile
+    import types
+    added = []
+    if "h5py" not in sys.modules:   # feature_process.py:1; the functions below never touch it
+        sys.modules["h5py"] = types.ModuleType("h5py")
+        added.append("h5py")
+    try:
+        from src.sfm.postprocess import feature_process as fp
+    finally:
+        for name in added:
+            del sys.modules[name]
+    out = {}
+    rs = np.random.RandomState(31)
+    for tag, n3, dtype in (("f32", 60, np.float32), ("f64", 24, np.float64)):
+        idxs = rs.randint(1, 17, size=n3).astype(np.int64)   # track lengths
+        m = int(idxs.sum())
+        desc = rs.randn(m, 256).astype(dtype)                 # [sum(idxs), 256], gather order
+        desc /= np.linalg.norm(desc, axis=1, keepdims=True)
+        scores = rs.rand(m, 1).astype(dtype)
+        xyzs = rs.uniform(-0.1, 0.1, (n3, 3))
+        avg_d = fp.mean_descriptors(desc, idxs)
+        avg_s = fp.mean_scores(scores, idxs)
+        with tempfile.TemporaryDirectory() as d:
+            fp.save_3d_anno(xyzs, avg_d, avg_s, os.path.join(d, "anno_3d_average.npz"))
+            fp.save_3d_anno(xyzs, desc, scores, os.path.join(d, "anno_3d_collect.npz"))
+            np.save(os.path.join(d, "idxs.npy"), idxs)                   # feature_process.py:362-363
+            for f in ("anno_3d_average", "anno_3d_collect"):
+                z = np.load(os.path.join(d, f + ".npz"))
+                for k in z.files:
+                    out[f"{tag}_{f}_{k}"] = z[k]
+            out[f"{tag}_idxs"] = np.load(os.path.join(d, "idxs.npy"))
+        # the inputs are the collect file's own arrays (descriptors3d = desc.T)
+        out[f"{tag}_inputs_sha"] = sha(desc, scores, idxs, xyzs)
+    np.savez_compressed(os.path.join(HERE, "anno3d.npz"), **out)
+    print("anno3d: ok")
+
+
 def superpoint_case():
     """SuperPoint.forward (superpoint.py:170-224) with the extraction config of
     extract_features.py:19-24 on seeded synthetic weights and images; also the dense score map
@@ -273,11 +325,13 @@ def main():
     matcher_case("matcher_b2", 128, 192, 8, 2, 2, True, True, False)
     matcher_case("matcher_ragged", 100, 77, 3, 1, 3, True, True, True)
     matcher_case("matcher_c2_idx", 1024, 4096, 8, 1, 4, True, False, False)
+    matcher_c3_idx()
     empty_case()
     sample_desc_case()
     evaluator_case()
     object_case()
     superpoint_case()
+    anno3d_case()
 
 
 if __name__ == "__main__":

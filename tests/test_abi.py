@@ -30,7 +30,25 @@ def test_library_exports_every_header_symbol():
     missing = [s for s in header_symbols() if not hasattr(lib, s)]
     assert not missing, missing
     assert set(header_symbols()) == set(_lib.PROTOTYPES), "ctypes prototypes out of sync"
-    assert lib.onepose_abi_version() == 1
+    assert lib.onepose_abi_version() == _lib.ABI_VERSION == 2
+
+
+def test_object_cache_size_follows_its_flags():
+    """The GAT prefix tables are reserved only when asked for and only for num_leaf <= 8,
+    2 num_leaf rows of 1 KB per point and GAT layer plus 16 sorted logits (header)."""
+    from onepose_amd import _lib
+    lib = _lib.load()
+    T = _lib.OBJ_GAT_TABLES
+    for n3 in (1, 77, 4096):
+        base = lib.onepose_object_cache_bytes(n3, 8, 0)
+        for L in (1, 3, 8):
+            assert lib.onepose_object_cache_bytes(n3, L, 0) == base
+            assert lib.onepose_object_cache_bytes(n3, L, T) - base == 3 * n3 * (2 * L * 1024 + 64)
+        assert lib.onepose_object_cache_bytes(n3, 12, T) == lib.onepose_object_cache_bytes(n3, 12, 0)
+    assert lib.onepose_object_cache_bytes(4096, 8, T) < 221e6
+    assert lib.onepose_object_cache_bytes(4096, 8, 0) < 18.1e6
+    assert lib.onepose_object_cache_bytes(0, 8, 0) == 0
+    assert lib.onepose_object_cache_bytes(16, 17, 0) == 0
 
 
 def test_tensor_list_matches_reference_state_dict():

@@ -1,0 +1,122 @@
+"""BASELINE configs 3 and 4 at their own batch (GATs_SuperGlue.py:203-278), through the bench's
+path: the object prepared once (onepose_object_prepare with the GAT prefix tables), then
+onepose_match_cached over the whole batch.
+
+  config 3: 1024 kpts x 16384 3D pts, B = 32.  Frame 0 of the batch is the reference-generated
+            fixture matcher_c3_idx (make_golden.py): indices exact, scores within 2e-5
+            (tests/parity.py).  Frames 1, 17 and 31 equal their own B = 1 runs (same contract:
+            the batch takes other tiles -- 128-row QKV, 64x64 MLP conv 2, kv_reduce + m_fold --
+            so only the summation order differs).
+  config 4: 1024 x 2500 (ragged: 2500 = 39 x 64 + 4), B = 32, the per-GPU shard of the 8-GPU
+            sweep.  Frames 0 and 31 against the numpy oracle (oracle/matcher_np.py, pinned to the
+            reference's fixtures by test_oracle_golden.py): conf within 2e-5, indices exact.
+The batch's per-object tensors are shared (batch stride 0), as the pipeline runs them."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden
+from onepose_amd import _lib, matcher, synthetic
+from parity import ATOL, assert_pred_equal
+
+pytestmark = pytest.mark.gpu
+
+
+def batch_inputs(n1, n3, L, seed, B):
+    """One object (batch 1 arrays) and B frames of it: frame b is make_matcher_inputs'
+    frame b for the same seed, so frame 0 is the fixture's frame."""
+    data, obj, _ = synthetic.make_matcher_inputs(n1, n3, L, seed=seed, batch=1)
+    frames = [synthetic.make_frame(obj, n1, seed * 131 + b) for b in range(B)]
+    d2 = np.stack([f.descriptors2d for f in frames])
+    return data, d2
+
+
+class CachedMatcher:
+    """onepose_object_prepare once + onepose_match_cached per call (the FramePipeline path)."""
+
+    def __init__(self, sd, data, device, flags=_lib.OBJ_GAT_TABLES, precision=0):
+        self.lib = lib = _lib.load()
+        self.device, self.flags, self.precision = device, flags, precision
+        m = matcher.from_state_dict(sd)
+        self.sf = float(m.hparams["scale_factor"])
+        self.thr = float(m.hparams["match_threshold"])
+        self.w = m.packed_weights(device)
+        f32 = dict(dtype=torch.float32, device=device)
+        self.n3 = n3 = data["descriptors3d_db"].shape[2]
+        self.L = L = data["descriptors2d_db"].shape[2] // n3
+        d3 = torch.from_numpy(data["descriptors3d_db"][0]).to(device).contiguous()
+        lv = torch.from_numpy(data["descriptors2d_db"][0]).to(device).contiguous()
+        s = _lib.stream_ptr(device)
+        self.pm = torch.empty(lib.onepose_leaves_prepared_bytes(1, n3, L) // 4, **f32)
+        _lib.check(lib.onepose_prepare_leaves(lv.data_ptr(), 0, 1, n3, L, self.pm.data_ptr(), s),
+                   "leaves")
+        self.cache = torch.empty(lib.onepose_object_cache_bytes(n3, L, flags) // 4, **f32)
+        wsb = lib.onepose_object_prepare_workspace_bytes(n3, L)
+        ws = torch.empty(wsb, dtype=torch.uint8, device=device)
+        _lib.check(lib.onepose_object_prepare(self.w.data_ptr(), d3.data_ptr(), self.pm.data_ptr(),
+                                              n3, L, precision, flags, self.cache.data_ptr(),
+                                              ws.data_ptr(), wsb, s), "prepare")
+        torch.cuda.synchronize()
+
+    def __call__(self, d2, with_conf=False):
+        """d2 [B, 256, n1] numpy -> per-frame pred dicts (and conf [B, n1, n3] if asked)."""
+        lib, dev = self.lib, self.device
+        B, _, n1 = d2.shape
+        n3 = self.n3
+        f32 = dict(dtype=torch.float32, device=dev)
+        t = torch.from_numpy(np.ascontiguousarray(d2)).to(dev)
+        o = dict(m0=torch.empty(B, n1, dtype=torch.int64, device=dev),
+                 m1=torch.empty(B, n3, dtype=torch.int64, device=dev),
+                 s0=torch.empty(B, n1, **f32), s1=torch.empty(B, n3, **f32))
+        conf = torch.empty(B, n1, n3, **f32) if with_conf else None
+        wsb = lib.onepose_match_workspace_bytes(B, n1, n3, self.L, int(with_conf))
+        ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
+        _lib.check(lib.onepose_match_cached(
+            self.w.data_ptr(), t.data_ptr(), 256 * n1, self.cache.data_ptr(), self.pm.data_ptr(),
+            0, B, n1, n3, self.L, self.sf, self.thr, self.precision, self.flags,
+            o["m0"].data_ptr(), o["m1"].data_ptr(), o["s0"].data_ptr(), o["s1"].data_ptr(),
+            _lib.ptr(conf), ws.data_ptr(), wsb, _lib.stream_ptr(dev)), "match_cached")
+        torch.cuda.synchronize()
+        h = {k: v.cpu().numpy() for k, v in o.items()}
+        preds = [{"matches0": h["m0"][b], "matches1": h["m1"][b], "matching_scores0": h["s0"][b],
+                  "matching_scores1": h["s1"][b]} for b in range(B)]
+        return preds, (conf.cpu().numpy() if with_conf else None)
+
+
+@pytest.mark.timeout(300)
+def test_config3_batch32_1024x16384(device):
+    g = golden("matcher_c3_idx")
+    n1, n3, L, seed = [int(g[k]) for k in ("n1", "n3", "num_leaf", "seed")]
+    assert (n1, n3, L) == (1024, 16384, 8)
+    sd = synthetic.make_state_dict(seed, well_conditioned=bool(int(g["well_conditioned"])))
+    data, d2 = batch_inputs(n1, n3, L, seed, 32)
+    cm = CachedMatcher(sd, data, device)
+    preds, _ = cm(d2)
+    assert_pred_equal(preds[0], g, "config 3, frame 0 of 32 vs the reference")
+    for b in (1, 17, 31):
+        one, _ = cm(d2[b:b + 1])
+        assert_pred_equal(preds[b], one[0], f"config 3, frame {b} of 32 vs alone")
+        assert (preds[b]["matches0"] > -1).sum() > 200
+    # mutual consistency over the whole batch
+    for p in preds:
+        m0, m1 = p["matches0"], p["matches1"]
+        ok = m0 > -1
+        assert np.array_equal(m1[m0[ok]], np.nonzero(ok)[0])
+        assert (m1 > -1).sum() == ok.sum()
+
+
+@pytest.mark.timeout(300)
+def test_config4_batch32_1024x2500_ragged(device):
+    from oracle import matcher_np as M
+    n1, n3, L, seed = 1024, 2500, 8, 12
+    sd = synthetic.make_state_dict(seed)
+    data, d2 = batch_inputs(n1, n3, L, seed, 32)
+    cm = CachedMatcher(sd, data, device)
+    preds, conf = cm(d2, with_conf=True)
+    for b in (0, 31):
+        one = dict(data)
+        one["descriptors2d_query"] = d2[b:b + 1]
+        opred, oconf = M.forward(sd, one)
+        np.testing.assert_allclose(conf[b], oconf[0], rtol=0, atol=ATOL)
+        assert_pred_equal(preds[b], opred, f"config 4, frame {b} of 32 vs oracle")
+        assert (preds[b]["matches0"] > -1).sum() > 200

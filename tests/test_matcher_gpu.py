@@ -1,23 +1,19 @@
 """HIP matcher (libonepose_hip.so through the drop-in module) vs the reference's fixtures and
 the numpy oracle.
 
-Tolerances: correspondence indices are compared exactly except on rows/columns whose
-reference margin (top-1 minus top-2 conf, or |mscore - match_threshold|) is below
-MARGIN -- there fp32 summation order may legitimately flip a decision; the tests count
-those and require them to be rare.  conf_matrix / matching scores: |diff| <= 2e-5
-(values lie in [0, 1]; fp32 MFMA products are exact, only the summation order differs
-from the CPU reference)."""
+Contract (tests/parity.py): correspondence indices EQUAL on every row and column, the one
+exemption being a score within 1e-6 of match_threshold (counted and printed);
+conf_matrix / matching scores within |diff| <= 2e-5 (values in [0, 1]; fp32 MFMA products
+are exact, only the summation order differs from the CPU reference)."""
 import numpy as np
 import pytest
 import torch
 
 from conftest import golden
 from onepose_amd import matcher, synthetic
+from parity import ATOL, assert_indices_exact, assert_pred_equal, assert_scores_close
 
 pytestmark = pytest.mark.gpu
-
-MARGIN = 1e-4
-ATOL = 2e-5
 
 
 def run_matcher(sd, data, device, expand=False, precision="fp32"):
@@ -33,39 +29,6 @@ def run_matcher(sd, data, device, expand=False, precision="fp32"):
     return {k: v.cpu().numpy() for k, v in pred.items()}, conf.cpu().numpy()
 
 
-def check_indices(got, ref, margin, what):
-    bad = got != ref
-    unexplained = bad & (margin > MARGIN)
-    assert not unexplained.any(), f"{what}: {int(unexplained.sum())} index mismatches " \
-                                  f"at rows {np.nonzero(unexplained)[0][:10]}"
-    assert bad.sum() <= max(1, 0.002 * bad.size), f"{what}: {int(bad.sum())} low-margin flips"
-
-
-def check_scores(got, ref, conf0, own_top2, other_top2, rows, what):
-    """Matching scores within ATOL, except where the mutual check flipped (one side is 0) and
-    a top-1 - top-2 conf margin below MARGIN explains it: the row's (column's) own, so its
-    best index may differ, or that of its best index on the other axis, so the mutual pick
-    may.  There the fp32 summation order legitimately decides.  `conf0` is the [n1, n3]
-    conf; `own_top2` / `other_top2` the top-2 conf values of this / the other axis, [2, n]."""
-    bad = np.abs(got - ref) > ATOL
-    if not bad.any():
-        return
-    best = conf0.argmax(axis=1 if rows else 0)
-    low = ((other_top2[0] - other_top2[1])[best] < MARGIN) | (own_top2[0] - own_top2[1] < MARGIN)
-    unexplained = bad & ~(((got == 0) | (ref == 0)) & low)
-    assert not unexplained.any(), f"{what}: {int(unexplained.sum())} score mismatches at " \
-                                  f"{np.nonzero(unexplained)[0][:10]}"
-    assert bad.sum() <= max(1, 0.002 * bad.size), f"{what}: {int(bad.sum())} mutual flips"
-
-
-def margins(g):
-    top = g["row_top2"][0]
-    row_margin = np.minimum(top[:, 0] - top[:, 1], np.abs(g["matching_scores0"] - 0.2))
-    ctop = g["col_top2"][0]
-    col_margin = np.minimum(ctop[0] - ctop[1], np.abs(g["matching_scores1"] - 0.2))
-    return row_margin, col_margin
-
-
 @pytest.mark.parametrize("precision", ["fp32", "fp32_split"])
 @pytest.mark.parametrize("name", ["matcher_c1_wc", "matcher_c1_rand", "matcher_b2",
                                   "matcher_ragged", "matcher_c2_idx"])
@@ -76,14 +39,8 @@ def test_matcher_matches_reference_fixture(name, precision, device):
     sd = synthetic.make_state_dict(seed, well_conditioned=bool(wc))
     data, _, _ = synthetic.make_matcher_inputs(n1, n3, L, seed=seed, batch=B)
     pred, conf = run_matcher(sd, data, device, precision=precision)
-    rm, cm = margins(g)
-    check_indices(pred["matches0"], g["matches0"], rm, "matches0")
-    check_indices(pred["matches1"], g["matches1"], cm, "matches1")
-    rt, ct = g["row_top2"][0].T, g["col_top2"][0]
-    check_scores(pred["matching_scores0"], g["matching_scores0"], conf[0], rt, ct, True,
-                 "matching_scores0")
-    check_scores(pred["matching_scores1"], g["matching_scores1"], conf[0], ct, rt, False,
-                 "matching_scores1")
+    exempt = assert_pred_equal(pred, g, name)
+    assert exempt == 0   # no committed fixture has a score within 1e-6 of the threshold
     if "conf" in g:
         np.testing.assert_allclose(conf, g["conf"], atol=ATOL)
     np.testing.assert_allclose(conf.sum(axis=2), g["conf_row_sum"], rtol=1e-4, atol=1e-4)
@@ -100,10 +57,7 @@ def test_matcher_vs_oracle_batch_shared_object(precision, device):
     pred, conf = run_matcher(sd, data, device, expand=True, precision=precision)
     opred, oconf = M.forward(sd, data)
     np.testing.assert_allclose(conf, oconf, atol=ATOL)
-    top = -np.sort(-oconf[0], axis=1)[:, :2]
-    check_indices(pred["matches0"], opred["matches0"],
-                  np.minimum(top[:, 0] - top[:, 1], np.abs(opred["matching_scores0"] - 0.2)),
-                  "matches0")
+    assert_pred_equal(pred, opred, "batch-shared object")
     assert (pred["matches0"] > -1).sum() > 20
 
 
@@ -135,9 +89,8 @@ def test_split_precision_is_fp32_accurate(n1, n3, L, seed, device):
     print("max |conf - oracle|:", err)
     assert err["fp32_split"] <= 2.0 * err["fp32"] + 1e-6
     assert err["fp32_split"] * 20 < err["bf16"]
-    top = -np.sort(-oconf[0], axis=1)[:, :2]
-    rm = np.minimum(top[:, 0] - top[:, 1], np.abs(opred["matching_scores0"] - 0.2))
-    check_indices(preds["fp32_split"]["matches0"], opred["matches0"], rm, "matches0")
+    assert_pred_equal(preds["fp32_split"], opred, "fp32_split")
+    assert_pred_equal(preds["fp32"], opred, "fp32")
     assert (preds["fp32_split"]["matches0"] > -1).sum() > 20
 
 
@@ -176,7 +129,7 @@ def test_wide_qkv_tile_batch_matches_single_frames(B, device):
         p1, c1 = run_matcher(sd, one, device)
         np.testing.assert_allclose(conf[b], c1[0], rtol=0, atol=ATOL)
         if b == 0:   # pred holds sample 0's correspondences, as the reference returns them
-            assert (pred["matches0"] == p1["matches0"]).mean() > 0.998
+            assert_pred_equal(pred, p1, f"B={B} frame 0 vs alone")
             assert (pred["matches0"] > -1).sum() > 100
 
 
@@ -260,24 +213,21 @@ def test_object_cache_is_bit_identical(device, n1, n3, L, B, prec):
     1000 x 3001 (B = 3 / 6): ragged sides with different per-side QKV tiles in layers 1-2 (2D
     32-row, 3D 64-row chunks, both with a partial last chunk), and at B = 6 a 2D source slot
     folded by kv_reduce + m_fold beside the 3D slot's kv_fold.  The cached forward's GAT
-    layers 1-3 read the leaves here (onepose_set_gat_tables(0)), as the uncached one does;
-    test_gat_tables_cached_forward covers the tables."""
+    layers 1-3 read the leaves here (object flags 0: no GAT prefix tables), as the uncached one
+    does; test_gat_tables_cached_forward covers the tables."""
     from onepose_amd import _lib
     lib = _lib.load()
-    prev = lib.onepose_set_gat_tables(0)
-    try:
-        outs = cached_and_uncached(lib, device, n1, n3, L, B, prec, seed=11)
-    finally:
-        lib.onepose_set_gat_tables(prev)
+    outs = cached_and_uncached(lib, device, n1, n3, L, B, prec, seed=11, flags=0)
     for k in outs[0]:
         np.testing.assert_array_equal(outs[0][k], outs[1][k], err_msg=k)
     if n1 == 1024 and prec == 0:
         assert (outs[1]["m0"] > -1).sum() > 100
 
 
-def cached_and_uncached(lib, device, n1, n3, L, B, prec, seed, sd_seed=0, modes=(False, True)):
+def cached_and_uncached(lib, device, n1, n3, L, B, prec, seed, sd_seed=0, modes=(False, True),
+                        flags=0):
     """Outputs of onepose_match_prepared_ex (False) / onepose_object_prepare +
-    onepose_match_cached (True) on one object shared by the batch."""
+    onepose_match_cached (True, object flags `flags`) on one object shared by the batch."""
     from onepose_amd import _lib
     sd = synthetic.make_state_dict(sd_seed)
     data, _, _ = synthetic.make_matcher_inputs(n1, n3, L, seed=seed, batch=B)
@@ -290,11 +240,12 @@ def cached_and_uncached(lib, device, n1, n3, L, B, prec, seed, sd_seed=0, modes=
     lv = torch.from_numpy(data["descriptors2d_db"][0]).to(device).contiguous()
     pm = torch.empty(lib.onepose_leaves_prepared_bytes(1, n3, L) // 4, **f32)
     _lib.check(lib.onepose_prepare_leaves(lv.data_ptr(), 0, 1, n3, L, pm.data_ptr(), s), "leaves")
-    cache = torch.empty(lib.onepose_object_cache_bytes(n3) // 4, **f32)
+    cache = torch.empty(lib.onepose_object_cache_bytes(n3, L, flags) // 4, **f32)
     wsb = lib.onepose_object_prepare_workspace_bytes(n3, L)
     ws = torch.empty(wsb, dtype=torch.uint8, device=device)
     _lib.check(lib.onepose_object_prepare(w.data_ptr(), d3.data_ptr(), pm.data_ptr(), n3, L, prec,
-                                          cache.data_ptr(), ws.data_ptr(), wsb, s), "prepare")
+                                          flags, cache.data_ptr(), ws.data_ptr(), wsb, s),
+               "prepare")
     ws_bytes = lib.onepose_match_workspace_bytes(B, n1, n3, L, 1)
     sf, thr = float(m.hparams["scale_factor"]), float(m.hparams["match_threshold"])
     outs = []
@@ -304,15 +255,16 @@ def cached_and_uncached(lib, device, n1, n3, L, B, prec, seed, sd_seed=0, modes=
                  s0=torch.empty(B, n1, **f32), s1=torch.empty(B, n3, **f32),
                  conf=torch.empty(B, n1, n3, **f32))
         wsm = torch.empty(ws_bytes, dtype=torch.uint8, device=device)
-        tail = (B, n1, n3, L, sf, thr, prec, o["m0"].data_ptr(), o["m1"].data_ptr(),
+        tail = (B, n1, n3, L, sf, thr, prec)
+        outp = (o["m0"].data_ptr(), o["m1"].data_ptr(),
                 o["s0"].data_ptr(), o["s1"].data_ptr(), o["conf"].data_ptr(), wsm.data_ptr(),
                 ws_bytes, s)
         if cached:
             rc = lib.onepose_match_cached(w.data_ptr(), d2.data_ptr(), 256 * n1, cache.data_ptr(),
-                                          pm.data_ptr(), 0, *tail)
+                                          pm.data_ptr(), 0, *tail, flags, *outp)
         else:
             rc = lib.onepose_match_prepared_ex(w.data_ptr(), d2.data_ptr(), 256 * n1,
-                                               d3.data_ptr(), 0, pm.data_ptr(), 0, *tail)
+                                               d3.data_ptr(), 0, pm.data_ptr(), 0, *tail, *outp)
         _lib.check(rc, "match")
         torch.cuda.synchronize()
         outs.append({k: v.cpu().numpy() for k, v in o.items()})
@@ -325,40 +277,29 @@ def cached_and_uncached(lib, device, n1, n3, L, B, prec, seed, sd_seed=0, modes=
 def test_gat_tables_cached_forward(device, n1, n3, L, B, prec):
     """The cached forward's GAT layers 1-3 from the object's prefix tables (sorted leaf logits,
     exp-weighted prefix / suffix sums; num_leaf <= 8) vs the same forward reading the leaves
-    (onepose_set_gat_tables(0), bit-identical to the uncached forward): conf and scores within
-    ATOL, indices equal except low-margin rows; at B = 1 also vs the numpy oracle.  prec 2:
-    the fp32-by-3xbf16 split mode (fp32-accurate, same bar)."""
+    (object flags 0, bit-identical to the uncached forward): conf and scores within ATOL,
+    indices equal except low-margin rows; at B = 1 also vs the numpy oracle.  prec 2: the
+    fp32-by-3xbf16 split mode (fp32-accurate, same bar)."""
     from onepose_amd import _lib
     lib = _lib.load()
-    assert lib.onepose_set_gat_tables(1) in (0, 1)
-    tab = cached_and_uncached(lib, device, n1, n3, L, B, prec, seed=5, modes=(True,))[0]
-    prev = lib.onepose_set_gat_tables(0)
-    try:
-        direct = cached_and_uncached(lib, device, n1, n3, L, B, prec, seed=5, modes=(True,))[0]
-    finally:
-        lib.onepose_set_gat_tables(prev)
+    tab = cached_and_uncached(lib, device, n1, n3, L, B, prec, seed=5, modes=(True,),
+                              flags=_lib.OBJ_GAT_TABLES)[0]
+    direct = cached_and_uncached(lib, device, n1, n3, L, B, prec, seed=5, modes=(True,),
+                                 flags=0)[0]
     assert np.isfinite(tab["conf"]).all()
     np.testing.assert_allclose(tab["conf"], direct["conf"], atol=ATOL)
+    def pred(o, b):
+        return {"matches0": o["m0"][b], "matches1": o["m1"][b], "matching_scores0": o["s0"][b],
+                "matching_scores1": o["s1"][b]}
     for b in range(B):
-        c = direct["conf"][b]
-        top = -np.sort(-c, axis=1)[:, :2] if n3 > 1 else np.stack([c[:, 0], 0 * c[:, 0]], 1)
-        ctop = -np.sort(-c, axis=0)[:2] if n1 > 1 else np.stack([c[0], 0 * c[0]])
-        rm = np.minimum(top[:, 0] - top[:, 1], np.abs(direct["s0"][b] - 0.2))
-        cm = np.minimum(ctop[0] - ctop[1], np.abs(direct["s1"][b] - 0.2))
-        check_indices(tab["m0"][b], direct["m0"][b], rm, "matches0")
-        check_indices(tab["m1"][b], direct["m1"][b], cm, "matches1")
-        check_scores(tab["s0"][b], direct["s0"][b], tab["conf"][b], top.T, ctop, True, "scores0")
+        assert_pred_equal(pred(tab, b), pred(direct, b), f"tables vs leaves, frame {b}")
     if B == 1:
         from oracle import matcher_np as M
         sd = synthetic.make_state_dict(0)
         data, _, _ = synthetic.make_matcher_inputs(n1, n3, L, seed=5, batch=1)
         opred, oconf = M.forward(sd, data)
         np.testing.assert_allclose(tab["conf"], oconf, atol=ATOL)
-        top = -np.sort(-oconf[0], axis=1)[:, :2]
-        ms0 = np.asarray(opred["matching_scores0"]).reshape(-1)
-        rm = np.minimum(top[:, 0] - top[:, 1], np.abs(ms0 - 0.2))
-        check_indices(tab["m0"][0], np.asarray(opred["matches0"]).reshape(-1), rm,
-                      "matches0 vs oracle")
+        assert_pred_equal(pred(tab, 0), opred, "tables vs oracle")
     if n1 >= 1000:
         assert (tab["m0"] > -1).sum() > 100
 
@@ -377,9 +318,4 @@ def test_matcher_tiny_and_odd_shapes(n1, n3, L, device):
     opred, oconf = M.forward(sd, data)
     assert np.isfinite(conf).all()
     np.testing.assert_allclose(conf, oconf, atol=ATOL)
-    top = -np.sort(-oconf[0], axis=1)[:, :2] if n3 > 1 else np.stack([oconf[0, :, 0], 0 * oconf[0, :, 0]], 1)
-    rm = np.minimum(top[:, 0] - top[:, 1], np.abs(opred["matching_scores0"] - 0.2))
-    check_indices(pred["matches0"], opred["matches0"], rm, "matches0")
-    ctop = -np.sort(-oconf[0], axis=0)[:2] if n1 > 1 else np.stack([oconf[0][0], 0 * oconf[0][0]])
-    check_scores(pred["matching_scores0"], opred["matching_scores0"], conf[0], top.T, ctop, True,
-                 "matching_scores0")
+    assert_pred_equal(pred, opred, f"{n1}x{n3} L={L}")

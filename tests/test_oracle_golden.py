@@ -95,13 +95,18 @@ def test_object_leaves_match_reference():
         np.testing.assert_array_equal(l_s.numpy(), g[f"{tag}_leaf_scores"])
 
 
-@pytest.mark.parametrize("name", CASES)
+@pytest.mark.parametrize("name", CASES + ["matcher_c2_idx", "matcher_c3_idx"])
 def test_torch_cpu_restatement_matches_reference(name):
     """oracle/matcher_torch.py (the PyTorch-CPU path bench.py's cpu_baseline times) against
     the reference's own outputs."""
     from oracle import matcher_torch as MT
     g = golden(name)
     sd, data, _ = regen(g)
+    import hashlib
+    h = hashlib.sha256()
+    for k in sorted(data):
+        h.update(np.ascontiguousarray(data[k]).tobytes())
+    assert h.hexdigest() == str(g["inputs_sha"]), "input generator drifted"
     pred, conf = MT.forward(MT.to_torch(sd), data)
     np.testing.assert_array_equal(pred["matches0"], g["matches0"])
     np.testing.assert_array_equal(pred["matches1"], g["matches1"])
