@@ -465,6 +465,22 @@ def main():
                   "achieved_tflops": round(ff * value / 1e12, 2),
                   "peak": peak, "frac": round(ff * value / 1e12 / peak, 4)}
 
+    pose_summary = {"cmd1": float(res[:, 14].mean()), "cmd3": float(res[:, 15].mean()),
+                    "cmd5": float(res[:, 16].mean()), "R_err_deg_mean": float(res[:, 12].mean()),
+                    "t_err_cm_mean": float(res[:, 13].mean()),
+                    "n_inliers_mean": float(res[:, 17].mean()),
+                    "status_ok": float((res[:, 18] == 0).mean())}
+    if args.e2e:
+        # Random-weight SuperPoint descriptors barely discriminate (cosine 0.97 between random
+        # keypoints of the synthetic images; trained weights are not available offline), so the
+        # synthetic object never matches the images' keypoints: the pose stage runs on every
+        # frame, but on ~0 correspondences.  The frame rate includes its launches; its result
+        # is not a pose measurement ("From images").
+        pose_summary = {"status": "skipped", "reason": "no correspondences between random-weight "
+                        "SuperPoint keypoints and the synthetic object; the pose stage still "
+                        "runs every frame (its launches are timed)",
+                        "n_inliers_mean": pose_summary["n_inliers_mean"],
+                        "status_ok": pose_summary["status_ok"]}
     cfg_name = {(1024, 4096): "config 2", (1024, 16384): "config 3",
                 (2048, 8192): "config 5"}.get((n1, n3), "custom")
     if args.precision == "bf16":
@@ -490,11 +506,7 @@ def main():
                                     + f"matcher + RANSAC-EPnP + cm/deg; {sched}"),
                        "n1": n1, "n3": n3, "num_leaf": L, "batch_per_gpu": B,
                        "parallelism": f"frame-dp{world}"},
-            "pose": {"cmd1": float(res[:, 14].mean()), "cmd3": float(res[:, 15].mean()),
-                     "cmd5": float(res[:, 16].mean()), "R_err_deg_mean": float(res[:, 12].mean()),
-                     "t_err_cm_mean": float(res[:, 13].mean()),
-                     "n_inliers_mean": float(res[:, 17].mean()),
-                     "status_ok": float((res[:, 18] == 0).mean())},
+            "pose": pose_summary,
             "roofline": roof,
             "frame_roofline": frame_roof,
             **({"detector": det} if det else {}),

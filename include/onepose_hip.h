@@ -166,7 +166,7 @@ int onepose_match_prepared(const void* packed_weights,
  * 0; the tables are never built for num_leaf > 8) the results are bit-identical to
  * onepose_match_prepared_ex's on the same object (the same kernels and tiles produce the cached
  * state), provided the cache was prepared with the same `precision`.  Without tables the cache
- * is 4 KB + 192 B per 3D point (17.6 MB at n3 = 4096) plus a 0.5 MB fixed part.
+ * is 4 KB + 192 B per 3D point (17.6 MB at n3 = 4096) plus a 0.75 MB fixed part.
  *   desc3d:          [256][n3] reference layout (descriptors3d_db of one object)
  *   leaves_prepared: [n3*L][256] point-major (onepose_prepare_leaves of the object)
  * The cache is shared by every sample of a batch (one object per call); it is read-only for

@@ -45,6 +45,14 @@ struct GemmProb {
   const float* W1;     // [N][ldw1] for k >= ksplit (null: W continues)
   int64_t w1_bs;
   int ldw1;
+  // bf16 modes: W (and W1) as bf16 planes instead -- one (PM_BF16: round to nearest even) or
+  // three (PM_SPLIT3: the exact split hi, mid, lo), each [N][ldw] (resp. [N][ldw1]), `wpl`
+  // elements apart, wp_bs per sample; copied to LDS as is (no conversion).  Set on every
+  // problem of a launch or on none; Wp1 set exactly when W1 is.
+  const uint16_t* Wp;
+  int64_t wp_bs, wpl;
+  const uint16_t* Wp1;
+  int64_t wp1_bs, wpl1;
   const float* bias;   // [N] or null
   float* Y;            // [batch][M][ldy]
   int64_t y_bs;

@@ -72,18 +72,30 @@ struct Tile {
   static constexpr int A4 = BM * KQ / NT;       // float4 of A per thread per stage
   static constexpr int W4 = BN * KQ / NT;
   static constexpr int STAGE = (BM + BN) * PITCH;
-  // bf16 mode: the stage is stored as bf16 rows of BKS + 8 elements (80 B at BKS 32: 16-byte
-  // aligned, and 16 rows at one k hit 16 distinct 4-bank groups -> conflict-free b128 reads)
-  static constexpr int PITCHB = BKS + 8;
-  static constexpr int STAGEB = (BM + BN) * PITCHB;   // bf16 elements (even)
+  // bf16 modes: each image (one per split piece) is [BM + BN] rows of BKS = 32 bf16 (64 B, no
+  // padding), the row's four 16-B k-chunks XOR-swizzled by (row >> 2) & 3, so that a
+  // ds_read_b128 lane group (16 rows, one chunk) hits 16 distinct 4-bank groups and a
+  // ds_write_b64 group (2 rows x 64 B) 32 distinct banks: conflict-free both ways, and 20% less
+  // LDS than padded 80-B rows (64x64 split: 48 KB for two stages, three workgroups per CU).
+  static constexpr int STAGEB = (BM + BN) * BKS;   // bf16 elements per image
   static_assert(WM * WN * KS == NW && FN >= 1 && A4 >= 1 && W4 >= 1 && KKW >= 2, "tile shape");
   static_assert(NT % KQ == 0 && BM * KQ % NT == 0 && BN * KQ % NT == 0, "one k-quad per thread");
 };
 
+// Element offset of (row, k) in a bf16 image (BKS = 32): chunk k / 8 swizzled by the row.
 template <class T>
+__device__ __forceinline__ int bsw(int row, int k) {
+  static_assert(T::BKS == 32, "swizzled bf16 images have 64-B rows");
+  return row * 32 + ((((k >> 3) ^ (row >> 2)) & 3) << 3) + (k & 7);
+}
+
+// Stage registers.  WPL: the W operand comes from NPL bf16 planes in HBM (pre-split weights /
+// folded message weights, gemm.h GemmProb::Wp): 8 B per plane and k-quad, copied to LDS as is.
+template <class T, bool WPL = false, int NPL = 1>
 struct Stage {
   float4 a[T::A4];
-  float4 w[T::W4];
+  float4 w[WPL ? 1 : T::W4];
+  uint2 wp[WPL ? T::W4 : 1][NPL];
   float4 mean, rstd;
 };
 
@@ -91,6 +103,8 @@ struct Stage {
 // dynamically indexed kernel-argument struct would be copied to scratch).
 struct Ctx {
   const float *a0, *a1, *w0, *w1, *mean, *rstd;
+  const uint16_t *wp0, *wp1;   // W planes of the two K ranges (WPL)
+  int64_t wpl0, wpl1;          // plane strides (elements)
   int lda0, lda1, ldw0, ldw1, ksplit, M, N, K;
 };
 
@@ -98,14 +112,14 @@ struct Ctx {
 // (columns) that are never stored, and every reducing epilogue masks them when it stages the
 // tile, so they need no zeroing -- a select right behind each load would make the wave wait
 // for the load it just issued.
-template <int PRO, class T>
-__device__ __forceinline__ void load_stage(const Ctx& c, int m0, int n0, int k0, Stage<T>& s) {
+template <int PRO, class T, bool WPL = false, int NPL = 1>
+__device__ __forceinline__ void load_stage(const Ctx& c, int m0, int n0, int k0,
+                                           Stage<T, WPL, NPL>& s) {
   const int t = threadIdx.x;
   const int kq = (t % T::KQ) * 4;
   const bool first = k0 < c.ksplit;
   const float* A = first ? c.a0 : c.a1;
   const int lda = first ? c.lda0 : c.lda1;
-  const float* W = first ? c.w0 : c.w1;
   const int ldw = first ? c.ldw0 : c.ldw1;
   const int kk = first ? (k0 + kq) : (k0 - c.ksplit + kq);
   if (PRO == PRO_NORM_RELU) {
@@ -117,66 +131,99 @@ __device__ __forceinline__ void load_stage(const Ctx& c, int m0, int n0, int k0,
     const int m = min(m0 + (t + T::NT * i) / T::KQ, c.M - 1);
     s.a[i] = *reinterpret_cast<const float4*>(A + (int64_t)m * lda + kk);
   }
+  if constexpr (WPL) {
+    const uint16_t* W = first ? c.wp0 : c.wp1;
+    const int64_t pl = first ? c.wpl0 : c.wpl1;
 #pragma unroll
-  for (int i = 0; i < T::W4; ++i) {
-    const int o = min(n0 + (t + T::NT * i) / T::KQ, c.N - 1);
-    s.w[i] = *reinterpret_cast<const float4*>(W + (int64_t)o * ldw + kk);
+    for (int i = 0; i < T::W4; ++i) {
+      const int o = min(n0 + (t + T::NT * i) / T::KQ, c.N - 1);
+#pragma unroll
+      for (int q = 0; q < NPL; ++q)
+        s.wp[i][q] = *reinterpret_cast<const uint2*>(W + q * pl + (int64_t)o * ldw + kk);
+    }
+  } else {
+    const float* W = first ? c.w0 : c.w1;
+#pragma unroll
+    for (int i = 0; i < T::W4; ++i) {
+      const int o = min(n0 + (t + T::NT * i) / T::KQ, c.N - 1);
+      s.w[i] = *reinterpret_cast<const float4*>(W + (int64_t)o * ldw + kk);
+    }
+  }
+}
+
+// fp32 -> the bf16 image(s) of one k-quad at `b16` (element offset `off`, images STAGEB apart):
+// PM_BF16 rounded to nearest even; PM_SPLIT3 the exact split hi + mid + lo.
+template <class T, int PM>
+__device__ __forceinline__ void store_quad_bf16(__bf16* b16, int off, float4 v) {
+  if constexpr (PM == PM_BF16) {
+    bf16x4 q;
+    q[0] = (__bf16)v.x;
+    q[1] = (__bf16)v.y;
+    q[2] = (__bf16)v.z;
+    q[3] = (__bf16)v.w;
+    *reinterpret_cast<bf16x4*>(b16 + off) = q;
+  } else {
+    bf16x4 q0, q1, q2;
+    const float x[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const __bf16 h = (__bf16)x[c];
+      const float r = x[c] - (float)h;
+      const __bf16 m = (__bf16)r;
+      q0[c] = h;
+      q1[c] = m;
+      q2[c] = (__bf16)(r - (float)m);
+    }
+    *reinterpret_cast<bf16x4*>(b16 + off) = q0;
+    *reinterpret_cast<bf16x4*>(b16 + off + T::STAGEB) = q1;
+    *reinterpret_cast<bf16x4*>(b16 + off + 2 * T::STAGEB) = q2;
   }
 }
 
 // Stage registers -> LDS image at `base` ([BM + BN] rows: A then W), applying the prologue;
-// fp32 rows of PITCH floats, or bf16 rows of PITCHB elements (PM_BF16: rounded to nearest even;
-// PM_SPLIT3: the hi, mid and lo images one after another, STAGEB elements apart).
-template <int PRO, class T, int PM>
-__device__ __forceinline__ void store_stage(float* base, Stage<T>& s) {
+// fp32 rows of PITCH floats, or swizzled bf16 images (Tile::STAGEB elements each).
+template <int PRO, class T, int PM, bool WPL = false, int NPL = 1>
+__device__ __forceinline__ void store_stage(float* base, Stage<T, WPL, NPL>& s) {
   const int t = threadIdx.x;
   const int kq = (t % T::KQ) * 4;
+  __bf16* b16 = reinterpret_cast<__bf16*>(base);
 #pragma unroll
-  for (int i = 0; i < T::A4 + T::W4; ++i) {
-    const bool is_a = i < T::A4;
-    float4 v = is_a ? s.a[i] : s.w[i - T::A4];
-    if (PRO == PRO_NORM_RELU && is_a) {
+  for (int i = 0; i < T::A4; ++i) {
+    float4 v = s.a[i];
+    if (PRO == PRO_NORM_RELU) {
       v.x = fmaxf((v.x - s.mean.x) * s.rstd.x, 0.f);
       v.y = fmaxf((v.y - s.mean.y) * s.rstd.y, 0.f);
       v.z = fmaxf((v.z - s.mean.z) * s.rstd.z, 0.f);
       v.w = fmaxf((v.w - s.mean.w) * s.rstd.w, 0.f);
     }
-    const int row = (is_a ? 0 : T::BM) + (t + T::NT * (is_a ? i : i - T::A4)) / T::KQ;
-    if constexpr (PM == PM_BF16) {
-      bf16x4 q;
-      q[0] = (__bf16)v.x;
-      q[1] = (__bf16)v.y;
-      q[2] = (__bf16)v.z;
-      q[3] = (__bf16)v.w;
-      *reinterpret_cast<bf16x4*>(reinterpret_cast<__bf16*>(base) + row * T::PITCHB + kq) = q;
-    } else if constexpr (PM == PM_SPLIT3) {
-      bf16x4 q0, q1, q2;
-      const float x[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        const __bf16 h = (__bf16)x[c];
-        const float r = x[c] - (float)h;
-        const __bf16 m = (__bf16)r;
-        q0[c] = h;
-        q1[c] = m;
-        q2[c] = (__bf16)(r - (float)m);
-      }
-      __bf16* b16 = reinterpret_cast<__bf16*>(base) + row * T::PITCHB + kq;
-      *reinterpret_cast<bf16x4*>(b16) = q0;
-      *reinterpret_cast<bf16x4*>(b16 + T::STAGEB) = q1;
-      *reinterpret_cast<bf16x4*>(b16 + 2 * T::STAGEB) = q2;
-    } else {
+    const int row = (t + T::NT * i) / T::KQ;
+    if constexpr (PM == PM_F32)
       *reinterpret_cast<float4*>(base + row * T::PITCH + kq) = v;
+    else
+      store_quad_bf16<T, PM>(b16, bsw<T>(row, kq), v);
+  }
+#pragma unroll
+  for (int i = 0; i < T::W4; ++i) {
+    const int row = T::BM + (t + T::NT * i) / T::KQ;
+    if constexpr (WPL) {
+      static_assert(PM != PM_F32 && NPL == (PM == PM_SPLIT3 ? 3 : 1), "W planes");
+#pragma unroll
+      for (int q = 0; q < NPL; ++q)
+        *reinterpret_cast<uint2*>(b16 + q * T::STAGEB + bsw<T>(row, kq)) = s.wp[i][q];
+    } else if constexpr (PM == PM_F32) {
+      *reinterpret_cast<float4*>(base + row * T::PITCH + kq) = s.w[i];
+    } else {
+      store_quad_bf16<T, PM>(b16, bsw<T>(row, kq), s.w[i]);
     }
   }
 }
 
-template <int EPI, int PRO, class T, int PM>
+template <int EPI, int PRO, class T, int PM, bool WPL>
 __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, StampLds* sl) {
   constexpr int BM = T::BM, BN = T::BN, FN = T::FN, PITCH = T::PITCH;
   constexpr bool BF = PM != PM_F32;   // bf16 LDS images and MFMAs
-  constexpr int STAGE = PM == PM_F32 ? T::STAGE : PM == PM_BF16 ? T::STAGEB / 2
-                                                                : 3 * T::STAGEB / 2;   // floats
+  constexpr int NPL = PM == PM_SPLIT3 ? 3 : 1;   // bf16 images per operand
+  constexpr int STAGE = PM == PM_F32 ? T::STAGE : NPL * T::STAGEB / 2;   // floats
   constexpr int LDSF = 2 * STAGE > BM * (BN + 1) ? 2 * STAGE : BM * (BN + 1);
   __shared__ __attribute__((aligned(16))) float lds[LDSF];
   __shared__ float zrow[2 * BM];
@@ -212,6 +259,13 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
   c.ldw1 = w1 ? F(ldw1) : c.ldw0;
   c.mean = F(pro_mean) + b * F(pro_bs);
   c.rstd = F(pro_rstd) + b * F(pro_bs);
+  if constexpr (WPL) {   // W planes (range 1: its own planes, or range 0's continuing)
+    const uint16_t* wp1 = F(Wp1);
+    c.wp0 = F(Wp) + b * F(wp_bs);
+    c.wpl0 = F(wpl);
+    c.wp1 = wp1 ? wp1 + b * F(wp1_bs) : c.wp0 + c.ksplit;
+    c.wpl1 = wp1 ? F(wpl1) : c.wpl0;
+  }
 
   const int t = threadIdx.x;
   const int lane = t & 63;
@@ -233,33 +287,35 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
   // so the matrix pipe is fed through the store / barrier / LDS-read phase of every stage.
   // Global loads run two stages ahead (register stage + LDS stage).
   const int nk = c.K / T::BKS;
-  Stage<T> s0, s1;
+  Stage<T, WPL, NPL> s0, s1;
   constexpr int KG = BF ? 16 : 8;                  // k per MFMA group
   constexpr int KKW = T::BKS / T::KS / KG;         // groups per wave per stage
   static_assert(KKW >= 2, "two MFMA groups per stage (pipeline shape)");
   using Frag = FragT<PM, KKW, FN>;
   Frag f0, f1;
   const int kofs = ks * (T::BKS / T::KS) + (lane >> 5) * (KG / 2);
-  constexpr int RP = BF ? T::PITCHB : PITCH;   // LDS row pitch in elements
-  const int a_off = (wm * 32 + (lane & 31)) * RP + kofs;
-  const int w_off = BM * RP + (wn * FN * 32 + (lane & 31)) * RP + kofs;
+  const int a_off = (wm * 32 + (lane & 31)) * PITCH + kofs;   // fp32 images
+  const int w_off = BM * PITCH + (wn * FN * 32 + (lane & 31)) * PITCH + kofs;
+  const int a_row = wm * 32 + (lane & 31);                  // bf16 images (bsw)
+  const int w_row = BM + wn * FN * 32 + (lane & 31);
   auto read_frag = [&](const float* buf, Frag& f) __attribute__((always_inline)) {
 #pragma unroll
     for (int kk = 0; kk < KKW; ++kk) {
       if constexpr (PM == PM_BF16) {
         const __bf16* b16 = reinterpret_cast<const __bf16*>(buf);
-        f.a[kk] = *reinterpret_cast<const bf16x8*>(b16 + a_off + kk * KG);
+        f.a[kk] = *reinterpret_cast<const bf16x8*>(b16 + bsw<T>(a_row, kofs + kk * KG));
 #pragma unroll
         for (int j = 0; j < FN; ++j)
-          f.w[kk][j] = *reinterpret_cast<const bf16x8*>(b16 + w_off + j * 32 * RP + kk * KG);
+          f.w[kk][j] = *reinterpret_cast<const bf16x8*>(b16 + bsw<T>(w_row + j * 32, kofs + kk * KG));
       } else if constexpr (PM == PM_SPLIT3) {
 #pragma unroll
         for (int pc = 0; pc < 3; ++pc) {
           const __bf16* b16 = reinterpret_cast<const __bf16*>(buf) + pc * T::STAGEB;
-          f.a[pc][kk] = *reinterpret_cast<const bf16x8*>(b16 + a_off + kk * KG);
+          f.a[pc][kk] = *reinterpret_cast<const bf16x8*>(b16 + bsw<T>(a_row, kofs + kk * KG));
 #pragma unroll
           for (int j = 0; j < FN; ++j)
-            f.w[pc][kk][j] = *reinterpret_cast<const bf16x8*>(b16 + w_off + j * 32 * RP + kk * KG);
+            f.w[pc][kk][j] =
+                *reinterpret_cast<const bf16x8*>(b16 + bsw<T>(w_row + j * 32, kofs + kk * KG));
         }
       } else {
         f.a[kk] = *reinterpret_cast<const float4*>(buf + a_off + kk * KG);
@@ -322,11 +378,11 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
         float4 a0, a1;
         if constexpr (PM == PM_BF16) {   // the phi(q) the bf16 MFMAs see
           const bf16x8 q = *reinterpret_cast<const bf16x8*>(
-              reinterpret_cast<const __bf16*>(buf) + zr * T::PITCHB + k8);
+              reinterpret_cast<const __bf16*>(buf) + bsw<T>(zr, k8));
           a0 = make_float4((float)q[0], (float)q[1], (float)q[2], (float)q[3]);
           a1 = make_float4((float)q[4], (float)q[5], (float)q[6], (float)q[7]);
         } else if constexpr (PM == PM_SPLIT3) {   // hi + mid + lo = the fp32 value, exactly
-          const __bf16* b16 = reinterpret_cast<const __bf16*>(buf) + zr * T::PITCHB + k8;
+          const __bf16* b16 = reinterpret_cast<const __bf16*>(buf) + bsw<T>(zr, k8);
           const bf16x8 q0 = *reinterpret_cast<const bf16x8*>(b16);
           const bf16x8 q1 = *reinterpret_cast<const bf16x8*>(b16 + T::STAGEB);
           const bf16x8 q2 = *reinterpret_cast<const bf16x8*>(b16 + 2 * T::STAGEB);
@@ -375,22 +431,22 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
 #pragma unroll
       for (int i = 0; i < 16; ++i) acc[j][i] = a0p[j * 1024 + i * 64];
   }
-  load_stage<PRO, T>(c, m0, n0, kt0 * T::BKS, s0);
-  load_stage<PRO, T>(c, m0, n0, (kt0 + 1) * T::BKS, s1);
+  load_stage<PRO, T, WPL, NPL>(c, m0, n0, kt0 * T::BKS, s0);
+  load_stage<PRO, T, WPL, NPL>(c, m0, n0, (kt0 + 1) * T::BKS, s1);
   tk = stamp_start(args.stamp, sl);
-  store_stage<PRO, T, PM>(lds, s0);
+  store_stage<PRO, T, PM, WPL, NPL>(lds, s0);
   __syncthreads();
   read_frag(lds, f0);
   zdot(lds, kt0);   // the first phi(q) stage's Z partials when the x range is skipped
 
-  auto step = [&](int kt, Stage<T>& next, Stage<T>& spare, const Frag& cur, Frag& nxt,
+  auto step = [&](int kt, Stage<T, WPL, NPL>& next, Stage<T, WPL, NPL>& spare, const Frag& cur, Frag& nxt,
                   floatx16 (&tg)[FN]) __attribute__((always_inline)) {
     // unconditional: past the end the last stage is re-read into the spare set and ignored
-    load_stage<PRO, T>(c, m0, n0, min(kt + 2, nk - 1) * T::BKS, spare);
+    load_stage<PRO, T, WPL, NPL>(c, m0, n0, min(kt + 2, nk - 1) * T::BKS, spare);
     mfma_kk(tg, cur, 0);
     ONEPOSE_SCHED_BARRIER();
     float* na = lds + ((kt + 1) & 1) * STAGE;
-    store_stage<PRO, T, PM>(na, next);                // (unused after the last step)
+    store_stage<PRO, T, PM, WPL, NPL>(na, next);                // (unused after the last step)
     ONEPOSE_SCHED_BARRIER();
 #pragma unroll
     for (int kk = 1; kk < KKW - 1; ++kk) mfma_kk(tg, cur, kk);
@@ -705,12 +761,12 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
 #undef F
 }
 
-template <int EPI, int PRO, class T, int PM>
+template <int EPI, int PRO, class T, int PM, bool WPL>
 __global__ __launch_bounds__(T::NT) __attribute__((amdgpu_waves_per_eu(3)))
 void gemm_kernel(GemmArgs args) {
   __shared__ StampLds sl;
   StampTick tk{0ull, 0ull};
-  gemm_body<EPI, PRO, T, PM>(args, tk, &sl);
+  gemm_body<EPI, PRO, T, PM, WPL>(args, tk, &sl);
   stamp_end(args.stamp, tk, &sl);
 }
 
@@ -722,9 +778,9 @@ using T128x128 = Tile<128, 128, 1, 4, 32>;
 using T128x64W8 = Tile<128, 64, 1, 8, 32>;
 
 
-template <int EPI, int PRO, class T, int PM>
+template <int EPI, int PRO, class T, int PM, bool WPL = false>
 void launch_one(GemmArgs& args, int grid, hipStream_t stream) {
-  hipLaunchKernelGGL((gemm_kernel<EPI, PRO, T, PM>), dim3(grid), dim3(T::NT), 0, stream, args);
+  hipLaunchKernelGGL((gemm_kernel<EPI, PRO, T, PM, WPL>), dim3(grid), dim3(T::NT), 0, stream, args);
 }
 
 struct TileDims {
@@ -796,40 +852,52 @@ int gemm_launch(int epi, int pro, int tile, GemmArgs& args, hipStream_t stream, 
     grid += P.tiles;
   }
   if (grid == 0) return ONEPOSE_OK;
-  args.stamp = nullptr;
-#define CASE(E, PR, TI, T, PMV)                          \
-  if (epi == E && pro == PR && tile == TI && pm == PMV) { \
-    prof_pre(kind, stream);                              \
-    args.stamp = prof_stamp_slot(kind);                  \
-    launch_one<E, PR, T, PMV>(args, grid, stream);       \
-    prof_post(kind, stream);                             \
-    OP_LAUNCHED();                                       \
-    return ONEPOSE_OK;                                   \
+  // W from bf16 planes (every problem of the launch, or none)
+  const bool wpl = args.p[0].Wp != nullptr;
+  for (int i = 0; i < args.nprob; ++i) {
+    const GemmProb& P = args.p[i];
+    OP_REQUIRE((P.Wp != nullptr) == wpl, "gemm: W planes on some problems only");
+    OP_REQUIRE(!wpl || (pm != PM_F32 && td.bks == 32 && P.ldw % 4 == 0 &&
+                        (P.W1 == nullptr) == (P.Wp1 == nullptr)),
+               "gemm: W planes need a bf16 mode, 32-deep stages and planes for both K ranges");
   }
-  CASE(EPI_QKV, PRO_PLAIN, TILE_32x128, T32x128, PM_F32)
-  CASE(EPI_QKV, PRO_PLAIN, TILE_64x128, T64x128, PM_F32)
-  CASE(EPI_QKV, PRO_PLAIN, TILE_128x128, T128x128, PM_F32)
-  CASE(EPI_STATS, PRO_HEADZ, TILE_64x64, T64x64, PM_F32)
-  CASE(EPI_RESID, PRO_NORM_RELU, TILE_64x64, T64x64, PM_F32)
-  CASE(EPI_RESID, PRO_NORM_RELU, TILE_64x32K2, T64x32K2, PM_F32)
-  CASE(EPI_SCORE, PRO_PLAIN, TILE_64x64, T64x64, PM_F32)
-  CASE(EPI_SCORE, PRO_PLAIN, TILE_128x64W8, T128x64W8, PM_F32)
-  CASE(EPI_BIAS, PRO_PLAIN, TILE_64x64, T64x64, PM_F32)
-  CASE(EPI_ACC, PRO_PLAIN, TILE_64x64, T64x64, PM_F32)
-  CASE(EPI_ACC, PRO_PLAIN, TILE_64x64, T64x64, PM_BF16)
-  CASE(EPI_ACC, PRO_PLAIN, TILE_64x64, T64x64, PM_SPLIT3)
+  args.stamp = nullptr;
+#define CASE(E, PR, TI, T, PMV, WP)                                     \
+  if (epi == E && pro == PR && tile == TI && pm == PMV && wpl == WP) { \
+    prof_pre(kind, stream);                                             \
+    args.stamp = prof_stamp_slot(kind);                                 \
+    launch_one<E, PR, T, PMV, WP>(args, grid, stream);                  \
+    prof_post(kind, stream);                                            \
+    OP_LAUNCHED();                                                      \
+    return ONEPOSE_OK;                                                  \
+  }
+  CASE(EPI_QKV, PRO_PLAIN, TILE_32x128, T32x128, PM_F32, false)
+  CASE(EPI_QKV, PRO_PLAIN, TILE_64x128, T64x128, PM_F32, false)
+  CASE(EPI_QKV, PRO_PLAIN, TILE_128x128, T128x128, PM_F32, false)
+  CASE(EPI_STATS, PRO_HEADZ, TILE_64x64, T64x64, PM_F32, false)
+  CASE(EPI_RESID, PRO_NORM_RELU, TILE_64x64, T64x64, PM_F32, false)
+  CASE(EPI_RESID, PRO_NORM_RELU, TILE_64x32K2, T64x32K2, PM_F32, false)
+  CASE(EPI_SCORE, PRO_PLAIN, TILE_64x64, T64x64, PM_F32, false)
+  CASE(EPI_SCORE, PRO_PLAIN, TILE_128x64W8, T128x64W8, PM_F32, false)
+  CASE(EPI_BIAS, PRO_PLAIN, TILE_64x64, T64x64, PM_F32, false)
+  CASE(EPI_ACC, PRO_PLAIN, TILE_64x64, T64x64, PM_F32, false)
+  // attention-layer GEMMs in the bf16 mode: W from the packed bf16 plane (rounded on the host,
+  // Mf by the KV fold), A rounded as the stage is stored
+  CASE(EPI_ACC, PRO_PLAIN, TILE_64x64, T64x64, PM_BF16, true)
+  CASE(EPI_ACC, PRO_PLAIN, TILE_64x64, T64x64, PM_SPLIT3, false)
   // bf16-MFMA attention layers (precision mode ONEPOSE_PREC_BF16_ATTN)
-  CASE(EPI_QKV, PRO_PLAIN, TILE_32x128, T32x128, PM_BF16)
-  CASE(EPI_STATS, PRO_HEADZ, TILE_64x64, T64x64, PM_BF16)
-  CASE(EPI_RESID, PRO_NORM_RELU, TILE_64x64, T64x64, PM_BF16)
+  CASE(EPI_QKV, PRO_PLAIN, TILE_32x128, T32x128, PM_BF16, true)
+  CASE(EPI_STATS, PRO_HEADZ, TILE_64x64, T64x64, PM_BF16, true)
+  CASE(EPI_RESID, PRO_NORM_RELU, TILE_64x64, T64x64, PM_BF16, true)
   // fp32 by exact 3-way bf16 split (precision mode ONEPOSE_PREC_FP32_SPLIT)
-  CASE(EPI_QKV, PRO_PLAIN, TILE_32x128, T32x128, PM_SPLIT3)
-  CASE(EPI_STATS, PRO_HEADZ, TILE_64x64, T64x64, PM_SPLIT3)
-  CASE(EPI_RESID, PRO_NORM_RELU, TILE_64x64, T64x64, PM_SPLIT3)
-  CASE(EPI_SCORE, PRO_PLAIN, TILE_64x64, T64x64, PM_SPLIT3)
-  CASE(EPI_BIAS, PRO_PLAIN, TILE_64x64, T64x64, PM_SPLIT3)
+  CASE(EPI_QKV, PRO_PLAIN, TILE_32x128, T32x128, PM_SPLIT3, false)
+  CASE(EPI_STATS, PRO_HEADZ, TILE_64x64, T64x64, PM_SPLIT3, false)
+  CASE(EPI_RESID, PRO_NORM_RELU, TILE_64x64, T64x64, PM_SPLIT3, false)
+  CASE(EPI_SCORE, PRO_PLAIN, TILE_64x64, T64x64, PM_SPLIT3, false)
+  CASE(EPI_BIAS, PRO_PLAIN, TILE_64x64, T64x64, PM_SPLIT3, false)
 #undef CASE
-  set_error("gemm: unsupported epilogue/prologue/tile/mode %d/%d/%d/%d", epi, pro, tile, pm);
+  set_error("gemm: unsupported epilogue/prologue/tile/mode/planes %d/%d/%d/%d/%d", epi, pro, tile,
+            pm, (int)wpl);
   return ONEPOSE_ERR_INVALID;
 }
 

@@ -136,13 +136,24 @@ constexpr int64_t kApFloats = kApWqkv + kApBqkv + kApW1a + kApC + kApB1 + kApW2 
 constexpr int64_t kGatFloats = 512;
 constexpr int64_t kFinalFloats = 256 * 256 + 256;
 constexpr int64_t kPackedFloats = kApLayers * kApFloats + kGatLayers * kGatFloats + kFinalFloats;
+// ... then, per attention layer, the bf16 planes of its three weight matrices for the bf16
+// modes (gemm.h GemmProb::Wp): Wqkv, W1a and W2 split exactly into hi / mid / lo
+// (hi = bf16(x) rounded to nearest even: PM_BF16's operand), [3][rows][cols] uint16 each.
+constexpr int64_t kPlWqkv = 768 * 256, kPlW1a = 512 * 256, kPlW2 = 256 * 512;
+constexpr int64_t kApPlanes = 3 * (kPlWqkv + kPlW1a + kPlW2);   // uint16 per layer
+constexpr int64_t kPackedBytes = kPackedFloats * 4 + kApLayers * kApPlanes * 2;
 
 struct ApW {
   const float *wqkv, *bqkv, *w1a, *c, *b1, *w2, *b2, *ct;
+  const uint16_t *wqkv_p, *w1a_p, *w2_p;   // bf16 planes
 };
 ApW ap_weights(const float* base, int ap) {
   const float* p = base + (int64_t)ap * kApFloats;
   ApW w;
+  const uint16_t* pl = reinterpret_cast<const uint16_t*>(base + kPackedFloats) + (int64_t)ap * kApPlanes;
+  w.wqkv_p = pl;
+  w.w1a_p = pl + 3 * kPlWqkv;
+  w.w2_p = w.w1a_p + 3 * kPlW1a;
   w.wqkv = p; p += kApWqkv;
   w.bqkv = p; p += kApBqkv;
   w.w1a = p; p += kApW1a;
@@ -152,6 +163,31 @@ ApW ap_weights(const float* base, int ap) {
   w.b2 = p; p += kApB2;
   w.ct = p;
   return w;
+}
+
+// bf16 bits of x rounded to nearest even (the device's (__bf16)x for finite x)
+uint16_t bf16_rne(float x) {
+  uint32_t u;
+  memcpy(&u, &x, 4);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+float bf16_val(uint16_t b) {
+  const uint32_t u = (uint32_t)b << 16;
+  float f;
+  memcpy(&f, &u, 4);
+  return f;
+}
+// the exact split x = hi + mid + lo of gemm.hip's store_quad_bf16, into planes n elements apart
+void split_planes(const float* x, int64_t n, uint16_t* out) {
+  for (int64_t i = 0; i < n; ++i) {
+    const uint16_t h = bf16_rne(x[i]);
+    const float r = x[i] - bf16_val(h);
+    const uint16_t m = bf16_rne(r);
+    out[i] = h;
+    out[n + i] = m;
+    out[2 * n + i] = bf16_rne(r - bf16_val(m));
+  }
 }
 const float* gat_weights(const float* base, int g) {
   return base + kApLayers * kApFloats + (int64_t)g * kGatFloats;
@@ -266,6 +302,7 @@ struct KvArgs {
 };
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 
 // Sum the chunk partials -> KV[h][d][q], ksum[256].  Each workgroup owns 64 float4 outputs
 // of one (source, sample); its four waves sum interleaved quarters of the chunks (eight
@@ -322,12 +359,24 @@ __global__ __launch_bounds__(256) void kv_reduce_kernel(KvArgs args, float* kv, 
 // are L2-resident (C: 512 KB per layer, KV: 64 KB per source).
 struct FoldProb {
   const float* kv;    // [B][4][64][64] of the source
-  float* mf;          // [B][512][256]
+  float* mf;          // [B][512][256] fp32, or [B][3][512][256] bf16 planes (planes != 0)
 };
 struct FoldArgs {
   FoldProb p[2];
   const float* c;     // [512][256]
+  int planes;         // bf16 modes: Mf as the exact hi / mid / lo planes (GemmProb::Wp1)
 };
+constexpr int64_t kMfElems = 512 * 256;
+constexpr int64_t kMfFloats = 3 * kMfElems / 2;   // a sample's Mf region (room for the planes;
+                                                  // the fp32 Mf uses its first kMfElems)
+
+// x -> (hi, mid, lo): the exact split of gemm.hip's store_quad_bf16
+__device__ __forceinline__ void split_bf16(float x, __bf16& h, __bf16& m, __bf16& l) {
+  h = (__bf16)x;
+  const float r = x - (float)h;
+  m = (__bf16)r;
+  l = (__bf16)(r - (float)m);
+}
 __global__ __launch_bounds__(256) void m_fold_kernel(FoldArgs args, int batch) {
   const int ot = blockIdx.x & 7, h = (blockIdx.x >> 3) & 3;
   const int bs = blockIdx.x >> 5, b = bs % batch, side = bs / batch;
@@ -348,7 +397,17 @@ __global__ __launch_bounds__(256) void m_fold_kernel(FoldArgs args, int batch) {
     acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av.z, wv.z, acc, 0, 0, 0);
     acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av.w, wv.w, acc, 0, 0, 0);
   }
-  float* out = P.mf + (int64_t)b * 512 * 256 + (ot * 64 + wm * 32) * 256 + h * 64 + wn * 32 + l32;
+  const int64_t e0 = (int64_t)(ot * 64 + wm * 32) * 256 + h * 64 + wn * 32 + l32;
+  if (args.planes) {
+    __bf16* out = reinterpret_cast<__bf16*>(P.mf) + (int64_t)b * 3 * kMfElems + e0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int64_t e = ((i & 3) + 8 * (i >> 2) + 4 * half) * 256;
+      split_bf16(acc[i], out[e], out[kMfElems + e], out[2 * kMfElems + e]);
+    }
+    return;
+  }
+  float* out = P.mf + (int64_t)b * kMfFloats + e0;
 #pragma unroll
   for (int i = 0; i < 16; ++i) out[((i & 3) + 8 * (i >> 2) + 4 * half) * 256] = acc[i];
 }
@@ -360,8 +419,9 @@ __global__ __launch_bounds__(256) void m_fold_kernel(FoldArgs args, int batch) {
 // sample) is sum phi(k) (chunk sum only).
 struct KvFoldArgs {
   KvProb p[2];     // chunk partials of source slot 0 / 1
-  float* mf[2];    // [B][512][256] Mf of the side that attends to slot 0 / 1
+  float* mf[2];    // Mf of the side that attends to slot 0 / 1 (FoldProb::mf's layouts)
   const float* ct; // [4][64][512]  C transposed per head (packed weights)
+  int planes;      // bf16 modes: Mf as bf16 planes
 };
 typedef float f2v __attribute__((ext_vector_type(2)));
 
@@ -461,7 +521,25 @@ __global__ __launch_bounds__(256) void kv_fold256_kernel(KvFoldArgs args, float*
     y01 = qq == 0 ? a01 : y01 + a01;
     y23 = qq == 0 ? a23 : y23 + a23;
   }
-  float* mf = (src ? args.mf[1] : args.mf[0]) + (int64_t)b * 512 * 256 + (int64_t)o * 256 + h * 64 + d0;
+  const int64_t e0 = (int64_t)o * 256 + h * 64 + d0;
+  if (args.planes) {
+    bf16x4 q0, q1, q2;
+    const float y[4] = {y01.x, y01.y, y23.x, y23.y};
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      __bf16 h, m, l;
+      split_bf16(y[c], h, m, l);
+      q0[c] = h;
+      q1[c] = m;
+      q2[c] = l;
+    }
+    __bf16* mp = reinterpret_cast<__bf16*>(src ? args.mf[1] : args.mf[0]) + (int64_t)b * 3 * kMfElems + e0;
+    *reinterpret_cast<bf16x4*>(mp) = q0;
+    *reinterpret_cast<bf16x4*>(mp + kMfElems) = q1;
+    *reinterpret_cast<bf16x4*>(mp + 2 * kMfElems) = q2;
+    return;
+  }
+  float* mf = (src ? args.mf[1] : args.mf[0]) + (int64_t)b * kMfFloats + e0;
   *reinterpret_cast<float4*>(mf) = make_float4(y01.x, y01.y, y23.x, y23.y);
 }
 
@@ -1125,7 +1203,7 @@ Plan make_plan(void* ws, int B, int n1, int n3, int L, bool with_conf) {
   p.kspart3 = c.take<float>((size_t)B * ceil_div(n3, kvr) * 256);
   p.kv = c.take<float>((size_t)2 * B * 16384);
   p.ksum = c.take<float>((size_t)2 * B * 256);
-  p.mf = c.take<float>((size_t)2 * B * 512 * 256);
+  p.mf = c.take<float>((size_t)2 * B * kMfFloats);
   p.phiq2 = c.take<float>(t2 * 256);
   p.phiq3 = c.take<float>(t3 * 256);
   p.y12 = c.take<float>(t2 * 512);
@@ -1273,7 +1351,7 @@ int64_t onepose_matcher_tensor_numel(int i) {
   return s[i].numel;
 }
 
-size_t onepose_matcher_packed_bytes(void) { return (size_t)kPackedFloats * sizeof(float); }
+size_t onepose_matcher_packed_bytes(void) { return (size_t)kPackedBytes; }
 
 int onepose_matcher_pack(const float* const* tensors, int n_tensors, void* packed_host) {
   clear_error();
@@ -1358,6 +1436,10 @@ int onepose_matcher_pack(const float* const* tensors, int n_tensors, void* packe
     float* ct = b2 + kApB2;
     for (int o = 0; o < 512; ++o)
       for (int cp = 0; cp < 256; ++cp) ct[(int64_t)cp * 512 + o] = cw[(int64_t)o * 256 + cp];
+    uint16_t* pl = reinterpret_cast<uint16_t*>(out + kPackedFloats) + (int64_t)ap * kApPlanes;
+    split_planes(wq, kPlWqkv, pl);   // wq: the whole [768][256] panel (q rows, then k_h / v_h)
+    split_planes(w1a, kPlW1a, pl + 3 * kPlWqkv);
+    split_planes(w2, kPlW2, pl + 3 * (kPlWqkv + kPlW1a));
     ++ap;
   }
   float* fin = out + kApLayers * kApFloats + kGatLayers * kGatFloats;
@@ -1428,6 +1510,19 @@ bool valid_precision(int p) {
 int attention_pm(int precision) {
   return precision == ONEPOSE_PREC_BF16_ATTN ? PM_BF16
          : precision == ONEPOSE_PREC_FP32_SPLIT ? PM_SPLIT3 : PM_F32;
+}
+
+// W of a GEMM as the packed bf16 planes (bf16 modes; gemm.h GemmProb::Wp)
+void set_w_planes(GemmProb& g, const uint16_t* wp, int64_t rows_x_cols) {
+  g.Wp = wp;
+  g.wp_bs = 0;
+  g.wpl = rows_x_cols;
+}
+// MLP conv 1's second K range: the Mf planes of a Mf region (kMfFloats per sample; bs 0: shared)
+void set_mf_planes(GemmProb& g, const float* mf, int64_t sample_floats) {
+  g.Wp1 = reinterpret_cast<const uint16_t*>(mf);
+  g.wp1_bs = sample_floats * 2;
+  g.wpl1 = kMfElems;
 }
 
 // One side of an attention layer: its input state (x_bs 0 = shared by the batch: the object
@@ -1521,7 +1616,7 @@ ObjLayout obj_layout(int n3, int num_leaf, int flags) {
   L.acc = L.phiq + (int64_t)n3 * 256;
   L.ksum = L.acc + (int64_t)ceil_div(n3, 64) * 64 * 512;   // TILE_64x64 tiles of N = 512
   L.mf = L.ksum + 256;
-  L.slogs = L.mf + 512 * 256;
+  L.slogs = L.mf + kMfFloats;
   L.tab = L.slogs + (L.tables ? (int64_t)3 * n3 * kLogitStride : 0);
   L.total = L.tab + (L.tables ? (int64_t)3 * n3 * 2 * num_leaf * 256 : 0);
   return L;
@@ -1581,6 +1676,7 @@ int attention_layer(const ApW& w, const Side* sd, int nside, int B, const Plan& 
       g.kvpart = s.kvpart;
       g.kspart = s.kspart;
       g.y_bs = (int64_t)s.n * 256;
+      if (pm == PM_BF16) set_w_planes(g, w.wqkv_p, kPlWqkv);
     }
     return gemm_launch(EPI_QKV, PRO_PLAIN, tl.qkv[i0], a, st, K_QKV_GEMM, pm);
   });
@@ -1593,7 +1689,11 @@ int attention_layer(const ApW& w, const Side* sd, int nside, int B, const Plan& 
   for (int i = 0; i < nside; ++i) reader[sd[i].src] = i;
   for (int i = 0; i < nsrc; ++i)
     OP_REQUIRE(reader[i] >= 0, "attention layer: source slot %d has no reader", i);
-  auto mf_of = [&](int side) { return p.mf + (size_t)side * B * 512 * 256; };
+  auto mf_of = [&](int side) { return p.mf + (size_t)side * B * kMfFloats; };
+  // bf16 mode: W operands as bf16 planes (gemm.h GemmProb::Wp; in the split mode three b64 plane
+  // loads per k-quad measured slower than one fp32 b128 load + the VALU split: 1517-1538 vs
+  // 1599 frames/s)
+  const bool planes = pm == PM_BF16;
   auto chunks = [&](int i) { return ceil_div(sd[i].n, gemm_tile_rows(tl.qkv[i])); };
   rc = groups(nsrc, [&](int a, int b) { return tl.fused_fold[a] == tl.fused_fold[b]; },
               [&](int i0, int i1) -> int {
@@ -1603,6 +1703,7 @@ int attention_layer(const ApW& w, const Side* sd, int nside, int B, const Plan& 
     if (tl.fused_fold[i0]) {
       KvFoldArgs ka;
       ka.ct = w.ct;
+      ka.planes = planes ? 1 : 0;
       for (int i = i0; i < i1; ++i) {
         ka.p[i - i0] = {sd[i].kvpart, sd[i].kspart, chunks(i)};
         ka.mf[i - i0] = mf_of(reader[i]);
@@ -1632,6 +1733,7 @@ int attention_layer(const ApW& w, const Side* sd, int nside, int B, const Plan& 
     }
     FoldArgs fa;   // Mf of the sides attending to these slots
     fa.c = w.c;
+    fa.planes = planes ? 1 : 0;
     for (int i = i0; i < i1; ++i)
       fa.p[i - i0] = {p.kv + (size_t)i * B * 16384, mf_of(reader[i])};
     OP_LAUNCH(K_MFOLD, st, m_fold_kernel, dim3(ns * B * 32), dim3(256), 0, st, fa, B);
@@ -1652,7 +1754,11 @@ int attention_layer(const ApW& w, const Side* sd, int nside, int B, const Plan& 
       a.p[i].ksplit = 256;
       a.p[i].W1 = mf_of(i);
       a.p[i].ldw1 = 256;
-      a.p[i].w1_bs = 512 * 256;
+      a.p[i].w1_bs = kMfFloats;
+      if (planes) {
+        set_w_planes(a.p[i], w.w1a_p, kPlW1a);
+        set_mf_planes(a.p[i], mf_of(i), kMfFloats);
+      }
       a.p[i].stats = s.stats;
       a.p[i].st_cnt = cnt + (size_t)i * B * kCntPerSide;
       a.p[i].st_mean = p.mean + (size_t)i * B * 512;
@@ -1664,6 +1770,7 @@ int attention_layer(const ApW& w, const Side* sd, int nside, int B, const Plan& 
     if (xc) {   // the object's halves: shared by the batch (batch stride 0)
       a.p[0].W1 = xc->mf;
       a.p[0].w1_bs = 0;
+      if (planes) set_mf_planes(a.p[0], xc->mf, 0);
       a.p[0].ksum = xc->ksum;
       a.p[0].ksum_bs = 0;
       a.p[1].A1 = xc->phiq;
@@ -1706,6 +1813,7 @@ int attention_layer(const ApW& w, const Side* sd, int nside, int B, const Plan& 
       g.pro_mean = p.mean + (size_t)i * B * 512;
       g.pro_rstd = p.rstd + (size_t)i * B * 512;
       g.pro_bs = 512;
+      if (pm == PM_BF16) set_w_planes(g, w.w2_p, kPlW2);
     }
     return gemm_launch(EPI_RESID, PRO_NORM_RELU, tl.mlp2[i0], a, st, K_MLP2, pm);
   });
@@ -1950,12 +2058,14 @@ int object_prepare_impl(const void* packed_weights, const float* desc3d, const f
     a.p[0].vdiv = (float)n3;
     a.p[0].kvpart = p.kvpart3;
     a.p[0].kspart = p.kspart3;
+    if (pm == PM_BF16) set_w_planes(a.p[0], w.wqkv_p, kPlWqkv);
     if ((rc = gemm_launch(EPI_QKV, PRO_PLAIN, tl.qkv[0], a, st, K_QKV_GEMM, pm)) != ONEPOSE_OK)
       return rc;
   }
   {  // sum phi(k) into the cache, and the 2D side's Mf = C KV_3D
     KvFoldArgs ka;
     ka.ct = w.ct;
+    ka.planes = pm == PM_BF16 ? 1 : 0;
     ka.p[0] = {p.kvpart3, p.kspart3, ceil_div(n3, gemm_tile_rows(tl.qkv[0]))};
     ka.mf[0] = cache + L.mf;
     ka.mf[1] = nullptr;
@@ -1968,6 +2078,7 @@ int object_prepare_impl(const void* packed_weights, const float* desc3d, const f
     GemmArgs a;
     a.nprob = 1;
     a.p[0] = gemm_prob(cache, 256, w.w1a, 256, nullptr, cache + L.acc, 512, n3, 512, 256, 1);
+    if (pm == PM_BF16) set_w_planes(a.p[0], w.w1a_p, kPlW1a);
     if ((rc = gemm_launch(EPI_ACC, PRO_PLAIN, kTileMLP1, a, st, K_MLP1, pm)) != ONEPOSE_OK)
       return rc;
   }

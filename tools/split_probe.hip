@@ -181,6 +181,209 @@ __global__ __launch_bounds__(256) void split_gemm(const float* __restrict__ A, i
     }
 }
 
+
+// v2: W through a 3-stage LDS-DMA ring (issued two stages ahead), A through two register sets
+// loaded by inline-asm global_load_dwordx4 (two stages ahead; hipcc does not count asm loads,
+// so every wait is an explicit counted vmcnt), raw s_barrier (no vmcnt(0) drain).
+typedef float f4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ f4v gload4(const float* p) {
+  f4v v;
+  asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
+  return v;
+}
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+// the wait also "defines" the registers of the set it retires, so no consumer of them can be
+// scheduled above it (an asm load's result is otherwise available to the compiler at once)
+template <int N, int CH>
+__device__ __forceinline__ void wait_vm_set(f4v (&s)[CH][2]) {
+  if constexpr (CH == 1) {
+    asm volatile("s_waitcnt vmcnt(%2)" : "+v"(s[0][0]), "+v"(s[0][1]) : "n"(N) : "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(%4)"
+                 : "+v"(s[0][0]), "+v"(s[0][1]), "+v"(s[1][0]), "+v"(s[1][1])
+                 : "n"(N)
+                 : "memory");
+  }
+}
+
+template <int BM, int BN, int MODE>
+__global__ __launch_bounds__(256) void split_gemm2(const float* __restrict__ A, int lda,
+                                                   const __bf16* __restrict__ Wp, int64_t wplane,
+                                                   int ldw, const float* __restrict__ bias,
+                                                   float* __restrict__ Y, int ldy, int M, int N,
+                                                   int K) {
+  constexpr int NP = MODE == 0 ? 3 : 1;
+  constexpr int FM = BM / 64, FN = BN / 64;
+  constexpr int APL = BM * 64, WPL = BN * 64;
+  constexpr int ASTAGE = NP * APL, WSTAGE = NP * WPL;
+  constexpr int CH = BM * 4 / 256;
+  constexpr int WI = NP * BN / 16;
+  static_assert(WI % 4 == 0, "W pieces split over 4 waves");
+  constexpr int VM_PER_STEP = 2 * CH + WI / 4;   // vector-memory ops one step issues per wave
+  __shared__ __attribute__((aligned(16))) char lds[2 * ASTAGE + 3 * WSTAGE];
+  char* abuf = lds;
+  char* wring = lds + 2 * ASTAGE;
+  const int ntiles = (N + BN - 1) / BN;
+  const int bid = xcd_contiguous(blockIdx.x, gridDim.x);
+  const int mt = bid / ntiles, nt = bid - mt * ntiles;
+  const int m0 = mt * BM, n0 = nt * BN;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int r = lane & 31, hh = lane >> 5;
+  f16v acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+  f4v ra[2][CH][2];
+  auto load_a = [&](int k0, f4v (&dst)[CH][2]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      const int e = t + 256 * c, row = e >> 2, ch = e & 3;
+      const float* p = A + (int64_t)min(m0 + row, M - 1) * lda + k0 + ch * 8;
+      dst[c][0] = gload4(p);
+      dst[c][1] = gload4(p + 4);
+    }
+  };
+  auto store_a = [&](char* buf, const f4v (&src)[CH][2]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      const int e = t + 256 * c, row = e >> 2, ch = e & 3;
+      const int off = row * 64 + ((ch ^ ((row >> 2) & 3)) << 4);
+      if constexpr (MODE == 0) {
+        bf16x8_t h, m, l;
+        split8(make_float4(src[c][0][0], src[c][0][1], src[c][0][2], src[c][0][3]),
+               make_float4(src[c][1][0], src[c][1][1], src[c][1][2], src[c][1][3]), h, m, l);
+        *reinterpret_cast<bf16x8_t*>(buf + off) = h;
+        *reinterpret_cast<bf16x8_t*>(buf + APL + off) = m;
+        *reinterpret_cast<bf16x8_t*>(buf + 2 * APL + off) = l;
+      } else {
+        bf16x8_t h;
+        const float x[8] = {src[c][0][0], src[c][0][1], src[c][0][2], src[c][0][3],
+                            src[c][1][0], src[c][1][1], src[c][1][2], src[c][1][3]};
+#pragma unroll
+        for (int j = 0; j < 8; ++j) h[j] = (__bf16)x[j];
+        *reinterpret_cast<bf16x8_t*>(buf + off) = h;
+      }
+    }
+  };
+  auto dma_w = [&](int k0, char* buf) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < WI / 4; ++i) {
+      const int j = wave + 4 * i;
+      const int p = j / (BN / 16), rb = (j % (BN / 16)) * 16;
+      const int row = rb + (lane >> 2), ch = (lane & 3) ^ ((row >> 2) & 3);
+      const __bf16* src = Wp + p * wplane + (int64_t)min(n0 + row, N - 1) * ldw + k0 + ch * 8;
+      __builtin_amdgcn_global_load_lds(src, buf + p * WPL + rb * 64, 16, 0, 0);
+    }
+  };
+  auto compute = [&](const char* ab, const char* wb) __attribute__((always_inline)) {
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8_t fa[NP][FM], fw[NP][FN];
+#pragma unroll
+      for (int p = 0; p < NP; ++p) {
+#pragma unroll
+        for (int i = 0; i < FM; ++i) {
+          const int row = wm * (BM / 2) + i * 32 + r;
+          const int off = row * 64 + (((2 * kk + hh) ^ ((row >> 2) & 3)) << 4);
+          fa[p][i] = *reinterpret_cast<const bf16x8_t*>(ab + p * APL + off);
+        }
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          const int row = wn * (BN / 2) + j * 32 + r;
+          const int off = row * 64 + (((2 * kk + hh) ^ ((row >> 2) & 3)) << 4);
+          fw[p][j] = *reinterpret_cast<const bf16x8_t*>(wb + p * WPL + off);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          if constexpr (MODE == 0) {
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[2][i], fw[0][j], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[1][i], fw[1][j], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0][i], fw[2][j], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[1][i], fw[0][j], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0][i], fw[1][j], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0][i], fw[0][j], acc[i][j], 0, 0, 0);
+          } else {
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0][i], fw[0][j], acc[i][j], 0, 0, 0);
+          }
+        }
+    }
+  };
+  const int nk = K / 32;   // >= 2
+  // prologue: stages 0 and 1 in flight; stage 0 split into A buffer 0
+  load_a(0, ra[0]);
+  dma_w(0, wring);
+  load_a(32, ra[1]);
+  dma_w(32, wring + WSTAGE);
+  wait_vm_set<VM_PER_STEP>(ra[0]);   // stage 0 landed (stage 1 may still be in flight)
+  store_a(abuf, ra[0]);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  for (int kt = 0; kt < nk; ++kt) {
+    const bool pre = kt + 2 < nk;   // wave-uniform
+    if (pre) {
+      if (kt & 1) load_a((kt + 2) * 32, ra[1]);
+      else load_a((kt + 2) * 32, ra[0]);
+      dma_w((kt + 2) * 32, wring + ((kt + 2) % 3) * WSTAGE);
+    }
+    compute(abuf + (kt & 1) * ASTAGE, wring + (kt % 3) * WSTAGE);
+    if (kt + 1 < nk) {   // stage kt + 1 landed: its A registers are set (kt + 1) & 1
+      if (kt & 1) {
+        if (pre) wait_vm_set<VM_PER_STEP>(ra[0]); else wait_vm_set<0>(ra[0]);
+        store_a(abuf, ra[0]);
+      } else {
+        if (pre) wait_vm_set<VM_PER_STEP>(ra[1]); else wait_vm_set<0>(ra[1]);
+        store_a(abuf + ASTAGE, ra[1]);
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  }
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int gn = n0 + wn * (BN / 2) + j * 32 + r;
+      if (gn >= N) continue;
+      const float bv = bias[gn];
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int gm = m0 + wm * (BM / 2) + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * hh;
+        if (gm < M) Y[(int64_t)gm * ldy + gn] = acc[i][j][e] + bv;
+      }
+    }
+}
+
+template <int BM, int BN, int MODE>
+float time_split2(const float* A, const __bf16* Wp, int64_t wplane, const float* bias, float* Y,
+                  int M, int N, int K, int iters) {
+  const int grid = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+  hipEvent_t e0, e1;
+  hipEventCreate(&e0);
+  hipEventCreate(&e1);
+  for (int w = 0; w < 3; ++w)
+    hipLaunchKernelGGL((split_gemm2<BM, BN, MODE>), dim3(grid), dim3(256), 0, 0, A, K, Wp, wplane, K,
+                       bias, Y, N, M, N, K);
+  hipEventRecord(e0);
+  for (int it = 0; it < iters; ++it)
+    hipLaunchKernelGGL((split_gemm2<BM, BN, MODE>), dim3(grid), dim3(256), 0, 0, A, K, Wp, wplane, K,
+                       bias, Y, N, M, N, K);
+  hipEventRecord(e1);
+  hipEventSynchronize(e1);
+  float ms;
+  hipEventElapsedTime(&ms, e0, e1);
+  return ms * 1e3f / iters;
+}
+
 // host split of W into three bf16 planes (round to nearest even, exact residuals)
 static uint16_t bf16_bits(float x) {
   uint32_t u;
@@ -306,6 +509,16 @@ int main(int argc, char** argv) {
     d12 = 0;
     for (size_t i = 0; i < y1.size(); ++i) d12 = fmax(d12, fabs(y1[i] - y2[i]));
     printf("max |fp32 - bf16(64x128)| %.3g\n", d12);
+    time_split2<64, 128, 0>(A, Wp, wpl, b, Y2, M, N, K, 1);
+    hipMemcpy(y2.data(), Y2, y2.size() * 4, hipMemcpyDeviceToHost);
+    d12 = 0;
+    for (size_t i = 0; i < y1.size(); ++i) d12 = fmax(d12, fabs(y1[i] - y2[i]));
+    printf("v2: max |fp32 - split3(64x128)| %.3g\n", d12);
+    time_split2<64, 64, 0>(A, Wp, wpl, b, Y2, M, N, K, 1);
+    hipMemcpy(y2.data(), Y2, y2.size() * 4, hipMemcpyDeviceToHost);
+    d12 = 0;
+    for (size_t i = 0; i < y1.size(); ++i) d12 = fmax(d12, fabs(y1[i] - y2[i]));
+    printf("v2: max |fp32 - split3(64x64)| %.3g\n", d12);
   }
   for (int M : Ms) {
     const double gf = 2.0 * M * N * K * 1e-9;
@@ -320,6 +533,13 @@ int main(int argc, char** argv) {
            "128x128 %7.2f (%5.1f) | bf16 64x128 %7.2f (%5.1f) 128x128 %7.2f (%5.1f)\n",
            M, f, gf / f * 1e3, s1, gf / s1 * 1e3, s2, gf / s2 * 1e3, s3, gf / s3 * 1e3, q1, gf / q1 * 1e3,
            q2, gf / q2 * 1e3);
+    const float v1 = time_split2<64, 64, 0>(A, Wp, wpl, b, Y2, M, N, K, it);
+    const float v2 = time_split2<64, 128, 0>(A, Wp, wpl, b, Y2, M, N, K, it);
+    const float v3 = time_split2<128, 64, 0>(A, Wp, wpl, b, Y2, M, N, K, it);
+    const float w1 = time_split2<64, 128, 1>(A, Wp, wpl, b, Y2, M, N, K, it);
+    const float w2 = time_split2<128, 128, 1>(A, Wp, wpl, b, Y2, M, N, K, it);
+    printf("   v2 split3 64x64 %7.2f (%5.1f) 64x128 %7.2f (%5.1f) 128x64 %7.2f (%5.1f) | bf16 64x128 %7.2f (%5.1f) 128x128 %7.2f (%5.1f)\n",
+           v1, gf / v1 * 1e3, v2, gf / v2 * 1e3, v3, gf / v3 * 1e3, w1, gf / w1 * 1e3, w2, gf / w2 * 1e3);
   }
   return 0;
 }
