@@ -59,9 +59,10 @@ struct FragT<PM_SPLIT3, KKW, FN> {   // hi / mid / lo pieces
 };
 
 
-template <int BM_, int BN_, int KS_, int NW_, int BKS_>
+template <int BM_, int BN_, int KS_, int NW_, int BKS_, int WPE_ = 3>
 struct Tile {
   static constexpr int BM = BM_, BN = BN_, KS = KS_, NW = NW_, BKS = BKS_;
+  static constexpr int WPE = WPE_;              // amdgpu_waves_per_eu hint
   static constexpr int NT = 64 * NW;            // threads
   static constexpr int WM = BM / 32;            // waves along M
   static constexpr int WN = NW / (WM * KS);     // waves along N
@@ -72,21 +73,25 @@ struct Tile {
   static constexpr int A4 = BM * KQ / NT;       // float4 of A per thread per stage
   static constexpr int W4 = BN * KQ / NT;
   static constexpr int STAGE = (BM + BN) * PITCH;
-  // bf16 modes: each image (one per split piece) is [BM + BN] rows of BKS = 32 bf16 (64 B, no
-  // padding), the row's four 16-B k-chunks XOR-swizzled by (row >> 2) & 3, so that a
-  // ds_read_b128 lane group (16 rows, one chunk) hits 16 distinct 4-bank groups and a
-  // ds_write_b64 group (2 rows x 64 B) 32 distinct banks: conflict-free both ways, and 20% less
-  // LDS than padded 80-B rows (64x64 split: 48 KB for two stages, three workgroups per CU).
+  // bf16 modes: each image (one per split piece) is [BM + BN] rows of BKS bf16 (64 or 128 B, no
+  // padding), the row's 16-B k-chunks XOR-swizzled by the row (bsw), so that a ds_read_b128
+  // lane group (16 rows, one chunk) hits 16 distinct 4-bank groups and a ds_write_b64 group
+  // (one or two rows of contiguous lanes) 32 distinct banks: conflict-free both ways, and 20%
+  // less LDS than padded rows (64x64 split: 48 KB for two stages, three workgroups per CU).
   static constexpr int STAGEB = (BM + BN) * BKS;   // bf16 elements per image
   static_assert(WM * WN * KS == NW && FN >= 1 && A4 >= 1 && W4 >= 1 && KKW >= 2, "tile shape");
   static_assert(NT % KQ == 0 && BM * KQ % NT == 0 && BN * KQ % NT == 0, "one k-quad per thread");
 };
 
-// Element offset of (row, k) in a bf16 image (BKS = 32): chunk k / 8 swizzled by the row.
+// Element offset of (row, k) in a bf16 image: 16-B chunk k / 8 XOR-swizzled by the row --
+// 64-B rows (BKS 32): by (row >> 2) & 3; 128-B rows (BKS 64): by (row >> 1) & 7.  The 16 rows
+// of a ds_read_b128 lane group ({0-3, 12-15, 20-27} etc. of lane & 31) then cover 16 distinct
+// (row-in-bank-line, chunk) pairs.
 template <class T>
 __device__ __forceinline__ int bsw(int row, int k) {
-  static_assert(T::BKS == 32, "swizzled bf16 images have 64-B rows");
-  return row * 32 + ((((k >> 3) ^ (row >> 2)) & 3) << 3) + (k & 7);
+  static_assert(T::BKS == 32 || T::BKS == 64, "swizzled bf16 images have 64- or 128-B rows");
+  if constexpr (T::BKS == 32) return row * 32 + ((((k >> 3) ^ (row >> 2)) & 3) << 3) + (k & 7);
+  else return row * 64 + ((((k >> 3) ^ (row >> 1)) & 7) << 3) + (k & 7);
 }
 
 // Stage registers.  WPL: the W operand comes from NPL bf16 planes in HBM (pre-split weights /
@@ -762,7 +767,7 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
 }
 
 template <int EPI, int PRO, class T, int PM, bool WPL>
-__global__ __launch_bounds__(T::NT) __attribute__((amdgpu_waves_per_eu(3)))
+__global__ __launch_bounds__(T::NT) __attribute__((amdgpu_waves_per_eu(T::WPE)))
 void gemm_kernel(GemmArgs args) {
   __shared__ StampLds sl;
   StampTick tk{0ull, 0ull};
@@ -857,7 +862,7 @@ int gemm_launch(int epi, int pro, int tile, GemmArgs& args, hipStream_t stream, 
   for (int i = 0; i < args.nprob; ++i) {
     const GemmProb& P = args.p[i];
     OP_REQUIRE((P.Wp != nullptr) == wpl, "gemm: W planes on some problems only");
-    OP_REQUIRE(!wpl || (pm != PM_F32 && td.bks == 32 && P.ldw % 4 == 0 &&
+    OP_REQUIRE(!wpl || (pm != PM_F32 && P.ldw % 4 == 0 &&
                         (P.W1 == nullptr) == (P.Wp1 == nullptr)),
                "gemm: W planes need a bf16 mode, 32-deep stages and planes for both K ranges");
   }

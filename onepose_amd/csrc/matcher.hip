@@ -1182,6 +1182,11 @@ struct Plan {
 // 14% faster alone, +0.3% frames/s) and 128 rows from 4096 (config 3/4 at B = 32).  The tile's
 // rows are the KV chunk length, so wider tiles also cut the KV partials the chunk sum reads
 // (config 3: 570 MB per launch at 64 rows).
+// (bf16 mode: a 64 x 128 / 64-deep tile -- 8 bf16 MFMAs per wave and barrier instead of 2 --
+// measured slower in the frame: MLP conv 1 67 vs 42 us per launch at config 5, its accumulators,
+// head accumulators and two fragment sets need 256+ VGPRs, one wave per SIMD)
+int mlp1_tile(int) { return kTileMLP1; }
+
 int qkv_tile_for(int n3, int B) {
   const int64_t t64 = (int64_t)ceil_div(n3, 64) * 6 * (B > kFusedFoldMaxBatch ? B : 1);
   return t64 >= kQkvWiderTiles ? TILE_128x128 : t64 >= kQkvWideTiles ? TILE_64x128 : kTileKV;
@@ -1778,7 +1783,7 @@ int attention_layer(const ApW& w, const Side* sd, int nside, int B, const Plan& 
       a.p[1].acc0 = xc->acc;
       a.p[1].acc0_bs = 0;
     }
-    if ((rc = gemm_launch(EPI_STATS, PRO_HEADZ, kTileMLP1, a, st, K_MLP1, pm)) != ONEPOSE_OK)
+    if ((rc = gemm_launch(EPI_STATS, PRO_HEADZ, mlp1_tile(pm), a, st, K_MLP1, pm)) != ONEPOSE_OK)
       return rc;
   }
   // 5. InstanceNorm statistics: finalized inside MLP conv 1 by each column block's last
@@ -2079,7 +2084,7 @@ int object_prepare_impl(const void* packed_weights, const float* desc3d, const f
     a.nprob = 1;
     a.p[0] = gemm_prob(cache, 256, w.w1a, 256, nullptr, cache + L.acc, 512, n3, 512, 256, 1);
     if (pm == PM_BF16) set_w_planes(a.p[0], w.w1a_p, kPlW1a);
-    if ((rc = gemm_launch(EPI_ACC, PRO_PLAIN, kTileMLP1, a, st, K_MLP1, pm)) != ONEPOSE_OK)
+    if ((rc = gemm_launch(EPI_ACC, PRO_PLAIN, mlp1_tile(pm), a, st, K_MLP1, pm)) != ONEPOSE_OK)
       return rc;
   }
   return ONEPOSE_OK;
