@@ -18,6 +18,7 @@
 // older stage.  One barrier per stage.
 #include "gemm.h"
 
+#include <cstdlib>
 #include <cstring>
 
 // Pins the pipeline's phase order (the compiler's own schedule measured within +-2%,
@@ -58,6 +59,8 @@ struct FragT<PM_SPLIT3, KKW, FN> {   // hi / mid / lo pieces
   bf16x8 w[3][KKW][FN];
 };
 
+
+constexpr int kScoreGroup = 8;   // N-tiles per column group of the score grid
 
 template <int BM_, int BN_, int KS_, int NW_, int BKS_, int WPE_ = 3>
 struct Tile {
@@ -117,7 +120,7 @@ struct Ctx {
 // (columns) that are never stored, and every reducing epilogue masks them when it stages the
 // tile, so they need no zeroing -- a select right behind each load would make the wave wait
 // for the load it just issued.
-template <int PRO, class T, bool WPL = false, int NPL = 1>
+template <int PRO, class T, bool WPL = false, int NPL = 1, bool DOW = true>
 __device__ __forceinline__ void load_stage(const Ctx& c, int m0, int n0, int k0,
                                            Stage<T, WPL, NPL>& s) {
   const int t = threadIdx.x;
@@ -136,7 +139,9 @@ __device__ __forceinline__ void load_stage(const Ctx& c, int m0, int n0, int k0,
     const int m = min(m0 + (t + T::NT * i) / T::KQ, c.M - 1);
     s.a[i] = *reinterpret_cast<const float4*>(A + (int64_t)m * lda + kk);
   }
-  if constexpr (WPL) {
+  if constexpr (!DOW) {
+    (void)ldw;
+  } else if constexpr (WPL) {
     const uint16_t* W = first ? c.wp0 : c.wp1;
     const int64_t pl = first ? c.wpl0 : c.wpl1;
 #pragma unroll
@@ -153,6 +158,33 @@ __device__ __forceinline__ void load_stage(const Ctx& c, int m0, int n0, int k0,
       const int o = min(n0 + (t + T::NT * i) / T::KQ, c.N - 1);
       s.w[i] = *reinterpret_cast<const float4*>(W + (int64_t)o * ldw + kk);
     }
+  }
+}
+
+// W planes of one stage (k0) -> the W rows of the bf16 images at `base` by global_load_lds:
+// 16 B per lane, one 1-KB piece = 16 rows of 64 B per wave-instruction (the wave-uniform LDS
+// base + 16 x lane: rows of 4 chunks, lane l -> row l / 4, slot l % 4), the slot holding the
+// chunk bsw's swizzle puts there (the source address is permuted, the destination is linear).
+template <class T, int NPL>
+__device__ __forceinline__ void dma_w_stage(const Ctx& c, int n0, int k0, float* base) {
+  static_assert(T::BKS == 32 && T::BN % 16 == 0 && (NPL * T::BN / 16) % T::NW == 0, "W pieces");
+  constexpr int PIECES = NPL * T::BN / 16, PPW = PIECES / T::NW;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const bool first = k0 < c.ksplit;
+  const uint16_t* W = first ? c.wp0 : c.wp1;
+  const int64_t pl = first ? c.wpl0 : c.wpl1;
+  const int ldw = first ? c.ldw0 : c.ldw1;
+  const int kk = first ? k0 : k0 - c.ksplit;
+#pragma unroll
+  for (int i = 0; i < PPW; ++i) {
+    const int p = wave + T::NW * i;
+    const int q = p / (T::BN / 16), rb = (p % (T::BN / 16)) * 16;
+    const int row = T::BM + rb + (lane >> 2);   // image row
+    const int chunk = ((lane & 3) ^ (row >> 2)) & 3;
+    const int o = min(n0 + rb + (lane >> 2), c.N - 1);
+    const uint16_t* src = W + q * pl + (int64_t)o * ldw + kk + chunk * 8;
+    char* dst = reinterpret_cast<char*>(base) + (int64_t)q * T::STAGEB * 2 + (T::BM + rb) * 64;
+    __builtin_amdgcn_global_load_lds(src, dst, 16, 0, 0);
   }
 }
 
@@ -187,7 +219,7 @@ __device__ __forceinline__ void store_quad_bf16(__bf16* b16, int off, float4 v) 
 
 // Stage registers -> LDS image at `base` ([BM + BN] rows: A then W), applying the prologue;
 // fp32 rows of PITCH floats, or swizzled bf16 images (Tile::STAGEB elements each).
-template <int PRO, class T, int PM, bool WPL = false, int NPL = 1>
+template <int PRO, class T, int PM, bool WPL = false, int NPL = 1, bool DOW = true>
 __device__ __forceinline__ void store_stage(float* base, Stage<T, WPL, NPL>& s) {
   const int t = threadIdx.x;
   const int kq = (t % T::KQ) * 4;
@@ -208,7 +240,7 @@ __device__ __forceinline__ void store_stage(float* base, Stage<T, WPL, NPL>& s) 
       store_quad_bf16<T, PM>(b16, bsw<T>(row, kq), v);
   }
 #pragma unroll
-  for (int i = 0; i < T::W4; ++i) {
+  for (int i = 0; i < (DOW ? T::W4 : 0); ++i) {
     const int row = T::BM + (t + T::NT * i) / T::KQ;
     if constexpr (WPL) {
       static_assert(PM != PM_F32 && NPL == (PM == PM_SPLIT3 ? 3 : 1), "W planes");
@@ -223,7 +255,7 @@ __device__ __forceinline__ void store_stage(float* base, Stage<T, WPL, NPL>& s) 
   }
 }
 
-template <int EPI, int PRO, class T, int PM, bool WPL>
+template <int EPI, int PRO, class T, int PM, bool WPL, bool DMA = false>
 __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, StampLds* sl) {
   constexpr int BM = T::BM, BN = T::BN, FN = T::FN, PITCH = T::PITCH;
   constexpr bool BF = PM != PM_F32;   // bf16 LDS images and MFMAs
@@ -244,8 +276,17 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
   const int per_sample = mtiles * ntiles;
   const int b = bid / per_sample;
   const int r = bid - b * per_sample;
-  const int mt = r / ntiles;
-  const int nt = r - mt * ntiles;
+  int mt = r / ntiles;
+  int nt = r - mt * ntiles;
+  if (EPI == EPI_SCORE && ntiles % kScoreGroup == 0) {
+    // score grid in column groups of kScoreGroup N-tiles (D3 rows), all M-tiles of a group
+    // consecutive: an XCD's contiguous run of logical tiles then covers one group, so each XCD
+    // reads all of D2 and its own slice of D3 once, instead of a D2 slice and all of D3 (the
+    // D3 re-fetch by every XCD, 4 MB x 8 at config 2).  Per-tile results are unchanged.
+    const int g = r / (mtiles * kScoreGroup), rr = r - g * mtiles * kScoreGroup;
+    mt = rr / kScoreGroup;
+    nt = g * kScoreGroup + (rr - mt * kScoreGroup);
+  }
   const int m0 = mt * BM, n0 = nt * BN;
   Ctx c;
   c.a0 = F(A0) + b * F(a0_bs);
@@ -436,6 +477,54 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
 #pragma unroll
       for (int i = 0; i < 16; ++i) acc[j][i] = a0p[j * 1024 + i * 64];
   }
+  if constexpr (DMA) {
+    // W planes by global_load_lds, A through registers (its rounding / split and prologue in
+    // VALU), one stage ahead in two LDS buffers; one barrier per stage.  The register-light loop
+    // (no fragment or second register stage) leaves room for three workgroups per CU, whose
+    // overlap hides the loads.  Same images, fragments and MFMA order as the register-staged
+    // loop, so the same bits.
+    static_assert(WPL && PM != PM_F32, "DMA loop: bf16 images, W planes");
+    Stage<T, WPL, NPL> sa;
+    load_stage<PRO, T, WPL, NPL, false>(c, m0, n0, kt0 * T::BKS, sa);
+    dma_w_stage<T, NPL>(c, n0, kt0 * T::BKS, lds);
+    tk = stamp_start(args.stamp, sl);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    store_stage<PRO, T, PM, WPL, NPL, false>(lds, sa);
+    __syncthreads();
+    int fold_par = -1, hpar = 0;
+    for (int kt = kt0; kt < nk; ++kt) {
+      float* cur = lds + (kt & 1) * STAGE;
+      float* nxt = lds + ((kt + 1) & 1) * STAGE;
+      if (PRO == PRO_HEADZ && fold_par >= 0) {   // the last head's Z rows, after the barrier
+        fold(fold_par);
+        fold_par = -1;
+      }
+      const bool more = kt + 1 < nk;
+      if (more) {
+        load_stage<PRO, T, WPL, NPL, false>(c, m0, n0, (kt + 1) * T::BKS, sa);
+        dma_w_stage<T, NPL>(c, n0, (kt + 1) * T::BKS, nxt);
+      }
+      read_frag(cur, f0);
+      const bool head = PRO == PRO_HEADZ && kt >= xs;
+      if (head) {
+        zdot(cur, kt);
+#pragma unroll
+        for (int kk = 0; kk < KKW; ++kk) mfma_kk(acc_h, f0, kk);
+        if ((kt - xs) % HS == HS - 1) {   // the head's last stage: its Z rows
+          zfinal(hpar);
+          fold_par = hpar;
+          hpar ^= 1;
+        }
+      } else {
+#pragma unroll
+        for (int kk = 0; kk < KKW; ++kk) mfma_kk(acc, f0, kk);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (more) store_stage<PRO, T, PM, WPL, NPL, false>(nxt, sa);
+      __syncthreads();
+    }
+    if (PRO == PRO_HEADZ && fold_par >= 0) fold(fold_par);
+  } else {
   load_stage<PRO, T, WPL, NPL>(c, m0, n0, kt0 * T::BKS, s0);
   load_stage<PRO, T, WPL, NPL>(c, m0, n0, (kt0 + 1) * T::BKS, s1);
   tk = stamp_start(args.stamp, sl);
@@ -490,6 +579,7 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
       }
     }
   }
+  }   // (register-staged loop)
   __syncthreads();   // every wave done with the LDS stages before they are reused below
   // profiling ticket after the K loop: no in-loop wait (vmcnt counts in order) includes the
   // atomic; its value is needed only at the end
@@ -766,12 +856,12 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
 #undef F
 }
 
-template <int EPI, int PRO, class T, int PM, bool WPL>
+template <int EPI, int PRO, class T, int PM, bool WPL, bool DMA>
 __global__ __launch_bounds__(T::NT) __attribute__((amdgpu_waves_per_eu(T::WPE)))
 void gemm_kernel(GemmArgs args) {
   __shared__ StampLds sl;
   StampTick tk{0ull, 0ull};
-  gemm_body<EPI, PRO, T, PM, WPL>(args, tk, &sl);
+  gemm_body<EPI, PRO, T, PM, WPL, DMA>(args, tk, &sl);
   stamp_end(args.stamp, tk, &sl);
 }
 
@@ -783,9 +873,10 @@ using T128x128 = Tile<128, 128, 1, 4, 32>;
 using T128x64W8 = Tile<128, 64, 1, 8, 32>;
 
 
-template <int EPI, int PRO, class T, int PM, bool WPL = false>
+template <int EPI, int PRO, class T, int PM, bool WPL = false, bool DMA = false>
 void launch_one(GemmArgs& args, int grid, hipStream_t stream) {
-  hipLaunchKernelGGL((gemm_kernel<EPI, PRO, T, PM, WPL>), dim3(grid), dim3(T::NT), 0, stream, args);
+  hipLaunchKernelGGL((gemm_kernel<EPI, PRO, T, PM, WPL, DMA>), dim3(grid), dim3(T::NT), 0, stream,
+                     args);
 }
 
 struct TileDims {
@@ -867,14 +958,25 @@ int gemm_launch(int epi, int pro, int tile, GemmArgs& args, hipStream_t stream, 
                "gemm: W planes need a bf16 mode, 32-deep stages and planes for both K ranges");
   }
   args.stamp = nullptr;
-#define CASE(E, PR, TI, T, PMV, WP)                                     \
-  if (epi == E && pro == PR && tile == TI && pm == PMV && wpl == WP) { \
-    prof_pre(kind, stream);                                             \
-    args.stamp = prof_stamp_slot(kind);                                 \
-    launch_one<E, PR, T, PMV, WP>(args, grid, stream);                  \
-    prof_post(kind, stream);                                            \
-    OP_LAUNCHED();                                                      \
-    return ONEPOSE_OK;                                                  \
+  // split mode: W planes stream into LDS by global_load_lds (the DMA loop: config 2 at
+  // 1645-1655 frames/s against 1538 for the register-staged split loop, which needs 160+ VGPRs
+  // and spills).  bf16 mode: the register-staged loop (config 5: MLP conv 1 41 vs 53 us in the
+  // frame; its two MFMAs per wave and stage leave a latency-bound DMA loop nothing to hide
+  // behind).
+  const bool dma = pm == PM_SPLIT3;
+#define CASE(E, PR, TI, T, PMV, WP)                                      \
+  if (epi == E && pro == PR && tile == TI && pm == PMV && wpl == WP) {  \
+    prof_pre(kind, stream);                                              \
+    args.stamp = prof_stamp_slot(kind);                                  \
+    if constexpr (WP) {                                                  \
+      if (dma) launch_one<E, PR, T, PMV, WP, true>(args, grid, stream);  \
+      else launch_one<E, PR, T, PMV, WP, false>(args, grid, stream);     \
+    } else {                                                             \
+      launch_one<E, PR, T, PMV, WP, false>(args, grid, stream);          \
+    }                                                                    \
+    prof_post(kind, stream);                                             \
+    OP_LAUNCHED();                                                       \
+    return ONEPOSE_OK;                                                   \
   }
   CASE(EPI_QKV, PRO_PLAIN, TILE_32x128, T32x128, PM_F32, false)
   CASE(EPI_QKV, PRO_PLAIN, TILE_64x128, T64x128, PM_F32, false)
@@ -886,18 +988,17 @@ int gemm_launch(int epi, int pro, int tile, GemmArgs& args, hipStream_t stream, 
   CASE(EPI_SCORE, PRO_PLAIN, TILE_128x64W8, T128x64W8, PM_F32, false)
   CASE(EPI_BIAS, PRO_PLAIN, TILE_64x64, T64x64, PM_F32, false)
   CASE(EPI_ACC, PRO_PLAIN, TILE_64x64, T64x64, PM_F32, false)
-  // attention-layer GEMMs in the bf16 mode: W from the packed bf16 plane (rounded on the host,
-  // Mf by the KV fold), A rounded as the stage is stored
+  // attention-layer GEMMs in the bf16 modes: W from the packed bf16 planes (weights rounded /
+  // split on the host, Mf by the KV fold), A rounded / split as the stage is stored
   CASE(EPI_ACC, PRO_PLAIN, TILE_64x64, T64x64, PM_BF16, true)
-  CASE(EPI_ACC, PRO_PLAIN, TILE_64x64, T64x64, PM_SPLIT3, false)
-  // bf16-MFMA attention layers (precision mode ONEPOSE_PREC_BF16_ATTN)
+  CASE(EPI_ACC, PRO_PLAIN, TILE_64x64, T64x64, PM_SPLIT3, true)
   CASE(EPI_QKV, PRO_PLAIN, TILE_32x128, T32x128, PM_BF16, true)
   CASE(EPI_STATS, PRO_HEADZ, TILE_64x64, T64x64, PM_BF16, true)
   CASE(EPI_RESID, PRO_NORM_RELU, TILE_64x64, T64x64, PM_BF16, true)
-  // fp32 by exact 3-way bf16 split (precision mode ONEPOSE_PREC_FP32_SPLIT)
-  CASE(EPI_QKV, PRO_PLAIN, TILE_32x128, T32x128, PM_SPLIT3, false)
-  CASE(EPI_STATS, PRO_HEADZ, TILE_64x64, T64x64, PM_SPLIT3, false)
-  CASE(EPI_RESID, PRO_NORM_RELU, TILE_64x64, T64x64, PM_SPLIT3, false)
+  CASE(EPI_QKV, PRO_PLAIN, TILE_32x128, T32x128, PM_SPLIT3, true)
+  CASE(EPI_STATS, PRO_HEADZ, TILE_64x64, T64x64, PM_SPLIT3, true)
+  CASE(EPI_RESID, PRO_NORM_RELU, TILE_64x64, T64x64, PM_SPLIT3, true)
+  // final projection and score GEMM in the split mode (activations as W: VALU split)
   CASE(EPI_SCORE, PRO_PLAIN, TILE_64x64, T64x64, PM_SPLIT3, false)
   CASE(EPI_BIAS, PRO_PLAIN, TILE_64x64, T64x64, PM_SPLIT3, false)
 #undef CASE

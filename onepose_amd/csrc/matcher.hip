@@ -1681,7 +1681,7 @@ int attention_layer(const ApW& w, const Side* sd, int nside, int B, const Plan& 
       g.kvpart = s.kvpart;
       g.kspart = s.kspart;
       g.y_bs = (int64_t)s.n * 256;
-      if (pm == PM_BF16) set_w_planes(g, w.wqkv_p, kPlWqkv);
+      if (pm != PM_F32) set_w_planes(g, w.wqkv_p, kPlWqkv);
     }
     return gemm_launch(EPI_QKV, PRO_PLAIN, tl.qkv[i0], a, st, K_QKV_GEMM, pm);
   });
@@ -1695,10 +1695,8 @@ int attention_layer(const ApW& w, const Side* sd, int nside, int B, const Plan& 
   for (int i = 0; i < nsrc; ++i)
     OP_REQUIRE(reader[i] >= 0, "attention layer: source slot %d has no reader", i);
   auto mf_of = [&](int side) { return p.mf + (size_t)side * B * kMfFloats; };
-  // bf16 mode: W operands as bf16 planes (gemm.h GemmProb::Wp; in the split mode three b64 plane
-  // loads per k-quad measured slower than one fp32 b128 load + the VALU split: 1517-1538 vs
-  // 1599 frames/s)
-  const bool planes = pm == PM_BF16;
+  // bf16 modes: W operands as bf16 planes (gemm.h GemmProb::Wp)
+  const bool planes = pm != PM_F32;
   auto chunks = [&](int i) { return ceil_div(sd[i].n, gemm_tile_rows(tl.qkv[i])); };
   rc = groups(nsrc, [&](int a, int b) { return tl.fused_fold[a] == tl.fused_fold[b]; },
               [&](int i0, int i1) -> int {
@@ -1818,7 +1816,7 @@ int attention_layer(const ApW& w, const Side* sd, int nside, int B, const Plan& 
       g.pro_mean = p.mean + (size_t)i * B * 512;
       g.pro_rstd = p.rstd + (size_t)i * B * 512;
       g.pro_bs = 512;
-      if (pm == PM_BF16) set_w_planes(g, w.w2_p, kPlW2);
+      if (pm != PM_F32) set_w_planes(g, w.w2_p, kPlW2);
     }
     return gemm_launch(EPI_RESID, PRO_NORM_RELU, tl.mlp2[i0], a, st, K_MLP2, pm);
   });
@@ -2063,14 +2061,14 @@ int object_prepare_impl(const void* packed_weights, const float* desc3d, const f
     a.p[0].vdiv = (float)n3;
     a.p[0].kvpart = p.kvpart3;
     a.p[0].kspart = p.kspart3;
-    if (pm == PM_BF16) set_w_planes(a.p[0], w.wqkv_p, kPlWqkv);
+    if (pm != PM_F32) set_w_planes(a.p[0], w.wqkv_p, kPlWqkv);
     if ((rc = gemm_launch(EPI_QKV, PRO_PLAIN, tl.qkv[0], a, st, K_QKV_GEMM, pm)) != ONEPOSE_OK)
       return rc;
   }
   {  // sum phi(k) into the cache, and the 2D side's Mf = C KV_3D
     KvFoldArgs ka;
     ka.ct = w.ct;
-    ka.planes = pm == PM_BF16 ? 1 : 0;
+    ka.planes = pm != PM_F32 ? 1 : 0;
     ka.p[0] = {p.kvpart3, p.kspart3, ceil_div(n3, gemm_tile_rows(tl.qkv[0]))};
     ka.mf[0] = cache + L.mf;
     ka.mf[1] = nullptr;
@@ -2083,7 +2081,7 @@ int object_prepare_impl(const void* packed_weights, const float* desc3d, const f
     GemmArgs a;
     a.nprob = 1;
     a.p[0] = gemm_prob(cache, 256, w.w1a, 256, nullptr, cache + L.acc, 512, n3, 512, 256, 1);
-    if (pm == PM_BF16) set_w_planes(a.p[0], w.w1a_p, kPlW1a);
+    if (pm != PM_F32) set_w_planes(a.p[0], w.w1a_p, kPlW1a);
     if ((rc = gemm_launch(EPI_ACC, PRO_PLAIN, mlp1_tile(pm), a, st, K_MLP1, pm)) != ONEPOSE_OK)
       return rc;
   }

@@ -442,6 +442,53 @@ float time_f32(float* A, float* W, float* Y, float* bias, int M, int N, int K, i
   return ms * 1e3f / iters;
 }
 
+// the production gemm.hip kernels in the split mode with W planes (DMA loop), by epilogue
+template <int EPI, int PRO, int PM, bool DMA>
+float time_prod(float* A, const __bf16* Wp, int64_t wplane, float* bias, float* Y, int M, int N,
+                int K, int iters, float* stats, unsigned* cnt, float* mean, float* rstd,
+                float* ksum) {
+  GemmArgs a;
+  memset(&a, 0, sizeof(a));
+  a.nprob = 1;
+  GemmProb& p = a.p[0];
+  p = gemm_prob(A, K, nullptr, K, bias, Y, N, M, N, K, 1);
+  p.Wp = reinterpret_cast<const uint16_t*>(Wp);
+  p.wpl = wplane;
+  p.stats = stats;
+  p.st_cnt = cnt;
+  p.st_mean = mean;
+  p.st_rstd = rstd;
+  if (PRO == PRO_HEADZ) {   // K = [x (256) | phi(q) (256)], the second range from the same A
+    p.ksplit = 256;
+    p.A1 = A + 256;
+    p.lda1 = K;
+    p.ksum = ksum;
+    p.ns = 4096.f;
+  }
+  p.mtiles = (M + 63) / 64;
+  p.ntiles = (N + 63) / 64;
+  p.tiles = p.mtiles * p.ntiles;
+  hipEvent_t e0, e1;
+  hipEventCreate(&e0);
+  hipEventCreate(&e1);
+  for (int w = 0; w < 3; ++w) {
+    if (cnt) hipMemset(cnt, 0, 4096);
+    launch_one<EPI, PRO, T64x64, PM, true, DMA>(a, p.tiles, nullptr);
+  }
+  float tot = 0.f;
+  for (int it = 0; it < iters; ++it) {
+    if (cnt) hipMemsetAsync(cnt, 0, 4096);
+    hipEventRecord(e0);
+    launch_one<EPI, PRO, T64x64, PM, true, DMA>(a, p.tiles, nullptr);
+    hipEventRecord(e1);
+    hipEventSynchronize(e1);
+    float ms;
+    hipEventElapsedTime(&ms, e0, e1);
+    tot += ms;
+  }
+  return tot * 1e3f / iters;
+}
+
 int main(int argc, char** argv) {
   const int N = 512, K = 512;
   const int Ms[] = {5120, 10240, 16384 + 1024, 32 * 17408 / 8};
@@ -519,6 +566,27 @@ int main(int argc, char** argv) {
     d12 = 0;
     for (size_t i = 0; i < y1.size(); ++i) d12 = fmax(d12, fabs(y1[i] - y2[i]));
     printf("v2: max |fp32 - split3(64x64)| %.3g\n", d12);
+  }
+  {
+    float *stats, *mean, *rstd, *ksum;
+    unsigned* cnt;
+    hipMalloc(&stats, 8 << 20);
+    hipMalloc(&mean, 4096);
+    hipMalloc(&rstd, 4096);
+    hipMalloc(&ksum, 4096);
+    hipMalloc(&cnt, 4096);
+    std::vector<float> ks(1024, 30.f);
+    hipMemcpy(ksum, ks.data(), 4096, hipMemcpyHostToDevice);
+    const int M = 5120, it = 30;
+    printf("production kernels, M 5120 N 512 K 512, per-launch events (serial):\n");
+    printf("  fp32 BIAS              %7.2f us\n", time_f32(A, W, Y, b, M, N, K, it));
+    printf("  split DMA BIAS         %7.2f us\n", time_prod<EPI_BIAS, PRO_PLAIN, PM_SPLIT3, true>(A, Wp, wpl, b, Y, M, N, K, it, stats, nullptr, mean, rstd, ksum));
+    printf("  split DMA STATS        %7.2f us\n", time_prod<EPI_STATS, PRO_PLAIN, PM_SPLIT3, true>(A, Wp, wpl, b, Y, M, N, K, it, stats, nullptr, mean, rstd, ksum));
+    printf("  split DMA STATS+fin    %7.2f us\n", time_prod<EPI_STATS, PRO_PLAIN, PM_SPLIT3, true>(A, Wp, wpl, b, Y, M, N, K, it, stats, cnt, mean, rstd, ksum));
+    printf("  split DMA STATS+HEADZ  %7.2f us\n", time_prod<EPI_STATS, PRO_HEADZ, PM_SPLIT3, true>(A, Wp, wpl, b, Y, M, N, K, it, stats, cnt, mean, rstd, ksum));
+    printf("  split reg STATS+HEADZ  %7.2f us\n", time_prod<EPI_STATS, PRO_HEADZ, PM_SPLIT3, false>(A, Wp, wpl, b, Y, M, N, K, it, stats, cnt, mean, rstd, ksum));
+    printf("  bf16 DMA STATS+HEADZ   %7.2f us\n", time_prod<EPI_STATS, PRO_HEADZ, PM_BF16, true>(A, Wp, wpl, b, Y, M, N, K, it, stats, cnt, mean, rstd, ksum));
+    printf("  bf16 reg STATS+HEADZ   %7.2f us\n", time_prod<EPI_STATS, PRO_HEADZ, PM_BF16, false>(A, Wp, wpl, b, Y, M, N, K, it, stats, cnt, mean, rstd, ksum));
   }
   for (int M : Ms) {
     const double gf = 2.0 * M * N * K * 1e-9;
