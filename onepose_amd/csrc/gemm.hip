@@ -963,7 +963,7 @@ int gemm_launch(int epi, int pro, int tile, GemmArgs& args, hipStream_t stream, 
   // and spills).  bf16 mode: the register-staged loop (config 5: MLP conv 1 41 vs 53 us in the
   // frame; its two MFMAs per wave and stage leave a latency-bound DMA loop nothing to hide
   // behind).
-  const bool dma = pm == PM_SPLIT3;
+  const bool dma = pm == PM_SPLIT3 || (pm == PM_BF16 && tile == TILE_64x128);
 #define CASE(E, PR, TI, T, PMV, WP)                                      \
   if (epi == E && pro == PR && tile == TI && pm == PMV && wpl == WP) {  \
     prof_pre(kind, stream);                                              \
@@ -995,6 +995,10 @@ int gemm_launch(int epi, int pro, int tile, GemmArgs& args, hipStream_t stream, 
   CASE(EPI_QKV, PRO_PLAIN, TILE_32x128, T32x128, PM_BF16, true)
   CASE(EPI_STATS, PRO_HEADZ, TILE_64x64, T64x64, PM_BF16, true)
   CASE(EPI_RESID, PRO_NORM_RELU, TILE_64x64, T64x64, PM_BF16, true)
+  CASE(EPI_QKV, PRO_PLAIN, TILE_64x128, T64x128, PM_BF16, true)
+  CASE(EPI_STATS, PRO_HEADZ, TILE_64x128, T64x128, PM_BF16, true)
+  CASE(EPI_RESID, PRO_NORM_RELU, TILE_64x128, T64x128, PM_BF16, true)
+  CASE(EPI_ACC, PRO_PLAIN, TILE_64x128, T64x128, PM_BF16, true)
   CASE(EPI_QKV, PRO_PLAIN, TILE_32x128, T32x128, PM_SPLIT3, true)
   CASE(EPI_STATS, PRO_HEADZ, TILE_64x64, T64x64, PM_SPLIT3, true)
   CASE(EPI_RESID, PRO_NORM_RELU, TILE_64x64, T64x64, PM_SPLIT3, true)

@@ -1185,7 +1185,11 @@ struct Plan {
 // (bf16 mode: a 64 x 128 / 64-deep tile -- 8 bf16 MFMAs per wave and barrier instead of 2 --
 // measured slower in the frame: MLP conv 1 67 vs 42 us per launch at config 5, its accumulators,
 // head accumulators and two fragment sets need 256+ VGPRs, one wave per SIMD)
-int mlp1_tile(int) { return kTileMLP1; }
+// bf16 mode: QKV and MLP conv 1 on 64 x 128 tiles (4 bf16 MFMAs per wave and stage, W planes by
+// global_load_lds; config 5 QKV 0.204 -> 0.181 ms per step, config 2 bf16 1801 -> 2422 frames/s
+// with the W planes); MLP conv 2 keeps 64 x 64
+constexpr int kTileBf16 = TILE_64x128;
+int mlp1_tile(int pm) { return pm == PM_BF16 ? kTileBf16 : kTileMLP1; }
 
 int qkv_tile_for(int n3, int B) {
   const int64_t t64 = (int64_t)ceil_div(n3, 64) * 6 * (B > kFusedFoldMaxBatch ? B : 1);
@@ -1562,13 +1566,15 @@ int mlp2_tile_for(int64_t t64, int pm) {
   // fp32: the 64x32 K-split tile doubles the workgroup count where 64x64 tiles would leave
   // CUs idle (config 2: 320 -> 640 tiles, 23.2 -> 19.7 us); with >= 4 tiles per CU anyway
   // (batched configs) 64x64 moves less data per FLOP (config 3: 9.5 vs 12.3 ms per step)
+  // (bf16: the 64 x 128 DMA tile measured slower for MLP conv 2 at config 5, 0.211 vs 0.158 ms
+  // per step: N = 256 gives it half the workgroups)
   return pm == PM_F32 && t64 < kMlp2WideTiles ? kTileMLP2F32 : kTileMLP2;
 }
 
 // Every side the same choices, from the launch as a whole (layers 4-11, sharded frames).
 LayerTiles layer_tiles(int qkv_n3, const Side* sd, int nside, int B, int pm, bool sharded) {
   LayerTiles t;
-  const int q = pm == PM_F32 ? qkv_tile_for(qkv_n3, B) : kTileKV;
+  const int q = pm == PM_F32 ? qkv_tile_for(qkv_n3, B) : pm == PM_BF16 ? kTileBf16 : kTileKV;
   // kv_fold re-reads the whole 128 KB C_h panel per workgroup (64 of them per side and
   // sample): one launch instead of two pays at small batches; at B = 32 the separate MFMA
   // m_fold (16 KB of C per workgroup) is cheaper (config 3: 1.68 vs 2.02 ms per step).
@@ -1592,8 +1598,8 @@ LayerTiles layer_tiles(int qkv_n3, const Side* sd, int nside, int B, int pm, boo
 // take the choice over both sides there.
 LayerTiles side_tiles(int n1, int n3, int B, int pm, bool cross) {
   LayerTiles t;
-  t.qkv[0] = pm == PM_F32 ? qkv_tile_for(n1, B) : kTileKV;
-  t.qkv[1] = pm == PM_F32 ? qkv_tile_for(n3, 1) : kTileKV;
+  t.qkv[0] = pm == PM_F32 ? qkv_tile_for(n1, B) : pm == PM_BF16 ? kTileBf16 : kTileKV;
+  t.qkv[1] = pm == PM_F32 ? qkv_tile_for(n3, 1) : pm == PM_BF16 ? kTileBf16 : kTileKV;
   t.fused_fold[0] = B <= kFusedFoldMaxBatch;
   t.fused_fold[1] = true;
   const int64_t t2 = (int64_t)ceil_div(n1, 64) * 4 * B, t3 = (int64_t)ceil_div(n3, 64) * 4;
