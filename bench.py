@@ -106,12 +106,13 @@ def kernel_work(kind, B, n1, n3, L, cached=False):
     return table.get(kind)
 
 
-def pmc_traffic(kernel):
+def pmc_traffic(kernel, subdir="pmc"):
     """HBM bytes per launch of `kernel` from the newest committed PMC summary
-    (profiles/r*/pmc/pmc_traffic.json, written by tools/gpu_pmc.sh + tools/pmc_summary.py:
-    FETCH_SIZE x2 (gfx950) + WRITE_SIZE, separate rocprofv3 passes).  None if absent."""
+    (profiles/r*/<subdir>/pmc_traffic.json, written by tools/gpu_r03_b.sh + tools/pmc_summary.py:
+    FETCH_SIZE x2 (gfx950) + WRITE_SIZE, separate rocprofv3 passes; "pmc" = config 2 fp32,
+    "pmc_c5" = config 5 bf16).  None if absent."""
     import glob
-    files = sorted(glob.glob(os.path.join(REPO, "profiles", "r*", "pmc", "pmc_traffic.json")))
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "r*", subdir, "pmc_traffic.json")))
     if not files:
         return None, None
     d = json.load(open(files[-1]))
@@ -456,8 +457,11 @@ def main():
     achieved = work / (dom_ms * 1e-3) / 1e12
     bf_dom = args.precision == "bf16" and dominant in ("qkv_gemm", "mlp1_gemm", "mlp2_gemm")
     peak = BF16_MFMA_PEAK_TFLOPS if bf_dom else FP32_MFMA_PEAK_TFLOPS
-    traffic, traffic_src = pmc_traffic(dominant) \
-        if (B, n1, n3, L) == (1, 1024, 4096, 8) and args.precision == "fp32" else (None, None)
+    traffic, traffic_src = None, None
+    if (B, n1, n3, L) == (1, 1024, 4096, 8) and args.precision == "fp32":
+        traffic, traffic_src = pmc_traffic(dominant)
+    elif (B, n1, n3, L) == (1, 2048, 8192, 8) and args.precision == "bf16":
+        traffic, traffic_src = pmc_traffic(dominant + ("_bf16" if bf_dom else ""), "pmc_c5")
     roof = {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak,
             "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
             "traffic": traffic, "traffic_unit": "HBM bytes per launch (PMC)",
@@ -506,6 +510,8 @@ def main():
                 (2048, 8192): "config 5"}.get((n1, n3), "custom")
     if args.precision == "bf16":
         cfg_name += " (bf16-MFMA attention)"
+    elif args.precision == "fp32_split":
+        cfg_name += " (fp32 attention as 3-piece bf16 split)"
     if rank == 0:
         sched = (f"matchers of consecutive steps on {args.match_streams} concurrent stream(s), "
                  "each step's pose stage on its own stream overlapping the next matchers"
@@ -518,7 +524,10 @@ def main():
             "steps": args.steps, "warmup": args.warmup, "settle_steps": settle,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None,
-            "dtype": "fp32" if args.precision == "fp32" else "bf16 attention GEMMs, fp32 rest",
+            "dtype": {"fp32": "fp32",
+                      "fp32_split": "fp32 (attention GEMMs as the exact 3-piece bf16 split on "
+                                    "bf16 MFMA, fp32 accumulation)",
+                      "bf16": "bf16 attention GEMMs, fp32 rest"}[args.precision],
             "data": "synthetic",
             "config": {"workload": (f"{cfg_name}: {n1} kpts x {n3} 3D pts, L={L}, {B} frame(s) per "
                                     f"GPU per step; "

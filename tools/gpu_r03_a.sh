@@ -17,3 +17,14 @@ mkdir -p $O/prof
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- \
   python3 bench.py --steps 100 --warmup 5 --no-cpu-baseline > $O/prof/bench.json 2> $O/prof/bench.err || exit $?
 echo prof ok
+mkdir -p $O/configs
+cfg() {
+  local name=$1; shift
+  timeout -k 10 300 python bench.py "$@" > $O/configs/$name.json 2> $O/configs/$name.err || return $?
+  python -c "import json; d=json.loads(open('$O/configs/$name.json').read().strip().splitlines()[-1]); print('$name', d['value'], d['ms_per_step'], d['roofline']['kernel'], d['roofline']['frac'], d['frame_roofline']['frac'], d['frame_roofline']['executed']['frac'])"
+}
+cfg config3 --n3 16384 --batch 32 --steps 10 --warmup 2 --no-cpu-baseline || exit $?
+cfg config4 --n3 2500 --batch 32 --steps 10 --warmup 2 --no-cpu-baseline || exit $?
+cfg config5_bf16 --n1 2048 --n3 8192 --precision bf16 --steps 100 --warmup 3 --no-cpu-baseline || exit $?
+cfg config2_split --precision fp32_split --steps 300 --warmup 5 --no-cpu-baseline || exit $?
+cfg config2_bf16 --precision bf16 --steps 300 --warmup 5 --no-cpu-baseline || exit $?
