@@ -24,6 +24,11 @@
 // Pins the pipeline's phase order (the compiler's own schedule measured within +-2%,
 // DESIGN.md §3d).
 #define ONEPOSE_SCHED_BARRIER() __builtin_amdgcn_sched_barrier(0)
+// Measurement hook: tools/phase_probe.hip defines it to stamp each workgroup's prologue / loop /
+// epilogue boundaries (s_memtime); empty in the library.
+#ifndef ONEPOSE_GEMM_PHASE
+#define ONEPOSE_GEMM_PHASE(i)
+#endif
 
 namespace onepose {
 
@@ -188,6 +193,13 @@ __device__ __forceinline__ void dma_w_stage(const Ctx& c, int n0, int k0, float*
   }
 }
 
+// One 16-B-per-lane global_load_lds (1 KB per wave at the wave-uniform LDS base `dst` + 16 x lane).
+// (A __device__ function: the builtin cannot appear in the loop's lambdas, which the host pass
+// also compiles.)
+__device__ __forceinline__ void dma16(const void* src, void* dst) {
+  __builtin_amdgcn_global_load_lds(src, dst, 16, 0, 0);
+}
+
 // fp32 -> the bf16 image(s) of one k-quad at `b16` (element offset `off`, images STAGEB apart):
 // PM_BF16 rounded to nearest even; PM_SPLIT3 the exact split hi + mid + lo.
 template <class T, int PM>
@@ -261,7 +273,10 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
   constexpr bool BF = PM != PM_F32;   // bf16 LDS images and MFMAs
   constexpr int NPL = PM == PM_SPLIT3 ? 3 : 1;   // bf16 images per operand
   constexpr int STAGE = PM == PM_F32 ? T::STAGE : NPL * T::STAGEB / 2;   // floats
-  constexpr int LDSF = 2 * STAGE > BM * (BN + 1) ? 2 * STAGE : BM * (BN + 1);
+  // epilogue staging tile [BM][TP]: rows of BN + 4 (16-B aligned, read back as float4 rows by
+  // the row-store pass), or BN + 1 where columns are read across rows (score, QKV)
+  constexpr int TP = (EPI == EPI_SCORE || EPI == EPI_QKV) ? BN + 1 : BN + 4;
+  constexpr int LDSF = 2 * STAGE > BM * TP ? 2 * STAGE : BM * TP;
   __shared__ __attribute__((aligned(16))) float lds[LDSF];
   __shared__ float zrow[2 * BM];
   __shared__ float part[(EPI == EPI_STATS) ? T::NT * 2 : 1];
@@ -478,58 +493,116 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
       for (int i = 0; i < 16; ++i) acc[j][i] = a0p[j * 1024 + i * 64];
   }
   if constexpr (DMA) {
-    // W planes by global_load_lds, A through registers (its rounding / split and prologue in
-    // VALU), one stage ahead in two LDS buffers; one barrier per stage.  The register-light loop
-    // (no fragment or second register stage) leaves room for three workgroups per CU, whose
-    // overlap hides the loads.  Same images, fragments and MFMA order as the register-staged
-    // loop, so the same bits.
+    // The lean DMA loop.  A bf16 stage is only 4-12 MFMAs per wave, so the loop is bound by the
+    // instructions around them and by load latency, not by the matrix pipe:
+    //  - row / piece offsets are computed once (32-bit, added to a wave-uniform base per stage);
+    //  - the x range and each phi(q) head run in loops of their own with the accumulator set
+    //    fixed (no accumulator copies or per-stage branches on the head state);
+    //  - the stage's LDS reads come before the next stages' loads in program order, and the
+    //    barrier is a raw s_barrier after lgkmcnt(0): __syncthreads()' fence would drain every
+    //    load and DMA in flight (vmcnt(0)) and undo the lookahead.
+    // A and W one stage ahead in two LDS buffers.  (Two stages ahead -- two A register sets,
+    // three LDS buffers -- measured no faster: the stage is bound by its own instruction
+    // latencies at 1-3 waves per SIMD)  Same images, fragments and MFMA
+    // order as the register-staged loop, so the same bits.
     static_assert(WPL && PM != PM_F32, "DMA loop: bf16 images, W planes");
+    // a W piece = one 1-KB global_load_lds: RP rows of BKS bf16 (CPR 16-B chunks per row)
+    constexpr int CPR = T::BKS / 8, RP = 64 / CPR;
+    constexpr int PIECES = NPL * T::BN / RP, PPW = PIECES / T::NW;
+    static_assert((T::BKS == 32 || T::BKS == 64) && T::BN % RP == 0 && PIECES % T::NW == 0,
+                  "W pieces");
+    const int kq = (t % T::KQ) * 4;
+    unsigned aoff0[T::A4], aoff1[T::A4];   // bytes from the stage's base, per K range
+#pragma unroll
+    for (int i = 0; i < T::A4; ++i) {
+      const int m = min(m0 + (t + T::NT * i) / T::KQ, c.M - 1);
+      aoff0[i] = (unsigned)((m * c.lda0 + kq) * 4);
+      aoff1[i] = (unsigned)((m * c.lda1 + kq) * 4);
+    }
+    unsigned woff0[PPW], woff1[PPW];
+    int wdst[PPW];
+#pragma unroll
+    for (int i = 0; i < PPW; ++i) {
+      const int p = wave + T::NW * i;
+      const int q = p / (T::BN / RP), rb = (p % (T::BN / RP)) * RP;
+      const int row = T::BM + rb + lane / CPR;   // image row; LDS slot lane % CPR holds the
+      const int chunk = bsw<T>(row, (lane % CPR) * 8) - row * T::BKS;   // chunk bsw puts there
+      const int o = min(n0 + rb + lane / CPR, c.N - 1);
+      woff0[i] = (unsigned)((q * c.wpl0 + (int64_t)o * c.ldw0 + chunk) * 2);
+      woff1[i] = (unsigned)((q * c.wpl1 + (int64_t)o * c.ldw1 + chunk) * 2);
+      wdst[i] = q * T::STAGEB * 2 + (T::BM + rb) * T::BKS * 2;
+    }
     Stage<T, WPL, NPL> sa;
-    load_stage<PRO, T, WPL, NPL, false>(c, m0, n0, kt0 * T::BKS, sa);
-    dma_w_stage<T, NPL>(c, n0, kt0 * T::BKS, lds);
+    auto load_a = [&](int k0) __attribute__((always_inline)) {
+      const bool first = PRO != PRO_HEADZ || k0 < c.ksplit;   // one K range but for HEADZ
+      const char* base =
+          reinterpret_cast<const char*>(first ? c.a0 + k0 : c.a1 + (k0 - c.ksplit));
+#pragma unroll
+      for (int i = 0; i < T::A4; ++i)
+        sa.a[i] = *reinterpret_cast<const float4*>(base + (first ? aoff0[i] : aoff1[i]));
+      if (PRO == PRO_NORM_RELU) {
+        sa.mean = *reinterpret_cast<const float4*>(c.mean + k0 + kq);
+        sa.rstd = *reinterpret_cast<const float4*>(c.rstd + k0 + kq);
+      }
+    };
+    auto buf = [&](int st) __attribute__((always_inline)) { return lds + (st & 1) * STAGE; };
+    auto dma_w = [&](int st) __attribute__((always_inline)) {
+      const int k0 = st * T::BKS;
+      const bool first = PRO != PRO_HEADZ || k0 < c.ksplit;
+      const char* base =
+          reinterpret_cast<const char*>(first ? c.wp0 + k0 : c.wp1 + (k0 - c.ksplit));
+      char* dst = reinterpret_cast<char*>(buf(st));
+#pragma unroll
+      for (int i = 0; i < PPW; ++i)
+        dma16(base + (first ? woff0[i] : woff1[i]), dst + wdst[i]);
+    };
+    auto raw_barrier = [&]() __attribute__((always_inline)) {
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    };
+    load_a(kt0 * T::BKS);
+    dma_w(kt0);
     tk = stamp_start(args.stamp, sl);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    store_stage<PRO, T, PM, WPL, NPL, false>(lds, sa);
-    __syncthreads();
-    int fold_par = -1, hpar = 0;
-    for (int kt = kt0; kt < nk; ++kt) {
-      float* cur = lds + (kt & 1) * STAGE;
-      float* nxt = lds + ((kt + 1) & 1) * STAGE;
-      if (PRO == PRO_HEADZ && fold_par >= 0) {   // the last head's Z rows, after the barrier
-        fold(fold_par);
-        fold_par = -1;
-      }
+    store_stage<PRO, T, PM, WPL, NPL, false>(buf(kt0), sa);
+    raw_barrier();
+    ONEPOSE_GEMM_PHASE(1);
+    // one stage: kt's fragments into tg (zd: phi(q) stage, its Z partials; zf >= 0: the head's
+    // last stage, its Z rows to zrow[zf])
+    auto stage = [&](int kt, floatx16 (&tg)[FN], bool zd, int zf) __attribute__((always_inline)) {
+      float* cur = buf(kt);
+      read_frag(cur, f0);
+      if (zd) zdot(cur, kt);
       const bool more = kt + 1 < nk;
       if (more) {
-        load_stage<PRO, T, WPL, NPL, false>(c, m0, n0, (kt + 1) * T::BKS, sa);
-        dma_w_stage<T, NPL>(c, n0, (kt + 1) * T::BKS, nxt);
+        dma_w(kt + 1);
+        load_a((kt + 1) * T::BKS);
       }
-      read_frag(cur, f0);
-      const bool head = PRO == PRO_HEADZ && kt >= xs;
-      if (head) {
-        zdot(cur, kt);
 #pragma unroll
-        for (int kk = 0; kk < KKW; ++kk) mfma_kk(acc_h, f0, kk);
-        if ((kt - xs) % HS == HS - 1) {   // the head's last stage: its Z rows
-          zfinal(hpar);
-          fold_par = hpar;
-          hpar ^= 1;
-        }
-      } else {
-#pragma unroll
-        for (int kk = 0; kk < KKW; ++kk) mfma_kk(acc, f0, kk);
-      }
+      for (int kk = 0; kk < KKW; ++kk) mfma_kk(tg, f0, kk);
+      if (zf >= 0) zfinal(zf);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (more) store_stage<PRO, T, PM, WPL, NPL, false>(nxt, sa);
-      __syncthreads();
+      if (more) store_stage<PRO, T, PM, WPL, NPL, false>(buf(kt + 1), sa);
+      raw_barrier();
+    };
+    if (PRO != PRO_HEADZ) {
+      for (int kt = kt0; kt < nk; ++kt) stage(kt, acc, false, -1);
+    } else {
+      for (int kt = kt0; kt < xs; ++kt) stage(kt, acc, false, -1);
+#pragma unroll 1
+      for (int h = 0; h < 4; ++h) {
+#pragma unroll 1
+        for (int st = 0; st < HS; ++st) stage(xs + h * HS + st, acc_h, true, st == HS - 1 ? (h & 1) : -1);
+        fold(h & 1);   // after the stage's barrier: every row's Z is in zrow
+      }
     }
-    if (PRO == PRO_HEADZ && fold_par >= 0) fold(fold_par);
+    ONEPOSE_GEMM_PHASE(2);
   } else {
   load_stage<PRO, T, WPL, NPL>(c, m0, n0, kt0 * T::BKS, s0);
   load_stage<PRO, T, WPL, NPL>(c, m0, n0, (kt0 + 1) * T::BKS, s1);
   tk = stamp_start(args.stamp, sl);
   store_stage<PRO, T, PM, WPL, NPL>(lds, s0);
   __syncthreads();
+  ONEPOSE_GEMM_PHASE(1);
   read_frag(lds, f0);
   zdot(lds, kt0);   // the first phi(q) stage's Z partials when the x range is skipped
 
@@ -579,6 +652,7 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
       }
     }
   }
+  ONEPOSE_GEMM_PHASE(2);
   }   // (register-staged loop)
   __syncthreads();   // every wave done with the LDS stages before they are reused below
   // profiling ticket after the K loop: no in-loop wait (vmcnt counts in order) includes the
@@ -614,9 +688,12 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
   const float* biasp = F(bias);
   float* Y = F(Y) + b * F(y_bs);
   const int ldy = F(ldy);
-  float* tile = lds;   // [BM][BN+1] staging for the reducing epilogues
-  constexpr int TP = BN + 1;
+  float* tile = lds;   // [BM][TP] staging
   constexpr bool kStage = EPI == EPI_STATS || EPI == EPI_SCORE || EPI == EPI_QKV;
+  // BIAS / STATS / RESID: the tile is staged and stored by rows of float4 (1 KB per wave
+  // instruction) instead of 4-B stores in the accumulator layout (2 rows x 128 B each): the
+  // store-issue-bound tail of the epilogue is 4x shorter; RESID reads R the same way.
+  constexpr bool kRowStore = EPI == EPI_BIAS || EPI == EPI_STATS || EPI == EPI_RESID;
   const bool q_tile = EPI == EPI_QKV && n0 < 256;   // phi(q) columns: stored, no reduction
 
   if (EPI == EPI_ACC) {   // raw accumulators in register order (a later PRO_HEADZ's acc0)
@@ -629,27 +706,15 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
     }
     return;
   }
+  const int rows = min(BM, M - m0);
   if (ks == 0) {
-    float res[FN][16];
-    if (EPI == EPI_RESID) {   // all residual loads issued before the first store
-      const float* R = F(R) + b * F(r_bs);
-      const int ldr = F(ldr);
-#pragma unroll
-      for (int j = 0; j < FN; ++j) {
-        const int gn = min(n0 + wn * FN * 32 + j * 32 + (lane & 31), N - 1);
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const int gm = min(m0 + wm * 32 + (i & 3) + 8 * (i >> 2) + 4 * (lane >> 5), M - 1);
-          res[j][i] = R[(int64_t)gm * ldr + gn];
-        }
-      }
-    }
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
       const int col = wn * FN * 32 + j * 32 + (lane & 31);
       const int gn = n0 + col;
       const bool col_ok = gn < N;
       const float bias = (EPI != EPI_SCORE && biasp != nullptr && col_ok) ? biasp[gn] : 0.f;
+      float yv[16];
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const int row = wm * 32 + (i & 3) + 8 * (i >> 2) + 4 * (lane >> 5);
@@ -661,39 +726,77 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
           y = acc[j][i] + bias;
           if (EPI == EPI_QKV) y = (q_tile || col < 64) ? (elu1(y) + 1.0f) : (y / F(vdiv));
         }
-        if (EPI == EPI_BIAS || EPI == EPI_STATS || EPI == EPI_SCORE || EPI == EPI_RESID ||
-            (EPI == EPI_QKV && q_tile)) {
-          if (gm < M && col_ok) {
-            if (EPI == EPI_RESID) y = res[j][i] + y;
-            Y[(int64_t)gm * ldy + gn] = y;
-          }
+        if (EPI == EPI_SCORE || (EPI == EPI_QKV && q_tile)) {
+          if (gm < M && col_ok) Y[(int64_t)gm * ldy + gn] = y;
         }
-        if (kStage) tile[row * TP + col] = (gm < M) ? y : 0.f;
+        yv[i] = (gm < M) ? y : 0.f;
+        if (kStage || kRowStore) tile[row * TP + col] = yv[i];
+      }
+      if (EPI == EPI_STATS) {
+        // the column's (mean, M2) over this wave's 32 rows, from the registers: each lane's 16
+        // rows, then the lane pair (lane, lane ^ 32) added in the same order on both lanes
+        const int cw = max(min(rows - wm * 32, 32), 0);   // valid rows of the wave's block
+        float su = 0.f;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) su += yv[i];          // invalid rows hold 0
+        const float so = __shfl_xor(su, 32, 64);
+        const float ssum = (lane < 32) ? su + so : so + su;
+        const float wmean = cw ? ssum / (float)cw : 0.f;
+        float m2 = 0.f;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int row = wm * 32 + (i & 3) + 8 * (i >> 2) + 4 * (lane >> 5);
+          const float d = yv[i] - wmean;
+          m2 += (row < rows) ? d * d : 0.f;
+        }
+        const float mo = __shfl_xor(m2, 32, 64);
+        if (lane < 32) {
+          part[(wm * BN + col) * 2] = wmean;
+          part[(wm * BN + col) * 2 + 1] = m2 + mo;
+        }
       }
     }
   }
-  if (!kStage || q_tile) return;
+  if ((!kStage && !kRowStore) || q_tile) return;
   __syncthreads();
-  const int rows = min(BM, M - m0);
+  if constexpr (kRowStore) {
+    constexpr int C4 = BN / 4, PER = BM * C4 / T::NT;   // float4 per row, per thread
+    static_assert(BM * C4 % T::NT == 0, "row-store pass");
+    float4 rv[EPI == EPI_RESID ? PER : 1];
+    if (EPI == EPI_RESID) {   // all residual loads issued before the first store
+      const float* R = F(R) + b * F(r_bs);
+      const int ldr = F(ldr);
+#pragma unroll
+      for (int p = 0; p < PER; ++p) {
+        const int idx = t + T::NT * p, r = idx / C4, cc = (idx % C4) * 4;
+        const int gm = min(m0 + r, M - 1), gn = min(n0 + cc, N - 4);
+        rv[p] = *reinterpret_cast<const float4*>(R + (int64_t)gm * ldr + gn);
+      }
+    }
+#pragma unroll
+    for (int p = 0; p < PER; ++p) {
+      const int idx = t + T::NT * p, r = idx / C4, cc = (idx % C4) * 4;
+      const int gm = m0 + r, gn = n0 + cc;
+      if (gm < M && gn < N) {   // N % 4 == 0 (checked at launch)
+        float4 v = *reinterpret_cast<const float4*>(tile + r * TP + cc);
+        if (EPI == EPI_RESID) {   // R + (acc + bias), as the reference adds
+          v.x = rv[p].x + v.x;
+          v.y = rv[p].y + v.y;
+          v.z = rv[p].z + v.z;
+          v.w = rv[p].w + v.w;
+        }
+        *reinterpret_cast<float4*>(Y + (int64_t)gm * ldy + gn) = v;
+      }
+    }
+    if (!kStage) return;
+  }
 
   if (EPI == EPI_STATS) {
-    // per column: NRG row groups -> (mean, M2 about the group mean), Chan-merged in order
-    static_assert(EPI != EPI_STATS || (T::NT % BN == 0 && BM % (T::NT / BN) == 0), "stats tile");
-    constexpr int NRG = T::NT / BN, RG = BM / NRG;
-    const int col = t % BN, rg = t / BN;
-    const int r0 = rg * RG, r1 = min(r0 + RG, rows);
-    const int cnt = max(r1 - r0, 0);
-    float s = 0.f;
-    for (int rr = r0; rr < r1; ++rr) s += tile[rr * TP + col];
-    const float gmean = cnt ? s / (float)cnt : 0.f;
-    float m2 = 0.f;
-    for (int rr = r0; rr < r1; ++rr) {
-      const float d = tile[rr * TP + col] - gmean;
-      m2 += d * d;
-    }
-    part[(rg * BN + col) * 2] = gmean;
-    part[(rg * BN + col) * 2 + 1] = m2;
-    __syncthreads();
+    // per column: the WM wave-row blocks' (mean, M2 about the block mean) (staged in `part`
+    // before the barrier above), Chan-merged in order
+    static_assert(EPI != EPI_STATS || (T::KS == 1 && T::NT >= BN && T::WM * BN <= T::NT),
+                  "stats tile");
+    constexpr int NRG = T::WM, RG = 32;
     if (t < BN && n0 + t < N) {
       float n = 0.f, mean = 0.f, M2 = 0.f;
       for (int g = 0; g < NRG; ++g) {
@@ -939,6 +1042,9 @@ int gemm_launch(int epi, int pro, int tile, GemmArgs& args, hipStream_t stream, 
     OP_REQUIRE(P.ksplit % td.bks == 0, "gemm: ksplit=%d", P.ksplit);
     OP_REQUIRE(P.lda0 % 4 == 0 && P.ldw % 4 == 0, "gemm: unaligned leading dimension");
     OP_REQUIRE(epi != EPI_QKV || (td.bn == 128 && P.N == 768), "gemm: QKV tiling");
+    OP_REQUIRE((epi != EPI_BIAS && epi != EPI_STATS && epi != EPI_RESID) ||
+                   (P.N % 4 == 0 && P.ldy % 4 == 0 && (epi != EPI_RESID || P.ldr % 4 == 0)),
+               "gemm: row-stored epilogues need N, ldy (and ldr) multiples of 4");
     OP_REQUIRE(pro != PRO_HEADZ || (P.ksplit % 64 == 0 && P.K - P.ksplit == 256 &&
                                     (td.bks == 32 || td.bks == 64) && P.ksum != nullptr),
                "gemm: HEADZ needs 4 heads x 64 after ksplit");
@@ -958,11 +1064,10 @@ int gemm_launch(int epi, int pro, int tile, GemmArgs& args, hipStream_t stream, 
                "gemm: W planes need a bf16 mode, 32-deep stages and planes for both K ranges");
   }
   args.stamp = nullptr;
-  // split mode: W planes stream into LDS by global_load_lds (the DMA loop: config 2 at
-  // 1645-1655 frames/s against 1538 for the register-staged split loop, which needs 160+ VGPRs
-  // and spills).  bf16 mode: the register-staged loop (config 5: MLP conv 1 41 vs 53 us in the
-  // frame; its two MFMAs per wave and stage leave a latency-bound DMA loop nothing to hide
-  // behind).
+  // split mode: W planes stream into LDS by global_load_lds (the lean DMA loop; the
+  // register-staged split loop needs 160+ VGPRs and spills).  bf16 mode: the DMA loop for the
+  // 64 x 128 tiles (QKV, MLP conv 1), the register-staged loop for 64 x 64 (MLP conv 2, whose
+  // two MFMAs per wave and stage leave a DMA loop nothing to hide behind).
   const bool dma = pm == PM_SPLIT3 || (pm == PM_BF16 && tile == TILE_64x128);
 #define CASE(E, PR, TI, T, PMV, WP)                                      \
   if (epi == E && pro == PR && tile == TI && pm == PMV && wpl == WP) {  \

@@ -1566,8 +1566,9 @@ int mlp2_tile_for(int64_t t64, int pm) {
   // fp32: the 64x32 K-split tile doubles the workgroup count where 64x64 tiles would leave
   // CUs idle (config 2: 320 -> 640 tiles, 23.2 -> 19.7 us); with >= 4 tiles per CU anyway
   // (batched configs) 64x64 moves less data per FLOP (config 3: 9.5 vs 12.3 ms per step)
-  // (bf16: the 64 x 128 DMA tile measured slower for MLP conv 2 at config 5, 0.211 vs 0.158 ms
-  // per step: N = 256 gives it half the workgroups)
+  // (bf16: 64 x 128 tiles -- 32- or 64-deep stages on the DMA loop -- measured slower for MLP
+  // conv 2 in the frame than the register-staged 64 x 64: N = 256 gives them half the
+  // workgroups; config 2: 0.138 vs 0.108 ms per step)
   return pm == PM_F32 && t64 < kMlp2WideTiles ? kTileMLP2F32 : kTileMLP2;
 }
 

@@ -1,0 +1,256 @@
+// Where does a production GEMM launch spend its time?  Wraps gemm.hip's gemm_body in a kernel
+// that stamps every workgroup (s_memrealtime / s_memtime at entry and after its last barrier,
+// plus its CU from HW_ID / XCC_ID), and reports per launch: event time, device span, the
+// in-kernel clock, workgroup duration spread, dispatch skew and per-CU load.
+//
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -w -o tools/phase_probe tools/phase_probe.hip
+__device__ unsigned long long* g_phase;
+#define ONEPOSE_GEMM_PHASE(i) \
+  if (threadIdx.x == 0) g_phase[blockIdx.x * 4 + (i)] = __builtin_amdgcn_s_memtime();
+#include "../onepose_amd/csrc/gemm.hip"
+#include <algorithm>
+#include <cstdio>
+#include <map>
+#include <cstdarg>
+#include <vector>
+
+namespace onepose {
+void set_error(const char* fmt, ...) { va_list ap; va_start(ap, fmt); vprintf(fmt, ap); va_end(ap); printf("\n"); }
+void clear_error() {}
+void prof_pre(int, hipStream_t) {}
+void prof_post(int, hipStream_t) {}
+StampAcc* prof_stamp_slot(int) { return nullptr; }
+}
+using namespace onepose;
+
+struct WgRec {
+  unsigned long long rt0, rt1, mt0, mt1;
+  unsigned hwid, xcc, pad0, pad1;
+};
+
+template <int EPI, int PRO, class T, int PM, bool WPL, bool DMA>
+__global__ __launch_bounds__(T::NT) __attribute__((amdgpu_waves_per_eu(T::WPE)))
+void phase_kernel(GemmArgs args, WgRec* rec) {
+  __shared__ StampLds sl;
+  StampTick tk{0ull, 0ull};
+  const unsigned long long rt0 = __builtin_amdgcn_s_memrealtime();
+  const unsigned long long mt0 = __builtin_amdgcn_s_memtime();
+  if (threadIdx.x == 0) g_phase[blockIdx.x * 4] = mt0;
+  gemm_body<EPI, PRO, T, PM, WPL, DMA>(args, tk, &sl);
+  __syncthreads();
+  if (threadIdx.x == 0) g_phase[blockIdx.x * 4 + 3] = __builtin_amdgcn_s_memtime();
+  if (threadIdx.x == 0) {
+    WgRec r;
+    r.mt1 = __builtin_amdgcn_s_memtime();
+    r.rt1 = __builtin_amdgcn_s_memrealtime();
+    r.rt0 = rt0;
+    r.mt0 = mt0;
+    r.hwid = __builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_REG_HW_ID
+    r.xcc = __builtin_amdgcn_s_getreg((15 << 11) | 20);    // HW_REG_XCC_ID
+    r.pad0 = r.pad1 = 0;
+    rec[blockIdx.x] = r;
+  }
+}
+
+struct Bufs {
+  float *A, *W, *b, *Y, *stats, *mean, *rstd, *ksum;
+  uint16_t* Wp;   // 3 bf16 planes of W ([N][K] each, MMAX-sized stride)
+  int64_t wpl;
+  unsigned* cnt;
+  WgRec* rec;
+};
+
+template <int EPI, int PRO, class T, int PM = PM_F32, bool DMA = false>
+void run(const char* name, Bufs& B, int M, int N, int K, bool fin, int iters) {
+  GemmArgs a;
+  memset(&a, 0, sizeof(a));
+  a.nprob = 1;
+  GemmProb& p = a.p[0];
+  p = gemm_prob(B.A, K, B.W, K, B.b, B.Y, N, M, N, K, 1);
+  if (PM != PM_F32) {
+    p.Wp = B.Wp;
+    p.wpl = B.wpl;
+  }
+  p.stats = B.stats;
+  p.st_cnt = fin ? B.cnt : nullptr;
+  p.st_mean = B.mean;
+  p.st_rstd = B.rstd;
+  if (PRO == PRO_HEADZ) {   // K = [x (256) | phi(q) (256)] from the same A rows
+    p.ksplit = K - 256;
+    p.A1 = B.A + (K - 256);
+    p.lda1 = K;
+    p.ksum = B.ksum;
+    p.ns = 4096.f;
+  }
+  if (PRO == PRO_NORM_RELU) {
+    p.pro_mean = B.mean;
+    p.pro_rstd = B.rstd;
+    p.R = B.Y;
+    p.ldr = N;
+  }
+  p.mtiles = (M + T::BM - 1) / T::BM;
+  p.ntiles = (N + T::BN - 1) / T::BN;
+  p.tiles = p.mtiles * p.ntiles;
+  const int grid = p.tiles;
+  hipEvent_t e0, e1;
+  hipEventCreate(&e0);
+  hipEventCreate(&e1);
+  std::vector<WgRec> h(grid);
+  std::vector<unsigned long long> ph((size_t)grid * 4);
+  double pro = 0, loop = 0, epi = 0;
+  double ev_sum = 0, span_sum = 0, clk_sum = 0, dur_med = 0, dur_max = 0, dur_min = 0, skew50 = 0,
+         skew_max = 0, tail = 0, cu_max = 0, cu_mean = 0, busy = 0;
+  int cus = 0, maxper = 0;
+  for (int it = -3; it < iters; ++it) {
+    if (fin) hipMemsetAsync(B.cnt, 0, 4096);
+    hipEventRecord(e0);
+    hipLaunchKernelGGL((phase_kernel<EPI, PRO, T, PM, PM != PM_F32, DMA>), dim3(grid), dim3(T::NT), 0,
+                       0, a, B.rec);
+    hipEventRecord(e1);
+    hipEventSynchronize(e1);
+    if (it < 0) continue;
+    float ms;
+    hipEventElapsedTime(&ms, e0, e1);
+    hipMemcpy(h.data(), B.rec, grid * sizeof(WgRec), hipMemcpyDeviceToHost);
+    {
+      unsigned long long* dp;
+      hipMemcpyFromSymbol(&dp, HIP_SYMBOL(g_phase), sizeof(dp));
+      hipMemcpy(ph.data(), dp, ph.size() * 8, hipMemcpyDeviceToHost);
+      double a = 0, b = 0, c2 = 0;
+      for (int i = 0; i < grid; ++i) {
+        a += (double)(ph[4 * i + 1] - ph[4 * i]);
+        b += (double)(ph[4 * i + 2] - ph[4 * i + 1]);
+        c2 += (double)(ph[4 * i + 3] - ph[4 * i + 2]);
+      }
+      pro += a / grid;
+      loop += b / grid;
+      epi += c2 / grid;
+    }
+    unsigned long long s0 = ~0ull, s1 = 0;
+    double dm = 0, dr = 0;
+    std::vector<double> dur, st, en;
+    std::map<unsigned, std::vector<int>> percu;
+    for (int i = 0; i < grid; ++i) {
+      s0 = std::min(s0, h[i].rt0);
+      s1 = std::max(s1, h[i].rt1);
+      dm += (double)(h[i].mt1 - h[i].mt0);
+      dr += (double)(h[i].rt1 - h[i].rt0);
+      const unsigned cu = ((h[i].xcc & 0xf) << 16) | (((h[i].hwid >> 13) & 7) << 8) |
+                          (((h[i].hwid >> 12) & 1) << 4) | ((h[i].hwid >> 8) & 0xf);
+      percu[cu].push_back(i);
+    }
+    for (int i = 0; i < grid; ++i) {
+      dur.push_back((h[i].rt1 - h[i].rt0) * 0.01);   // us (100 MHz)
+      st.push_back((h[i].rt0 - s0) * 0.01);
+      en.push_back((h[i].rt1 - s0) * 0.01);
+    }
+    std::vector<double> d2 = dur, s2 = st, e2 = en;
+    std::sort(d2.begin(), d2.end());
+    std::sort(s2.begin(), s2.end());
+    std::sort(e2.begin(), e2.end());
+    ev_sum += ms * 1e3;
+    span_sum += (s1 - s0) * 0.01;
+    clk_sum += dm / dr * 0.1;   // GHz
+    dur_min += d2.front();
+    dur_med += d2[grid / 2];
+    dur_max += d2.back();
+    skew50 += s2[grid / 2];
+    skew_max += s2.back();
+    tail += e2.back() - e2[grid / 2];
+    double cmax = 0, csum = 0;
+    int mp = 0;
+    for (auto& kv : percu) {
+      double lastend = 0, sumd = 0;
+      for (int i : kv.second) {
+        lastend = std::max(lastend, en[i]);
+        sumd += dur[i];
+      }
+      cmax = std::max(cmax, lastend);
+      csum += sumd;
+      mp = std::max(mp, (int)kv.second.size());
+    }
+    cu_max += cmax;
+    cu_mean += csum / percu.size();
+    busy += csum / (percu.size() * ((s1 - s0) * 0.01));
+    cus = (int)percu.size();
+    maxper = mp;
+  }
+  const double n = iters;
+  printf("   phases (cycles, mean per WG): prologue %.0f  loop %.0f (%.0f per stage)  epilogue %.0f\n",
+           pro / n, loop / n, loop / n / (K / T::BKS), epi / n);
+  printf("%-26s M %6d N %4d K %4d grid %5d | event %6.2f us span %6.2f | clock %.2f GHz | wg dur "
+         "min/med/max %5.2f/%5.2f/%5.2f | start skew med/max %5.2f/%5.2f | tail(50%%->last) %5.2f | "
+         "CUs %d, max wg/CU %d, sum wg-us/CU %6.2f, wg-occupancy %.2f\n",
+         name, M, N, K, grid, ev_sum / n, span_sum / n, clk_sum / n, dur_min / n, dur_med / n,
+         dur_max / n, skew50 / n, skew_max / n, tail / n, cus, maxper, cu_mean / n, busy / n);
+  hipEventDestroy(e0);
+  hipEventDestroy(e1);
+}
+
+int main() {
+  const int MMAX = 16384, K = 512, N = 512;
+  srand(1);
+  std::vector<float> hA((size_t)MMAX * K), hW((size_t)N * K), hb(N), hk(256, 30.f), hm(N, 0.1f),
+      hr(N, 1.5f);
+  for (auto& x : hA) x = (float)rand() / RAND_MAX * 2.f - 1.f;
+  for (auto& x : hW) x = ((float)rand() / RAND_MAX * 2.f - 1.f) * 0.05f;
+  for (auto& x : hb) x = (float)rand() / RAND_MAX - 0.5f;
+  Bufs B;
+  hipMalloc(&B.A, hA.size() * 4);
+  hipMalloc(&B.W, hW.size() * 4);
+  hipMalloc(&B.b, N * 4);
+  hipMalloc(&B.Y, (size_t)MMAX * N * 4);
+  hipMalloc(&B.stats, 16 << 20);
+  hipMalloc(&B.mean, 4096);
+  hipMalloc(&B.rstd, 4096);
+  hipMalloc(&B.ksum, 4096);
+  hipMalloc(&B.cnt, 4096);
+  hipMalloc(&B.rec, 65536 * sizeof(WgRec));
+  {
+    unsigned long long* dp;
+    hipMalloc(&dp, 65536 * 4 * 8);
+    hipMemset(dp, 0, 65536 * 4 * 8);
+    hipMemcpyToSymbol(HIP_SYMBOL(g_phase), &dp, sizeof(dp));
+  }
+  hipMemcpy(B.A, hA.data(), hA.size() * 4, hipMemcpyHostToDevice);
+  hipMemcpy(B.W, hW.data(), hW.size() * 4, hipMemcpyHostToDevice);
+  hipMemcpy(B.b, hb.data(), N * 4, hipMemcpyHostToDevice);
+  hipMemcpy(B.ksum, hk.data(), 1024, hipMemcpyHostToDevice);
+  hipMemcpy(B.mean, hm.data(), N * 4, hipMemcpyHostToDevice);
+  hipMemcpy(B.rstd, hr.data(), N * 4, hipMemcpyHostToDevice);
+  hipMemset(B.Y, 0, (size_t)MMAX * N * 4);
+  {
+    std::vector<uint16_t> pl((size_t)3 * N * K);
+    auto bits = [](float x) { uint32_t u; memcpy(&u, &x, 4); return (uint16_t)((u + 0x7FFF + ((u >> 16) & 1)) >> 16); };
+    auto val = [](uint16_t h) { uint32_t u = (uint32_t)h << 16; float x; memcpy(&x, &u, 4); return x; };
+    for (size_t i = 0; i < (size_t)N * K; ++i) {
+      const float x = hW[i];
+      const uint16_t h = bits(x);
+      const float r = x - val(h);
+      const uint16_t m = bits(r);
+      pl[i] = h;
+      pl[(size_t)N * K + i] = m;
+      pl[(size_t)2 * N * K + i] = bits(r - val(m));
+    }
+    hipMalloc(&B.Wp, pl.size() * 2);
+    hipMemcpy(B.Wp, pl.data(), pl.size() * 2, hipMemcpyHostToDevice);
+    B.wpl = (int64_t)N * K;
+  }
+  const int it = 20;
+  using T64x128 = Tile<64, 128, 1, 4, 32>;
+  using T64x128B = Tile<64, 128, 1, 4, 64>;
+  for (int r = 0; r < 2; ++r) run<EPI_STATS, PRO_HEADZ, T64x64>("warm", B, 5120, 512, 512, true, 200);
+  for (int M : {5120, 10240}) {
+    printf("--- mlp1 STATS+HEADZ+fin, M %d N 512 K 512 ---\n", M);
+    run<EPI_STATS, PRO_HEADZ, T64x64>("fp32 64x64 (production)", B, M, 512, 512, true, it);
+    run<EPI_STATS, PRO_HEADZ, T64x64, PM_SPLIT3, true>("split 64x64 lean", B, M, 512, 512, true, it);
+    run<EPI_STATS, PRO_HEADZ, T64x128, PM_BF16, true>("bf16 64x128 lean", B, M, 512, 512, true, it);
+    run<EPI_STATS, PRO_HEADZ, T64x128B, PM_BF16, true>("bf16 64x128 bks64 lean", B, M, 512, 512, true, it);
+    printf("--- mlp2 RESID+NORM, M %d N 256 K 512 ---\n", M);
+    run<EPI_RESID, PRO_NORM_RELU, T64x32K2>("fp32 64x32K2 (production)", B, M, 256, 512, false, it);
+    run<EPI_RESID, PRO_NORM_RELU, T64x64, PM_SPLIT3, true>("split 64x64 lean", B, M, 256, 512, false, it);
+    run<EPI_RESID, PRO_NORM_RELU, T64x128, PM_BF16, true>("bf16 64x128 lean", B, M, 256, 512, false, it);
+    run<EPI_RESID, PRO_NORM_RELU, T64x128B, PM_BF16, true>("bf16 64x128 bks64 lean", B, M, 256, 512, false, it);
+  }
+  return 0;
+}
