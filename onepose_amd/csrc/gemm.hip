@@ -275,8 +275,11 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
   constexpr int STAGE = PM == PM_F32 ? T::STAGE : NPL * T::STAGEB / 2;   // floats
   // epilogue staging tile [BM][TP]: rows of BN + 4 (16-B aligned, read back as float4 rows by
   // the row-store pass), or BN + 1 where columns are read across rows (score, QKV)
-  constexpr int TP = (EPI == EPI_SCORE || EPI == EPI_QKV) ? BN + 1 : BN + 4;
-  constexpr int LDSF = 2 * STAGE > BM * TP ? 2 * STAGE : BM * TP;
+  constexpr int TP = EPI == EPI_SCORE ? BN + 1 : BN + 4;
+  // QKV's [k_h | v_h] tiles are staged transposed, [BN][BM + 4]
+  constexpr int QKVL = EPI == EPI_QKV ? BN * (BM + 4) : 0;
+  constexpr int LDS0 = 2 * STAGE > BM * TP ? 2 * STAGE : BM * TP;
+  constexpr int LDSF = LDS0 > QKVL ? LDS0 : QKVL;
   __shared__ __attribute__((aligned(16))) float lds[LDSF];
   __shared__ float zrow[2 * BM];
   __shared__ float part[(EPI == EPI_STATS) ? T::NT * 2 : 1];
@@ -689,12 +692,11 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
   float* Y = F(Y) + b * F(y_bs);
   const int ldy = F(ldy);
   float* tile = lds;   // [BM][TP] staging
-  constexpr bool kStage = EPI == EPI_STATS || EPI == EPI_SCORE || EPI == EPI_QKV;
+  constexpr bool kStage = EPI == EPI_STATS || EPI == EPI_SCORE;
   // BIAS / STATS / RESID: the tile is staged and stored by rows of float4 (1 KB per wave
   // instruction) instead of 4-B stores in the accumulator layout (2 rows x 128 B each): the
   // store-issue-bound tail of the epilogue is 4x shorter; RESID reads R the same way.
   constexpr bool kRowStore = EPI == EPI_BIAS || EPI == EPI_STATS || EPI == EPI_RESID;
-  const bool q_tile = EPI == EPI_QKV && n0 < 256;   // phi(q) columns: stored, no reduction
 
   if (EPI == EPI_ACC) {   // raw accumulators in register order (a later PRO_HEADZ's acc0)
     if (ks == 0) {
@@ -707,6 +709,110 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
     return;
   }
   const int rows = min(BM, M - m0);
+  if constexpr (EPI == EPI_QKV) {
+    // 128-column tiles of [q (256) | k_0 v_0 | .. | k_3 v_3].  q tiles: phi(q) = elu(q) + 1,
+    // stored by float4 rows.  [k_h | v_h] tiles: phi(k) and v / vdiv staged transposed,
+    // [column][even rows | odd rows], so that KV_h = phi(k)^T v's MFMAs (MFMA m takes rows 2m,
+    // 2m + 1 from lane halves 0, 1) read their operands as float4 runs of one column, and the
+    // phi(k) column sums run down the column in row order: the same sums, in the same order, as
+    // a row-major staging.
+    static_assert(BN == 128 && T::NW == 4 && T::KS == 1, "QKV tile is [k_h | v_h]");
+    constexpr int PT = BM + 4;
+    const bool q_tile = n0 < 256;
+    constexpr int HALF = BM / 2;
+    float* tileT = lds;                 // [BN][PT]: even rows at [0, HALF), odd at [HALF, BM)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int col = wn * FN * 32 + j * 32 + (lane & 31);
+      const float bias = biasp != nullptr ? biasp[n0 + col] : 0.f;
+      // v / vdiv: for a power-of-two source length the product with its reciprocal is the
+      // same number (exact scaling), without the division's instruction sequence
+      const float vdiv = F(vdiv), vrcp = 1.0f / vdiv;
+      const bool vpow2 = __builtin_amdgcn_frexp_mant(vdiv) == 0.5f;
+      float yv[16];
+      auto fill = [&](auto f) __attribute__((always_inline)) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int gm = m0 + wm * 32 + (i & 3) + 8 * (i >> 2) + 4 * (lane >> 5);
+          yv[i] = gm < M ? f(acc[j][i] + bias) : 0.f;
+        }
+      };
+      // (the column kind is uniform over the wave's 32-column accumulator block)
+      if (q_tile || col < 64)
+        fill([&](float y) { return elu1(y) + 1.0f; });   // phi(q), phi(k)
+      else if (vpow2)
+        fill([&](float y) { return y * vrcp; });          // v / vdiv
+      else
+        fill([&](float y) { return y / vdiv; });
+      if (q_tile) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+          tile[(wm * 32 + (i & 3) + 8 * (i >> 2) + 4 * (lane >> 5)) * TP + col] = yv[i];
+      } else {
+        // rows wm 32 + 8 a + 4 h + {0..3}: two even (j = 0, 2) and two odd (j = 1, 3) rows,
+        // consecutive within their halves
+#pragma unroll
+        for (int a = 0; a < 4; ++a) {
+          const int e = col * PT + wm * 16 + 4 * a + 2 * (lane >> 5);
+          *reinterpret_cast<float2*>(tileT + e) = make_float2(yv[4 * a], yv[4 * a + 2]);
+          *reinterpret_cast<float2*>(tileT + e + HALF) = make_float2(yv[4 * a + 1], yv[4 * a + 3]);
+        }
+      }
+    }
+    __syncthreads();
+    if (q_tile) {
+      constexpr int C4 = BN / 4, PER = BM * C4 / T::NT;
+#pragma unroll
+      for (int p = 0; p < PER; ++p) {
+        const int idx = t + T::NT * p, r = idx / C4, cc = (idx % C4) * 4;
+        if (m0 + r < M)
+          *reinterpret_cast<float4*>(Y + (int64_t)(m0 + r) * ldy + n0 + cc) =
+              *reinterpret_cast<const float4*>(tile + r * TP + cc);
+      }
+      return;
+    }
+    const int h = (n0 - 256) / 128;
+    if (t < 64) {   // sum phi(k) over the tile's rows, in row order (invalid rows hold 0)
+      const float* cp = tileT + t * PT;
+      float s = 0.f;
+#pragma unroll
+      for (int q = 0; q < HALF; q += 4) {
+        const float4 ev = *reinterpret_cast<const float4*>(cp + q);
+        const float4 od = *reinterpret_cast<const float4*>(cp + HALF + q);
+        s += ev.x;
+        s += od.x;
+        s += ev.y;
+        s += od.y;
+        s += ev.z;
+        s += od.z;
+        s += ev.w;
+        s += od.w;
+      }
+      F(kspart)[((int64_t)b * mtiles + mt) * 256 + h * 64 + t] = s;
+    }
+    const int wd = wave >> 1, wq = wave & 1;
+    floatx16 kv;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) kv[i] = 0.f;
+    const float* ka = tileT + (wd * 32 + (lane & 31)) * PT + HALF * (lane >> 5);
+    const float* vb = tileT + (64 + wq * 32 + (lane & 31)) * PT + HALF * (lane >> 5);
+#pragma unroll
+    for (int q = 0; q < HALF; q += 4) {   // MFMAs m = q .. q + 3: rows 2m + lane half
+      const float4 a4 = *reinterpret_cast<const float4*>(ka + q);
+      const float4 b4 = *reinterpret_cast<const float4*>(vb + q);
+      kv = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.x, b4.x, kv, 0, 0, 0);
+      kv = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.y, b4.y, kv, 0, 0, 0);
+      kv = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.z, b4.z, kv, 0, 0, 0);
+      kv = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.w, b4.w, kv, 0, 0, 0);
+    }
+    float* out = F(kvpart) + (((int64_t)b * mtiles + mt) * 4 + h) * 4096;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int d = wd * 32 + (i & 3) + 8 * (i >> 2) + 4 * (lane >> 5);
+      out[d * 64 + wq * 32 + (lane & 31)] = kv[i];
+    }
+    return;
+  }
   if (ks == 0) {
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
@@ -724,9 +830,8 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
           y = acc[j][i] / F(scale);
         } else {
           y = acc[j][i] + bias;
-          if (EPI == EPI_QKV) y = (q_tile || col < 64) ? (elu1(y) + 1.0f) : (y / F(vdiv));
         }
-        if (EPI == EPI_SCORE || (EPI == EPI_QKV && q_tile)) {
+        if (EPI == EPI_SCORE) {
           if (gm < M && col_ok) Y[(int64_t)gm * ldy + gn] = y;
         }
         yv[i] = (gm < M) ? y : 0.f;
@@ -757,7 +862,7 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
       }
     }
   }
-  if ((!kStage && !kRowStore) || q_tile) return;
+  if (!kStage && !kRowStore) return;
   __syncthreads();
   if constexpr (kRowStore) {
     constexpr int C4 = BN / 4, PER = BM * C4 / T::NT;   // float4 per row, per thread
@@ -927,33 +1032,6 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
         o[0] = r.x;
         o[1] = r.y;
       }
-    }
-  }
-  if (EPI == EPI_QKV) {
-    // KV_h[d][q] = sum_rows phi(k)[row][d] * v[row][q]   (columns 0..63 | 64..127 of the tile)
-    static_assert(EPI != EPI_QKV || (BN == 128 && T::NW == 4), "QKV tile is [k_h | v_h]");
-    const int h = (n0 - 256) / 128;
-    if (t < 64) {
-      float s = 0.f;
-      for (int rr = 0; rr < rows; ++rr) s += tile[rr * TP + t];
-      F(kspart)[((int64_t)b * mtiles + mt) * 256 + h * 64 + t] = s;
-    }
-    const int wd = wave >> 1, wq = wave & 1;
-    floatx16 kv;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) kv[i] = 0.f;
-    const float* ka = tile + wd * 32 + (lane & 31);
-    const float* vb = tile + 64 + wq * 32 + (lane & 31);
-#pragma unroll 8
-    for (int k = 0; k < BM; k += 2) {
-      const int rr = (k + (lane >> 5)) * TP;
-      kv = __builtin_amdgcn_mfma_f32_32x32x2f32(ka[rr], vb[rr], kv, 0, 0, 0);
-    }
-    float* out = F(kvpart) + (((int64_t)b * mtiles + mt) * 4 + h) * 4096;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int d = wd * 32 + (i & 3) + 8 * (i >> 2) + 4 * (lane >> 5);
-      out[d * 64 + wq * 32 + (lane & 31)] = kv[i];
     }
   }
 #undef F

@@ -2,7 +2,7 @@
 # Full GPU suite, then config 2 fp32 (x2), config 2 bf16 and config 5 bf16 benches.
 set -u
 export TMPDIR=/tmp
-O=gpurun_out/lean2
+O=gpurun_out/${OUT:-lean2}
 mkdir -p $O
 timeout -k 10 150 ./tools/phase_probe > $O/probe.txt 2>&1 || exit $?
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/tests.log 2>&1 || { tail -30 $O/tests.log; exit 1; }

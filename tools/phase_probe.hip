@@ -82,6 +82,11 @@ void run(const char* name, Bufs& B, int M, int N, int K, bool fin, int iters) {
     p.ksum = B.ksum;
     p.ns = 4096.f;
   }
+  if (EPI == EPI_QKV) {
+    p.kvpart = B.stats;    // [mtiles][4][64][64]: 80 x 64 KB = 5 MB < 16 MB
+    p.kspart = B.stats + (6 << 20);
+    p.vdiv = 4096.f;
+  }
   if (PRO == PRO_NORM_RELU) {
     p.pro_mean = B.mean;
     p.pro_rstd = B.rstd;
@@ -188,7 +193,7 @@ void run(const char* name, Bufs& B, int M, int N, int K, bool fin, int iters) {
 }
 
 int main() {
-  const int MMAX = 16384, K = 512, N = 512;
+  const int MMAX = 16384, K = 512, N = 768;   // W rows: up to 768 (QKV)
   srand(1);
   std::vector<float> hA((size_t)MMAX * K), hW((size_t)N * K), hb(N), hk(256, 30.f), hm(N, 0.1f),
       hr(N, 1.5f);
@@ -200,7 +205,7 @@ int main() {
   hipMalloc(&B.W, hW.size() * 4);
   hipMalloc(&B.b, N * 4);
   hipMalloc(&B.Y, (size_t)MMAX * N * 4);
-  hipMalloc(&B.stats, 16 << 20);
+  hipMalloc(&B.stats, 32 << 20);
   hipMalloc(&B.mean, 4096);
   hipMalloc(&B.rstd, 4096);
   hipMalloc(&B.ksum, 4096);
@@ -240,17 +245,17 @@ int main() {
   using T64x128 = Tile<64, 128, 1, 4, 32>;
   using T64x128B = Tile<64, 128, 1, 4, 64>;
   for (int r = 0; r < 2; ++r) run<EPI_STATS, PRO_HEADZ, T64x64>("warm", B, 5120, 512, 512, true, 200);
-  for (int M : {5120, 10240}) {
-    printf("--- mlp1 STATS+HEADZ+fin, M %d N 512 K 512 ---\n", M);
-    run<EPI_STATS, PRO_HEADZ, T64x64>("fp32 64x64 (production)", B, M, 512, 512, true, it);
-    run<EPI_STATS, PRO_HEADZ, T64x64, PM_SPLIT3, true>("split 64x64 lean", B, M, 512, 512, true, it);
-    run<EPI_STATS, PRO_HEADZ, T64x128, PM_BF16, true>("bf16 64x128 lean", B, M, 512, 512, true, it);
-    run<EPI_STATS, PRO_HEADZ, T64x128B, PM_BF16, true>("bf16 64x128 bks64 lean", B, M, 512, 512, true, it);
-    printf("--- mlp2 RESID+NORM, M %d N 256 K 512 ---\n", M);
-    run<EPI_RESID, PRO_NORM_RELU, T64x32K2>("fp32 64x32K2 (production)", B, M, 256, 512, false, it);
-    run<EPI_RESID, PRO_NORM_RELU, T64x64, PM_SPLIT3, true>("split 64x64 lean", B, M, 256, 512, false, it);
-    run<EPI_RESID, PRO_NORM_RELU, T64x128, PM_BF16, true>("bf16 64x128 lean", B, M, 256, 512, false, it);
-    run<EPI_RESID, PRO_NORM_RELU, T64x128B, PM_BF16, true>("bf16 64x128 bks64 lean", B, M, 256, 512, false, it);
-  }
+  using T32x128 = Tile<32, 128, 1, 4, 32>;
+  printf("--- QKV (M 5120 N 768 K 256) ---\n");
+  run<EPI_QKV, PRO_PLAIN, T64x128>("fp32 qkv 64x128 (production)", B, 5120, 768, 256, false, it);
+  run<EPI_QKV, PRO_PLAIN, T32x128>("fp32 qkv 32x128", B, 5120, 768, 256, false, it);
+  run<EPI_BIAS, PRO_PLAIN, T64x64>("fp32 BIAS same shape", B, 5120, 768, 256, false, it);
+  printf("--- QKV 2D only (M 1024 N 768 K 256) ---\n");
+  run<EPI_QKV, PRO_PLAIN, T32x128>("fp32 qkv 32x128 (production)", B, 1024, 768, 256, false, it);
+  run<EPI_QKV, PRO_PLAIN, T64x128>("fp32 qkv 64x128", B, 1024, 768, 256, false, it);
+  printf("--- mlp1 / mlp2 (M 5120) ---\n");
+  run<EPI_STATS, PRO_HEADZ, T64x64>("fp32 mlp1 64x64 (production)", B, 5120, 512, 512, true, it);
+  run<EPI_RESID, PRO_NORM_RELU, T64x32K2>("fp32 mlp2 64x32K2 (production)", B, 5120, 256, 512, false, it);
+  run<EPI_BIAS, PRO_PLAIN, T64x64>("fp32 final 64x64 (production)", B, 5120, 256, 256, false, it);
   return 0;
 }
