@@ -864,7 +864,8 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
   }
   if (!kStage && !kRowStore) return;
   __syncthreads();
-  if constexpr (kRowStore) {
+  // the row-store pass (STATS: issued behind its ticket's round trip, below)
+  auto row_store = [&]() __attribute__((always_inline)) {
     constexpr int C4 = BN / 4, PER = BM * C4 / T::NT;   // float4 per row, per thread
     static_assert(BM * C4 % T::NT == 0, "row-store pass");
     float4 rv[EPI == EPI_RESID ? PER : 1];
@@ -893,7 +894,10 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
         *reinterpret_cast<float4*>(Y + (int64_t)gm * ldy + gn) = v;
       }
     }
-    if (!kStage) return;
+  };
+  if constexpr (EPI == EPI_BIAS || EPI == EPI_RESID) {
+    row_store();
+    return;
   }
 
   if (EPI == EPI_STATS) {
@@ -930,16 +934,19 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
     // release (it would write back the XCD's L2, this tile's Y in it) nor an acquire (an L1
     // invalidate, ~1.7 us) is needed.  The counters are zeroed by the forward's first kernel.
     unsigned* tickets = F(st_cnt);
-    if (tickets != nullptr) {
+    if (tickets == nullptr) {
+      row_store();
+    } else {
       if (t < BN) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the storing wave drains
       __syncthreads();   // partial stores drained; `part` no longer read
       int* last = reinterpret_cast<int*>(part);
-      if (t == 0) {
-        const unsigned ticket = __hip_atomic_fetch_add(tickets + b * ntiles + nt, 1u, __ATOMIC_RELAXED,
-                                                       __HIP_MEMORY_SCOPE_AGENT);
-        last[0] = ticket == (unsigned)(mtiles - 1) ? 1 : 0;
-      }
-      __syncthreads();
+      unsigned ticket = 0u;
+      if (t == 0)
+        ticket = __hip_atomic_fetch_add(tickets + b * ntiles + nt, 1u, __ATOMIC_RELAXED,
+                                        __HIP_MEMORY_SCOPE_AGENT);
+      row_store();   // the tile's Y rows, while the ticket is in flight
+      if (t == 0) last[0] = ticket == (unsigned)(mtiles - 1) ? 1 : 0;
+      __syncthreads();   // (also: the row-store's tile reads are done before `red` reuses it)
       if (last[0]) {
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // (no instruction: keeps the
                                                                  // loads below the ticket)
