@@ -3,7 +3,7 @@
 # baseline), the harness's 20-step line, and a rocprofv3 kernel-trace/stats pass.
 set -u
 export TMPDIR=/tmp
-O=gpurun_out/r03
+O=gpurun_out/${OUT:-r03}
 mkdir -p $O
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q -s --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1 || { tail -40 $O/gpu_tests.log; exit 1; }
 tail -1 $O/gpu_tests.log

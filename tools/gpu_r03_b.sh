@@ -4,7 +4,7 @@
 # config 5 (bf16 attention).  Each pass is its own rocprofv3 run with --kernel-trace only.
 set -u
 export TMPDIR=/tmp
-O=gpurun_out/r03
+O=gpurun_out/${OUT:-r03}
 for cfg in c2 c5; do
   if [ $cfg = c5 ]; then ARGS="--precision bf16 --n1 2048 --n3 8192"; else ARGS=""; fi
   mkdir -p $O/pmc_$cfg
