@@ -864,6 +864,7 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
   }
   if (!kStage && !kRowStore) return;
   __syncthreads();
+  ONEPOSE_GEMM_PHASE(4);
   // the row-store pass (STATS: issued behind its ticket's round trip, below)
   auto row_store = [&]() __attribute__((always_inline)) {
     constexpr int C4 = BN / 4, PER = BM * C4 / T::NT;   // float4 per row, per thread
@@ -939,6 +940,7 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
     } else {
       if (t < BN) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the storing wave drains
       __syncthreads();   // partial stores drained; `part` no longer read
+      ONEPOSE_GEMM_PHASE(5);
       int* last = reinterpret_cast<int*>(part);
       unsigned ticket = 0u;
       if (t == 0)
@@ -947,10 +949,11 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
       row_store();   // the tile's Y rows, while the ticket is in flight
       if (t == 0) last[0] = ticket == (unsigned)(mtiles - 1) ? 1 : 0;
       __syncthreads();   // (also: the row-store's tile reads are done before `red` reuses it)
+      ONEPOSE_GEMM_PHASE(6);
       if (last[0]) {
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // (no instruction: keeps the
                                                                  // loads below the ticket)
-        // one pass over the partials (sc1 loads, 16 tiles in flight per thread), shifted by
+        // one pass over the partials (sc1 loads, FD tiles in flight per thread), shifted by
         // tile 0's mean c:  S1 = sum n_i (mean_i - c),  S2 = sum M2_i + n_i (mean_i - c)^2,
         // mean = c + S1 / n,  M2 = S2 - S1^2 / n  (double; no per-merge division, unlike a
         // pairwise Chan merge).  NG tile-interleaved groups per column, added in group order.
@@ -965,16 +968,18 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
         };
         const double c0 = (double)ld(0, 0);
         double s1 = 0.0, s2 = 0.0;
-        for (int t0 = grp; t0 < mtiles; t0 += 16 * NG) {
-          float mv[16], qv[16];
+        // FD tiles' partials in flight per thread (one round trip for up to FD x NG tiles)
+        constexpr int FD = 40;
+        for (int t0 = grp; t0 < mtiles; t0 += FD * NG) {
+          float mv[FD], qv[FD];
 #pragma unroll
-          for (int u = 0; u < 16; ++u) {
+          for (int u = 0; u < FD; ++u) {
             const int ti = min(t0 + u * NG, mtiles - 1);
             mv[u] = ld(ti, 0);
             qv[u] = ld(ti, 1);
           }
 #pragma unroll
-          for (int u = 0; u < 16; ++u) {
+          for (int u = 0; u < FD; ++u) {
             const int ti = t0 + u * NG;
             const double nb = (double)min(BM, M - ti * BM), d = (double)mv[u] - c0;
             if (ti < mtiles) {

@@ -6,9 +6,10 @@
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -w -o tools/phase_probe tools/phase_probe.hip
 __device__ unsigned long long* g_phase;
 #define ONEPOSE_GEMM_PHASE(i) \
-  if (threadIdx.x == 0) g_phase[blockIdx.x * 4 + (i)] = __builtin_amdgcn_s_memtime();
+  if (threadIdx.x == 0) g_phase[blockIdx.x * 8 + (i)] = __builtin_amdgcn_s_memtime();
 #include "../onepose_amd/csrc/gemm.hip"
 #include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <map>
 #include <cstdarg>
@@ -35,10 +36,10 @@ void phase_kernel(GemmArgs args, WgRec* rec) {
   StampTick tk{0ull, 0ull};
   const unsigned long long rt0 = __builtin_amdgcn_s_memrealtime();
   const unsigned long long mt0 = __builtin_amdgcn_s_memtime();
-  if (threadIdx.x == 0) g_phase[blockIdx.x * 4] = mt0;
+  if (threadIdx.x == 0) g_phase[blockIdx.x * 8] = mt0;
   gemm_body<EPI, PRO, T, PM, WPL, DMA>(args, tk, &sl);
   __syncthreads();
-  if (threadIdx.x == 0) g_phase[blockIdx.x * 4 + 3] = __builtin_amdgcn_s_memtime();
+  if (threadIdx.x == 0) g_phase[blockIdx.x * 8 + 3] = __builtin_amdgcn_s_memtime();
   if (threadIdx.x == 0) {
     WgRec r;
     r.mt1 = __builtin_amdgcn_s_memtime();
@@ -52,9 +53,12 @@ void phase_kernel(GemmArgs args, WgRec* rec) {
   }
 }
 
+static std::vector<float> g_lastY;   // Y of the last run (first M x N)
+
 struct Bufs {
   float *A, *W, *b, *Y, *stats, *mean, *rstd, *ksum;
   uint16_t* Wp;   // 3 bf16 planes of W ([N][K] each, MMAX-sized stride)
+  uint16_t* Ab;   // bf16 copy of A ([MMAX][K], round to nearest even)
   int64_t wpl;
   unsigned* cnt;
   WgRec* rec;
@@ -101,8 +105,8 @@ void run(const char* name, Bufs& B, int M, int N, int K, bool fin, int iters) {
   hipEventCreate(&e0);
   hipEventCreate(&e1);
   std::vector<WgRec> h(grid);
-  std::vector<unsigned long long> ph((size_t)grid * 4);
-  double pro = 0, loop = 0, epi = 0;
+  std::vector<unsigned long long> ph((size_t)grid * 8);
+  double pro = 0, loop = 0, epi = 0, e_stage = 0, e_merge = 0, e_ticket = 0, e_fin = 0;
   double ev_sum = 0, span_sum = 0, clk_sum = 0, dur_med = 0, dur_max = 0, dur_min = 0, skew50 = 0,
          skew_max = 0, tail = 0, cu_max = 0, cu_mean = 0, busy = 0;
   int cus = 0, maxper = 0;
@@ -121,15 +125,30 @@ void run(const char* name, Bufs& B, int M, int N, int K, bool fin, int iters) {
       unsigned long long* dp;
       hipMemcpyFromSymbol(&dp, HIP_SYMBOL(g_phase), sizeof(dp));
       hipMemcpy(ph.data(), dp, ph.size() * 8, hipMemcpyDeviceToHost);
-      double a = 0, b = 0, c2 = 0;
+      double a = 0, b = 0, c2 = 0, s4 = 0, s5 = 0, s6 = 0, s7 = 0;
+      int n5 = 0;
       for (int i = 0; i < grid; ++i) {
-        a += (double)(ph[4 * i + 1] - ph[4 * i]);
-        b += (double)(ph[4 * i + 2] - ph[4 * i + 1]);
-        c2 += (double)(ph[4 * i + 3] - ph[4 * i + 2]);
+        const unsigned long long* q = &ph[8 * i];
+        a += (double)(q[1] - q[0]);
+        b += (double)(q[2] - q[1]);
+        c2 += (double)(q[3] - q[2]);
+        if (q[4] > q[2] && q[4] <= q[3]) s4 += (double)(q[4] - q[2]);
+        if (q[5] > q[4] && q[6] > q[5] && q[6] <= q[3]) {
+          s5 += (double)(q[5] - q[4]);
+          s6 += (double)(q[6] - q[5]);
+          s7 += (double)(q[3] - q[6]);
+          ++n5;
+        }
       }
       pro += a / grid;
       loop += b / grid;
       epi += c2 / grid;
+      e_stage += s4 / grid;
+      if (n5) {
+        e_merge += s5 / n5;
+        e_ticket += s6 / n5;
+        e_fin += s7 / n5;
+      }
     }
     unsigned long long s0 = ~0ull, s1 = 0;
     double dm = 0, dr = 0;
@@ -181,8 +200,10 @@ void run(const char* name, Bufs& B, int M, int N, int K, bool fin, int iters) {
     maxper = mp;
   }
   const double n = iters;
-  printf("   phases (cycles, mean per WG): prologue %.0f  loop %.0f (%.0f per stage)  epilogue %.0f\n",
-           pro / n, loop / n, loop / n / (K / T::BKS), epi / n);
+  printf("   phases (cycles, mean per WG): prologue %.0f  loop %.0f (%.0f per stage)  epilogue %.0f"
+         " [stage+sync %.0f | stats merge+drain %.0f | ticket+rows %.0f | rest %.0f]\n",
+         pro / n, loop / n, loop / n / (K / T::BKS), epi / n, e_stage / n, e_merge / n,
+         e_ticket / n, e_fin / n);
   printf("%-26s M %6d N %4d K %4d grid %5d | event %6.2f us span %6.2f | clock %.2f GHz | wg dur "
          "min/med/max %5.2f/%5.2f/%5.2f | start skew med/max %5.2f/%5.2f | tail(50%%->last) %5.2f | "
          "CUs %d, max wg/CU %d, sum wg-us/CU %6.2f, wg-occupancy %.2f\n",
@@ -190,6 +211,13 @@ void run(const char* name, Bufs& B, int M, int N, int K, bool fin, int iters) {
          dur_max / n, skew50 / n, skew_max / n, tail / n, cus, maxper, cu_mean / n, busy / n);
   hipEventDestroy(e0);
   hipEventDestroy(e1);
+  g_lastY.resize((size_t)M * N);
+  hipMemcpy(g_lastY.data(), B.Y, g_lastY.size() * 4, hipMemcpyDeviceToHost);
+}
+static double maxdiff(const std::vector<float>& a, const std::vector<float>& b) {
+  double d = 0;
+  for (size_t i = 0; i < a.size() && i < b.size(); ++i) d = std::max(d, (double)std::fabs(a[i] - b[i]));
+  return d;
 }
 
 int main() {
@@ -213,8 +241,8 @@ int main() {
   hipMalloc(&B.rec, 65536 * sizeof(WgRec));
   {
     unsigned long long* dp;
-    hipMalloc(&dp, 65536 * 4 * 8);
-    hipMemset(dp, 0, 65536 * 4 * 8);
+    hipMalloc(&dp, 65536 * 8 * 8);
+    hipMemset(dp, 0, 65536 * 8 * 8);
     hipMemcpyToSymbol(HIP_SYMBOL(g_phase), &dp, sizeof(dp));
   }
   hipMemcpy(B.A, hA.data(), hA.size() * 4, hipMemcpyHostToDevice);
@@ -237,6 +265,10 @@ int main() {
       pl[(size_t)N * K + i] = m;
       pl[(size_t)2 * N * K + i] = bits(r - val(m));
     }
+    std::vector<uint16_t> ab(hA.size());
+    for (size_t i = 0; i < hA.size(); ++i) ab[i] = bits(hA[i]);
+    hipMalloc(&B.Ab, ab.size() * 2);
+    hipMemcpy(B.Ab, ab.data(), ab.size() * 2, hipMemcpyHostToDevice);
     hipMalloc(&B.Wp, pl.size() * 2);
     hipMemcpy(B.Wp, pl.data(), pl.size() * 2, hipMemcpyHostToDevice);
     B.wpl = (int64_t)N * K;
@@ -245,17 +277,13 @@ int main() {
   using T64x128 = Tile<64, 128, 1, 4, 32>;
   using T64x128B = Tile<64, 128, 1, 4, 64>;
   for (int r = 0; r < 2; ++r) run<EPI_STATS, PRO_HEADZ, T64x64>("warm", B, 5120, 512, 512, true, 200);
-  using T32x128 = Tile<32, 128, 1, 4, 32>;
-  printf("--- QKV (M 5120 N 768 K 256) ---\n");
-  run<EPI_QKV, PRO_PLAIN, T64x128>("fp32 qkv 64x128 (production)", B, 5120, 768, 256, false, it);
-  run<EPI_QKV, PRO_PLAIN, T32x128>("fp32 qkv 32x128", B, 5120, 768, 256, false, it);
-  run<EPI_BIAS, PRO_PLAIN, T64x64>("fp32 BIAS same shape", B, 5120, 768, 256, false, it);
-  printf("--- QKV 2D only (M 1024 N 768 K 256) ---\n");
-  run<EPI_QKV, PRO_PLAIN, T32x128>("fp32 qkv 32x128 (production)", B, 1024, 768, 256, false, it);
-  run<EPI_QKV, PRO_PLAIN, T64x128>("fp32 qkv 64x128", B, 1024, 768, 256, false, it);
-  printf("--- mlp1 / mlp2 (M 5120) ---\n");
-  run<EPI_STATS, PRO_HEADZ, T64x64>("fp32 mlp1 64x64 (production)", B, 5120, 512, 512, true, it);
-  run<EPI_RESID, PRO_NORM_RELU, T64x32K2>("fp32 mlp2 64x32K2 (production)", B, 5120, 256, 512, false, it);
-  run<EPI_BIAS, PRO_PLAIN, T64x64>("fp32 final 64x64 (production)", B, 5120, 256, 256, false, it);
+  printf("--- mlp1 epilogue breakdown (M 5120) ---\n");
+  run<EPI_STATS, PRO_HEADZ, T64x64>("fp32 mlp1", B, 5120, 512, 512, true, it);
+  run<EPI_STATS, PRO_HEADZ, T64x128, PM_BF16, 1>("bf16 mlp1", B, 5120, 512, 512, true, it);
+  run<EPI_STATS, PRO_HEADZ, T64x64>("fp32 mlp1 (no finalize)", B, 5120, 512, 512, false, it);
+  run<EPI_STATS, PRO_HEADZ, T64x128, PM_BF16, 1>("bf16 mlp1 (no fin)", B, 5120, 512, 512, false, it);
+  printf("--- M 10240 ---\n");
+  run<EPI_STATS, PRO_HEADZ, T64x64>("fp32 mlp1", B, 10240, 512, 512, true, it);
+  run<EPI_STATS, PRO_HEADZ, T64x128, PM_BF16, 1>("bf16 mlp1", B, 10240, 512, 512, true, it);
   return 0;
 }
