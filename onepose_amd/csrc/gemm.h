@@ -64,9 +64,13 @@ struct GemmProb {
   const float* pro_rstd;
   int64_t pro_bs;
   float* stats;        // EPI_STATS: [batch][mtiles][2][N]  (mtiles = ceil(M / tile rows))
-  unsigned* st_cnt;    // EPI_STATS: [batch][ntiles] arrival counters, zero before the launch;
-                       //   null = partials only.  The last M-tile to arrive at a column block
-                       //   merges its partials into st_mean / st_rstd [batch][N] (InstanceNorm)
+  unsigned* st_cnt;    // EPI_STATS: arrival counters, zero before the launch, st_cnt_bs per
+                       //   sample: [ntiles] column-block counters, then [ntiles][ngroups] group
+                       //   counters; null = partials only.  Two levels (gemm.hip): the last
+                       //   M-tile of each group (stats_group_size) merges the group into
+                       //   st_grp, the last group merger the groups into st_mean / st_rstd
+  int st_cnt_bs;
+  double* st_grp;      // EPI_STATS with st_cnt: [batch][ngroups][2][N] group (mean, M2)
   float* st_mean;
   float* st_rstd;
   float* rowstat;      // EPI_SCORE: [batch][M][ntiles][2]
@@ -121,6 +125,19 @@ int gemm_launch(int epi, int pro, int tile, GemmArgs& args, hipStream_t stream, 
                 int pm = PM_F32);
 // Rows per M-tile of a configuration (the chunk size of the STATS / KVPART partials).
 int gemm_tile_rows(int tile);
+
+// InstanceNorm finalize: M-tiles per first-level group (at least kStatsGroup, and at most
+// kStatsMaxGroups groups: batched launches with many tiles per CU keep few mergers), and the
+// groups a STATS launch over M rows with `rows`-row tiles has per sample and column block.
+constexpr int kStatsGroup = 8, kStatsMaxGroups = 8;
+__host__ __device__ inline int stats_group_size(int mtiles) {
+  const int g = (mtiles + kStatsMaxGroups - 1) / kStatsMaxGroups;
+  return g > kStatsGroup ? g : kStatsGroup;
+}
+inline int stats_groups(int M, int rows) {
+  const int mtiles = (M + rows - 1) / rows, g = stats_group_size(mtiles);
+  return (mtiles + g - 1) / g;
+}
 
 // Zero-initialised problem with the common fields set.
 GemmProb gemm_prob(const float* A, int lda, const float* W, int ldw, const float* bias,

@@ -938,69 +938,111 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
     if (tickets == nullptr) {
       row_store();
     } else {
+      // Two-level finalize.  Every store and load of the handed-off partials is sc1
+      // (write-through / L2), so neither an agent-scope release (it would write back the XCD's
+      // L2, this tile's Y in it) nor an acquire (an L1 invalidate, ~1.7 us) is needed.
+      //  1. each M-tile takes a ticket on its group (kStatsGroup consecutive M-tiles) after its
+      //     partial stores drained; the group's last tile merges the group's partials in tile
+      //     order (shifted by the group's first mean) into st_grp -- while the other groups'
+      //     tiles still compute;
+      //  2. that merger takes a ticket on the column block; the last one merges the groups in
+      //     group order (shifted by group 0's mean) into mean / rstd.
+      // Deterministic: neither result depends on which tile or group arrives last.
+      static_assert(EPI != EPI_STATS || T::NT >= BN, "finalize threads");
+      const int G = stats_group_size(mtiles);
+      const int ngroups = (mtiles + G - 1) / G, g1 = mt / G;
+      unsigned* cb = tickets + (int64_t)b * F(st_cnt_bs);   // [ntiles] then [ntiles][ngroups]
+      double* gp = F(st_grp) + (int64_t)b * ngroups * 2 * N;
+      const int col = min(n0 + t, N - 1);
       if (t < BN) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the storing wave drains
       __syncthreads();   // partial stores drained; `part` no longer read
       ONEPOSE_GEMM_PHASE(5);
       int* last = reinterpret_cast<int*>(part);
       unsigned ticket = 0u;
       if (t == 0)
-        ticket = __hip_atomic_fetch_add(tickets + b * ntiles + nt, 1u, __ATOMIC_RELAXED,
+        ticket = __hip_atomic_fetch_add(cb + ntiles + nt * ngroups + g1, 1u, __ATOMIC_RELAXED,
                                         __HIP_MEMORY_SCOPE_AGENT);
       row_store();   // the tile's Y rows, while the ticket is in flight
-      if (t == 0) last[0] = ticket == (unsigned)(mtiles - 1) ? 1 : 0;
-      __syncthreads();   // (also: the row-store's tile reads are done before `red` reuses it)
+      const int gt0 = g1 * G, gsz = min(G, mtiles - gt0);
+      if (t == 0) last[0] = ticket == (unsigned)(gsz - 1) ? 1 : 0;
+      __syncthreads();
       ONEPOSE_GEMM_PHASE(6);
       if (last[0]) {
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // (no instruction: keeps the
                                                                  // loads below the ticket)
-        // one pass over the partials (sc1 loads, FD tiles in flight per thread), shifted by
-        // tile 0's mean c:  S1 = sum n_i (mean_i - c),  S2 = sum M2_i + n_i (mean_i - c)^2,
-        // mean = c + S1 / n,  M2 = S2 - S1^2 / n  (double; no per-merge division, unlike a
-        // pairwise Chan merge).  NG tile-interleaved groups per column, added in group order.
-        static_assert(EPI != EPI_STATS || T::NT % BN == 0, "finalize groups");
-        constexpr int NG = T::NT / BN;
-        const int col = t % BN, grp = t / BN;
-        float* sp = F(stats) + (int64_t)b * mtiles * 2 * N + min(n0 + col, N - 1);
-        double* red = reinterpret_cast<double*>(lds);   // [2][NG][BN]
-        auto ld = [&](int ti, int half) __attribute__((always_inline)) {
-          return __hip_atomic_load(sp + (int64_t)ti * 2 * N + half * N, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-        };
-        const double c0 = (double)ld(0, 0);
-        double s1 = 0.0, s2 = 0.0;
-        // FD tiles' partials in flight per thread (one round trip for up to FD x NG tiles)
-        constexpr int FD = 40;
-        for (int t0 = grp; t0 < mtiles; t0 += FD * NG) {
-          float mv[FD], qv[FD];
+        if (t < BN) {
+          const float* sp = F(stats) + (int64_t)b * mtiles * 2 * N + col;
+          auto ld = [&](int ti, int half) __attribute__((always_inline)) {
+            return __hip_atomic_load(sp + (int64_t)ti * 2 * N + half * N, __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_AGENT);
+          };
+          const double c = (double)ld(gt0, 0);
+          double s1 = 0.0, s2 = 0.0, ng = 0.0;
+          constexpr int UD = 16;   // tiles' partials in flight per thread
+          for (int u0 = 0; u0 < gsz; u0 += UD) {
+            float mv[UD], qv[UD];
 #pragma unroll
-          for (int u = 0; u < FD; ++u) {
-            const int ti = min(t0 + u * NG, mtiles - 1);
-            mv[u] = ld(ti, 0);
-            qv[u] = ld(ti, 1);
-          }
+            for (int u = 0; u < UD; ++u) {
+              const int ti = gt0 + min(u0 + u, gsz - 1);
+              mv[u] = ld(ti, 0);
+              qv[u] = ld(ti, 1);
+            }
 #pragma unroll
-          for (int u = 0; u < FD; ++u) {
-            const int ti = t0 + u * NG;
-            const double nb = (double)min(BM, M - ti * BM), d = (double)mv[u] - c0;
-            if (ti < mtiles) {
-              s1 += nb * d;
-              s2 += (double)qv[u] + nb * d * d;
+            for (int u = 0; u < UD; ++u) {
+              if (u0 + u < gsz) {
+                const double nb = (double)min(BM, M - (gt0 + u0 + u) * BM), d = (double)mv[u] - c;
+                s1 += nb * d;
+                s2 += (double)qv[u] + nb * d * d;
+                ng += nb;
+              }
             }
           }
+          if (n0 + t < N) {
+            __hip_atomic_store(gp + (int64_t)g1 * 2 * N + n0 + t, c + s1 / ng, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(gp + (int64_t)g1 * 2 * N + N + n0 + t, s2 - s1 * s1 / ng,
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
-        red[grp * BN + col] = s1;
-        red[(NG + grp) * BN + col] = s2;
         __syncthreads();
-        if (grp == 0 && n0 + col < N) {
+        if (t == 0) {
+          const unsigned t2 = __hip_atomic_fetch_add(cb + nt, 1u, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_AGENT);
+          last[1] = t2 == (unsigned)(ngroups - 1) ? 1 : 0;
+        }
+        __syncthreads();
+        if (last[1] && t < BN && n0 + t < N) {
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+          const double* g2 = gp + n0 + t;
+          auto ld2 = [&](int g, int half) __attribute__((always_inline)) {
+            return __hip_atomic_load(g2 + (int64_t)g * 2 * N + half * N, __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_AGENT);
+          };
+          const double c = ld2(0, 0);
           double S1 = 0.0, S2 = 0.0;
-          for (int g = 0; g < NG; ++g) {
-            S1 += red[g * BN + col];
-            S2 += red[(NG + g) * BN + col];
+          constexpr int GD = kStatsMaxGroups;   // every group's partials in flight at once
+          for (int q0 = 0; q0 < ngroups; q0 += GD) {
+            double mg[GD], m2g[GD];
+#pragma unroll
+            for (int u = 0; u < GD; ++u) {
+              const int g = min(q0 + u, ngroups - 1);
+              mg[u] = ld2(g, 0);
+              m2g[u] = ld2(g, 1);
+            }
+#pragma unroll
+            for (int u = 0; u < GD; ++u) {
+              const int g = q0 + u;
+              if (g < ngroups) {
+                const double ngr = (double)min(G * BM, M - g * G * BM), d = mg[u] - c;
+                S1 += ngr * d;
+                S2 += m2g[u] + ngr * d * d;
+              }
+            }
           }
           const double n = (double)M;
-          F(st_mean)[(int64_t)b * N + n0 + col] = (float)(c0 + S1 / n);
-          F(st_rstd)[(int64_t)b * N + n0 + col] =
-              (float)(1.0 / sqrt((S2 - S1 * S1 / n) / n + 1e-5));
+          F(st_mean)[(int64_t)b * N + n0 + t] = (float)(c + S1 / n);
+          F(st_rstd)[(int64_t)b * N + n0 + t] = (float)(1.0 / sqrt((S2 - S1 * S1 / n) / n + 1e-5));
         }
       }
     }
@@ -1132,6 +1174,11 @@ int gemm_launch(int epi, int pro, int tile, GemmArgs& args, hipStream_t stream, 
     OP_REQUIRE(P.ksplit % td.bks == 0, "gemm: ksplit=%d", P.ksplit);
     OP_REQUIRE(P.lda0 % 4 == 0 && P.ldw % 4 == 0, "gemm: unaligned leading dimension");
     OP_REQUIRE(epi != EPI_QKV || (td.bn == 128 && P.N == 768), "gemm: QKV tiling");
+    OP_REQUIRE(epi != EPI_STATS || P.st_cnt == nullptr ||
+                   (P.st_grp != nullptr &&
+                    P.st_cnt_bs >= ceil_div(P.N, td.bn) * (1 + stats_groups(P.M, td.bm))),
+               "gemm: STATS finalize needs group partials and %d counters per sample",
+               ceil_div(P.N, td.bn) * (1 + stats_groups(P.M, td.bm)));
     OP_REQUIRE((epi != EPI_BIAS && epi != EPI_STATS && epi != EPI_RESID) ||
                    (P.N % 4 == 0 && P.ldy % 4 == 0 && (epi != EPI_RESID || P.ldr % 4 == 0)),
                "gemm: row-stored epilogues need N, ldy (and ldr) multiples of 4");

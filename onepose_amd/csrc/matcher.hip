@@ -1168,8 +1168,9 @@ struct Plan {
   float *kv, *ksum, *mf;
   float *phiq2, *phiq3, *y12, *y13;
   float *stats2, *stats3, *mean, *rstd;
-  unsigned* cnt;      // in-launch arrival counters: [attention layer][side][B][mlp1 N-tiles]
-  int ncnt;
+  unsigned* cnt;      // in-launch arrival counters: [attention layer][side][B][cps]
+  int ncnt, cps;      //   (cps: MLP conv 1's column-block and group counters, gemm.h st_cnt)
+  double *grp2, *grp3;   // InstanceNorm group partials of the two sides (gemm.h st_grp)
   float *f2, *f3, *s;
   float *rowpart, *colpart, *rowmax, *rowsum, *colmax, *colsum;
   unsigned long long *rowbest, *colbest;
@@ -1221,8 +1222,11 @@ Plan make_plan(void* ws, int B, int n1, int n3, int L, bool with_conf) {
   p.stats3 = c.take<float>((size_t)B * ceil_div(n3, str) * 1024);
   p.mean = c.take<float>((size_t)2 * B * 512);
   p.rstd = c.take<float>((size_t)2 * B * 512);
-  p.ncnt = kApLayers * 2 * B * kCntPerSide;
+  p.cps = kCntPerSide * (1 + stats_groups(std::max(n1, n3), str));
+  p.ncnt = kApLayers * 2 * B * p.cps;
   p.cnt = c.take<unsigned>((size_t)p.ncnt);
+  p.grp2 = c.take<double>((size_t)B * stats_groups(n1, str) * 1024);
+  p.grp3 = c.take<double>((size_t)B * stats_groups(n3, str) * 1024);
   p.f2 = c.take<float>(t2 * 256);
   p.f3 = c.take<float>(t3 * 256);
   p.s = with_conf ? nullptr : c.take<float>((size_t)B * n1 * n3);
@@ -1770,7 +1774,9 @@ int attention_layer(const ApW& w, const Side* sd, int nside, int B, const Plan& 
         set_mf_planes(a.p[i], mf_of(i), kMfFloats);
       }
       a.p[i].stats = s.stats;
-      a.p[i].st_cnt = cnt + (size_t)i * B * kCntPerSide;
+      a.p[i].st_cnt = cnt + (size_t)i * B * p.cps;
+      a.p[i].st_cnt_bs = p.cps;
+      a.p[i].st_grp = s.stats == p.stats2 ? p.grp2 : p.grp3;
       a.p[i].st_mean = p.mean + (size_t)i * B * 512;
       a.p[i].st_rstd = p.rstd + (size_t)i * B * 512;
       a.p[i].ksum = p.ksum + (size_t)s.src * B * 256;
@@ -1902,7 +1908,7 @@ int match_impl(const void* packed_weights, const float* desc2d, int64_t desc2d_b
     sd[1] = {x3r, x3bs, p.x3[c3 ^ 1], p.phiq3, p.kvpart3, p.kspart3, p.y13, p.stats3, n3,
              (float)n3g, kind == 1 ? 1 : 0, sh ? sh->max_shard : n3};
     const int qkv_n3 = sh ? sh->max_shard : n3;
-    unsigned* lcnt = p.cnt + (size_t)(ap - 1) * 2 * B * kCntPerSide;
+    unsigned* lcnt = p.cnt + (size_t)(ap - 1) * 2 * B * p.cps;
     // layers 1-2 of a whole frame: per-side choices (the 3D side's are the object prefix's,
     // so cached and uncached forwards agree bit for bit at any batch); later layers and
     // sharded frames: one set for the launch

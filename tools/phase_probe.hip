@@ -57,6 +57,7 @@ static std::vector<float> g_lastY;   // Y of the last run (first M x N)
 
 struct Bufs {
   float *A, *W, *b, *Y, *stats, *mean, *rstd, *ksum;
+  double* grp;   // InstanceNorm group partials (gemm.h st_grp)
   uint16_t* Wp;   // 3 bf16 planes of W ([N][K] each, MMAX-sized stride)
   uint16_t* Ab;   // bf16 copy of A ([MMAX][K], round to nearest even)
   int64_t wpl;
@@ -77,6 +78,8 @@ void run(const char* name, Bufs& B, int M, int N, int K, bool fin, int iters) {
   }
   p.stats = B.stats;
   p.st_cnt = fin ? B.cnt : nullptr;
+  p.st_cnt_bs = 1024;   // one sample: the whole counter buffer
+  p.st_grp = B.grp;
   p.st_mean = B.mean;
   p.st_rstd = B.rstd;
   if (PRO == PRO_HEADZ) {   // K = [x (256) | phi(q) (256)] from the same A rows
@@ -238,6 +241,7 @@ int main() {
   hipMalloc(&B.rstd, 4096);
   hipMalloc(&B.ksum, 4096);
   hipMalloc(&B.cnt, 4096);
+  hipMalloc(&B.grp, 1 << 20);
   hipMalloc(&B.rec, 65536 * sizeof(WgRec));
   {
     unsigned long long* dp;
