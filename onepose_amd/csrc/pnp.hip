@@ -16,6 +16,10 @@
 // pose is a workgroup-parallel EPnP over the inliers.
 #include "common.h"
 
+#ifndef ONEPOSE_PNP_PHASE
+#define ONEPOSE_PNP_PHASE(i)   // tools/pnp_probe.hip: stamps the pose kernels' phases
+#endif
+
 namespace onepose {
 namespace {
 
@@ -1154,6 +1158,7 @@ __device__ __forceinline__ void epnp_refit(Shared& sh, const float* p2, const fl
     m6[5] += p2_ * p2_;
   }
   block_sum<6>(m6, sh.red);
+  ONEPOSE_PNP_PHASE(9);
   if (t == 0) {
     double m[9] = {m6[0], m6[1], m6[2], m6[1], m6[3], m6[4], m6[2], m6[4], m6[5]}, dc[3], uct[9];
     jacobi3(m, dc, uct);
@@ -1238,8 +1243,10 @@ __device__ __forceinline__ void epnp_refit(Shared& sh, const float* p2, const fl
       sh.jA[i] = v;
     }
     __syncthreads();
+    ONEPOSE_PNP_PHASE(10);
     jacobi12_block(sh);   // workgroup-collective -> sh.vs
     __syncthreads();
+    ONEPOSE_PNP_PHASE(11);
     if (t < 60) {   // compute_L_6x10, one entry per thread
       constexpr int pa[6] = {0, 0, 0, 1, 1, 2}, pb[6] = {1, 2, 3, 2, 3, 3};
       constexpr int cp[10] = {0, 0, 1, 0, 1, 2, 0, 1, 2, 3}, cq[10] = {0, 1, 1, 2, 2, 2, 3, 3, 3, 3};
@@ -1311,6 +1318,7 @@ __device__ __forceinline__ void epnp_refit(Shared& sh, const float* p2, const fl
     }
   }
   __syncthreads();
+  ONEPOSE_PNP_PHASE(12);
   // compute_pose's three approximations, one per wave (waves 0..2), each reducing over the
   // points with wave-level sums; wave 3 waits
   if (wave < 3) {
@@ -1389,6 +1397,7 @@ __device__ __forceinline__ void epnp_refit(Shared& sh, const float* p2, const fl
     }
   }
   __syncthreads();
+  ONEPOSE_PNP_PHASE(13);
   int N = 1;
   if (sh.sol_err[2] < sh.sol_err[1]) N = 2;
   if (sh.sol_err[3] < sh.sol_err[N]) N = 3;
@@ -1574,6 +1583,7 @@ __global__ __launch_bounds__(kThreads) void pnp_ransac_kernel(
   float* p3 = p2 + 2 * max_points;
   const int b = blockIdx.x;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  ONEPOSE_PNP_PHASE(0);
   int n;
   if (sel.matches0 != nullptr) {   // select: compact the valid matches (block-wide scan)
     const int64_t* m = sel.matches0 + (int64_t)b * sel.n1;
@@ -1644,6 +1654,7 @@ __global__ __launch_bounds__(kThreads) void pnp_ransac_kernel(
     }
   }
   const float thr = (float)((double)reproj * (double)reproj);
+  ONEPOSE_PNP_PHASE(1);
   if (t == 0) {
     sh.iter = 0;
     sh.niters = max(max_iters, 1);
@@ -1771,6 +1782,7 @@ __global__ __launch_bounds__(kThreads) void pnp_ransac_kernel(
       }
     }
     __syncthreads();
+    ONEPOSE_PNP_PHASE(2);
     // one EPnP model per hypothesis: wave 0 the eigenvectors (lane h = hypothesis h), then
     // waves 1..3 one approximation each for every hypothesis; the smallest mean error wins
     // (ties to the earlier approximation, as compute_pose's sequential comparison)
@@ -1779,6 +1791,7 @@ __global__ __launch_bounds__(kThreads) void pnp_ransac_kernel(
       sh.count[lane] = 0;
     }
     __syncthreads();
+    ONEPOSE_PNP_PHASE(3);
     double Rw[9], tw[3];
     if (wave > 0) {
       epnp5_approx(wave, sh.subset[lane], p2, p3, K4, sh.hh + lane, kRound, Rw, tw,
@@ -1801,6 +1814,7 @@ __global__ __launch_bounds__(kThreads) void pnp_ransac_kernel(
       }
     }
     __syncthreads();
+    ONEPOSE_PNP_PHASE(4);
     // inlier counts and OpenCV's acceptance rule, 16 iterations at a time: iterations past
     // the stopping point are neither counted nor accepted (wave w counts w, w + 4, ...;
     // lanes sweep the points)
@@ -1836,6 +1850,7 @@ __global__ __launch_bounds__(kThreads) void pnp_ransac_kernel(
       __syncthreads();
       if (sh.done) break;
     }
+    ONEPOSE_PNP_PHASE(5);
   }
 
   int nin;
@@ -1873,6 +1888,7 @@ __global__ __launch_bounds__(kThreads) void pnp_ransac_kernel(
     }
     nin = sh.n_inl;
   }
+  ONEPOSE_PNP_PHASE(6);
   if (n == kModelPoints)
     for (int i = t; i < n; i += kThreads) mask[i] = 1;
   if (t == 0) {   // the refit kernel reads these
@@ -1893,6 +1909,7 @@ __global__ __launch_bounds__(kThreads) void pnp_refit_kernel(
   const int b = blockIdx.x;
   const int t = threadIdx.x;
   double* pose = pose34 + (int64_t)b * 12;
+  ONEPOSE_PNP_PHASE(8);
   // pose_gt (onepose_pose_stage): query_pose_error of the frame's final pose, fused
   auto errors = [&]() {
     if (pose_gt != nullptr && t == 0)
@@ -1909,6 +1926,7 @@ __global__ __launch_bounds__(kThreads) void pnp_refit_kernel(
   const float* p3 = pts3d + (int64_t)b * max_points * 3;
   double Rf[9], tf[3], rv[3], Rr[9];
   epnp_refit(sh, p2, p3, idx_ws + (int64_t)b * max_points, nin, K4, Rf, tf);
+  ONEPOSE_PNP_PHASE(14);
   rodrigues_m2v(Rf, rv);
   rodrigues_v2m(rv, Rr);
   if (t == 0) {

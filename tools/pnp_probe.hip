@@ -1,12 +1,25 @@
-// Dev tool (not shipped): phase timeline of the EPnP refit kernel on one synthetic frame.
-//   hipcc -O3 --offload-arch=gfx950 -std=c++17 tools/pnp_probe.hip -o tools/pnp_probe
-#define ONEPOSE_PNP_PHASES 1
+// Where does the pose stage's time go?  Wraps pnp.hip's kernels with phase stamps (thread 0 of
+// workgroup 0 records s_memtime at each ONEPOSE_PNP_PHASE hook) and runs onepose_pnp_ransac on
+// one synthetic frame (tests/test_pnp_gpu.py's scene: cube of points 0.35-0.55 m away, 0.5 px
+// noise, a fraction of uniform outliers), serially, reporting per phase the median cycles.
+//
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -w -o tools/pnp_probe tools/pnp_probe.hip
+//   ./tools/pnp_probe [n] [outlier_frac]
+__device__ unsigned long long g_pph[16];
+__device__ unsigned g_pcnt[16];
+#define ONEPOSE_PNP_PHASE(i)                                   \
+  if (threadIdx.x == 0 && blockIdx.x == 0) {                   \
+    g_pph[(i)] = __builtin_amdgcn_s_memtime();                 \
+    g_pcnt[(i)] += 1u;                                         \
+  }
 #include "../onepose_amd/csrc/pnp.hip"
+#include <algorithm>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
 #include <random>
 #include <vector>
+
 namespace onepose {
 void set_error(const char* fmt, ...) { va_list ap; va_start(ap, fmt); vprintf(fmt, ap); va_end(ap); printf("\n"); }
 void clear_error() {}
@@ -14,47 +27,103 @@ void prof_pre(int, hipStream_t) {}
 void prof_post(int, hipStream_t) {}
 StampAcc* prof_stamp_slot(int) { return nullptr; }
 }
+
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e)); return 1; } } while (0)
+
 int main(int argc, char** argv) {
   const int n = argc > 1 ? atoi(argv[1]) : 700;
-  const double outl = argc > 2 ? atof(argv[2]) : 0.0;   // fraction of gross outliers
-  std::uniform_real_distribution<float> U01(0.f, 1.f), UI(0.f, 512.f);
-  std::mt19937 rng(3);
-  std::uniform_real_distribution<float> U(-100.f, 100.f);
-  std::normal_distribution<float> N(0.f, 0.5f);
+  const double out_frac = argc > 2 ? atof(argv[2]) : 0.3;
+  std::mt19937_64 rng(7);
+  std::uniform_real_distribution<double> U(0.0, 1.0);
+  std::normal_distribution<double> N01(0.0, 1.0);
   const double K[9] = {600, 0, 256, 0, 600, 256, 0, 0, 1};
-  const double R[9] = {0.36, 0.48, -0.8, -0.8, 0.6, 0, 0.48, 0.64, 0.6}, t[3] = {10, -20, 450};
+  double ax[3] = {N01(rng), N01(rng), N01(rng)};
+  const double an = std::sqrt(ax[0] * ax[0] + ax[1] * ax[1] + ax[2] * ax[2]), th = 2.0 * U(rng);
+  double R[9];
+
+  {
+    const double k0 = ax[0] / an, k1 = ax[1] / an, k2 = ax[2] / an, c = std::cos(th), s = std::sin(th);
+    const double C = 1 - c;
+    const double r[9] = {c + k0 * k0 * C, k0 * k1 * C - k2 * s, k0 * k2 * C + k1 * s,
+                         k1 * k0 * C + k2 * s, c + k1 * k1 * C, k1 * k2 * C - k0 * s,
+                         k2 * k0 * C - k1 * s, k2 * k1 * C + k0 * s, c + k2 * k2 * C};
+    for (int i = 0; i < 9; ++i) R[i] = r[i];
+  }
+  const double t[3] = {0.03 * (2 * U(rng) - 1), 0.03 * (2 * U(rng) - 1), 0.35 + 0.2 * U(rng)};
   std::vector<float> p2(2 * n), p3(3 * n);
   for (int i = 0; i < n; ++i) {
-    for (int k = 0; k < 3; ++k) p3[3 * i + k] = U(rng);
     double X[3];
-    for (int r = 0; r < 3; ++r) X[r] = R[3 * r] * p3[3 * i] + R[3 * r + 1] * p3[3 * i + 1] + R[3 * r + 2] * p3[3 * i + 2] + t[r];
-    p2[2 * i] = (float)(600 * X[0] / X[2] + 256) + N(rng);
-    p2[2 * i + 1] = (float)(600 * X[1] / X[2] + 256) + N(rng);
-    if (U01(rng) < outl) {
-      p2[2 * i] = UI(rng);
-      p2[2 * i + 1] = UI(rng);
+    for (int k = 0; k < 3; ++k) X[k] = (float)(0.2 * U(rng) - 0.1);
+    const double Xc = R[0] * X[0] + R[1] * X[1] + R[2] * X[2] + t[0];
+    const double Yc = R[3] * X[0] + R[4] * X[1] + R[5] * X[2] + t[1];
+    const double Zc = R[6] * X[0] + R[7] * X[1] + R[8] * X[2] + t[2];
+    double u = K[0] * Xc / Zc + K[2] + 0.5 * N01(rng), v = K[4] * Yc / Zc + K[5] + 0.5 * N01(rng);
+    if (U(rng) < out_frac) {
+      u = 512 * U(rng);
+      v = 512 * U(rng);
     }
+    p2[2 * i] = (float)u;
+    p2[2 * i + 1] = (float)v;
+    for (int k = 0; k < 3; ++k) p3[3 * i + k] = (float)(X[k] * 1000.0);
   }
-  float *d2, *d3; double *dK, *pose; int *cnt, *nin, *st; uint8_t* mask; void* ws;
-  hipMalloc(&d2, 8 * n); hipMalloc(&d3, 12 * n); hipMalloc(&dK, 72); hipMalloc(&pose, 96);
-  hipMalloc(&cnt, 4); hipMalloc(&nin, 4); hipMalloc(&st, 4); hipMalloc(&mask, n);
-  const size_t wsb = onepose_pnp_workspace_bytes(1, n, 10000); hipMalloc(&ws, wsb);
-  hipMemcpy(d2, p2.data(), 8 * n, hipMemcpyHostToDevice); hipMemcpy(d3, p3.data(), 12 * n, hipMemcpyHostToDevice);
-  hipMemcpy(dK, K, 72, hipMemcpyHostToDevice); hipMemcpy(cnt, &n, 4, hipMemcpyHostToDevice);
-  hipEvent_t e0, e1; hipEventCreate(&e0); hipEventCreate(&e1);
-  for (int it = 0; it < 3; ++it) {
-    hipEventRecord(e0);
-    onepose_pnp_ransac(d2, d3, cnt, n, dK, 0, 1, 1.0, 5.0f, 10000, 0.99, pose, mask, nin, st, ws, wsb, nullptr);
-    hipEventRecord(e1); hipEventSynchronize(e1);
-    float ms; hipEventElapsedTime(&ms, e0, e1);
-    unsigned long long ph[16]; hipMemcpyFromSymbol(ph, HIP_SYMBOL(g_pnp_phase), sizeof(ph));
-    int ni; hipMemcpy(&ni, nin, 4, hipMemcpyDeviceToHost);
-    printf("n=%d inliers=%d ransac+refit %.1f us | refit phases (us): MtM+reduce %.1f  assemble %.1f  eig+L %.1f  approx %.1f  total %.1f\n",
-           n, ni, ms * 1e3, (ph[1] - ph[0]) / 100.0, (ph[2] - ph[1]) / 100.0, (ph[3] - ph[2]) / 100.0,
-           (ph[4] - ph[3]) / 100.0, (ph[5] - ph[0]) / 100.0);
-    printf("  ransac phases (us, last round): load %.1f  subsets %.1f  epnp5 x64 %.1f  count %.1f  accept %.1f  mask %.1f\n",
-           (ph[8] - 0) * 0.0, (ph[9] - ph[8]) / 100.0, (ph[10] - ph[9]) / 100.0, (ph[11] - ph[10]) / 100.0,
-           (ph[12] - ph[11]) / 100.0, (ph[13] - ph[12]) / 100.0);
+  float *d2, *d3;
+  int *dcnt, *dnin, *dst;
+  double *dK, *dpose;
+  uint8_t* dmask;
+  void* ws;
+  const size_t wsb = onepose_pnp_workspace_bytes(1, n, 1000);
+  CK(hipMalloc(&d2, 8 * n));
+  CK(hipMalloc(&d3, 12 * n));
+  CK(hipMalloc(&dcnt, 4));
+  CK(hipMalloc(&dnin, 4));
+  CK(hipMalloc(&dst, 4));
+  CK(hipMalloc(&dK, 72));
+  CK(hipMalloc(&dpose, 96));
+  CK(hipMalloc(&dmask, n));
+  CK(hipMalloc(&ws, wsb));
+  CK(hipMemcpy(d2, p2.data(), 8 * n, hipMemcpyHostToDevice));
+  CK(hipMemcpy(d3, p3.data(), 12 * n, hipMemcpyHostToDevice));
+  CK(hipMemcpy(dcnt, &n, 4, hipMemcpyHostToDevice));
+  CK(hipMemcpy(dK, K, 72, hipMemcpyHostToDevice));
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  const int reps = 30;
+  std::vector<std::vector<double>> ph(16);
+  std::vector<double> ev;
+  unsigned cnt0[16] = {0}, cnt1[16];
+  int nin = 0;
+  for (int r = 0; r < reps; ++r) {
+    CK(hipMemcpyToSymbol(HIP_SYMBOL(g_pcnt), cnt0, sizeof(cnt0)));
+    CK(hipEventRecord(e0, 0));
+    if (onepose_pnp_ransac(d2, d3, dcnt, n, dK, 0, 1, 1000.0, 5.0f, 1000, 0.99, dpose, dmask, dnin,
+                           dst, ws, wsb, 0) != 0)
+      return 1;
+    CK(hipEventRecord(e1, 0));
+    CK(hipDeviceSynchronize());
+    float ms;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    ev.push_back(ms * 1e3);
+    unsigned long long st[16];
+    CK(hipMemcpyFromSymbol(st, HIP_SYMBOL(g_pph), sizeof(st)));
+    CK(hipMemcpyFromSymbol(cnt1, HIP_SYMBOL(g_pcnt), sizeof(cnt1)));
+    for (int i = 1; i < 16; ++i)
+      if (cnt1[i] && cnt1[i - 1]) ph[i].push_back((double)(long long)(st[i] - st[i - 1]));
+    CK(hipMemcpy(&nin, dnin, 4, hipMemcpyDeviceToHost));
   }
+  auto med = [](std::vector<double> v) {
+    if (v.empty()) return -1.0;
+    std::sort(v.begin(), v.end());
+    return v[v.size() / 2];
+  };
+  printf("n %d outliers %.2f inliers %d ransac rounds %u (hook 2 count)\n", n, out_frac, nin, cnt1[2]);
+  printf("both kernels, event-timed: median %.1f us\n", med(ev));
+  const char* names[16] = {"", "ransac: load / select", "ransac: deal subsets (last round)",
+                           "ransac: eig (last round)", "ransac: 3 approximations (last round)",
+                           "ransac: counts + accept (last round)", "ransac: inlier mask",
+                           "", "", "refit: centroid + PCA", "refit: M^T M sums", "refit: jacobi12",
+                           "refit: L, rho", "refit: 3 approximations", "refit: rest of epnp_refit", ""};
+  for (int i = 1; i < 15; ++i)
+    if (names[i][0]) printf("  %-40s %8.0f cycles (s_memtime)\n", names[i], med(ph[i]));
   return 0;
 }
