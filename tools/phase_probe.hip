@@ -281,6 +281,13 @@ int main() {
   using T64x128 = Tile<64, 128, 1, 4, 32>;
   using T64x128B = Tile<64, 128, 1, 4, 64>;
   for (int r = 0; r < 2; ++r) run<EPI_STATS, PRO_HEADZ, T64x64>("warm", B, 5120, 512, 512, true, 200);
+  printf("--- fp32 mlp1 stage time vs workgroups per CU (256 / 512 / 640 / 768 tiles) ---\n");
+  run<EPI_STATS, PRO_HEADZ, T64x64>("fp32 mlp1 1/CU", B, 2048, 512, 512, true, it);
+  run<EPI_STATS, PRO_HEADZ, T64x64>("fp32 mlp1 2/CU", B, 4096, 512, 512, true, it);
+  run<EPI_STATS, PRO_HEADZ, T64x64>("fp32 mlp1 2.5/CU", B, 5120, 512, 512, true, it);
+  run<EPI_STATS, PRO_HEADZ, T64x64>("fp32 mlp1 3/CU", B, 6144, 512, 512, true, it);
+  run<EPI_BIAS, PRO_PLAIN, T64x64>("fp32 plain 1/CU", B, 2048, 512, 512, false, it);
+  run<EPI_BIAS, PRO_PLAIN, T64x64>("fp32 plain 3/CU", B, 6144, 512, 512, false, it);
   printf("--- mlp1 epilogue breakdown (M 5120) ---\n");
   run<EPI_STATS, PRO_HEADZ, T64x64>("fp32 mlp1", B, 5120, 512, 512, true, it);
   run<EPI_STATS, PRO_HEADZ, T64x128, PM_BF16, 1>("bf16 mlp1", B, 5120, 512, 512, true, it);
