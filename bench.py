@@ -246,6 +246,8 @@ def main():
                     help="start each step from images: SuperPoint (max_keypoints = n1, nms 3, "
                          "threshold 0.005) on the GPU produces the query keypoints/descriptors")
     ap.add_argument("--image-size", type=int, default=512)
+    ap.add_argument("--pose-priority", type=int, default=0,
+                    help="diagnostic: HIP stream priority of the pose stream (lower = higher)")
     ap.add_argument("--unfused-pose", action="store_true",
                     help="pose stage as select + RANSAC-EPnP + errors (4 launches) instead of "
                          "onepose_pose_stage (2)")
@@ -291,6 +293,7 @@ def main():
                          image_hw=(args.image_size, args.image_size),
                          object_cache=not args.no_object_cache)
     pipe.fused_pose = not args.unfused_pose
+    pipe.pose_priority = args.pose_priority
     cached = pipe.object_cache is not None
     pipe.set_frames(data["descriptors2d_query"], data["keypoints2d"],
                     np.stack([f.K for f in frames]), np.stack([f.pose_gt for f in frames]))

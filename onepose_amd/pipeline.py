@@ -270,7 +270,8 @@ class FramePipeline:
         ms0 = match_stream or torch.cuda.current_stream(self.device)
         ps = pose_stream or getattr(self, "_pose_stream", None)
         if ps is None:
-            ps = self._pose_stream = torch.cuda.Stream(self.device)
+            ps = self._pose_stream = torch.cuda.Stream(
+                self.device, priority=getattr(self, "pose_priority", 0))
         extra = getattr(self, "_match_streams", [])
         while len(extra) < match_streams - 1:
             extra.append(torch.cuda.Stream(self.device))

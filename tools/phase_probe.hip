@@ -94,6 +94,13 @@ void run(const char* name, Bufs& B, int M, int N, int K, bool fin, int iters) {
     p.kspart = B.stats + (6 << 20);
     p.vdiv = 4096.f;
   }
+  if (EPI == EPI_SCORE) {   // S = D2 D3^T / scale: D3 rows from A's buffer (W holds 768 rows)
+    p.W = B.A + (size_t)8192 * 512;
+    p.ldw = K;
+    p.rowstat = B.stats;
+    p.colstat = B.stats + (4 << 20);
+    p.scale = 16.f;
+  }
   if (PRO == PRO_NORM_RELU) {
     p.pro_mean = B.mean;
     p.pro_rstd = B.rstd;
@@ -281,6 +288,12 @@ int main() {
   using T64x128 = Tile<64, 128, 1, 4, 32>;
   using T64x128B = Tile<64, 128, 1, 4, 64>;
   for (int r = 0; r < 2; ++r) run<EPI_STATS, PRO_HEADZ, T64x64>("warm", B, 5120, 512, 512, true, 200);
+  printf("--- score GEMM (config 2: 1024 x 4096, K 256) ---\n");
+  using T128x64W8 = Tile<128, 64, 1, 8, 32>;
+  for (int r = 0; r < 2; ++r) {
+    run<EPI_SCORE, PRO_PLAIN, T128x64W8>("fp32 score 128x64 W8", B, 1024, 4096, 256, false, it);
+    run<EPI_SCORE, PRO_PLAIN, T64x64>("fp32 score 64x64", B, 1024, 4096, 256, false, it);
+  }
   printf("--- fp32 mlp1 stage time vs workgroups per CU (256 / 512 / 640 / 768 tiles) ---\n");
   run<EPI_STATS, PRO_HEADZ, T64x64>("fp32 mlp1 1/CU", B, 2048, 512, 512, true, it);
   run<EPI_STATS, PRO_HEADZ, T64x64>("fp32 mlp1 2/CU", B, 4096, 512, 512, true, it);
