@@ -246,6 +246,9 @@ def main():
                     help="start each step from images: SuperPoint (max_keypoints = n1, nms 3, "
                          "threshold 0.005) on the GPU produces the query keypoints/descriptors")
     ap.add_argument("--image-size", type=int, default=512)
+    ap.add_argument("--diag-no-pose", action="store_true",
+                    help="diagnostic only (not the metric): skip the pose stage in the timed "
+                         "region, to measure what it costs the matcher streams")
     ap.add_argument("--pose-priority", type=int, default=0,
                     help="diagnostic: HIP stream priority of the pose stream (lower = higher)")
     ap.add_argument("--unfused-pose", action="store_true",
@@ -349,7 +352,7 @@ def main():
         if overlap:
             pipe.run_stream(k, graphs=stage_graphs,
                             marks=marks if record and args.stage_marks else None,
-                            match_streams=args.match_streams)
+                            match_streams=args.match_streams, pose=not args.diag_no_pose)
             return pipe.slots[(k - 1) % len(pipe.slots)]
         for _ in range(k):
             if step_graph is not None:
@@ -544,6 +547,8 @@ def main():
             "frame_roofline": frame_roof,
             **({"detector": det} if det else {}),
             "host_enqueue_ms_per_step": round(host_enqueue / args.steps * 1e3, 4),
+            **({"diagnostic": "pose stage skipped (--diag-no-pose): not the metric"}
+               if args.diag_no_pose else {}),
             **({"stage_ms": stage_ms} if stage_ms else {}),
             "kernel_ms_per_step": {k: round(v, 4) for k, v in sorted(total.items(),
                                                                      key=lambda kv: -kv[1])},

@@ -259,7 +259,7 @@ class FramePipeline:
         return out
 
     def run_stream(self, steps: int, match_stream=None, pose_stream=None, graphs=None,
-                   marks=None, match_streams: int = 1):
+                   marks=None, match_streams: int = 1, pose: bool = True):
         """Enqueue `steps` frames (batches) with matcher(k+1) overlapping pose(k); with
         `graphs` (from ``capture_stages``) each stage is one graph replay.  With
         `match_streams` = m > 1, consecutive frames' matchers run on m streams concurrently
@@ -303,10 +303,11 @@ class FramePipeline:
                     mk[1].record(ms)
             with torch.cuda.stream(ps):
                 ps.wait_event(matched[sl])
-                if graphs:
-                    graphs[sl][1].replay()
-                else:
-                    self.enqueue_pose(sl)
+                if pose:   # (False: a diagnostic of the matcher streams alone, bench.py)
+                    if graphs:
+                        graphs[sl][1].replay()
+                    else:
+                        self.enqueue_pose(sl)
                 posed[sl].record(ps)
                 if mk:
                     mk[2].record(ps)
