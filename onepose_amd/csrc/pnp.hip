@@ -16,6 +16,13 @@
 // pose is a workgroup-parallel EPnP over the inliers.
 #include "common.h"
 
+// Waves per SIMD the pose kernels are compiled for (amdgpu_waves_per_eu): 1 lets a wave use a
+// whole SIMD's register file; more caps its registers (spilling the rest) so that the one pose
+// workgroup per frame can share a CU with the matcher GEMMs' waves.
+#ifndef ONEPOSE_PNP_WPE
+#define ONEPOSE_PNP_WPE 1
+#endif
+
 #ifndef ONEPOSE_PNP_PHASE
 #define ONEPOSE_PNP_PHASE(i)   // tools/pnp_probe.hip: stamps the pose kernels' phases
 #endif
@@ -1571,7 +1578,8 @@ struct SelArgs {
   double scale3d;
 };
 
-__global__ __launch_bounds__(kThreads) void pnp_ransac_kernel(
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(ONEPOSE_PNP_WPE)))
+void pnp_ransac_kernel(
     const float* __restrict__ pts2d, const float* __restrict__ pts3d, const int* __restrict__ counts,
     int max_points, const double* __restrict__ Kmat, int64_t K_bs, double scale, float reproj,
     int max_iters, double confidence, double* __restrict__ pose34, uint8_t* __restrict__ mask_out,
@@ -1899,7 +1907,8 @@ __global__ __launch_bounds__(kThreads) void pnp_ransac_kernel(
 
 // EPnP on the RANSAC inliers (solvePnPRansac's final solvePnP call), then
 // Rodrigues(R) -> rvec -> Rodrigues(rvec) as eval_utils.py:31 rebuilds R, t / scale.
-__global__ __launch_bounds__(kThreads) void pnp_refit_kernel(
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(ONEPOSE_PNP_WPE)))
+void pnp_refit_kernel(
     const float* __restrict__ pts2d, const float* __restrict__ pts3d, int max_points,
     const double* __restrict__ Kmat, int64_t K_bs, double scale, double* __restrict__ pose34,
     const int* __restrict__ n_inliers, const int* __restrict__ status,
