@@ -249,6 +249,9 @@ def main():
     ap.add_argument("--diag-no-pose", action="store_true",
                     help="diagnostic only (not the metric): skip the pose stage in the timed "
                          "region, to measure what it costs the matcher streams")
+    ap.add_argument("--match-priority", type=int, default=0,
+                    help="diagnostic: HIP stream priority of the second and later matcher streams "
+                         "(lower = higher; the caller's stream keeps the default)")
     ap.add_argument("--pose-priority", type=int, default=0,
                     help="diagnostic: HIP stream priority of the pose stream (lower = higher)")
     ap.add_argument("--unfused-pose", action="store_true",
@@ -297,6 +300,7 @@ def main():
                          object_cache=not args.no_object_cache)
     pipe.fused_pose = not args.unfused_pose
     pipe.pose_priority = args.pose_priority
+    pipe.match_priority = args.match_priority
     cached = pipe.object_cache is not None
     pipe.set_frames(data["descriptors2d_query"], data["keypoints2d"],
                     np.stack([f.K for f in frames]), np.stack([f.pose_gt for f in frames]))

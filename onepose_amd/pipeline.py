@@ -274,7 +274,8 @@ class FramePipeline:
                 self.device, priority=getattr(self, "pose_priority", 0))
         extra = getattr(self, "_match_streams", [])
         while len(extra) < match_streams - 1:
-            extra.append(torch.cuda.Stream(self.device))
+            extra.append(torch.cuda.Stream(self.device,
+                                           priority=getattr(self, "match_priority", 0)))
         self._match_streams = extra
         mss = [ms0] + extra[:match_streams - 1]
         n = len(self.slots)
