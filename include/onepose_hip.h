@@ -171,6 +171,18 @@ int onepose_match_prepared(const void* packed_weights,
  *   leaves_prepared: [n3*L][256] point-major (onepose_prepare_leaves of the object)
  * The cache is shared by every sample of a batch (one object per call); it is read-only for
  * onepose_match_cached, so any number of streams may use one cache concurrently.
+ *
+ * The library records, per cache address, the (n3, num_leaf, precision, flags) that
+ * onepose_object_prepare built it with (host-side; nothing is read back from the device).
+ * onepose_match_cached returns ONEPOSE_ERR_INVALID for a cache it has no record of, or whose
+ * record differs from its own arguments: the layout depends on n3, num_leaf and flags, and
+ * the folded Mf weights are fp32 for ONEPOSE_PREC_FP32 and bf16 planes for the other
+ * precisions, so a mismatched call would read the wrong bytes. A copy of a cache at another
+ * address is therefore refused; prepare it there instead. onepose_object_release forgets a
+ * cache's record (call it before the memory is freed, if the allocator may hand the address
+ * to another cache that is not prepared again); a new onepose_object_prepare at the same
+ * address replaces the record. onepose_object_cache_bytes returns 0 for flags that prepare
+ * would refuse.
  * ------------------------------------------------------------------------------------ */
 enum {
   ONEPOSE_OBJ_GAT_TABLES = 1    /* build / use the GAT prefix tables (num_leaf <= 8)          */
@@ -181,6 +193,7 @@ int onepose_object_prepare(const void* packed_weights, const float* desc3d,
                            const float* leaves_prepared, int n3, int num_leaf, int precision,
                            int flags, float* cache, void* workspace, size_t workspace_bytes,
                            void* stream);
+void onepose_object_release(const float* cache);
 /* Workspace: onepose_match_workspace_bytes(batch, n1, n3, num_leaf, conf != NULL). */
 int onepose_match_cached(const void* packed_weights,
                          const float* desc2d, int64_t desc2d_bstride,

@@ -20,7 +20,7 @@ c_void_p, c_char_p = ctypes.c_void_p, ctypes.c_char_p
 
 # onepose_allgather_fn: int (*)(size_t bytes_per_rank, void* stream, void* user)
 ALLGATHER_FN = ctypes.CFUNCTYPE(c_int, c_size_t, c_void_p, c_void_p)
-ABI_VERSION = 2
+ABI_VERSION = 3
 OBJ_GAT_TABLES = 1   # ONEPOSE_OBJ_GAT_TABLES
 
 # name -> (restype, argtypes); mirrors include/onepose_hip.h
@@ -53,6 +53,7 @@ PROTOTYPES = {
     "onepose_object_prepare_workspace_bytes": (c_size_t, [c_int, c_int]),
     "onepose_object_prepare": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
                                        c_int, c_void_p, c_void_p, c_size_t, c_void_p]),
+    "onepose_object_release": (None, [c_void_p]),
     "onepose_match_cached": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_int64,
                                      c_int, c_int, c_int, c_int, c_float, c_float, c_int, c_int,
                                      c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,

@@ -24,11 +24,8 @@
 // Pins the pipeline's phase order (the compiler's own schedule measured within +-2%,
 // DESIGN.md §3d).
 #define ONEPOSE_SCHED_BARRIER() __builtin_amdgcn_sched_barrier(0)
-// Measurement hook: tools/phase_probe.hip defines it to stamp each workgroup's prologue / loop /
-// epilogue boundaries (s_memtime); empty in the library.
-#ifndef ONEPOSE_GEMM_PHASE
-#define ONEPOSE_GEMM_PHASE(i)
-#endif
+// "// @phase N" comments mark a workgroup's prologue / loop / epilogue boundaries; the
+// phase probe's generated copy of this file (tools/probe_src.sh) turns them into stamps.
 
 namespace onepose {
 
@@ -568,7 +565,7 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     store_stage<PRO, T, PM, WPL, NPL, false>(buf(kt0), sa);
     raw_barrier();
-    ONEPOSE_GEMM_PHASE(1);
+    // @phase 1
     // one stage: kt's fragments into tg (zd: phi(q) stage, its Z partials; zf >= 0: the head's
     // last stage, its Z rows to zrow[zf])
     auto stage = [&](int kt, floatx16 (&tg)[FN], bool zd, int zf) __attribute__((always_inline)) {
@@ -598,14 +595,14 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
         fold(h & 1);   // after the stage's barrier: every row's Z is in zrow
       }
     }
-    ONEPOSE_GEMM_PHASE(2);
+    // @phase 2
   } else {
   load_stage<PRO, T, WPL, NPL>(c, m0, n0, kt0 * T::BKS, s0);
   load_stage<PRO, T, WPL, NPL>(c, m0, n0, (kt0 + 1) * T::BKS, s1);
   tk = stamp_start(args.stamp, sl);
   store_stage<PRO, T, PM, WPL, NPL>(lds, s0);
   __syncthreads();
-  ONEPOSE_GEMM_PHASE(1);
+  // @phase 1
   read_frag(lds, f0);
   zdot(lds, kt0);   // the first phi(q) stage's Z partials when the x range is skipped
 
@@ -655,7 +652,7 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
       }
     }
   }
-  ONEPOSE_GEMM_PHASE(2);
+  // @phase 2
   }   // (register-staged loop)
   __syncthreads();   // every wave done with the LDS stages before they are reused below
   // profiling ticket after the K loop: no in-loop wait (vmcnt counts in order) includes the
@@ -864,7 +861,7 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
   }
   if (!kStage && !kRowStore) return;
   __syncthreads();
-  ONEPOSE_GEMM_PHASE(4);
+  // @phase 4
   // the row-store pass (STATS: issued behind its ticket's round trip, below)
   auto row_store = [&]() __attribute__((always_inline)) {
     constexpr int C4 = BN / 4, PER = BM * C4 / T::NT;   // float4 per row, per thread
@@ -956,7 +953,7 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
       const int col = min(n0 + t, N - 1);
       if (t < BN) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the storing wave drains
       __syncthreads();   // partial stores drained; `part` no longer read
-      ONEPOSE_GEMM_PHASE(5);
+      // @phase 5
       int* last = reinterpret_cast<int*>(part);
       unsigned ticket = 0u;
       if (t == 0)
@@ -966,7 +963,7 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
       const int gt0 = g1 * G, gsz = min(G, mtiles - gt0);
       if (t == 0) last[0] = ticket == (unsigned)(gsz - 1) ? 1 : 0;
       __syncthreads();
-      ONEPOSE_GEMM_PHASE(6);
+      // @phase 6
       if (last[0]) {
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // (no instruction: keeps the
                                                                  // loads below the ticket)
@@ -1133,6 +1130,14 @@ TileDims tile_dims(int tile) {
 }  // namespace
 
 int gemm_tile_rows(int tile) { return tile_dims(tile).bm; }
+
+static_assert(gemm_tile_bm(TILE_64x64) == 64 && gemm_tile_bn(TILE_64x64) == 64 &&
+                  gemm_tile_bm(TILE_32x128) == 32 && gemm_tile_bn(TILE_32x128) == 128 &&
+                  gemm_tile_bm(TILE_64x32K2) == 64 && gemm_tile_bn(TILE_64x32K2) == 32 &&
+                  gemm_tile_bm(TILE_64x128) == 64 && gemm_tile_bn(TILE_64x128) == 128 &&
+                  gemm_tile_bm(TILE_128x128) == 128 && gemm_tile_bn(TILE_128x128) == 128 &&
+                  gemm_tile_bm(TILE_128x64W8) == 128 && gemm_tile_bn(TILE_128x64W8) == 64,
+              "gemm.h tile shapes must match tile_dims");
 
 GemmProb gemm_prob(const float* A, int lda, const float* W, int ldw, const float* bias,
                    float* Y, int ldy, int M, int N, int K, int batch) {

@@ -35,6 +35,8 @@
 
 #include <algorithm>
 #include <atomic>
+#include <mutex>
+#include <unordered_map>
 
 namespace onepose {
 
@@ -1191,6 +1193,14 @@ struct Plan {
 // with the W planes); MLP conv 2 keeps 64 x 64
 constexpr int kTileBf16 = TILE_64x128;
 int mlp1_tile(int pm) { return pm == PM_BF16 ? kTileBf16 : kTileMLP1; }
+// make_plan sizes MLP conv 1's InstanceNorm partials (stats rows `str`), its arrival counters
+// (kCntPerSide column blocks) and group partials once for every precision: each precision's
+// MLP conv 1 tile must have those rows and at most that many column blocks over N = 512.
+static_assert(gemm_tile_bm(kTileBf16) == gemm_tile_bm(kTileMLP1),
+              "MLP conv 1 tiles of all precisions must share their row count");
+static_assert(512 / gemm_tile_bn(kTileMLP1) <= kCntPerSide &&
+                  512 / gemm_tile_bn(kTileBf16) <= kCntPerSide,
+              "MLP conv 1 column blocks exceed the plan's counters");
 
 int qkv_tile_for(int n3, int B) {
   const int64_t t64 = (int64_t)ceil_div(n3, 64) * 6 * (B > kFusedFoldMaxBatch ? B : 1);
@@ -1206,7 +1216,7 @@ Plan make_plan(void* ws, int B, int n1, int n3, int L, bool with_conf) {
     p.x3[i] = c.take<float>(t3 * 256);
   }
   const int ch2 = ceil_div(n1, 64), ch3 = ceil_div(n3, 64);   // score tiles
-  const int kvr = gemm_tile_rows(kTileKV), str = gemm_tile_rows(kTileMLP1);
+  const int kvr = gemm_tile_rows(kTileKV), str = gemm_tile_bm(kTileMLP1);   // = every mlp1_tile
   p.kvpart2 = c.take<float>((size_t)B * ceil_div(n1, kvr) * 16384);
   p.kvpart3 = c.take<float>((size_t)B * ceil_div(n3, kvr) * 16384);
   p.kspart2 = c.take<float>((size_t)B * ceil_div(n1, kvr) * 256);
@@ -1255,7 +1265,7 @@ using namespace onepose;
 extern "C" {
 
 const char* onepose_last_error(void) { return g_last_error.c_str(); }
-int onepose_abi_version(void) { return 2; }
+int onepose_abi_version(void) { return 3; }
 
 int onepose_profile_begin(uint64_t kind_mask, int capacity) {
   clear_error();
@@ -2226,6 +2236,7 @@ int onepose_match_prepared(const void* packed_weights, const float* desc2d,
 
 size_t onepose_object_cache_bytes(int n3, int num_leaf, int flags) {
   if (n3 <= 0 || num_leaf < 1 || num_leaf > 16) return 0;
+  if ((flags & ~ONEPOSE_OBJ_GAT_TABLES) != 0) return 0;   // the flags prepare / match refuse
   return (size_t)obj_layout(n3, num_leaf, flags).total * sizeof(float);
 }
 
@@ -2234,6 +2245,25 @@ size_t onepose_object_prepare_workspace_bytes(int n3, int num_leaf) {
   if (n3 <= 0 || num_leaf < 1 || num_leaf > 16) return 0;
   return make_plan(nullptr, 1, 1, n3, num_leaf, false).bytes;
 }
+
+}  // extern "C"
+
+namespace onepose {
+namespace {
+// What onepose_object_prepare built into each cache, keyed by the cache's device address. The
+// cache's layout depends on (n3, num_leaf, flags) and its Mf region's format on the precision
+// (fp32, or bf16 planes), and the device copy cannot be read back without a synchronisation,
+// which a graph-captured launch must not do. So the host records them at prepare time and
+// onepose_match_cached refuses a cache whose record is missing or differs from its arguments.
+struct CacheRecord {
+  int n3, num_leaf, precision, flags;
+};
+std::mutex g_cache_mu;
+std::unordered_map<const void*, CacheRecord> g_caches;
+}  // namespace
+}  // namespace onepose
+
+extern "C" {
 
 int onepose_object_prepare(const void* packed_weights, const float* desc3d,
                            const float* leaves_prepared, int n3, int num_leaf, int precision,
@@ -2253,8 +2283,22 @@ int onepose_object_prepare(const void* packed_weights, const float* desc3d,
     return ONEPOSE_ERR_WORKSPACE;
   }
   const Plan p = make_plan(workspace, 1, 1, n3, num_leaf, false);
-  return object_prepare_impl(packed_weights, desc3d, leaves_prepared, n3, num_leaf, precision,
-                             flags, cache, p, static_cast<hipStream_t>(stream_));
+  {
+    std::lock_guard<std::mutex> lk(g_cache_mu);
+    g_caches.erase(cache);   // whatever it held before is gone from here on
+  }
+  const int rc = object_prepare_impl(packed_weights, desc3d, leaves_prepared, n3, num_leaf,
+                                     precision, flags, cache, p, static_cast<hipStream_t>(stream_));
+  if (rc == ONEPOSE_OK) {
+    std::lock_guard<std::mutex> lk(g_cache_mu);
+    g_caches[cache] = {n3, num_leaf, precision, flags};
+  }
+  return rc;
+}
+
+void onepose_object_release(const float* cache) {
+  std::lock_guard<std::mutex> lk(g_cache_mu);
+  g_caches.erase(cache);
 }
 
 int onepose_match_cached(const void* packed_weights, const float* desc2d, int64_t desc2d_bstride,
@@ -2273,6 +2317,19 @@ int onepose_match_cached(const void* packed_weights, const float* desc2d, int64_
                             num_leaf, scale_factor, matches0, matches1, mscores0, mscores1,
                             workspace);
   if (rc != ONEPOSE_OK) return rc;
+  {
+    std::lock_guard<std::mutex> lk(g_cache_mu);
+    const auto it = g_caches.find(object_cache);
+    OP_REQUIRE(it != g_caches.end(),
+               "match_cached: object_cache was not built by onepose_object_prepare (or was "
+               "released)");
+    const CacheRecord& c = it->second;
+    OP_REQUIRE(c.n3 == n3 && c.num_leaf == num_leaf && c.precision == precision &&
+                   c.flags == object_flags,
+               "match_cached: cache prepared for n3=%d num_leaf=%d precision=%d flags=%d, "
+               "called with n3=%d num_leaf=%d precision=%d flags=%d",
+               c.n3, c.num_leaf, c.precision, c.flags, n3, num_leaf, precision, object_flags);
+  }
   const Plan need = make_plan(nullptr, batch, n1, n3, num_leaf, conf != nullptr);
   if (workspace_bytes < need.bytes) {
     set_error("match_cached: workspace %zu < %zu bytes", workspace_bytes, need.bytes);

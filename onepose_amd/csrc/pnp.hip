@@ -16,16 +16,10 @@
 // pose is a workgroup-parallel EPnP over the inliers.
 #include "common.h"
 
-// Waves per SIMD the pose kernels are compiled for (amdgpu_waves_per_eu): 1 lets a wave use a
-// whole SIMD's register file; more caps its registers (spilling the rest) so that the one pose
-// workgroup per frame can share a CU with the matcher GEMMs' waves.
-#ifndef ONEPOSE_PNP_WPE
-#define ONEPOSE_PNP_WPE 1
-#endif
-
-#ifndef ONEPOSE_PNP_PHASE
-#define ONEPOSE_PNP_PHASE(i)   // tools/pnp_probe.hip: stamps the pose kernels' phases
-#endif
+// The pose kernels are compiled for one wave per SIMD (amdgpu_waves_per_eu(1)): a wave may use
+// a whole SIMD's register file. 2 and 4 were measured slower or equal.
+// "// @phase N" comments mark the pose kernels' phases; the pose probe's generated copy of
+// this file (tools/probe_src.sh) turns them into stamps.
 
 namespace onepose {
 namespace {
@@ -1165,7 +1159,7 @@ __device__ __forceinline__ void epnp_refit(Shared& sh, const float* p2, const fl
     m6[5] += p2_ * p2_;
   }
   block_sum<6>(m6, sh.red);
-  ONEPOSE_PNP_PHASE(9);
+  // @phase 9
   if (t == 0) {
     double m[9] = {m6[0], m6[1], m6[2], m6[1], m6[3], m6[4], m6[2], m6[4], m6[5]}, dc[3], uct[9];
     jacobi3(m, dc, uct);
@@ -1250,10 +1244,10 @@ __device__ __forceinline__ void epnp_refit(Shared& sh, const float* p2, const fl
       sh.jA[i] = v;
     }
     __syncthreads();
-    ONEPOSE_PNP_PHASE(10);
+    // @phase 10
     jacobi12_block(sh);   // workgroup-collective -> sh.vs
     __syncthreads();
-    ONEPOSE_PNP_PHASE(11);
+    // @phase 11
     if (t < 60) {   // compute_L_6x10, one entry per thread
       constexpr int pa[6] = {0, 0, 0, 1, 1, 2}, pb[6] = {1, 2, 3, 2, 3, 3};
       constexpr int cp[10] = {0, 0, 1, 0, 1, 2, 0, 1, 2, 3}, cq[10] = {0, 1, 1, 2, 2, 2, 3, 3, 3, 3};
@@ -1325,7 +1319,7 @@ __device__ __forceinline__ void epnp_refit(Shared& sh, const float* p2, const fl
     }
   }
   __syncthreads();
-  ONEPOSE_PNP_PHASE(12);
+  // @phase 12
   // compute_pose's three approximations, one per wave (waves 0..2), each reducing over the
   // points with wave-level sums; wave 3 waits
   if (wave < 3) {
@@ -1404,7 +1398,7 @@ __device__ __forceinline__ void epnp_refit(Shared& sh, const float* p2, const fl
     }
   }
   __syncthreads();
-  ONEPOSE_PNP_PHASE(13);
+  // @phase 13
   int N = 1;
   if (sh.sol_err[2] < sh.sol_err[1]) N = 2;
   if (sh.sol_err[3] < sh.sol_err[N]) N = 3;
@@ -1578,7 +1572,7 @@ struct SelArgs {
   double scale3d;
 };
 
-__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(ONEPOSE_PNP_WPE)))
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(1)))
 void pnp_ransac_kernel(
     const float* __restrict__ pts2d, const float* __restrict__ pts3d, const int* __restrict__ counts,
     int max_points, const double* __restrict__ Kmat, int64_t K_bs, double scale, float reproj,
@@ -1591,7 +1585,7 @@ void pnp_ransac_kernel(
   float* p3 = p2 + 2 * max_points;
   const int b = blockIdx.x;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  ONEPOSE_PNP_PHASE(0);
+  // @phase 0
   int n;
   if (sel.matches0 != nullptr) {   // select: compact the valid matches (block-wide scan)
     const int64_t* m = sel.matches0 + (int64_t)b * sel.n1;
@@ -1662,7 +1656,7 @@ void pnp_ransac_kernel(
     }
   }
   const float thr = (float)((double)reproj * (double)reproj);
-  ONEPOSE_PNP_PHASE(1);
+  // @phase 1
   if (t == 0) {
     sh.iter = 0;
     sh.niters = max(max_iters, 1);
@@ -1790,7 +1784,7 @@ void pnp_ransac_kernel(
       }
     }
     __syncthreads();
-    ONEPOSE_PNP_PHASE(2);
+    // @phase 2
     // one EPnP model per hypothesis: wave 0 the eigenvectors (lane h = hypothesis h), then
     // waves 1..3 one approximation each for every hypothesis; the smallest mean error wins
     // (ties to the earlier approximation, as compute_pose's sequential comparison)
@@ -1799,7 +1793,7 @@ void pnp_ransac_kernel(
       sh.count[lane] = 0;
     }
     __syncthreads();
-    ONEPOSE_PNP_PHASE(3);
+    // @phase 3
     double Rw[9], tw[3];
     if (wave > 0) {
       epnp5_approx(wave, sh.subset[lane], p2, p3, K4, sh.hh + lane, kRound, Rw, tw,
@@ -1822,7 +1816,7 @@ void pnp_ransac_kernel(
       }
     }
     __syncthreads();
-    ONEPOSE_PNP_PHASE(4);
+    // @phase 4
     // inlier counts and OpenCV's acceptance rule, 16 iterations at a time: iterations past
     // the stopping point are neither counted nor accepted (wave w counts w, w + 4, ...;
     // lanes sweep the points)
@@ -1858,7 +1852,7 @@ void pnp_ransac_kernel(
       __syncthreads();
       if (sh.done) break;
     }
-    ONEPOSE_PNP_PHASE(5);
+    // @phase 5
   }
 
   int nin;
@@ -1896,7 +1890,7 @@ void pnp_ransac_kernel(
     }
     nin = sh.n_inl;
   }
-  ONEPOSE_PNP_PHASE(6);
+  // @phase 6
   if (n == kModelPoints)
     for (int i = t; i < n; i += kThreads) mask[i] = 1;
   if (t == 0) {   // the refit kernel reads these
@@ -1907,7 +1901,7 @@ void pnp_ransac_kernel(
 
 // EPnP on the RANSAC inliers (solvePnPRansac's final solvePnP call), then
 // Rodrigues(R) -> rvec -> Rodrigues(rvec) as eval_utils.py:31 rebuilds R, t / scale.
-__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(ONEPOSE_PNP_WPE)))
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(1)))
 void pnp_refit_kernel(
     const float* __restrict__ pts2d, const float* __restrict__ pts3d, int max_points,
     const double* __restrict__ Kmat, int64_t K_bs, double scale, double* __restrict__ pose34,
@@ -1918,7 +1912,7 @@ void pnp_refit_kernel(
   const int b = blockIdx.x;
   const int t = threadIdx.x;
   double* pose = pose34 + (int64_t)b * 12;
-  ONEPOSE_PNP_PHASE(8);
+  // @phase 8
   // pose_gt (onepose_pose_stage): query_pose_error of the frame's final pose, fused
   auto errors = [&]() {
     if (pose_gt != nullptr && t == 0)
@@ -1935,7 +1929,7 @@ void pnp_refit_kernel(
   const float* p3 = pts3d + (int64_t)b * max_points * 3;
   double Rf[9], tf[3], rv[3], Rr[9];
   epnp_refit(sh, p2, p3, idx_ws + (int64_t)b * max_points, nin, K4, Rf, tf);
-  ONEPOSE_PNP_PHASE(14);
+  // @phase 14
   rodrigues_m2v(Rf, rv);
   rodrigues_v2m(rv, Rr);
   if (t == 0) {

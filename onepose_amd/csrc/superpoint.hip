@@ -1009,22 +1009,11 @@ int conv_launch(const float* x, int B, int H, int W, const float* packed, int la
   return ONEPOSE_OK;
 }
 
-// Tile sweep hook for the 512^2..128^2 layers (ONEPOSE_SP_TILE, measurement only).
+// The 512^2..128^2 layers on TileBig (the tile sweep of docs/EXPERIMENTS.md §3b chose it).
 template <int CIN, bool POOL>
 int big_conv(const float* x, int B, int H, int W, const float* packed, int layer, float* y,
              hipStream_t st) {
-  static const int v = [] {
-    const char* e = getenv("ONEPOSE_SP_TILE");
-    return e ? atoi(e) : 0;
-  }();
-  switch (v) {
-    case 1: return conv_launch<CIN, 3, ConvTile<4, 1, 2, 1>, POOL, CE_RELU>(x, B, H, W, packed, layer, y, st);
-    case 2: return conv_launch<CIN, 3, ConvTile<2, 2, 1, 2>, POOL, CE_RELU>(x, B, H, W, packed, layer, y, st);
-    case 3: return conv_launch<CIN, 3, ConvTile<2, 1, 2, 1>, POOL, CE_RELU>(x, B, H, W, packed, layer, y, st);
-    case 5: return conv_launch<CIN, 3, ConvTile<4, 2, 1, 1>, POOL, CE_RELU>(x, B, H, W, packed, layer, y, st);
-    case 6: return conv_launch<CIN, 3, ConvTile<2, 2, 1, 3>, POOL, CE_RELU>(x, B, H, W, packed, layer, y, st);
-    default: return conv_launch<CIN, 3, TileBig, POOL, CE_RELU>(x, B, H, W, packed, layer, y, st);
-  }
+  return conv_launch<CIN, 3, TileBig, POOL, CE_RELU>(x, B, H, W, packed, layer, y, st);
 }
 
 constexpr int kMaxSortKeypoints = 16384;

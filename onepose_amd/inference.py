@@ -1,21 +1,45 @@
 """``inference.py``-compatible driver on the HIP engine (reference ``inference.py:17-200``).
 
-Same inputs (an object's SfM annotation directory, a sequence directory of cropped images
-with per-image ``intrin_ba`` / ``poses_ba`` text files, a matcher checkpoint, a keypoint
-extractor) and the same per-frame steps and outputs (cm/deg evaluator summary). What
-changes against the reference loop:
+The reference's entry chain, with its signatures and ``cfg`` keys (any attribute-style
+object: a Hydra ``DictConfig``, ``types.SimpleNamespace``; Hydra itself is out of scope):
 
-* the object's tensors go to the GPU once per object; ``pack_data`` re-uploads them every
-  frame (``inference.py:80-94``);
-* the matcher is ``onepose_amd.matcher.GATsSuperGlue`` (C-ABI, HIP), the pose solve
-  ``onepose_amd.pose.ransac_PnP`` (HIP RANSAC-EPnP), the evaluator ``onepose_amd.pose.Evaluator``;
-* the extractor is any callable ``image [1,1,H,W] -> {'keypoints', 'descriptors', ...}``.
-  The reference's SuperPoint module is one; this repository's GPU backbone is §8f's next row.
+* ``inference(cfg)`` (``inference.py:185-198``): ``cfg.input.data_dirs`` /
+  ``cfg.input.sfm_model_dirs``, each data dir ``"<data_root> <seq> <seq> ..."``;
+* ``inference_core(cfg, data_root, seq_dir, sfm_model_dir)`` (``:97-182``): per frame
+  extractor -> ``pack_data`` -> ``pred, _ = matching_model(inp)`` -> valid matches ->
+  ``ransac_PnP(K_crop, mkpts2d, mkpts3d, scale=1000)`` -> ``Evaluator``; then
+  ``record_eval_result(cfg.output.eval_dir, obj, seq, summary)`` (``eval_utils.py:7-15``);
+* ``load_model(cfg)`` (``:49-77``): ``cfg.model.onepose_model_path`` (a ``LitModelGATsSPG``
+  checkpoint) and ``cfg.model.extractor_model_path`` (SuperPoint weights),
+  ``cfg.network.detection``;
+* ``get_default_paths(cfg, data_root, data_dir, sfm_model_dir)`` (``:17-46``),
+  ``pack_data(...)`` (``:80-94``), ``cfg.num_leaf``, ``cfg.object_detect_mode``.
 
-Frames keep their own keypoint count (the detector thresholds at 0.6,
-``extract_features.py:19-24``), so each frame runs at its true size: padding would change
-the matcher's attention and InstanceNorm results. For fixed-size streams, ``FramePipeline``
-is the graph-replayed throughput path.
+What changes against the reference loop:
+
+* the matcher is ``onepose_amd.matcher.GATsSuperGlue`` (C-ABI, HIP) inside
+  ``onepose_amd.lightning_model.LitModelGATsSPG``, the extractor ``onepose_amd.superpoint.SuperPoint``
+  (HIP), the pose solve ``onepose_amd.pose.ransac_PnP`` (HIP RANSAC-EPnP), the evaluator
+  ``onepose_amd.pose.Evaluator``;
+* the object's descriptors are moved to the GPU once per sequence, before the frame loop;
+  ``pack_data``'s ``.cuda()`` is then a no-op instead of a per-frame re-upload
+  (``inference.py:89-90``);
+* images are read with PIL instead of ``cv2.imread`` (cv2 is absent here; for the 8-bit
+  grayscale crops OnePose stores the two give the same array), and listed in sorted order
+  (the reference takes ``glob`` order);
+* ``cfg.save_wis3d`` visualisation is out of scope and is skipped.
+
+Frames keep their own keypoint count: the detector keeps every keypoint above its threshold,
+up to ``max_keypoints`` = 4096. That threshold is SuperPoint's default 0.005:
+``extract_features.py:19-24`` spells the key ``keypoints_threshold``, which
+``SuperPoint.default_config`` (``keypoint_threshold``) does not read, so its 0.6 never
+applies. Each frame runs at its true size: padding would change the matcher's attention and
+InstanceNorm results. For fixed-size streams, ``FramePipeline`` is the graph-replayed
+throughput path.
+
+The round-1 helpers stay, under their own names: ``default_paths`` (``get_default_paths``
+without a cfg), ``inference_core_with_models`` (``inference_core`` over already-built
+models), ``run_frames`` and ``match_and_pose``.
 """
 from __future__ import annotations
 
@@ -56,10 +80,10 @@ def get_intrin_path_by_color(color_path: str, det_type: str = "GT_box") -> str:
     raise NotImplementedError(det_type)
 
 
-def get_default_paths(data_dir: str, sfm_model_dir: str, detection: str = "superpoint",
-                      matching: str = "superglue", object_detect_mode: str = "GT_box"):
-    """inference.py:17-47: (image list, paths). Images are sorted (the reference takes glob
-    order)."""
+def default_paths(data_dir: str, sfm_model_dir: str, detection: str = "superpoint",
+                  matching: str = "superglue", object_detect_mode: str = "GT_box"):
+    """inference.py:17-47 without the cfg: (image list, paths). Images are sorted (the
+    reference takes glob order)."""
     anno_dir = os.path.join(sfm_model_dir, f"outputs_{detection}_{matching}", "anno")
     if object_detect_mode == "GT_box":
         color_dir = os.path.join(data_dir, "color")
@@ -79,6 +103,14 @@ def get_default_paths(data_dir: str, sfm_model_dir: str, detection: str = "super
     return img_lists, paths
 
 
+def get_default_paths(cfg, data_root, data_dir, sfm_model_dir):
+    """``inference.py:17-46``: the reference signature; ``cfg.network.detection`` /
+    ``.matching`` name the annotation directory, ``cfg.object_detect_mode`` the image one."""
+    img_lists, paths = default_paths(data_dir, sfm_model_dir, cfg.network.detection,
+                                     cfg.network.matching, cfg.object_detect_mode)
+    return img_lists, {"data_root": data_root, **paths}
+
+
 # ------------------------------------------------------------------ model and object
 def load_matcher(model_path: str | None = None, state_dict=None, hparams=None) -> GATsSuperGlue:
     """The matcher of a ``LitModelGATsSPG`` checkpoint (``inference.py:50-59``).
@@ -89,18 +121,17 @@ def load_matcher(model_path: str | None = None, state_dict=None, hparams=None) -
     the matcher config unless ``hparams`` is given. A checkpoint whose hyper-parameters need
     unpickling of foreign classes is refused by the safe loader; pass ``state_dict`` +
     ``hparams`` explicitly then."""
+    from .lightning_model import matcher_hparams, read_checkpoint
     if state_dict is None:
-        ckpt = torch.load(model_path, map_location="cpu", weights_only=True)
-        sd = ckpt.get("state_dict", ckpt)
-        if hparams is None and isinstance(ckpt.get("hyper_parameters"), dict):
-            hparams = dict(ckpt["hyper_parameters"])
+        sd, ckpt_hp = read_checkpoint(model_path)
+        if hparams is None:
+            hparams = ckpt_hp
     else:
         sd = state_dict
-    if any(k.startswith("matcher.") for k in sd):
-        sd = {k[len("matcher."):]: v for k, v in sd.items() if k.startswith("matcher.")}
+        if any(k.startswith("matcher.") for k in sd):
+            sd = {k[len("matcher."):]: v for k, v in sd.items() if k.startswith("matcher.")}
     if hparams is not None:
-        from .synthetic import DEFAULT_HPARAMS
-        hparams = {**DEFAULT_HPARAMS, **{k: hparams[k] for k in DEFAULT_HPARAMS if k in hparams}}
+        hparams = matcher_hparams(hparams)
     return from_state_dict(sd, hparams)
 
 
@@ -169,14 +200,16 @@ def run_frames(matcher: GATsSuperGlue, obj: OnePoseObject, frames, scale: float 
     return ev.summarize(), out
 
 
-def inference_core(matcher: GATsSuperGlue, extractor, seq_dir: str, sfm_model_dir: str,
-                   num_leaf: int = 8, object_detect_mode: str = "GT_box", device="cuda",
-                   detection: str = "superpoint", matching: str = "superglue"):
-    """inference.py:97-177 for one sequence (no visualisation): returns the evaluator summary.
-    ``extractor(image [1,1,H,W] on device)`` returns the reference SuperPoint's output dict
-    (keys 'keypoints' [1][n,2], 'descriptors' [1][256,n])."""
-    img_lists, paths = get_default_paths(seq_dir, sfm_model_dir, detection, matching,
-                                         object_detect_mode)
+def inference_core_with_models(matcher: GATsSuperGlue, extractor, seq_dir: str,
+                               sfm_model_dir: str, num_leaf: int = 8,
+                               object_detect_mode: str = "GT_box", device="cuda",
+                               detection: str = "superpoint", matching: str = "superglue"):
+    """inference.py:97-177 for one sequence over already-built models (no visualisation, no
+    result file): returns the evaluator summary. ``extractor(image [1,1,H,W] on device)``
+    returns the reference SuperPoint's output dict (keys 'keypoints' [1][n,2],
+    'descriptors' [1][256,n])."""
+    img_lists, paths = default_paths(seq_dir, sfm_model_dir, detection, matching,
+                                     object_detect_mode)
     obj = OnePoseObject.from_anno_dir(paths["anno_dir"], num_leaf, device)
     ev = pose.Evaluator()
     for img_path in img_lists:
@@ -194,3 +227,159 @@ def seed_reference_stream(seed: int = REFERENCE_SEED):
     """The numpy / torch seeding ``inference.py:14`` performs at import."""
     np.random.seed(seed)
     torch.manual_seed(seed)
+
+
+# ------------------------------------------------------------------ the reference entry chain
+def load_matching_model(model_path):
+    """``inference.py:51-60``: the checkpoint's ``LitModelGATsSPG``, on the GPU, frozen."""
+    from .lightning_model import LitModelGATsSPG
+    trained_model = LitModelGATsSPG.load_from_checkpoint(checkpoint_path=model_path)
+    trained_model.cuda()
+    trained_model.eval()
+    trained_model.freeze()
+    return trained_model
+
+
+def load_extractor_model(cfg, model_path):
+    """``inference.py:62-73``: SuperPoint with ``confs[cfg.network.detection]['conf']``
+    (``extract_features.py:7-26``), weights by ``model_io.load_network`` semantics."""
+    from .superpoint import SuperPoint, confs
+    extractor_model = SuperPoint(confs[cfg.network.detection]["conf"])
+    extractor_model.cuda()
+    extractor_model.eval()
+    extractor_model.load_network(model_path)
+    return extractor_model
+
+
+def load_model(cfg):
+    """``inference.py:49-77``: ``(matching_model, extractor_model)`` from
+    ``cfg.model.onepose_model_path`` and ``cfg.model.extractor_model_path``."""
+    matching_model = load_matching_model(cfg.model.onepose_model_path)
+    extractor_model = load_extractor_model(cfg, cfg.model.extractor_model_path)
+    return matching_model, extractor_model
+
+
+def pack_data(avg_descriptors3d, clt_descriptors, keypoints3d, detection, image_size):
+    """``inference.py:80-94``: the matcher's input dict (batch of one). Tensors already on
+    the GPU stay where they are (``.cuda()`` is a no-op for them)."""
+    keypoints2d = torch.Tensor(detection["keypoints"])
+    descriptors2d = torch.Tensor(detection["descriptors"])
+    return {
+        "keypoints2d": keypoints2d[None].cuda(),                 # [1, n1, 2]
+        "keypoints3d": keypoints3d[None].cuda(),                 # [1, n2, 3]
+        "descriptors2d_query": descriptors2d[None].cuda(),       # [1, dim, n1]
+        "descriptors3d_db": avg_descriptors3d[None].cuda(),      # [1, dim, n2]
+        "descriptors2d_db": clt_descriptors[None].cuda(),        # [1, dim, n2*num_leaf]
+        "image_size": image_size,
+    }
+
+
+class NormalizedDataset:
+    """``src/datasets/normalized_dataset.py:8-45`` (images already cropped): item ``{'path',
+    'image' [1,H,W] or [3,H,W] float32 / 255, 'size' [H, W]}``. PIL reads the file."""
+    default_conf = {"globs": ["*.jpg", "*.png"], "grayscale": True}
+
+    def __init__(self, img_lists, conf):
+        self.img_lists = img_lists
+        self.conf = {**self.default_conf, **conf}
+        if len(img_lists) == 0:
+            raise ValueError("Could not find any image.")
+
+    def __getitem__(self, index):
+        img_path = self.img_lists[index]
+        image, size = load_image(img_path, self.conf["grayscale"])
+        return {"path": str(img_path), "image": image, "size": np.array(size)}
+
+    def __len__(self):
+        return len(self.img_lists)
+
+    def batches(self):
+        """What ``DataLoader(dataset, num_workers=1)`` yields: each item collated into a
+        batch of one (``path`` a list, ``image`` [1,...] and ``size`` [1,2] tensors)."""
+        for i in range(len(self)):
+            d = self[i]
+            yield {"path": [d["path"]], "image": torch.from_numpy(d["image"])[None],
+                   "size": torch.from_numpy(d["size"])[None]}
+
+
+def load_object(paths, num_leaf):
+    """``inference.py:112-130``: keypoints3d, padded average descriptors and leaf descriptors
+    from the three annotation files (the leaves consume the global numpy stream)."""
+    avg_data = np.load(paths["avg_anno_3d_path"])
+    clt_data = np.load(paths["clt_anno_3d_path"])
+    idxs = np.load(paths["idxs_path"])
+    keypoints3d = torch.Tensor(clt_data["keypoints3d"]).cuda()
+    num_3d = keypoints3d.shape[0]
+    avg_descriptors3d, _ = data_utils.pad_features3d_random(
+        avg_data["descriptors3d"], avg_data["scores3d"], num_3d)
+    clt_descriptors, _ = data_utils.build_features3d_leaves(
+        clt_data["descriptors3d"], clt_data["scores3d"], idxs, num_3d, num_leaf)
+    return keypoints3d, avg_descriptors3d, clt_descriptors
+
+
+def frame_step(matching_model, extractor_model, data, K_crop, keypoints3d, avg_descriptors3d,
+               clt_descriptors):
+    """One iteration of ``inference.py:133-155`` up to the pose: ``(pose_pred,
+    pose_pred_homo, inliers, mkpts2d, mkpts3d, mconf)``."""
+    inp = data["image"].cuda()
+    pred_detection = extractor_model(inp)
+    pred_detection = {k: v[0].cpu().numpy() for k, v in pred_detection.items()}
+    inp_data = pack_data(avg_descriptors3d, clt_descriptors, keypoints3d, pred_detection,
+                         data["size"])
+    pred, _ = matching_model(inp_data)
+    matches = pred["matches0"].detach().cpu().numpy()
+    valid = matches > -1
+    kpts2d = pred_detection["keypoints"]
+    kpts3d = inp_data["keypoints3d"][0].detach().cpu().numpy()
+    confidence = pred["matching_scores0"].detach().cpu().numpy()
+    mkpts2d, mkpts3d, mconf = kpts2d[valid], kpts3d[matches[valid]], confidence[valid]
+    pose_pred, pose_pred_homo, inliers = pose.ransac_PnP(K_crop, mkpts2d, mkpts3d, scale=1000)
+    return pose_pred, pose_pred_homo, inliers, mkpts2d, mkpts3d, mconf
+
+
+@torch.no_grad()
+def inference_core(cfg, data_root, seq_dir, sfm_model_dir):
+    """``inference.py:97-182``: evaluate one sequence and write
+    ``<cfg.output.eval_dir>/<obj><seq>.txt``. Returns the evaluator summary (the reference
+    returns None; the file is the same)."""
+    from .superpoint import confs
+    matching_model, extractor_model = load_model(cfg)
+    img_lists, paths = get_default_paths(cfg, data_root, seq_dir, sfm_model_dir)
+    dataset = NormalizedDataset(img_lists, confs[cfg.network.detection]["preprocessing"])
+    evaluator = pose.Evaluator()
+    keypoints3d, avg_descriptors3d, clt_descriptors = load_object(paths, cfg.num_leaf)
+    # resident for the whole sequence: pack_data's .cuda() is then free per frame
+    avg_descriptors3d, clt_descriptors = avg_descriptors3d.cuda(), clt_descriptors.cuda()
+    if getattr(cfg, "save_wis3d", False):
+        print("onepose_amd: save_wis3d visualisation is out of scope; skipped")
+    for data in dataset.batches():
+        img_path = data["path"][0]
+        K_crop = np.loadtxt(get_intrin_path_by_color(img_path, det_type=cfg.object_detect_mode))
+        pose_pred, _, _, *_ = frame_step(matching_model, extractor_model, data, K_crop,
+                                         keypoints3d, avg_descriptors3d, clt_descriptors)
+        gt_pose_path = get_gt_pose_path_by_color(img_path, det_type=cfg.object_detect_mode)
+        evaluator.evaluate(pose_pred, np.loadtxt(gt_pose_path))
+    eval_result = evaluator.summarize()
+    obj_name = sfm_model_dir.split("/")[-1]
+    seq_name = seq_dir.split("/")[-1]
+    pose.record_eval_result(cfg.output.eval_dir, obj_name, seq_name, eval_result)
+    return eval_result
+
+
+def inference(cfg):
+    """``inference.py:185-198``: every ``"<data_root> <seq> ..."`` entry of
+    ``cfg.input.data_dirs`` against the matching ``cfg.input.sfm_model_dirs`` entry."""
+    data_dirs = cfg.input.data_dirs
+    sfm_model_dirs = cfg.input.sfm_model_dirs
+    if isinstance(data_dirs, str) and isinstance(sfm_model_dirs, str):
+        data_dirs = [data_dirs]
+        sfm_model_dirs = [sfm_model_dirs]
+    results = {}
+    for data_dir, sfm_model_dir in zip(data_dirs, sfm_model_dirs):
+        splits = data_dir.split(" ")
+        data_root = splits[0]
+        for seq_name in splits[1:]:
+            seq_dir = os.path.join(data_root, seq_name)
+            print(f"Eval {seq_dir}")
+            results[seq_dir] = inference_core(cfg, data_root, seq_dir, sfm_model_dir)
+    return results

@@ -130,6 +130,16 @@ class FramePipeline:
         self.slots = [_Slot(B, n1, self.n3, dev, with_conf, self.lib, self.L, self.iters,
                             self.image_hw) for _ in range(max(1, slots))]
 
+    def __del__(self):
+        # drop the library's record of this object cache before its memory goes back to the
+        # allocator (onepose_object_release; a later cache at the address is prepared anew)
+        cache = self.__dict__.get("object_cache")
+        if cache is not None:
+            try:
+                self.lib.onepose_object_release(cache.data_ptr())
+            except Exception:
+                pass
+
     def __getattr__(self, name):
         # slot-0 outputs as attributes (pipe.pose, pipe.matches0, ...) for the common case
         slots = self.__dict__.get("slots")

@@ -7,11 +7,15 @@ Drop-ins (same names, argument meaning and failure behaviour as the reference):
   (fewer than 4 points) it prints ``CV ERROR`` and returns ``eye(4)[:3], eye(4), []``.
 * ``query_pose_error(pose_pred, pose_gt)`` -- ``eval_utils.py:45-63``.
 * ``Evaluator`` -- ``src/evaluators/cmd_evaluator.py:3-62`` (1/3/5 cm-deg rates).
+* ``record_eval_result(out_dir, obj_name, seq_name, eval_result)`` -- ``eval_utils.py:7-15``.
 
 Batched device APIs used by the pipeline (no host round trip per frame):
 ``select_correspondences``, ``ransac_pnp_batch``, ``pose_errors``.
 """
 from __future__ import annotations
+
+import os
+from pathlib import Path
 
 import numpy as np
 import torch
@@ -124,6 +128,17 @@ def ransac_PnP(K, pts_2d, pts_3d, scale=1):
     pose_homo = np.concatenate([pose, np.array([[0, 0, 0, 1]])], axis=0)
     inliers = np.nonzero(mask[0].cpu().numpy())[0].astype(np.int32).reshape(-1, 1)
     return pose, pose_homo, inliers
+
+
+def record_eval_result(out_dir, obj_name, seq_name, eval_result):
+    """``eval_utils.record_eval_result``: one ``key: value`` line per summary entry in
+    ``<out_dir>/<obj_name><seq_name>.txt`` (the directory is created)."""
+    Path(out_dir).mkdir(exist_ok=True, parents=True)
+    out_file = os.path.join(out_dir, obj_name + seq_name + ".txt")
+    with open(out_file, "w") as f:
+        for k, v in eval_result.items():
+            f.write(f"{k}: {v}\n")
+    return out_file
 
 
 def query_pose_error(pose_pred, pose_gt):

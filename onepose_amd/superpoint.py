@@ -23,6 +23,20 @@ import torch
 from . import _lib
 
 
+# src/sfm/extract_features.py:7-26, as the reference writes it. The 'keypoints_threshold' key
+# is not SuperPoint's 'keypoint_threshold': the reference detector ignores it and keeps its
+# default 0.005, and so does this one (SuperPoint merges unknown keys without reading them).
+confs = {
+    "superpoint": {
+        "output": "feats-spp",
+        "model": {"name": "spp_det"},
+        "preprocessing": {"grayscale": True, "resize_h": 512, "resize_w": 512},
+        "conf": {"descriptor_dim": 256, "nms_radius": 3, "max_keypoints": 4096,
+                 "keypoints_threshold": 0.6},
+    }
+}
+
+
 def reference_align_corners() -> bool:
     return int(torch.__version__[2]) > 2
 

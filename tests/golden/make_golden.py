@@ -190,6 +190,38 @@ def evaluator_case():
     print("evaluator:", summ)
 
 
+def eval_record_case():
+    """eval_utils.record_eval_result (eval_utils.py:7-15) on the Evaluator summary of
+    evaluator_case's poses, written by the reference into a scratch directory; the file name
+    and text are stored. eval_utils.py:1 imports cv2, which record_eval_result never uses."""
+    import tempfile
+    import types
+    from src.evaluators.cmd_evaluator import Evaluator
+    added = []
+    if "cv2" not in sys.modules:
+        sys.modules["cv2"] = types.ModuleType("cv2")
+        added.append("cv2")
+    try:
+        from src.utils import eval_utils
+    finally:
+        for name in added:
+            del sys.modules[name]
+    z = np.load(os.path.join(HERE, "evaluator.npz"))
+    ev = Evaluator()
+    for p, g in zip(z["preds"], z["gts"]):
+        ev.evaluate(p, g)
+    summ = ev.summarize()
+    with tempfile.TemporaryDirectory() as d:
+        out_dir = os.path.join(d, "runs", "eval", "GATsSPG")
+        eval_utils.record_eval_result(out_dir, "0408-colorbox-box", "colorbox-4", summ)
+        names = os.listdir(out_dir)
+        text = open(os.path.join(out_dir, names[0])).read()
+    np.savez_compressed(os.path.join(HERE, "eval_record.npz"), names=np.array(names),
+                        text=np.array(text), summary=np.array([summ["cmd1"], summ["cmd3"],
+                                                               summ["cmd5"]]))
+    print("eval_record:", names, repr(text))
+
+
 def object_inputs(seed=21, n3=60, dim=256):
     """Synthetic SfM object: per-3D-point observation counts 1..12, unit descriptors."""
     rs = np.random.RandomState(seed)
@@ -329,6 +361,7 @@ def main():
     empty_case()
     sample_desc_case()
     evaluator_case()
+    eval_record_case()
     object_case()
     superpoint_case()
     anno3d_case()

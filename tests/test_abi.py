@@ -30,7 +30,7 @@ def test_library_exports_every_header_symbol():
     missing = [s for s in header_symbols() if not hasattr(lib, s)]
     assert not missing, missing
     assert set(header_symbols()) == set(_lib.PROTOTYPES), "ctypes prototypes out of sync"
-    assert lib.onepose_abi_version() == _lib.ABI_VERSION == 2
+    assert lib.onepose_abi_version() == _lib.ABI_VERSION == 3
 
 
 def test_object_cache_size_follows_its_flags():
@@ -49,6 +49,7 @@ def test_object_cache_size_follows_its_flags():
     assert lib.onepose_object_cache_bytes(4096, 8, 0) < 18.4e6
     assert lib.onepose_object_cache_bytes(0, 8, 0) == 0
     assert lib.onepose_object_cache_bytes(16, 17, 0) == 0
+    assert lib.onepose_object_cache_bytes(16, 8, 2) == 0 and lib.onepose_object_cache_bytes(16, 8, -1) == 0
 
 
 def test_tensor_list_matches_reference_state_dict():

@@ -10,7 +10,7 @@ import torch
 
 from onepose_amd import data_utils as DU
 from onepose_amd import inference as I
-from onepose_amd import matcher, synthetic as S
+from onepose_amd import matcher, pose, synthetic as S
 
 pytestmark = pytest.mark.gpu
 
@@ -21,7 +21,7 @@ def test_inference_core_on_disk(tmp_path, device):
     seq, sfm = tmp_path / "obj-1", tmp_path / "sfm" / "obj"
     for d in ("color", "intrin_ba", "poses_ba"):
         (seq / d).mkdir(parents=True)
-    _, paths = I.get_default_paths(str(seq), str(sfm))
+    _, paths = I.default_paths(str(seq), str(sfm))
     DU.save_object_annotations(paths["anno_dir"], obj.keypoints3d, obj.clt_descriptors,
                                obj.clt_scores, obj.idxs)
     frames = [S.make_frame(obj, 200 + 37 * i, seed=40 + i) for i in range(4)]   # ragged n1
@@ -40,7 +40,7 @@ def test_inference_core_on_disk(tmp_path, device):
 
     m = matcher.from_state_dict(S.make_state_dict(0))
     I.seed_reference_stream()
-    summary = I.inference_core(m, extractor, str(seq), str(sfm), num_leaf=8, device=device)
+    summary = I.inference_core_with_models(m, extractor, str(seq), str(sfm), num_leaf=8, device=device)
     assert calls == [0, 1, 2, 3]
     assert summary["cmd5"] == 1.0 and summary["cmd1"] == 1.0
 
@@ -65,7 +65,7 @@ def test_inference_core_with_gpu_superpoint(tmp_path, device):
     seq, sfm = tmp_path / "obj-2", tmp_path / "sfm" / "obj2"
     for d in ("color", "intrin_ba", "poses_ba"):
         (seq / d).mkdir(parents=True)
-    _, paths = I.get_default_paths(str(seq), str(sfm))
+    _, paths = I.default_paths(str(seq), str(sfm))
     DU.save_object_annotations(paths["anno_dir"], obj.keypoints3d, obj.clt_descriptors,
                                obj.clt_scores, obj.idxs)
     frames = [S.make_frame(obj, 300, seed=60 + i) for i in range(3)]
@@ -81,7 +81,7 @@ def test_inference_core_with_gpu_superpoint(tmp_path, device):
     sp.to(device)
     m = matcher.from_state_dict(S.make_state_dict(0))
     I.seed_reference_stream()
-    summary = I.inference_core(m, sp, str(seq), str(sfm), num_leaf=8, device=device)
+    summary = I.inference_core_with_models(m, sp, str(seq), str(sfm), num_leaf=8, device=device)
     dets = []
     for im in imgs:
         img = torch.from_numpy(im.astype(np.float32) / 255.0)[None, None].to(device)
@@ -94,3 +94,120 @@ def test_inference_core_with_gpu_superpoint(tmp_path, device):
           for (k, d), f in zip(dets, frames)]
     summary2, _ = I.run_frames(m, o, fr)
     assert summary2 == summary
+
+
+def _write_sequence(tmp_path, obj, frames, images):
+    """data_root/seq-1/{color,intrin_ba,poses_ba} + sfm/obj/outputs_superpoint_superglue/anno."""
+    from PIL import Image
+    root, sfm = tmp_path / "root", tmp_path / "sfm" / "obj"
+    seq = root / "seq-1"
+    for d in ("color", "intrin_ba", "poses_ba"):
+        (seq / d).mkdir(parents=True)
+    _, paths = I.default_paths(str(seq), str(sfm))
+    DU.save_object_annotations(paths["anno_dir"], obj.keypoints3d, obj.clt_descriptors,
+                               obj.clt_scores, obj.idxs)
+    for i, (f, im) in enumerate(zip(frames, images)):
+        Image.fromarray(im, mode="L").save(seq / "color" / f"{i}.png")
+        np.savetxt(seq / "intrin_ba" / f"{i}.txt", f.K)
+        np.savetxt(seq / "poses_ba" / f"{i}.txt", np.concatenate([f.pose_gt, [[0, 0, 0, 1]]]))
+    return root, seq, sfm, paths
+
+
+def _cfg(tmp_path, root, sfm, ckpt, spp):
+    """The keys configs/experiment/test_GATsSPG.yaml gives inference(cfg)."""
+    from types import SimpleNamespace as N
+    return N(type="inference", num_leaf=8, object_detect_mode="GT_box", save_wis3d=False,
+             model=N(onepose_model_path=str(ckpt), extractor_model_path=str(spp)),
+             network=N(detection="superpoint", matching="superglue"),
+             input=N(data_dirs=f"{root} seq-1", sfm_model_dirs=str(sfm)),
+             output=N(eval_dir=str(tmp_path / "runs" / "eval" / "GATsSPG")))
+
+
+def _write_models(tmp_path, sd):
+    ckpt = {"state_dict": {"matcher." + k: torch.from_numpy(v) for k, v in sd.items()},
+            "hyper_parameters": dict(S.DEFAULT_HPARAMS)}
+    torch.save(ckpt, tmp_path / "GATsSPG.ckpt")
+    torch.save({k: torch.from_numpy(v) for k, v in S.superpoint_state_dict(0).items()},
+               tmp_path / "superpoint_v1.pth")
+    return tmp_path / "GATsSPG.ckpt", tmp_path / "superpoint_v1.pth"
+
+
+def test_inference_cfg_entry_and_reference_call_sequence(tmp_path, device, monkeypatch):
+    """inference(cfg) (inference.py:185-198) over an on-disk sequence: the result file
+    eval_utils.record_eval_result writes; then one frame through the reference's own call
+    sequence (pack_data with image_size -> pred, _ = matching_model(inp) -> .detach().cpu()
+    .numpy() -> ransac_PnP(K, mkpts2d, mkpts3d, scale=1000)) equals FramePipeline's
+    device-resident result for that frame. The extractor returns the synthetic frames'
+    detections (random-weight SuperPoint descriptors never match a synthetic object)."""
+    from onepose_amd.pipeline import FramePipeline
+    obj = S.make_object(600, seed=8)
+    frames = [S.make_frame(obj, 200 + 37 * i, seed=40 + i) for i in range(3)]
+    images = [np.full((32, 32), 17 * i, np.uint8) for i in range(len(frames))]
+    root, seq, sfm, paths = _write_sequence(tmp_path, obj, frames, images)
+    ckpt, spp = _write_models(tmp_path, S.make_state_dict(0))
+
+    def fake_extractor(cfg, model_path):
+        assert model_path == str(spp)
+        def extract(img):   # frame i has a uniform image of value 17*i / 255
+            f = frames[int(round(float(img.flatten()[0]) * 255 / 17))]
+            return {"keypoints": [torch.from_numpy(f.keypoints2d)],
+                    "descriptors": [torch.from_numpy(f.descriptors2d)],
+                    "scores": [torch.ones(len(f.keypoints2d))]}
+        return extract
+    monkeypatch.setattr(I, "load_extractor_model", fake_extractor)
+    cfg = _cfg(tmp_path, root, sfm, ckpt, spp)
+    I.seed_reference_stream()
+    res = I.inference(cfg)
+    out_file = tmp_path / "runs" / "eval" / "GATsSPG" / "objseq-1.txt"
+    assert out_file.read_text() == "cmd1: 1.0\ncmd3: 1.0\ncmd5: 1.0\n"
+    assert list(res.values())[0] == {"cmd1": 1.0, "cmd3": 1.0, "cmd5": 1.0}
+
+    # frame 1 through the reference call sequence, over the same leaves (same numpy stream)
+    I.seed_reference_stream()
+    kp3, avg, clt = I.load_object(paths, 8)
+    matching_model, extract = I.load_model(cfg)
+    f = frames[1]
+    det = {k: v[0].cpu().numpy() for k, v in extract(torch.full((1, 1, 32, 32), 17 / 255.)).items()}
+    inp = I.pack_data(avg, clt, kp3, det, torch.tensor([[32, 32]]))
+    assert tuple(inp["descriptors2d_db"].shape) == (1, 256, 600 * 8)
+    pred, _ = matching_model(inp)
+    matches = pred["matches0"].detach().cpu().numpy()
+    valid = matches > -1
+    mk2, mk3 = det["keypoints"][valid], inp["keypoints3d"][0].detach().cpu().numpy()[matches[valid]]
+    pose_ref, pose_homo, inliers = pose.ransac_PnP(f.K, mk2, mk3, scale=1000)
+
+    pipe = FramePipeline(matching_model.matcher, kp3.cpu().numpy(), avg.numpy(), clt.numpy(), 1,
+                         len(f.keypoints2d), device, gat_tables=False)
+    pipe.set_frames(f.descriptors2d[None], f.keypoints2d[None], f.K, f.pose_gt)
+    pipe.enqueue(0)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(pipe.matches0[0].cpu().numpy(), matches)
+    assert int(pipe.status[0]) == 0 and int(pipe.n_inliers[0]) == len(inliers)
+    pose_pipe = pipe.pose[0].cpu().numpy()
+    # north_star tolerance: 1e-4 rad / 1e-3 translation; the two paths run the same kernels
+    np.testing.assert_allclose(pose_pipe, pose_ref, rtol=0, atol=1e-9)
+    assert np.array_equal(pose_homo[3], [0, 0, 0, 1])
+
+
+def test_inference_cfg_with_loaded_superpoint(tmp_path, device):
+    """inference(cfg) with the real load_model: the LitModelGATsSPG checkpoint and the
+    SuperPoint weights file; ragged textured frames. The result file equals the summary of
+    the round-1 driver over the same models (an independent loop), both seeded alike."""
+    from onepose_amd.superpoint import SuperPoint, confs
+    obj = S.make_object(500, seed=9)
+    frames = [S.make_frame(obj, 300, seed=60 + i) for i in range(3)]
+    images = [(S.superpoint_image(128, 128, 20 + i) * 255).round().astype(np.uint8)
+              for i in range(3)]
+    root, seq, sfm, paths = _write_sequence(tmp_path, obj, frames, images)
+    ckpt, spp = _write_models(tmp_path, S.make_state_dict(0))
+    cfg = _cfg(tmp_path, root, sfm, ckpt, spp)
+    I.seed_reference_stream()
+    res = list(I.inference(cfg).values())[0]
+    text = (tmp_path / "runs" / "eval" / "GATsSPG" / "objseq-1.txt").read_text()
+    assert text == "".join(f"{k}: {res[k]}\n" for k in ("cmd1", "cmd3", "cmd5"))
+    sp = SuperPoint(confs["superpoint"]["conf"]).cuda()
+    sp.load_network(str(spp))
+    I.seed_reference_stream()
+    summary = I.inference_core_with_models(I.load_matcher(str(ckpt)).to(device), sp, str(seq),
+                                           str(sfm), num_leaf=8, device=device)
+    assert summary == res

@@ -319,3 +319,57 @@ def test_matcher_tiny_and_odd_shapes(n1, n3, L, device):
     assert np.isfinite(conf).all()
     np.testing.assert_allclose(conf, oconf, atol=ATOL)
     assert_pred_equal(pred, opred, f"{n1}x{n3} L={L}")
+
+
+def test_object_cache_mismatch_is_refused(device):
+    """a cache prepared with (n3, num_leaf, precision, flags) and matched with any
+    other value would read the wrong layout (GAT tables past the allocation) or the wrong Mf
+    format (fp32 vs bf16 planes). onepose_match_cached refuses it before launching anything;
+    an unprepared or released cache is refused too."""
+    from onepose_amd import _lib
+    lib = _lib.load()
+    n1, n3, L = 64, 128, 8
+    sd = synthetic.make_state_dict(0)
+    data, _, _ = synthetic.make_matcher_inputs(n1, n3, L, seed=2)
+    m = matcher.from_state_dict(sd)
+    w = m.packed_weights(device)
+    f32 = dict(dtype=torch.float32, device=device)
+    s = _lib.stream_ptr(device)
+    d2 = torch.from_numpy(data["descriptors2d_query"]).to(device).contiguous()
+    d3 = torch.from_numpy(data["descriptors3d_db"][0]).to(device).contiguous()
+    lv = torch.from_numpy(data["descriptors2d_db"][0]).to(device).contiguous()
+    pm = torch.empty(lib.onepose_leaves_prepared_bytes(1, n3, L) // 4, **f32)
+    _lib.check(lib.onepose_prepare_leaves(lv.data_ptr(), 0, 1, n3, L, pm.data_ptr(), s), "leaves")
+    big = lib.onepose_object_cache_bytes(n3, L, _lib.OBJ_GAT_TABLES)
+    cache = torch.empty(big // 4, **f32)
+    other = torch.empty(big // 4, **f32)
+    wsb = lib.onepose_object_prepare_workspace_bytes(n3, L)
+    ws = torch.empty(wsb, dtype=torch.uint8, device=device)
+    _lib.check(lib.onepose_object_prepare(w.data_ptr(), d3.data_ptr(), pm.data_ptr(), n3, L, 0, 0,
+                                          cache.data_ptr(), ws.data_ptr(), wsb, s), "prepare")
+    wsm_b = lib.onepose_match_workspace_bytes(1, n1, n3, L, 0)
+    wsm = torch.empty(wsm_b, dtype=torch.uint8, device=device)
+    o = [torch.empty(n1, dtype=torch.int64, device=device),
+         torch.empty(n3, dtype=torch.int64, device=device),
+         torch.empty(n1, **f32), torch.empty(n3, **f32)]
+
+    def call(buf, n3_=n3, prec=0, flags=0):
+        return lib.onepose_match_cached(
+            w.data_ptr(), d2.data_ptr(), 256 * n1, buf.data_ptr(), pm.data_ptr(), 0, 1, n1, n3_, L,
+            0.07, 0.2, prec, flags, *[t.data_ptr() for t in o], None, wsm.data_ptr(), wsm_b, s)
+
+    assert call(cache) == 0
+    torch.cuda.synchronize()
+    for kw in ({"flags": _lib.OBJ_GAT_TABLES}, {"prec": 1}, {"prec": 2}, {"n3_": n3 - 1}):
+        assert call(cache, **kw) == 1, kw                 # ONEPOSE_ERR_INVALID
+        assert b"match_cached: cache prepared for" in lib.onepose_last_error()
+    assert call(other) == 1                               # never prepared
+    lib.onepose_object_release(cache.data_ptr())
+    assert call(cache) == 1                               # released
+    _lib.check(lib.onepose_object_prepare(w.data_ptr(), d3.data_ptr(), pm.data_ptr(), n3, L, 1,
+                                          _lib.OBJ_GAT_TABLES, cache.data_ptr(), ws.data_ptr(),
+                                          wsb, s), "prepare bf16 + tables")
+    assert call(cache, prec=1, flags=_lib.OBJ_GAT_TABLES) == 0
+    assert call(cache) == 1
+    torch.cuda.synchronize()
+    lib.onepose_object_release(cache.data_ptr())

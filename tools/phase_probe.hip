@@ -3,11 +3,11 @@
 // plus its CU from HW_ID / XCC_ID), and reports per launch: event time, device span, the
 // in-kernel clock, workgroup duration spread, dispatch skew and per-CU load.
 //
-//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -w -o tools/phase_probe tools/phase_probe.hip
+//   bash tools/probe_src.sh   (generates _gen/gemm.hip with the stamps, then builds)
 __device__ unsigned long long* g_phase;
 #define ONEPOSE_GEMM_PHASE(i) \
   if (threadIdx.x == 0) g_phase[blockIdx.x * 8 + (i)] = __builtin_amdgcn_s_memtime();
-#include "../onepose_amd/csrc/gemm.hip"
+#include "_gen/gemm.hip"   // tools/probe_src.sh
 #include <algorithm>
 #include <cmath>
 #include <cstdio>

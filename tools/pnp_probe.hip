@@ -1,9 +1,9 @@
 // Where does the pose stage's time go?  Wraps pnp.hip's kernels with phase stamps (thread 0 of
-// workgroup 0 records s_memtime at each ONEPOSE_PNP_PHASE hook) and runs onepose_pnp_ransac on
+// workgroup 0 records s_memtime at each "// @phase" marker) and runs onepose_pnp_ransac on
 // one synthetic frame (tests/test_pnp_gpu.py's scene: cube of points 0.35-0.55 m away, 0.5 px
 // noise, a fraction of uniform outliers), serially, reporting per phase the median cycles.
 //
-//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -w -o tools/pnp_probe tools/pnp_probe.hip
+//   bash tools/probe_src.sh   (generates _gen/pnp.hip with the stamps, then builds)
 //   ./tools/pnp_probe [n] [outlier_frac]
 __device__ unsigned long long g_pph[16];
 __device__ unsigned g_pcnt[16];
@@ -12,7 +12,7 @@ __device__ unsigned g_pcnt[16];
     g_pph[(i)] = __builtin_amdgcn_s_memtime();                 \
     g_pcnt[(i)] += 1u;                                         \
   }
-#include "../onepose_amd/csrc/pnp.hip"
+#include "_gen/pnp.hip"   // tools/probe_src.sh
 #include <algorithm>
 #include <cmath>
 #include <cstdarg>
