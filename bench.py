@@ -282,7 +282,13 @@ def main():
 
     B, n1, n3, L = args.batch, args.n1, args.n3, args.leaf
     sd = synthetic.make_state_dict(0)
-    data, obj, frames = synthetic.make_matcher_inputs(n1, n3, L, seed=rank * 7919, batch=B)
+    # One object's batch (BASELINE config 4): every rank builds the same object
+    # and weights; the global batch is world * B frames of that object's sequence, generated
+    # from one seed, and this rank runs its contiguous frame_shard slice of it.  The gathered
+    # result rows come back in global frame order.
+    n_global = world * B
+    fs, fe = D.frame_shard(n_global, world, rank)
+    data, obj, frames = synthetic.make_matcher_inputs(n1, n3, L, seed=0, frame_ids=range(fs, fe))
     m = matcher.from_state_dict(sd, {**synthetic.DEFAULT_HPARAMS,
                                      "attention_precision": args.precision})
     detector, images = None, None
@@ -292,7 +298,7 @@ def main():
                                "max_keypoints": n1, "remove_borders": 4})
         detector.load_state_dict(synthetic.superpoint_state_dict(0))
         S = args.image_size
-        images = np.stack([synthetic.superpoint_image(S, S, rank * 1000 + i) for i in range(B)])
+        images = np.stack([synthetic.superpoint_image(S, S, fs + i) for i in range(B)])
     pipe = FramePipeline(m, data["keypoints3d"][0], data["descriptors3d_db"][0],
                          data["descriptors2d_db"][0], B, n1, dev, scale=1000.0,
                          slots=args.slots or max(2, args.match_streams + 1), detector=detector,
@@ -365,10 +371,13 @@ def main():
                 pipe.enqueue()
         return pipe.slots[0]
 
-    def result_rows(slot):   # per-frame result row: pose, errors, cm/deg flags, inliers, status
+    frame_ids = torch.arange(fs, fe, dtype=torch.float64, device=dev)[:, None]
+
+    def result_rows(slot):   # per-frame result row: pose, errors, cm/deg flags, inliers, status,
+        # and the frame's index in the global batch (rank 0 checks the gathered order)
         return torch.cat([slot.pose.reshape(B, 12), slot.R_err[:, None], slot.t_err[:, None],
                           slot.cmd.double(), slot.n_inliers[:, None].double(),
-                          slot.status[:, None].double()], 1)
+                          slot.status[:, None].double(), frame_ids], 1)
 
     # first replay of each graph (upload) and the first use of every torch kernel the timed
     # region launches (ROCm loads a kernel's code object lazily at its first launch, which
@@ -500,7 +509,9 @@ def main():
                                "note": "MFMA FLOPs the kernels execute (the Mf fold removes the "
                                        "merge conv and the attention apply)"}}
 
-    pose_summary = {"cmd1": float(res[:, 14].mean()), "cmd3": float(res[:, 15].mean()),
+    # the gathered rows are the global batch, in frame order (one object's frames over ranks)
+    assert np.array_equal(res[:, 19], np.arange(n_global)), "gathered frame order"
+    pose_summary = {"frames": int(n_global), "cmd1": float(res[:, 14].mean()), "cmd3": float(res[:, 15].mean()),
                     "cmd5": float(res[:, 16].mean()), "R_err_deg_mean": float(res[:, 12].mean()),
                     "t_err_cm_mean": float(res[:, 13].mean()),
                     "n_inliers_mean": float(res[:, 17].mean()),
@@ -545,7 +556,9 @@ def main():
                                        if args.e2e else "")
                                     + f"matcher + RANSAC-EPnP + cm/deg; {sched}"),
                        "n1": n1, "n3": n3, "num_leaf": L, "batch_per_gpu": B,
-                       "parallelism": f"frame-dp{world}"},
+                       "global_batch": n_global,
+                       "parallelism": f"frame-dp{world} (one object; global batch of "
+                                      f"{n_global} frames sharded contiguously over ranks)"},
             "pose": pose_summary,
             "roofline": roof,
             "frame_roofline": frame_roof,

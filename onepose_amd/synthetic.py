@@ -206,11 +206,15 @@ def make_frame(obj: SynthObject, n1: int, seed: int = 0, inlier_frac: float = 0.
     return SynthFrame(kp[order], np.ascontiguousarray(desc[order].T), K, pose, truth[order])
 
 
-def make_matcher_inputs(n1: int, n3: int, num_leaf: int = 8, seed: int = 0, batch: int = 1):
+def make_matcher_inputs(n1: int, n3: int, num_leaf: int = 8, seed: int = 0, batch: int = 1,
+                        frame_ids=None):
     """Matcher inputs in the reference layout (GATs_SuperGlue.py:209-217), numpy float32.
 
     Leaves come from the build's own ``build_features3d_leaves`` restatement with a
     numpy RNG seeded here, as ``inference.py:113-130`` does after ``seed_everything``.
+    Frame b of the object is ``make_frame(obj, n1, seed * 131 + b)``; ``frame_ids`` picks
+    which frames of that one sequence to return (default ``range(batch)``), so a rank of a
+    frame-sharded run builds exactly its slice of one global batch (distributed.frame_shard).
     """
     from .data_utils import build_features3d_leaves, pad_features3d_random
     obj = make_object(n3, seed)
@@ -218,7 +222,9 @@ def make_matcher_inputs(n1: int, n3: int, num_leaf: int = 8, seed: int = 0, batc
     avg, _ = pad_features3d_random(obj.avg_descriptors, obj.avg_scores, n3)
     leaves, _ = build_features3d_leaves(obj.clt_descriptors, obj.clt_scores, obj.idxs, n3, num_leaf)
     avg, leaves = avg.numpy(), leaves.numpy()
-    frames = [make_frame(obj, n1, seed * 131 + b) for b in range(batch)]
+    ids = list(range(batch)) if frame_ids is None else list(frame_ids)
+    batch = len(ids)
+    frames = [make_frame(obj, n1, seed * 131 + b) for b in ids]
     return {
         "keypoints2d": np.stack([f.keypoints2d for f in frames]),
         "keypoints3d": np.broadcast_to(obj.keypoints3d[None], (batch, n3, 3)).copy(),

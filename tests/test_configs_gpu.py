@@ -120,3 +120,35 @@ def test_config4_batch32_1024x2500_ragged(device):
         np.testing.assert_allclose(conf[b], oconf[0], rtol=0, atol=ATOL)
         assert_pred_equal(preds[b], opred, f"config 4, frame {b} of 32 vs oracle")
         assert (preds[b]["matches0"] > -1).sum() > 200
+
+
+@pytest.mark.timeout(300)
+def test_config5_2048x8192_vs_oracle(device):
+    """BASELINE config 5 shape (2048 kpts x 8192 3D pts, L = 8) through the bench's cached path,
+    anchored to the numpy oracle (oracle/matcher_np.py, pinned to the reference fixtures):
+      fp32: conf within 2e-5 and indices exact (tests/parity.py);
+      bf16 attention (config 5's MFMA-bf16 mode, not bit-exact by construction), bounded against
+      the same oracle output: max |conf - oracle| <= 0.02, matches0 equal on every row whose
+      oracle score is > 0.5, and >= 99% of all rows equal."""
+    from oracle import matcher_np as M
+    n1, n3, L, seed = 2048, 8192, 8, 11
+    sd = synthetic.make_state_dict(0)
+    data, _, _ = synthetic.make_matcher_inputs(n1, n3, L, seed=seed, batch=1)
+    opred, oconf = M.forward(sd, data)
+    d2 = data["descriptors2d_query"]
+    p32, c32 = CachedMatcher(sd, data, device, precision=0)(d2, with_conf=True)
+    np.testing.assert_allclose(c32[0], oconf[0], rtol=0, atol=ATOL)
+    assert_pred_equal(p32[0], opred, "config 5 fp32 vs oracle")
+    om0, os0 = opred["matches0"].reshape(-1), opred["matching_scores0"].reshape(-1)
+    assert (om0 > -1).sum() > 0.2 * n1
+    p16, c16 = CachedMatcher(sd, data, device, precision=1)(d2, with_conf=True)
+    dconf = float(np.abs(c16[0] - oconf[0]).max())
+    m16 = p16[0]["matches0"]
+    conf_rows = os0 > 0.5
+    agree = float((m16 == om0).mean())
+    print(f"config 5 bf16 vs oracle: max |dconf| {dconf:.3e}, rows equal {agree:.5f}, "
+          f"confident rows {int(conf_rows.sum())} all equal: "
+          f"{bool((m16[conf_rows] == om0[conf_rows]).all())}")
+    assert dconf <= 0.02
+    assert (m16[conf_rows] == om0[conf_rows]).all()
+    assert agree >= 0.99

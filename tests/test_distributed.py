@@ -4,7 +4,8 @@ Each rank solves the pose of its contiguous shard of frames (the C RANSAC-EPnP o
 in for the GPU stage -- on the box the same helpers carry the HIP results), gathers the
 per-frame result rows, and every rank must hold exactly what one process computes for all
 frames, in frame order.  Uneven shards (7 frames on 2 ranks) and the max-over-ranks timer are
-covered."""
+covered.  The bench's own sharding (one object's global batch, each rank its frame_shard slice
+of one frame sequence, bench.py) is covered end to end with the CPU matcher oracle."""
 import os
 import socket
 
@@ -78,3 +79,62 @@ def test_two_rank_gloo_gather_matches_single_process(tmp_path):
         got = np.load(tmp_path / f"rank{r}.npy")
         np.testing.assert_array_equal(got, ref)
         assert float(np.load(tmp_path / f"max{r}.npy")[0]) == 2.0
+
+
+# ---- the bench's sharding: one object's global batch, frame_shard slices, global order ----
+N1, N3, LEAF, B_PER_RANK = 96, 160, 4, 3
+N_GLOBAL = 2 * B_PER_RANK   # world 2
+
+
+def shard_rows(world, rank):
+    """What one bench rank computes (bench.py): the object from seed 0, its frame_shard slice of
+    the global batch world * B, matcher (numpy oracle standing in for the HIP path) ->
+    correspondences -> RANSAC-EPnP (C oracle) -> errors; rows end with the global frame index."""
+    from onepose_amd import synthetic as S
+    from oracle import matcher_np as M
+    from oracle import pnp_oracle as O
+    s, e = D.frame_shard(N_GLOBAL, world, rank)
+    sd = S.make_state_dict(0)
+    data, obj, frames = S.make_matcher_inputs(N1, N3, LEAF, seed=0, frame_ids=range(s, e))
+    pred, _ = M.forward(sd, data)
+    rows = []
+    for i, f in enumerate(frames):
+        # M.forward returns sample 0's correspondences (as the reference does): one frame a call
+        one = {k: v[i:i + 1] for k, v in data.items()}
+        p = pred if i == 0 else M.forward(sd, one)[0]
+        m0 = p["matches0"].reshape(-1)
+        ok = m0 > -1
+        st, est, _, nin, _ = O.pnp_ransac(f.keypoints2d[ok].astype(np.float32),
+                                          obj.keypoints3d[m0[ok]].astype(np.float32) * 1000.0,
+                                          f.K, scale=1000.0)
+        r_err, t_err = O.pose_error(est, f.pose_gt)
+        rows.append(np.concatenate([est.reshape(-1), [r_err, t_err, nin, st, int(ok.sum()),
+                                                     s + i]]))
+    return torch.tensor(np.array(rows).reshape(-1, 18), dtype=torch.float64)
+
+
+def _bench_worker(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world),
+                      RANK=str(rank), LOCAL_RANK=str(rank))
+    assert D.init("gloo")
+    full = D.gather_frames(shard_rows(world, rank), N_GLOBAL)
+    np.save(os.path.join(out_dir, f"bench{rank}.npy"), full.numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_two_rank_bench_shards_one_objects_batch(tmp_path):
+    """world 2 x B 3: the gathered rows equal one process running the whole 6-frame batch of
+    the same object, in global frame order, and the frames are not all alike (distinct poses)."""
+    port = _free_port()
+    mp.start_processes(_bench_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True,
+                       start_method="spawn")
+    ref = shard_rows(1, 0)   # world 1: all 6 frames in one process
+    assert ref.shape[0] == N_GLOBAL
+    for r in range(2):
+        got = np.load(tmp_path / f"bench{r}.npy")
+        np.testing.assert_array_equal(got, ref.numpy())
+        np.testing.assert_array_equal(got[:, -1], np.arange(N_GLOBAL))
+    assert (ref[:, 16] > 20).all()                       # every frame has correspondences
+    assert len({tuple(np.round(r[:12], 6)) for r in ref.numpy()}) == N_GLOBAL
