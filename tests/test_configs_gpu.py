@@ -128,7 +128,7 @@ def test_config5_2048x8192_vs_oracle(device):
     anchored to the numpy oracle (oracle/matcher_np.py, pinned to the reference fixtures):
       fp32: conf within 2e-5 and indices exact (tests/parity.py);
       bf16 attention (config 5's MFMA-bf16 mode, not bit-exact by construction), bounded against
-      the same oracle output: max |conf - oracle| <= 0.02, matches0 equal on every row whose
+      the same oracle output: max |conf - oracle| <= 2e-3 (measured 5.5e-4), matches0 equal on every row whose
       oracle score is > 0.5, and >= 99% of all rows equal."""
     from oracle import matcher_np as M
     n1, n3, L, seed = 2048, 8192, 8, 11
@@ -149,6 +149,6 @@ def test_config5_2048x8192_vs_oracle(device):
     print(f"config 5 bf16 vs oracle: max |dconf| {dconf:.3e}, rows equal {agree:.5f}, "
           f"confident rows {int(conf_rows.sum())} all equal: "
           f"{bool((m16[conf_rows] == om0[conf_rows]).all())}")
-    assert dconf <= 0.02
+    assert dconf <= 2e-3
     assert (m16[conf_rows] == om0[conf_rows]).all()
     assert agree >= 0.99
