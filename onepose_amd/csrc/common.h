@@ -19,6 +19,8 @@ constexpr int kWave = 64;
 constexpr int kDim = 256;       // descriptor_dim (train_GATsSPG.yaml:44)
 constexpr int kHeads = 4;       // AttentionPropagation(feature_dim, 4)
 constexpr int kHeadDim = 64;
+// activation-plane buffers ([B][kPlanesMax][n][256] uint16) hold up to the split's 3 planes
+constexpr int kPlanesMax = 3;
 
 #define OP_REQUIRE(cond, ...)                         \
   do {                                                \
@@ -196,6 +198,32 @@ __device__ __forceinline__ void chan_merge(double& n, double& mean, double& m2, 
   mean += delta * (nb / nn);
   m2 += m2b + delta * delta * (n * nb / nn);
   n = nn;
+}
+
+// Activation planes: the bf16 modes' A operands, written by the producer of an activation
+// beside its fp32 copy, so the next GEMM moves them to LDS by global_load_lds instead of
+// rounding / splitting them in VALU every stage.  Plane q of x is the q-th piece of the exact
+// split x = hi + mid + lo (hi = bf16(x) rounded to nearest even, mid = bf16(x - hi),
+// lo = x - hi - mid; gemm.hip's store_quad_bf16 computes the same bits), `npl` planes (1: hi
+// only, PM_BF16; 3: PM_SPLIT3) `pl` elements apart.  Four consecutive elements per call.
+typedef __bf16 bf16x4_pl __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void store_planes4(uint16_t* p, int64_t pl, int npl, float4 v) {
+  const float x[4] = {v.x, v.y, v.z, v.w};
+  bf16x4_pl q0, q1, q2;
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const __bf16 h = (__bf16)x[c];
+    const float r = x[c] - (float)h;
+    const __bf16 m = (__bf16)r;
+    q0[c] = h;
+    q1[c] = m;
+    q2[c] = (__bf16)(r - (float)m);
+  }
+  *reinterpret_cast<bf16x4_pl*>(p) = q0;
+  if (npl > 1) {
+    *reinterpret_cast<bf16x4_pl*>(p + pl) = q1;
+    *reinterpret_cast<bf16x4_pl*>(p + 2 * pl) = q2;
+  }
 }
 
 // Bijection hardware block id -> logical id giving each XCD (hardware blocks b, b+8, ...)

@@ -53,10 +53,26 @@ struct GemmProb {
   int64_t wp_bs, wpl;
   const uint16_t* Wp1;
   int64_t wp1_bs, wpl1;
+  // bf16 modes: A (and A1) as activation planes (common.h store_planes4: the producer's exact
+  // split, NPL planes [M][ldap] per sample, apl elements apart, ap_bs per sample (0 = shared)),
+  // moved to LDS by global_load_lds like Wp -- the DMA loop then stages nothing through
+  // registers.  Set on every problem of a launch or on none; Ap1 set exactly when A1 is; not
+  // with PRO_NORM_RELU (its A is transformed per stage).  The LDS images, and so every result
+  // bit, equal the register-staged rounding / split of A.
+  const uint16_t* Ap;
+  int64_t ap_bs, apl;
+  int ldap;
+  const uint16_t* Ap1;
+  int64_t ap1_bs, apl1;
+  int ldap1;
   const float* bias;   // [N] or null
   float* Y;            // [batch][M][ldy]
   int64_t y_bs;
   int ldy;
+  // bf16 modes: the stored output's activation planes as well (EPI_RESID: y; EPI_QKV: the
+  // phi(q) tiles), NPL planes [M][ldy] per sample (yp_bs), ypl apart; null = fp32 only.
+  uint16_t* Yp;
+  int64_t yp_bs, ypl;
   const float* R;      // residual, [batch][M][ldr]
   int64_t r_bs;
   int ldr;

@@ -115,6 +115,9 @@ struct Ctx {
   const float *a0, *a1, *w0, *w1, *mean, *rstd;
   const uint16_t *wp0, *wp1;   // W planes of the two K ranges (WPL)
   int64_t wpl0, wpl1;          // plane strides (elements)
+  const uint16_t *ap0, *ap1;   // A planes of the two K ranges (DMA 2)
+  int64_t apl0, apl1;
+  int ldap0, ldap1;
   int lda0, lda1, ldw0, ldw1, ksplit, M, N, K;
 };
 
@@ -264,11 +267,14 @@ __device__ __forceinline__ void store_stage(float* base, Stage<T, WPL, NPL>& s) 
   }
 }
 
-template <int EPI, int PRO, class T, int PM, bool WPL, bool DMA = false>
+// DMA: 0 = register-staged loop; 1 = the lean loop, W planes by global_load_lds and A through
+// registers; 2 = the lean loop with A from activation planes by global_load_lds as well.
+template <int EPI, int PRO, class T, int PM, bool WPL, int DMA = 0>
 __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, StampLds* sl) {
   constexpr int BM = T::BM, BN = T::BN, FN = T::FN, PITCH = T::PITCH;
   constexpr bool BF = PM != PM_F32;   // bf16 LDS images and MFMAs
   constexpr int NPL = PM == PM_SPLIT3 ? 3 : 1;   // bf16 images per operand
+  constexpr int NPL_OUT = PM == PM_F32 ? 0 : NPL;  // activation planes of a stored output
   constexpr int STAGE = PM == PM_F32 ? T::STAGE : NPL * T::STAGEB / 2;   // floats
   // epilogue staging tile [BM][TP]: rows of BN + 4 (16-B aligned, read back as float4 rows by
   // the row-store pass), or BN + 1 where columns are read across rows (score, QKV)
@@ -326,6 +332,15 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
     c.wpl0 = F(wpl);
     c.wp1 = wp1 ? wp1 + b * F(wp1_bs) : c.wp0 + c.ksplit;
     c.wpl1 = wp1 ? F(wpl1) : c.wpl0;
+  }
+  if constexpr (DMA == 2) {   // A planes (range 1: its own planes, or range 0's continuing)
+    const uint16_t* ap1 = F(Ap1);
+    c.ap0 = F(Ap) + b * F(ap_bs);
+    c.apl0 = F(apl);
+    c.ldap0 = F(ldap);
+    c.ap1 = ap1 ? ap1 + b * F(ap1_bs) : c.ap0 + c.ksplit;
+    c.apl1 = ap1 ? F(apl1) : c.apl0;
+    c.ldap1 = ap1 ? F(ldap1) : c.ldap0;
   }
 
   const int t = threadIdx.x;
@@ -492,7 +507,7 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
 #pragma unroll
       for (int i = 0; i < 16; ++i) acc[j][i] = a0p[j * 1024 + i * 64];
   }
-  if constexpr (DMA) {
+  if constexpr (DMA >= 1) {
     // The lean DMA loop.  A bf16 stage is only 4-12 MFMAs per wave, so the loop is bound by the
     // instructions around them and by load latency, not by the matrix pipe:
     //  - row / piece offsets are computed once (32-bit, added to a wave-uniform base per stage);
@@ -506,6 +521,9 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
     // latencies at 1-3 waves per SIMD)  Same images, fragments and MFMA
     // order as the register-staged loop, so the same bits.
     static_assert(WPL && PM != PM_F32, "DMA loop: bf16 images, W planes");
+    // DMA 2: A from its activation planes too -- no VALU rounding / split, no LDS stores of A
+    constexpr bool ADMA = DMA == 2;
+    static_assert(!ADMA || PRO != PRO_NORM_RELU, "A planes: no prologue transform");
     // a W piece = one 1-KB global_load_lds: RP rows of BKS bf16 (CPR 16-B chunks per row)
     constexpr int CPR = T::BKS / 8, RP = 64 / CPR;
     constexpr int PIECES = NPL * T::BN / RP, PPW = PIECES / T::NW;
@@ -532,6 +550,25 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
       woff1[i] = (unsigned)((q * c.wpl1 + (int64_t)o * c.ldw1 + chunk) * 2);
       wdst[i] = q * T::STAGEB * 2 + (T::BM + rb) * T::BKS * 2;
     }
+    // A pieces (DMA 2): NPL planes x BM rows in 1-KB pieces, dealt to the waves in turn (a
+    // wave-uniform predicate skips the slots past the last piece)
+    constexpr int APIECES = NPL * BM / RP, APPW = (APIECES + T::NW - 1) / T::NW;
+    static_assert(!ADMA || BM % RP == 0, "A pieces");
+    unsigned apoff0[ADMA ? APPW : 1], apoff1[ADMA ? APPW : 1];
+    int adst[ADMA ? APPW : 1];
+    if constexpr (ADMA) {
+#pragma unroll
+      for (int i = 0; i < APPW; ++i) {
+        const int p = min(wave + T::NW * i, APIECES - 1);
+        const int q = p / (BM / RP), rb = (p % (BM / RP)) * RP;
+        const int row = rb + lane / CPR;   // A image row; slot lane % CPR holds bsw's chunk
+        const int chunk = bsw<T>(row, (lane % CPR) * 8) - row * T::BKS;
+        const int m = min(m0 + row, c.M - 1);
+        apoff0[i] = (unsigned)((q * c.apl0 + (int64_t)m * c.ldap0 + chunk) * 2);
+        apoff1[i] = (unsigned)((q * c.apl1 + (int64_t)m * c.ldap1 + chunk) * 2);
+        adst[i] = q * T::STAGEB * 2 + rb * T::BKS * 2;
+      }
+    }
     Stage<T, WPL, NPL> sa;
     auto load_a = [&](int k0) __attribute__((always_inline)) {
       const bool first = PRO != PRO_HEADZ || k0 < c.ksplit;   // one K range but for HEADZ
@@ -556,14 +593,31 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
       for (int i = 0; i < PPW; ++i)
         dma16(base + (first ? woff0[i] : woff1[i]), dst + wdst[i]);
     };
+    auto dma_a = [&](int st) __attribute__((always_inline)) {
+      const int k0 = st * T::BKS;
+      const bool first = PRO != PRO_HEADZ || k0 < c.ksplit;
+      const char* base =
+          reinterpret_cast<const char*>(first ? c.ap0 + k0 : c.ap1 + (k0 - c.ksplit));
+      char* dst = reinterpret_cast<char*>(buf(st));
+#pragma unroll
+      for (int i = 0; i < APPW; ++i)
+        if (APIECES % T::NW == 0 || wave + T::NW * i < APIECES)
+          dma16(base + (first ? apoff0[i] : apoff1[i]), dst + adst[i]);
+    };
+    // the next stage's A: its planes by DMA, or its fp32 values into registers (stored to LDS,
+    // rounded / split, once the stage's MFMAs are issued)
+    auto next_a = [&](int st) __attribute__((always_inline)) {
+      if constexpr (ADMA) dma_a(st);
+      else load_a(st * T::BKS);
+    };
     auto raw_barrier = [&]() __attribute__((always_inline)) {
       asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     };
-    load_a(kt0 * T::BKS);
+    next_a(kt0);
     dma_w(kt0);
     tk = stamp_start(args.stamp, sl);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    store_stage<PRO, T, PM, WPL, NPL, false>(buf(kt0), sa);
+    if constexpr (!ADMA) store_stage<PRO, T, PM, WPL, NPL, false>(buf(kt0), sa);
     raw_barrier();
     // @phase 1
     // one stage: kt's fragments into tg (zd: phi(q) stage, its Z partials; zf >= 0: the head's
@@ -575,13 +629,13 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
       const bool more = kt + 1 < nk;
       if (more) {
         dma_w(kt + 1);
-        load_a((kt + 1) * T::BKS);
+        next_a(kt + 1);
       }
 #pragma unroll
       for (int kk = 0; kk < KKW; ++kk) mfma_kk(tg, f0, kk);
       if (zf >= 0) zfinal(zf);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (more) store_stage<PRO, T, PM, WPL, NPL, false>(buf(kt + 1), sa);
+      if (!ADMA && more) store_stage<PRO, T, PM, WPL, NPL, false>(buf(kt + 1), sa);
       raw_barrier();
     };
     if (PRO != PRO_HEADZ) {
@@ -759,12 +813,18 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
     __syncthreads();
     if (q_tile) {
       constexpr int C4 = BN / 4, PER = BM * C4 / T::NT;
+      uint16_t* yp = F(Yp);   // phi(q)'s activation planes (bf16 modes), the next A operand
+      if (yp != nullptr) yp += b * F(yp_bs);
+      const int64_t ypl = F(ypl);
 #pragma unroll
       for (int p = 0; p < PER; ++p) {
         const int idx = t + T::NT * p, r = idx / C4, cc = (idx % C4) * 4;
-        if (m0 + r < M)
-          *reinterpret_cast<float4*>(Y + (int64_t)(m0 + r) * ldy + n0 + cc) =
-              *reinterpret_cast<const float4*>(tile + r * TP + cc);
+        if (m0 + r < M) {
+          const float4 v = *reinterpret_cast<const float4*>(tile + r * TP + cc);
+          *reinterpret_cast<float4*>(Y + (int64_t)(m0 + r) * ldy + n0 + cc) = v;
+          if (NPL_OUT > 0 && yp != nullptr)
+            store_planes4(yp + (int64_t)(m0 + r) * ldy + n0 + cc, ypl, NPL_OUT, v);
+        }
       }
       return;
     }
@@ -863,6 +923,9 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
   __syncthreads();
   // @phase 4
   // the row-store pass (STATS: issued behind its ticket's round trip, below)
+  uint16_t* yp = EPI == EPI_RESID ? F(Yp) : nullptr;   // RESID: the output's planes
+  if (yp != nullptr) yp += b * F(yp_bs);
+  const int64_t ypl = F(ypl);
   auto row_store = [&]() __attribute__((always_inline)) {
     constexpr int C4 = BN / 4, PER = BM * C4 / T::NT;   // float4 per row, per thread
     static_assert(BM * C4 % T::NT == 0, "row-store pass");
@@ -890,6 +953,8 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
           v.w = rv[p].w + v.w;
         }
         *reinterpret_cast<float4*>(Y + (int64_t)gm * ldy + gn) = v;
+        if (EPI == EPI_RESID && NPL_OUT > 0 && yp != nullptr)
+          store_planes4(yp + (int64_t)gm * ldy + gn, ypl, NPL_OUT, v);
       }
     }
   };
@@ -1088,7 +1153,7 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
 #undef F
 }
 
-template <int EPI, int PRO, class T, int PM, bool WPL, bool DMA>
+template <int EPI, int PRO, class T, int PM, bool WPL, int DMA>
 __global__ __launch_bounds__(T::NT) __attribute__((amdgpu_waves_per_eu(T::WPE)))
 void gemm_kernel(GemmArgs args) {
   __shared__ StampLds sl;
@@ -1105,10 +1170,18 @@ using T128x128 = Tile<128, 128, 1, 4, 32>;
 using T128x64W8 = Tile<128, 64, 1, 8, 32>;
 
 
-template <int EPI, int PRO, class T, int PM, bool WPL = false, bool DMA = false>
+template <int EPI, int PRO, class T, int PM, bool WPL = false, int DMA = 0>
 void launch_one(GemmArgs& args, int grid, hipStream_t stream) {
   hipLaunchKernelGGL((gemm_kernel<EPI, PRO, T, PM, WPL, DMA>), dim3(grid), dim3(T::NT), 0, stream,
                      args);
+}
+
+// DMA 2 is instantiated only for the combinations that use it (gemm_launch checks the rest):
+// the attention layers' QKV and MLP conv 1 in the bf16 modes
+template <int EPI, int PRO, class T, int PM>
+void launch_adma(GemmArgs& args, int grid, hipStream_t stream) {
+  if constexpr (PRO != PRO_NORM_RELU && (EPI == EPI_QKV || EPI == EPI_STATS))
+    launch_one<EPI, PRO, T, PM, true, 2>(args, grid, stream);
 }
 
 struct TileDims {
@@ -1211,15 +1284,31 @@ int gemm_launch(int epi, int pro, int tile, GemmArgs& args, hipStream_t stream, 
   // 64 x 128 tiles (QKV, MLP conv 1), the register-staged loop for 64 x 64 (MLP conv 2, whose
   // two MFMAs per wave and stage leave a DMA loop nothing to hide behind).
   const bool dma = pm == PM_SPLIT3 || (pm == PM_BF16 && tile == TILE_64x128);
+  // A from activation planes (every problem of the launch, or none): the DMA loop's DMA-2 form
+  const bool adma = args.p[0].Ap != nullptr;
+  const bool yplanes = args.p[0].Yp != nullptr;
+  for (int i = 0; i < args.nprob; ++i) {
+    const GemmProb& P = args.p[i];
+    OP_REQUIRE((P.Ap != nullptr) == adma && (P.Yp != nullptr) == yplanes,
+               "gemm: activation planes on some problems only");
+    OP_REQUIRE(!adma || ((P.A1 == nullptr) == (P.Ap1 == nullptr) && P.ldap % 8 == 0 &&
+                         (P.Ap1 == nullptr || P.ldap1 % 8 == 0)),
+               "gemm: A planes need planes for both K ranges and 16-B aligned rows");
+  }
+  OP_REQUIRE(!adma || (dma && wpl && pro != PRO_NORM_RELU && (epi == EPI_QKV || epi == EPI_STATS)),
+             "gemm: A planes: QKV / MLP conv 1 on the DMA loop (bf16 modes, W planes)");
+  OP_REQUIRE(!yplanes || (pm != PM_F32 && (epi == EPI_RESID || epi == EPI_QKV)),
+             "gemm: output planes are written by RESID / QKV launches in the bf16 modes");
 #define CASE(E, PR, TI, T, PMV, WP)                                      \
   if (epi == E && pro == PR && tile == TI && pm == PMV && wpl == WP) {  \
     prof_pre(kind, stream);                                              \
     args.stamp = prof_stamp_slot(kind);                                  \
     if constexpr (WP) {                                                  \
-      if (dma) launch_one<E, PR, T, PMV, WP, true>(args, grid, stream);  \
-      else launch_one<E, PR, T, PMV, WP, false>(args, grid, stream);     \
+      if (adma) launch_adma<E, PR, T, PMV>(args, grid, stream);          \
+      else if (dma) launch_one<E, PR, T, PMV, WP, 1>(args, grid, stream); \
+      else launch_one<E, PR, T, PMV, WP, 0>(args, grid, stream);         \
     } else {                                                             \
-      launch_one<E, PR, T, PMV, WP, false>(args, grid, stream);          \
+      launch_one<E, PR, T, PMV, WP, 0>(args, grid, stream);              \
     }                                                                    \
     prof_post(kind, stream);                                             \
     OP_LAUNCHED();                                                       \

@@ -245,11 +245,13 @@ struct TransProb {
   int64_t bs;
   int n, tiles;   // tokens, workgroups per sample (ceil(n/64) * 4)
   float* dst;
+  uint16_t* dstp = nullptr;   // bf16 modes: dst's activation planes ([B][3][n][256]; npl of them)
 };
 struct TransArgs {
   TransProb p[2];
   unsigned* zero;   // the forward's in-launch arrival counters, zeroed here (first kernel)
   int nzero;
+  int npl = 0;      // activation planes per dstp (0: none)
 };
 __global__ __launch_bounds__(256) void transpose_in_kernel(TransArgs args, int batch) {
   __shared__ float tile[64][65];
@@ -282,12 +284,16 @@ __global__ __launch_bounds__(256) void transpose_in_kernel(TransArgs args, int b
   }
   __syncthreads();
   float* d = P.dst + (int64_t)b * n * kDim;
+  uint16_t* dp = P.dstp != nullptr ? P.dstp + (int64_t)b * kPlanesMax * n * kDim : nullptr;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {   // 64 tokens x 16 float4 of channels
     const int e = t + 256 * i, tk = e >> 4, cq = (e & 15) * 4;
-    if (n0 + tk < n)
-      *reinterpret_cast<float4*>(d + (int64_t)(n0 + tk) * kDim + c0 + cq) =
-          make_float4(tile[cq][tk], tile[cq + 1][tk], tile[cq + 2][tk], tile[cq + 3][tk]);
+    if (n0 + tk < n) {
+      const float4 v = make_float4(tile[cq][tk], tile[cq + 1][tk], tile[cq + 2][tk], tile[cq + 3][tk]);
+      *reinterpret_cast<float4*>(d + (int64_t)(n0 + tk) * kDim + c0 + cq) = v;
+      if (dp != nullptr)
+        store_planes4(dp + (int64_t)(n0 + tk) * kDim + c0 + cq, (int64_t)n * kDim, args.npl, v);
+    }
   }
 }
 
@@ -722,7 +728,8 @@ __global__ __launch_bounds__(256) void gat_kernel(const float* __restrict__ x3,
                                                   int64_t leaves_bs, const float* __restrict__ wa,
                                                   const float* __restrict__ slog,
                                                   float* __restrict__ y3, int n3, int L,
-                                                  int batch) {
+                                                  int batch, uint16_t* __restrict__ y3p,
+                                                  int npl) {
   const int gw = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int b = gw / n3, p = gw - b * n3;
   if (b >= batch) return;
@@ -782,8 +789,11 @@ __global__ __launch_bounds__(256) void gat_kernel(const float* __restrict__ x3,
     acc.z += a * lf[j].z;
     acc.w += a * lf[j].w;
   }
-  reinterpret_cast<float4*>(y3 + ((int64_t)b * n3 + p) * kDim)[lane] =
-      make_float4(elu1(acc.x), elu1(acc.y), elu1(acc.z), elu1(acc.w));
+  const float4 y = make_float4(elu1(acc.x), elu1(acc.y), elu1(acc.z), elu1(acc.w));
+  reinterpret_cast<float4*>(y3 + ((int64_t)b * n3 + p) * kDim)[lane] = y;
+  if (y3p != nullptr)   // activation planes ([B][3][n3][256]) for the next GEMM's A
+    store_planes4(y3p + ((int64_t)b * kPlanesMax * n3 + p) * kDim + lane * 4, (int64_t)n3 * kDim,
+                  npl, y);
 }
 
 // GAT layers 1-3 of a cached forward from per-object prefix tables (onepose_object_prepare).
@@ -876,7 +886,8 @@ __global__ __launch_bounds__(256) void gat_tab_kernel(const float* __restrict__ 
                                                       const float* __restrict__ slogs,
                                                       const float* __restrict__ tab,
                                                       float* __restrict__ y3, int n3, int L,
-                                                      int batch) {
+                                                      int batch, uint16_t* __restrict__ y3p,
+                                                      int npl) {
   constexpr int MAXL = 8;
   const int gw = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int b = gw / n3, p = gw - b * n3;
@@ -920,8 +931,11 @@ __global__ __launch_bounds__(256) void gat_tab_kernel(const float* __restrict__ 
   acc.y = fmaf(an, Bv.y, fmaf(ap, A.y, a0 * h.y));
   acc.z = fmaf(an, Bv.z, fmaf(ap, A.z, a0 * h.z));
   acc.w = fmaf(an, Bv.w, fmaf(ap, A.w, a0 * h.w));
-  reinterpret_cast<float4*>(y3 + ((int64_t)b * n3 + p) * kDim)[lane] =
-      make_float4(elu1(acc.x), elu1(acc.y), elu1(acc.z), elu1(acc.w));
+  const float4 y = make_float4(elu1(acc.x), elu1(acc.y), elu1(acc.z), elu1(acc.w));
+  reinterpret_cast<float4*>(y3 + ((int64_t)b * n3 + p) * kDim)[lane] = y;
+  if (y3p != nullptr)
+    store_planes4(y3p + ((int64_t)b * kPlanesMax * n3 + p) * kDim + lane * 4, (int64_t)n3 * kDim,
+                  npl, y);
 }
 
 // F.normalize(x, p=2, dim=channels), one wave per token row (GATs_SuperGlue.py:245-246).
@@ -1169,6 +1183,9 @@ struct Plan {
   float *kvpart2, *kvpart3, *kspart2, *kspart3;
   float *kv, *ksum, *mf;
   float *phiq2, *phiq3, *y12, *y13;
+  // bf16 modes: activation planes of x2 / x3 (ping-pong, as x2 / x3) and of phi(q), each
+  // [B][kPlanesMax][n][256] (common.h store_planes4): the attention GEMMs' A operands
+  uint16_t *x2p[2], *x3p[2], *phiq2p, *phiq3p;
   float *stats2, *stats3, *mean, *rstd;
   unsigned* cnt;      // in-launch arrival counters: [attention layer][side][B][cps]
   int ncnt, cps;      //   (cps: MLP conv 1's column-block and group counters, gemm.h st_cnt)
@@ -1228,6 +1245,12 @@ Plan make_plan(void* ws, int B, int n1, int n3, int L, bool with_conf) {
   p.phiq3 = c.take<float>(t3 * 256);
   p.y12 = c.take<float>(t2 * 512);
   p.y13 = c.take<float>(t3 * 512);
+  for (int i = 0; i < 2; ++i) {
+    p.x2p[i] = c.take<uint16_t>(t2 * 256 * kPlanesMax);
+    p.x3p[i] = c.take<uint16_t>(t3 * 256 * kPlanesMax);
+  }
+  p.phiq2p = c.take<uint16_t>(t2 * 256 * kPlanesMax);
+  p.phiq3p = c.take<uint16_t>(t3 * 256 * kPlanesMax);
   p.stats2 = c.take<float>((size_t)B * ceil_div(n1, str) * 1024);
   p.stats3 = c.take<float>((size_t)B * ceil_div(n3, str) * 1024);
   p.mean = c.take<float>((size_t)2 * B * 512);
@@ -1534,12 +1557,28 @@ int attention_pm(int precision) {
   return precision == ONEPOSE_PREC_BF16_ATTN ? PM_BF16
          : precision == ONEPOSE_PREC_FP32_SPLIT ? PM_SPLIT3 : PM_F32;
 }
+// activation planes the producers write for a GEMM operand mode (0: none, fp32)
+int planes_of(int pm) { return pm == PM_BF16 ? 1 : pm == PM_SPLIT3 ? 3 : 0; }
 
 // W of a GEMM as the packed bf16 planes (bf16 modes; gemm.h GemmProb::Wp)
 void set_w_planes(GemmProb& g, const uint16_t* wp, int64_t rows_x_cols) {
   g.Wp = wp;
   g.wp_bs = 0;
   g.wpl = rows_x_cols;
+}
+// A of a GEMM as activation planes ([B][kPlanesMax][n][256]; bs per sample, 0 = shared)
+void set_a_planes(GemmProb& g, const uint16_t* ap, int64_t bs, int n) {
+  g.Ap = ap;
+  g.ap_bs = bs;
+  g.apl = (int64_t)n * 256;
+  g.ldap = 256;
+}
+// the stored output's activation planes ([B][kPlanesMax][n][256])
+void set_y_planes(GemmProb& g, uint16_t* yp, int n, int B) {
+  (void)B;
+  g.Yp = yp;
+  g.yp_bs = (int64_t)kPlanesMax * n * 256;
+  g.ypl = (int64_t)n * 256;
 }
 // MLP conv 1's second K range: the Mf planes of a Mf region (kMfFloats per sample; bs 0: shared)
 void set_mf_planes(GemmProb& g, const float* mf, int64_t sample_floats) {
@@ -1561,6 +1600,13 @@ struct Side {
   int src;      // slot of the side this one attends to
   int ntile;    // token count the tile choices use (n; a sharded 3D side: the largest shard,
                 // so that every rank picks the same tiles and rounds alike)
+  // bf16 modes: activation planes ([B][kPlanesMax][n][256], plane stride n * 256) of x (xp,
+  // xp_bs per sample; null: QKV / MLP conv 1 stage A through registers), of the output xo
+  // (written by MLP conv 2) and of phi(q) (written by QKV, read by MLP conv 1)
+  const uint16_t* xp = nullptr;
+  int64_t xp_bs = 0;
+  uint16_t* xop = nullptr;
+  uint16_t* phiqp = nullptr;
 };
 
 // Choices of one attention layer that change a side's summation order: the QKV tile of the
@@ -1631,7 +1677,7 @@ bool obj_tables(int num_leaf, int flags) {
   return (flags & ONEPOSE_OBJ_GAT_TABLES) != 0 && num_leaf <= 8;
 }
 struct ObjLayout {
-  int64_t logits, phiq, acc, ksum, mf, slogs, tab, total;
+  int64_t logits, phiq, acc, ksum, mf, phiqp, slogs, tab, total;
   bool tables;
 };
 ObjLayout obj_layout(int n3, int num_leaf, int flags) {
@@ -1642,7 +1688,10 @@ ObjLayout obj_layout(int n3, int num_leaf, int flags) {
   L.acc = L.phiq + (int64_t)n3 * 256;
   L.ksum = L.acc + (int64_t)ceil_div(n3, 64) * 64 * 512;   // TILE_64x64 tiles of N = 512
   L.mf = L.ksum + 256;
-  L.slogs = L.mf + kMfFloats;
+  // phi(q)'s activation planes [kPlanesMax][n3][256] uint16 (bf16 modes; reserved in every
+  // precision, so the size query needs none)
+  L.phiqp = L.mf + kMfFloats;
+  L.slogs = L.phiqp + (int64_t)kPlanesMax * n3 * 256 / 2;
   L.tab = L.slogs + (L.tables ? (int64_t)3 * n3 * kLogitStride : 0);
   L.total = L.tab + (L.tables ? (int64_t)3 * n3 * 2 * num_leaf * 256 : 0);
   return L;
@@ -1657,6 +1706,7 @@ struct SideCache {
   const float* acc;    // MLP conv 1 accumulators over K [0, 256) (EPI_ACC layout, TILE_64x64)
   const float* ksum;   // [256]      sum phi(k) of the 3D side
   const float* mf;     // [512][256] the 2D side's Mf
+  const uint16_t* phiqp;   // [3][n3][256] phi(q)'s activation planes (bf16 modes)
 };
 
 void launch_kv_fold(const KvFoldArgs& ka, int nslot, int B, float* kv, float* ksum, hipStream_t st) {
@@ -1690,9 +1740,18 @@ int attention_layer(const ApW& w, const Side* sd, int nside, int B, const Plan& 
     return ONEPOSE_OK;
   };
   // 1. [q | k_h v_h ...]: phi(q) stored, per-chunk KV / ksum partials
+  // activation planes (bf16 modes): A by DMA where every side of a launch has them; phi(q)'s
+  // planes written where every side has a buffer for them
+  auto all_of = [&](int i0, int i1, auto pred) {
+    for (int i = i0; i < i1; ++i)
+      if (!pred(i)) return false;
+    return true;
+  };
   rc = groups(nsrc, [&](int a, int b) { return tl.qkv[a] == tl.qkv[b]; }, [&](int i0, int i1) -> int {
     GemmArgs a;
     a.nprob = i1 - i0;
+    const bool ap = pm != PM_F32 && all_of(i0, i1, [&](int i) { return sd[i].xp != nullptr; });
+    const bool yp = pm != PM_F32 && all_of(i0, i1, [&](int i) { return sd[i].phiqp != nullptr; });
     for (int i = i0; i < i1; ++i) {
       const Side& s = sd[i];
       GemmProb& g = a.p[i - i0];
@@ -1703,6 +1762,8 @@ int attention_layer(const ApW& w, const Side* sd, int nside, int B, const Plan& 
       g.kspart = s.kspart;
       g.y_bs = (int64_t)s.n * 256;
       if (pm != PM_F32) set_w_planes(g, w.wqkv_p, kPlWqkv);
+      if (ap) set_a_planes(g, s.xp, s.xp_bs, s.n);
+      if (yp) set_y_planes(g, s.phiqp, s.n, B);
     }
     return gemm_launch(EPI_QKV, PRO_PLAIN, tl.qkv[i0], a, st, K_QKV_GEMM, pm);
   });
@@ -1768,6 +1829,13 @@ int attention_layer(const ApW& w, const Side* sd, int nside, int B, const Plan& 
      //    in-kernel (PRO_HEADZ), + InstanceNorm partials
     GemmArgs a;
     a.nprob = nside;
+    // A planes: x's (the cached 3D half of cross-attention 1 starts from acc0 and never reads
+    // its x range) and phi(q)'s
+    const bool ap = pm != PM_F32 && all_of(0, nside, [&](int i) {
+      const bool cached = xc && i == 1;
+      return (cached || sd[i].xp != nullptr) &&
+             (cached ? xc->phiqp != nullptr : sd[i].phiqp != nullptr);
+    });
     for (int i = 0; i < nside; ++i) {
       const Side& s = sd[i];
       a.p[i] = gemm_prob(s.x, 256, w.w1a, 256, w.b1, s.y1, 512, s.n, 512, 512, B);
@@ -1804,6 +1872,19 @@ int attention_layer(const ApW& w, const Side* sd, int nside, int B, const Plan& 
       a.p[1].acc0 = xc->acc;
       a.p[1].acc0_bs = 0;
     }
+    if (ap) {
+      for (int i = 0; i < nside; ++i) {
+        const bool cached = xc && i == 1;
+        const uint16_t* qp = cached ? xc->phiqp : sd[i].phiqp;
+        const int64_t qbs = cached ? 0 : (int64_t)kPlanesMax * sd[i].n * 256;
+        // (the cached side's x range is skipped: its A0 planes are never read)
+        set_a_planes(a.p[i], cached ? qp : sd[i].xp, cached ? 0 : sd[i].xp_bs, sd[i].n);
+        a.p[i].Ap1 = qp;
+        a.p[i].ap1_bs = qbs;
+        a.p[i].apl1 = (int64_t)sd[i].n * 256;
+        a.p[i].ldap1 = 256;
+      }
+    }
     if ((rc = gemm_launch(EPI_STATS, PRO_HEADZ, mlp1_tile(pm), a, st, K_MLP1, pm)) != ONEPOSE_OK)
       return rc;
   }
@@ -1829,6 +1910,7 @@ int attention_layer(const ApW& w, const Side* sd, int nside, int B, const Plan& 
   return groups(nside, [&](int a, int b) { return tl.mlp2[a] == tl.mlp2[b]; }, [&](int i0, int i1) -> int {
     GemmArgs a;
     a.nprob = i1 - i0;
+    const bool yp = pm != PM_F32 && all_of(i0, i1, [&](int i) { return sd[i].xop != nullptr; });
     for (int i = i0; i < i1; ++i) {
       const Side& s = sd[i];
       GemmProb& g = a.p[i - i0];
@@ -1840,6 +1922,7 @@ int attention_layer(const ApW& w, const Side* sd, int nside, int B, const Plan& 
       g.pro_rstd = p.rstd + (size_t)i * B * 512;
       g.pro_bs = 512;
       if (pm != PM_F32) set_w_planes(g, w.w2_p, kPlW2);
+      if (yp) set_y_planes(g, s.xop, s.n, B);
     }
     return gemm_launch(EPI_RESID, PRO_NORM_RELU, tl.mlp2[i0], a, st, K_MLP2, pm);
   });
@@ -1865,21 +1948,31 @@ int match_impl(const void* packed_weights, const float* desc2d, int64_t desc2d_b
   const float* leaves = leaves_pm;
   const int64_t leaves_bstride = leaves_pm_bs;
 
+  // bf16 modes: every producer of an attention GEMM's A operand also writes its activation
+  // planes (the token states x2 / x3, phi(q)), which those GEMMs then move by DMA
+  const int npl = planes_of(pm);
+  auto pl = [&](uint16_t* q) { return npl ? q : nullptr; };
   {
     TransArgs ta;
-    ta.p[0] = {desc2d, desc2d_bstride, n1, ceil_div(n1, 64) * 4, p.x2[0]};
-    ta.p[1] = {desc3d, desc3d_bstride, n3, obj_cache ? 0 : ceil_div(n3, 64) * 4, p.x3[0]};
+    ta.p[0] = {desc2d, desc2d_bstride, n1, ceil_div(n1, 64) * 4, p.x2[0], pl(p.x2p[0])};
+    ta.p[1] = {desc3d, desc3d_bstride, n3, obj_cache ? 0 : ceil_div(n3, 64) * 4, p.x3[0],
+               pl(p.x3p[0])};
     ta.zero = p.cnt;
     ta.nzero = p.ncnt;
+    ta.npl = npl;
     OP_LAUNCH(K_TRANSPOSE, st, transpose_in_kernel, dim3((ta.p[0].tiles + ta.p[1].tiles) * B),
               dim3(256), 0, st, ta, B);
   }
 
-  // Current states: side x is read from x?r (batch stride x?bs) and written to p.x?[c? ^ 1].
+  // Current states: side x is read from x?r (batch stride x?bs) and written to p.x?[c? ^ 1];
+  // their activation planes (bf16 modes) from x?pr (null: the object cache's state, which only
+  // cached halves read)
   int c2 = 0, c3 = 0, ap = 0, gat = 0;
   const float* x2r = p.x2[0];
   const float* x3r = obj_cache ? obj_cache : p.x3[0];
   int64_t x3bs = obj_cache ? 0 : (int64_t)n3 * 256;
+  const uint16_t* x2pr = pl(p.x2p[0]);
+  const uint16_t* x3pr = obj_cache ? nullptr : pl(p.x3p[0]);
   const int ch2 = ceil_div(n1, 64), ch3 = ceil_div(n3, 64);
   for (int layer = 0; layer < kLayers; ++layer) {
     const int kind = layer % 3;  // 0 GATs, 1 self, 2 cross
@@ -1893,18 +1986,22 @@ int match_impl(const void* packed_weights, const float* desc2d, int64_t desc2d_b
                                       (int64_t)(gat - 1) * n3 * kLogitStride
                                 : nullptr;
         const ObjLayout OL = obj_layout(n3, num_leaf, obj_flags);
+        uint16_t* yp = pl(p.x3p[c3 ^ 1]);
         if (slog != nullptr && OL.tables) {
           OP_LAUNCH(K_GAT, st, gat_tab_kernel, ggrid, dim3(256), 0, st, x3r, gat_weights(wbase, gat),
                     obj_cache + OL.slogs + (int64_t)(gat - 1) * n3 * kLogitStride,
                     obj_cache + OL.tab + (int64_t)(gat - 1) * n3 * 2 * num_leaf * 256,
-                    p.x3[c3 ^ 1], n3, num_leaf, B);
+                    p.x3[c3 ^ 1], n3, num_leaf, B, yp, npl);
         } else if (num_leaf <= 8)
           OP_LAUNCH(K_GAT, st, gat_kernel<8>, ggrid, dim3(256), 0, st, x3r, leaves,
-                    leaves_bstride, gat_weights(wbase, gat), slog, p.x3[c3 ^ 1], n3, num_leaf, B);
+                    leaves_bstride, gat_weights(wbase, gat), slog, p.x3[c3 ^ 1], n3, num_leaf, B,
+                    yp, npl);
         else
           OP_LAUNCH(K_GAT, st, gat_kernel<16>, ggrid, dim3(256), 0, st, x3r, leaves,
-                    leaves_bstride, gat_weights(wbase, gat), slog, p.x3[c3 ^ 1], n3, num_leaf, B);
+                    leaves_bstride, gat_weights(wbase, gat), slog, p.x3[c3 ^ 1], n3, num_leaf, B,
+                    yp, npl);
         x3r = p.x3[c3 ^ 1];
+        x3pr = yp;
         c3 ^= 1;
       }
       ++gat;
@@ -1917,6 +2014,15 @@ int match_impl(const void* packed_weights, const float* desc2d, int64_t desc2d_b
              p.stats2, n1, (float)n1, kind == 1 ? 0 : 1, n1};
     sd[1] = {x3r, x3bs, p.x3[c3 ^ 1], p.phiq3, p.kvpart3, p.kspart3, p.y13, p.stats3, n3,
              (float)n3g, kind == 1 ? 1 : 0, sh ? sh->max_shard : n3};
+    const int64_t pbs2 = (int64_t)kPlanesMax * n1 * 256, pbs3 = (int64_t)kPlanesMax * n3 * 256;
+    sd[0].xp = x2pr;
+    sd[0].xp_bs = pbs2;
+    sd[0].xop = pl(p.x2p[c2 ^ 1]);
+    sd[0].phiqp = pl(p.phiq2p);
+    sd[1].xp = x3pr;
+    sd[1].xp_bs = pbs3;
+    sd[1].xop = pl(p.x3p[c3 ^ 1]);
+    sd[1].phiqp = pl(p.phiq3p);
     const int qkv_n3 = sh ? sh->max_shard : n3;
     unsigned* lcnt = p.cnt + (size_t)(ap - 1) * 2 * B * p.cps;
     // layers 1-2 of a whole frame: per-side choices (the 3D side's are the object prefix's,
@@ -1931,16 +2037,19 @@ int match_impl(const void* packed_weights, const float* desc2d, int64_t desc2d_b
       // cross-attention 1: the 3D side's frame-independent half from the object cache
       const ObjLayout L = obj_layout(n3, num_leaf, obj_flags);
       const SideCache xc = {obj_cache + L.phiq, obj_cache + L.acc, obj_cache + L.ksum,
-                            obj_cache + L.mf};
+                            obj_cache + L.mf,
+                            npl ? reinterpret_cast<const uint16_t*>(obj_cache + L.phiqp) : nullptr};
       rc = attention_layer(w, sd, 2, B, p, lcnt, st, pm, nullptr, tl, &xc);
     } else {
       rc = attention_layer(w, sd, 2, B, p, lcnt, st, pm, sh, tl);
     }
     if (rc != ONEPOSE_OK) return rc;
     x2r = p.x2[c2 ^ 1];
+    x2pr = sd[0].xop;
     c2 ^= 1;
     if (!cached3) {
       x3r = p.x3[c3 ^ 1];
+      x3pr = sd[1].xop;
       x3bs = (int64_t)n3 * 256;
       c3 ^= 1;
     }
@@ -2036,6 +2145,9 @@ int object_prepare_impl(const void* packed_weights, const float* desc3d, const f
                         int n3, int num_leaf, int precision, int flags, float* cache,
                         const Plan& p, hipStream_t st) {
   const float* wbase = static_cast<const float*>(packed_weights);
+  const int pm = attention_pm(precision);
+  const int npl = planes_of(pm);   // activation planes (bf16 modes), as in match_impl
+  auto pl = [&](uint16_t* q) { return npl ? q : nullptr; };
   {
     TransArgs ta;
     ta.p[0] = {desc3d, 0, n3, ceil_div(n3, 64) * 4, p.x3[0]};
@@ -2049,7 +2161,7 @@ int object_prepare_impl(const void* packed_weights, const float* desc3d, const f
   float* slog = cache + (int64_t)n3 * 256;   // leaf logits of GAT layers 1-3
   if (num_leaf <= 8) {
     OP_LAUNCH(K_GAT, st, gat_kernel<8>, ggrid, dim3(256), 0, st, p.x3[0], leaves_pm, (int64_t)0,
-              gat_weights(wbase, 0), nolog, p.x3[1], n3, num_leaf, 1);
+              gat_weights(wbase, 0), nolog, p.x3[1], n3, num_leaf, 1, pl(p.x3p[1]), npl);
     OP_LAUNCH(K_GAT, st, gat_logits_kernel<8>, ggrid, dim3(256), 0, st, leaves_pm,
               gat_weights(wbase, 1), slog, n3, num_leaf);
     const ObjLayout OL = obj_layout(n3, num_leaf, flags);
@@ -2058,13 +2170,16 @@ int object_prepare_impl(const void* packed_weights, const float* desc3d, const f
                 gat_weights(wbase, 1), cache + OL.slogs, cache + OL.tab, n3, num_leaf);
   } else {
     OP_LAUNCH(K_GAT, st, gat_kernel<16>, ggrid, dim3(256), 0, st, p.x3[0], leaves_pm, (int64_t)0,
-              gat_weights(wbase, 0), nolog, p.x3[1], n3, num_leaf, 1);
+              gat_weights(wbase, 0), nolog, p.x3[1], n3, num_leaf, 1, pl(p.x3p[1]), npl);
     OP_LAUNCH(K_GAT, st, gat_logits_kernel<16>, ggrid, dim3(256), 0, st, leaves_pm,
               gat_weights(wbase, 1), slog, n3, num_leaf);
   }
-  const Side s3 = {p.x3[1], (int64_t)n3 * 256, cache, p.phiq3, p.kvpart3, p.kspart3, p.y13,
-                   p.stats3, n3, (float)n3, 0, n3};
-  const int pm = attention_pm(precision);
+  Side s3 = {p.x3[1], (int64_t)n3 * 256, cache, p.phiq3, p.kvpart3, p.kspart3, p.y13,
+             p.stats3, n3, (float)n3, 0, n3};
+  s3.xp = pl(p.x3p[1]);
+  s3.xp_bs = (int64_t)kPlanesMax * n3 * 256;
+  s3.xop = pl(p.x3p[0]);   // the cached state's planes: cross-attention 1's QKV below reads them
+  s3.phiqp = pl(p.phiq3p);
   int rc = attention_layer(ap_weights(wbase, 0), &s3, 1, 1, p, p.cnt, st, pm, nullptr,
                            layer_tiles(n3, &s3, 1, 1, pm, false));
   if (rc != ONEPOSE_OK) return rc;
@@ -2084,7 +2199,12 @@ int object_prepare_impl(const void* packed_weights, const float* desc3d, const f
     a.p[0].vdiv = (float)n3;
     a.p[0].kvpart = p.kvpart3;
     a.p[0].kspart = p.kspart3;
-    if (pm != PM_F32) set_w_planes(a.p[0], w.wqkv_p, kPlWqkv);
+    if (pm != PM_F32) {
+      set_w_planes(a.p[0], w.wqkv_p, kPlWqkv);
+      set_a_planes(a.p[0], p.x3p[0], 0, n3);
+      // phi(q)'s planes into the cache: a cached frame's MLP conv 1 reads them as its A1
+      set_y_planes(a.p[0], reinterpret_cast<uint16_t*>(cache + L.phiqp), n3, 1);
+    }
     if ((rc = gemm_launch(EPI_QKV, PRO_PLAIN, tl.qkv[0], a, st, K_QKV_GEMM, pm)) != ONEPOSE_OK)
       return rc;
   }

@@ -45,8 +45,9 @@ def test_object_cache_size_follows_its_flags():
             assert lib.onepose_object_cache_bytes(n3, L, 0) == base
             assert lib.onepose_object_cache_bytes(n3, L, T) - base == 3 * n3 * (2 * L * 1024 + 64)
         assert lib.onepose_object_cache_bytes(n3, 12, T) == lib.onepose_object_cache_bytes(n3, 12, 0)
-    assert lib.onepose_object_cache_bytes(4096, 8, T) < 221e6
-    assert lib.onepose_object_cache_bytes(4096, 8, 0) < 18.4e6
+    # (+ 3 bf16 activation planes of the cached phi(q), 1.5 KB per point, in every precision)
+    assert lib.onepose_object_cache_bytes(4096, 8, T) < 227.3e6
+    assert lib.onepose_object_cache_bytes(4096, 8, 0) < 24.7e6
     assert lib.onepose_object_cache_bytes(0, 8, 0) == 0
     assert lib.onepose_object_cache_bytes(16, 17, 0) == 0
     assert lib.onepose_object_cache_bytes(16, 8, 2) == 0 and lib.onepose_object_cache_bytes(16, 8, -1) == 0

@@ -1,0 +1,24 @@
+#!/bin/bash
+# Activation planes (A by DMA in the bf16 modes): bit identity against the round-start build
+# (tools/ab/lib_base.so), then same-box A/B of the bench lines the change touches.
+set -u
+export TMPDIR=/tmp
+O=gpurun_out/${OUT:-planes}
+mkdir -p $O
+ONEPOSE_LIB=$PWD/tools/ab/lib_base.so timeout -k 10 300 python tools/bitcmp.py dump $O/base.npz > $O/dump_base.log 2>&1 || { tail -20 $O/dump_base.log; exit 1; }
+timeout -k 10 300 python tools/bitcmp.py dump $O/new.npz > $O/dump_new.log 2>&1 || { tail -20 $O/dump_new.log; exit 1; }
+python tools/bitcmp.py cmp $O/base.npz $O/new.npz > $O/cmp.log 2>&1; tail -5 $O/cmp.log
+rm -f $O/base.npz $O/new.npz
+ab() {   # name, bench args
+  for r in 1 2; do
+    for v in A B; do
+      if [ $v = A ]; then lib=$PWD/tools/ab/lib_base.so; else lib=""; fi
+      ONEPOSE_LIB=$lib timeout -k 10 200 python bench.py --no-cpu-baseline $2 > $O/$1_$v$r.json 2> $O/$1_$v$r.err || exit $?
+      python -c "import json; d=json.loads(open('$O/$1_$v$r.json').read().strip().splitlines()[-1]); k=d['kernel_ms_per_step']; print('$1 $v$r', d['value'], d['roofline']['frac'], {x: k.get(x) for x in ('mlp1_gemm','qkv_gemm','mlp2_gemm','kv_reduce','gat','transpose_in')})"
+    done
+  done
+}
+ab c2split "--precision fp32_split --steps 200 --warmup 5"
+ab c2bf16 "--precision bf16 --steps 200 --warmup 5"
+ab c5bf16 "--precision bf16 --n1 2048 --n3 8192 --steps 200 --warmup 5"
+ab c2fp32 "--steps 200 --warmup 5"
