@@ -1168,6 +1168,7 @@ using T64x32K2 = Tile<64, 32, 2, 4, 64>;
 using T64x128 = Tile<64, 128, 1, 4, 32>;
 using T128x128 = Tile<128, 128, 1, 4, 32>;
 using T128x64W8 = Tile<128, 64, 1, 8, 32>;
+using T32x64W2 = Tile<32, 64, 1, 2, 32>;
 
 
 template <int EPI, int PRO, class T, int PM, bool WPL = false, int DMA = 0>
@@ -1195,6 +1196,7 @@ TileDims tile_dims(int tile) {
     case TILE_64x128: return {64, 128, 32};
     case TILE_128x128: return {128, 128, 32};
     case TILE_128x64W8: return {128, 64, 32};
+    case TILE_32x64W2: return {32, 64, 32};
 
     default: return {0, 0, 0};
   }
@@ -1209,7 +1211,8 @@ static_assert(gemm_tile_bm(TILE_64x64) == 64 && gemm_tile_bn(TILE_64x64) == 64 &
                   gemm_tile_bm(TILE_64x32K2) == 64 && gemm_tile_bn(TILE_64x32K2) == 32 &&
                   gemm_tile_bm(TILE_64x128) == 64 && gemm_tile_bn(TILE_64x128) == 128 &&
                   gemm_tile_bm(TILE_128x128) == 128 && gemm_tile_bn(TILE_128x128) == 128 &&
-                  gemm_tile_bm(TILE_128x64W8) == 128 && gemm_tile_bn(TILE_128x64W8) == 64,
+                  gemm_tile_bm(TILE_128x64W8) == 128 && gemm_tile_bn(TILE_128x64W8) == 64 &&
+                  gemm_tile_bm(TILE_32x64W2) == 32 && gemm_tile_bn(TILE_32x64W2) == 64,
               "gemm.h tile shapes must match tile_dims");
 
 GemmProb gemm_prob(const float* A, int lda, const float* W, int ldw, const float* bias,
@@ -1335,6 +1338,7 @@ int gemm_launch(int epi, int pro, int tile, GemmArgs& args, hipStream_t stream, 
   CASE(EPI_STATS, PRO_HEADZ, TILE_64x128, T64x128, PM_BF16, true)
   CASE(EPI_RESID, PRO_NORM_RELU, TILE_64x128, T64x128, PM_BF16, true)
   CASE(EPI_ACC, PRO_PLAIN, TILE_64x128, T64x128, PM_BF16, true)
+  CASE(EPI_RESID, PRO_NORM_RELU, TILE_32x64W2, T32x64W2, PM_SPLIT3, true)
   CASE(EPI_QKV, PRO_PLAIN, TILE_32x128, T32x128, PM_SPLIT3, true)
   CASE(EPI_STATS, PRO_HEADZ, TILE_64x64, T64x64, PM_SPLIT3, true)
   CASE(EPI_RESID, PRO_NORM_RELU, TILE_64x64, T64x64, PM_SPLIT3, true)

@@ -44,6 +44,10 @@ namespace onepose {
 constexpr int kTileKV = TILE_32x128, kTileMLP1 = TILE_64x64,
               kTileMLP2 = TILE_64x64, kTileMLP2F32 = TILE_64x32K2, kTileFinal = TILE_64x64;
 constexpr int kTileScore = TILE_128x64W8, kScoreBM = 128;
+// mlp2 in the split mode below 4 tiles per CU: 32 x 64 on 2 waves (config 2: 640 workgroups
+// instead of 320; 0.231 -> 0.213 ms per frame); the bf16 mode keeps 64 x 64 (32 x 64 measured
+// 0.110 -> 0.117 at config 2 and 0.154 -> 0.166 at config 5, profiles/r04/planes/)
+constexpr int kTileMLP2Split = TILE_32x64W2;
 constexpr int kFusedFoldMaxBatch = 4;   // kv_fold up to this batch, kv_reduce + m_fold above
 constexpr int kMlp2WideTiles = 1024;    // fp32 mlp2: 64x64 tiles from this many (4 per CU)
 constexpr int kQkvWideTiles = 256;      // fp32 qkv: 64x128 tiles from this many 64-row tiles
@@ -1629,7 +1633,9 @@ int mlp2_tile_for(int64_t t64, int pm) {
   // (bf16: 64 x 128 tiles -- 32- or 64-deep stages on the DMA loop -- measured slower for MLP
   // conv 2 in the frame than the register-staged 64 x 64: N = 256 gives them half the
   // workgroups; config 2: 0.138 vs 0.108 ms per step)
-  return pm == PM_F32 && t64 < kMlp2WideTiles ? kTileMLP2F32 : kTileMLP2;
+  if (pm == PM_SPLIT3) return t64 < kMlp2WideTiles ? kTileMLP2Split : kTileMLP2;
+  if (pm == PM_BF16) return kTileMLP2;
+  return t64 < kMlp2WideTiles ? kTileMLP2F32 : kTileMLP2;
 }
 
 // Every side the same choices, from the launch as a whole (layers 4-11, sharded frames).

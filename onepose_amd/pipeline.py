@@ -12,6 +12,11 @@ state and returns the same bits as the uncached forward (SURVEY.md §8b / §8d F
 All buffers are allocated at construction, so the enqueue
 methods only launch kernels on the current stream and can be captured in a HIP graph.
 
+The matcher's ``conf_matrix`` is not kept by default (``with_conf=False``): the reference
+driver discards it (``pred, _ = matching_model(inp)``, ``inference.py:146``), and without a
+caller buffer the dual-softmax kernel computes the row / column winners from the score matrix
+without storing the [B, n1, n3] product (16.8 MB per frame at config 2).
+
 Streaming (``run_stream``): the pose stage of frame k needs one CU (one workgroup per
 frame) while the matcher of frame k+1 needs the whole chip, so the two run on separate HIP
 streams with two buffer slots; events order matcher(k) -> pose(k) and pose(k) -> the
@@ -70,7 +75,7 @@ class _Slot:
 class FramePipeline:
     def __init__(self, matcher: GATsSuperGlue, keypoints3d, desc3d, leaves, batch: int, n1: int,
                  device, scale: float = 1000.0, reprojection_error: float = 5.0,
-                 iterations_count: int = 10000, confidence: float = 0.99, with_conf=True,
+                 iterations_count: int = 10000, confidence: float = 0.99, with_conf=False,
                  slots: int = 2, detector=None, image_hw=(512, 512), object_cache: bool = True,
                  gat_tables: bool = True):
         self.lib = _lib.load()
