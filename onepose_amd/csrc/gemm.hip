@@ -281,7 +281,13 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
   constexpr int TP = EPI == EPI_SCORE ? BN + 1 : BN + 4;
   // QKV's [k_h | v_h] tiles are staged transposed, [BN][BM + 4]
   constexpr int QKVL = EPI == EPI_QKV ? BN * (BM + 4) : 0;
-  constexpr int LDS0 = 2 * STAGE > BM * TP ? 2 * STAGE : BM * TP;
+  // LDS stage buffers: two (one stage of loads in flight ahead of the MFMAs), three for the bf16
+  // DMA-2 loop (two stages in flight: nothing is staged through registers there, and a bf16
+  // stage is small -- 12 KB at 64 x 128 -- so the third buffer fits the epilogue's LDS anyway)
+  // (the A pieces must deal evenly over the waves: every wave then waits for its own stage)
+  constexpr int NBUF =
+      (DMA == 2 && PM == PM_BF16 && (NPL * BM / (512 / T::BKS)) % T::NW == 0) ? 3 : 2;
+  constexpr int LDS0 = NBUF * STAGE > BM * TP ? NBUF * STAGE : BM * TP;
   constexpr int LDSF = LDS0 > QKVL ? LDS0 : QKVL;
   __shared__ __attribute__((aligned(16))) float lds[LDSF];
   __shared__ float zrow[2 * BM];
@@ -582,7 +588,14 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
         sa.rstd = *reinterpret_cast<const float4*>(c.rstd + k0 + kq);
       }
     };
-    auto buf = [&](int st) __attribute__((always_inline)) { return lds + (st & 1) * STAGE; };
+    auto buf = [&](int st) __attribute__((always_inline)) { return lds + (st % NBUF) * STAGE; };
+    // LA stages of loads in flight: stage kt's MFMAs run while stages kt + 1 .. kt + LA load;
+    // at the end of stage kt a wave waits only for stage kt + 1's OPS loads (vmcnt counts in
+    // order), so with LA = 2 a load has two stages' time to land instead of one
+    constexpr int LA = NBUF - 1;
+    constexpr int OPS = PPW + (ADMA ? APPW : 0);   // DMA instructions per wave and stage
+    static_assert(LA == 1 || (ADMA && APIECES % T::NW == 0 && OPS <= 63),
+                  "two stages ahead: A by DMA, the same instruction count on every wave");
     auto dma_w = [&](int st) __attribute__((always_inline)) {
       const int k0 = st * T::BKS;
       const bool first = PRO != PRO_HEADZ || k0 < c.ksplit;
@@ -615,8 +628,13 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
     };
     next_a(kt0);
     dma_w(kt0);
+    if (LA == 2 && kt0 + 1 < nk) {
+      next_a(kt0 + 1);
+      dma_w(kt0 + 1);
+    }
     tk = stamp_start(args.stamp, sl);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (LA == 2 && kt0 + 1 < nk) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(OPS) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if constexpr (!ADMA) store_stage<PRO, T, PM, WPL, NPL, false>(buf(kt0), sa);
     raw_barrier();
     // @phase 1
@@ -626,15 +644,16 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
       float* cur = buf(kt);
       read_frag(cur, f0);
       if (zd) zdot(cur, kt);
-      const bool more = kt + 1 < nk;
-      if (more) {
-        dma_w(kt + 1);
-        next_a(kt + 1);
+      const bool more = kt + LA < nk;   // (the buffer stage kt + LA loads into was last read
+      if (more) {                       //  in stage kt - 1, before that stage's barrier)
+        dma_w(kt + LA);
+        next_a(kt + LA);
       }
 #pragma unroll
       for (int kk = 0; kk < KKW; ++kk) mfma_kk(tg, f0, kk);
       if (zf >= 0) zfinal(zf);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (LA == 2 && more) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(OPS) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if (!ADMA && more) store_stage<PRO, T, PM, WPL, NPL, false>(buf(kt + 1), sa);
       raw_barrier();
     };
