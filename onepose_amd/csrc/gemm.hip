@@ -766,7 +766,8 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
   // BIAS / STATS / RESID: the tile is staged and stored by rows of float4 (1 KB per wave
   // instruction) instead of 4-B stores in the accumulator layout (2 rows x 128 B each): the
   // store-issue-bound tail of the epilogue is 4x shorter; RESID reads R the same way.
-  constexpr bool kRowStore = EPI == EPI_BIAS || EPI == EPI_STATS || EPI == EPI_RESID;
+  constexpr bool kRowStore =
+      EPI == EPI_BIAS || EPI == EPI_STATS || EPI == EPI_RESID || EPI == EPI_BIAS_L2;
 
   if (EPI == EPI_ACC) {   // raw accumulators in register order (a later PRO_HEADZ's acc0)
     if (ks == 0) {
@@ -981,6 +982,24 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
     row_store();
     return;
   }
+  if constexpr (EPI == EPI_BIAS_L2) {
+    // F.normalize(y, p=2, dim=channels) (GATs_SuperGlue.py:245-246) on the staged rows: one wave
+    // per row, lane l holding channels 4l..4l+3 -- the arithmetic of l2norm_kernel (the squares
+    // of a lane's four channels, then the wave butterfly, max(sqrt, 1e-12), four divisions), so
+    // the normalised rows are the bits the separate kernel wrote
+    static_assert(EPI != EPI_BIAS_L2 || BN == 256, "whole rows");
+    for (int r = wave; r < rows; r += T::NW) {
+      float4 v = *reinterpret_cast<const float4*>(tile + r * TP + lane * 4);
+      const float ss = wave_sum(v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w);
+      const float n = fmaxf(sqrtf(ss), 1e-12f);
+      v.x /= n;
+      v.y /= n;
+      v.z /= n;
+      v.w /= n;
+      *reinterpret_cast<float4*>(Y + (int64_t)(m0 + r) * ldy + lane * 4) = v;
+    }
+    return;
+  }
 
   if (EPI == EPI_STATS) {
     // per column: the WM wave-row blocks' (mean, M2 about the block mean) (staged in `part`
@@ -1188,6 +1207,7 @@ using T64x128 = Tile<64, 128, 1, 4, 32>;
 using T128x128 = Tile<128, 128, 1, 4, 32>;
 using T128x64W8 = Tile<128, 64, 1, 8, 32>;
 using T32x64W2 = Tile<32, 64, 1, 2, 32>;
+using T32x256 = Tile<32, 256, 1, 4, 32, 1>;
 
 
 template <int EPI, int PRO, class T, int PM, bool WPL = false, int DMA = 0>
@@ -1216,6 +1236,7 @@ TileDims tile_dims(int tile) {
     case TILE_128x128: return {128, 128, 32};
     case TILE_128x64W8: return {128, 64, 32};
     case TILE_32x64W2: return {32, 64, 32};
+    case TILE_32x256: return {32, 256, 32};
 
     default: return {0, 0, 0};
   }
@@ -1231,7 +1252,8 @@ static_assert(gemm_tile_bm(TILE_64x64) == 64 && gemm_tile_bn(TILE_64x64) == 64 &
                   gemm_tile_bm(TILE_64x128) == 64 && gemm_tile_bn(TILE_64x128) == 128 &&
                   gemm_tile_bm(TILE_128x128) == 128 && gemm_tile_bn(TILE_128x128) == 128 &&
                   gemm_tile_bm(TILE_128x64W8) == 128 && gemm_tile_bn(TILE_128x64W8) == 64 &&
-                  gemm_tile_bm(TILE_32x64W2) == 32 && gemm_tile_bn(TILE_32x64W2) == 64,
+                  gemm_tile_bm(TILE_32x64W2) == 32 && gemm_tile_bn(TILE_32x64W2) == 64 &&
+                  gemm_tile_bm(TILE_32x256) == 32 && gemm_tile_bn(TILE_32x256) == 256,
               "gemm.h tile shapes must match tile_dims");
 
 GemmProb gemm_prob(const float* A, int lda, const float* W, int ldw, const float* bias,
@@ -1279,6 +1301,8 @@ int gemm_launch(int epi, int pro, int tile, GemmArgs& args, hipStream_t stream, 
                     P.st_cnt_bs >= ceil_div(P.N, td.bn) * (1 + stats_groups(P.M, td.bm))),
                "gemm: STATS finalize needs group partials and %d counters per sample",
                ceil_div(P.N, td.bn) * (1 + stats_groups(P.M, td.bm)));
+    OP_REQUIRE(epi != EPI_BIAS_L2 || (td.bn == 256 && P.N == 256 && P.ldy % 4 == 0),
+               "gemm: BIAS_L2 tiles hold whole 256-column rows");
     OP_REQUIRE((epi != EPI_BIAS && epi != EPI_STATS && epi != EPI_RESID) ||
                    (P.N % 4 == 0 && P.ldy % 4 == 0 && (epi != EPI_RESID || P.ldr % 4 == 0)),
                "gemm: row-stored epilogues need N, ldy (and ldr) multiples of 4");
@@ -1345,6 +1369,7 @@ int gemm_launch(int epi, int pro, int tile, GemmArgs& args, hipStream_t stream, 
   CASE(EPI_SCORE, PRO_PLAIN, TILE_64x64, T64x64, PM_F32, false)
   CASE(EPI_SCORE, PRO_PLAIN, TILE_128x64W8, T128x64W8, PM_F32, false)
   CASE(EPI_BIAS, PRO_PLAIN, TILE_64x64, T64x64, PM_F32, false)
+  CASE(EPI_BIAS_L2, PRO_PLAIN, TILE_32x256, T32x256, PM_F32, false)
   CASE(EPI_ACC, PRO_PLAIN, TILE_64x64, T64x64, PM_F32, false)
   // attention-layer GEMMs in the bf16 modes: W from the packed bf16 planes (weights rounded /
   // split on the host, Mf by the KV fold), A rounded / split as the stage is stored

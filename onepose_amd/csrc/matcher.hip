@@ -43,7 +43,7 @@ namespace onepose {
 // GEMM tile per layer GEMM (gemm.h; measured per shape on config 2).
 constexpr int kTileKV = TILE_32x128, kTileMLP1 = TILE_64x64,
               kTileMLP2 = TILE_64x64, kTileMLP2F32 = TILE_64x32K2, kTileFinal = TILE_64x64;
-constexpr int kTileScore = TILE_128x64W8, kScoreBM = 128;
+constexpr int kTileScore = TILE_128x64W8, kScoreBM = 128, kTileFinalL2 = TILE_32x256;
 // mlp2 in the split mode below 4 tiles per CU: 32 x 64 on 2 waves (config 2: 640 workgroups
 // instead of 320; 0.231 -> 0.213 ms per frame); the bf16 mode keeps 64 x 64 (32 x 64 measured
 // 0.110 -> 0.117 at config 2 and 0.154 -> 0.166 at config 5, profiles/r04/planes/)
@@ -1070,7 +1070,9 @@ __global__ __launch_bounds__(256) void conf_kernel(float* S, int n1, int n3,
   // (0 = none yet; bits + 1 does not wrap for any conf the kernel can produce).
   unsigned cbu[4] = {0u, 0u, 0u, 0u};
   int cbi[4] = {0, 0, 0, 0};
-  unsigned long long rkey = 0ull;   // lane i: row 8 wave + i's winner
+  unsigned long long rk[8];   // this lane's best over its 4 columns, per row of the wave
+#pragma unroll
+  for (int i = 0; i < 8; ++i) rk[i] = 0ull;
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     const int n = tiler * 32 + wave * 8 + i;
@@ -1097,17 +1099,34 @@ __global__ __launch_bounds__(256) void conf_kernel(float* S, int n1, int n3,
           if (cok[j]) ps[col[j]] = c[j];
       }
     }
-    unsigned long long key = ru ? pack_best(__uint_as_float(ru - 1u), ri + col_offset) : 0ull;
+    rk[i] = ru ? pack_best(__uint_as_float(ru - 1u), ri + col_offset) : 0ull;
+  }
+  // The 8 rows' maxima over the wave's 64 lanes, transposed: at the xor-32 step each lane keeps
+  // 4 of the rows (lanes 0-31 rows 0-3, lanes 32-63 rows 4-7) and trades the other 4 with its
+  // partner, at xor 16 2 rows, at xor 8 one; then xor 4, 2, 1 finish that row.  Lane l ends
+  // with row (l >> 3)'s maximum: 10 exchanges instead of 8 full butterflies (48).  A max over
+  // the same keys, so the same winner.
+  {
 #pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) {
+    for (int st = 0; st < 3; ++st) {
+      const int half = 4 >> st, o = 32 >> st;
+      const bool hi = (lane & o) != 0;
+#pragma unroll
+      for (int j = 0; j < half; ++j) {
+        const unsigned long long send = hi ? rk[j] : rk[half + j];
+        const unsigned long long mine = hi ? rk[half + j] : rk[j];
+        const unsigned long long other = shfl_xor_u64(send, o);
+        rk[j] = other > mine ? other : mine;
+      }
+    }
+    unsigned long long key = rk[0];
+#pragma unroll
+    for (int o = 4; o >= 1; o >>= 1) {
       const unsigned long long other = shfl_xor_u64(key, o);
       key = other > key ? other : key;
     }
-    rkey = lane == i ? key : rkey;
-  }
-  {
-    const int n = tiler * 32 + wave * 8 + lane;
-    if (lane < 8 && n < n1) rowpart[((int64_t)b * n1 + n) * ct + tilec] = rkey;
+    const int n = tiler * 32 + wave * 8 + (lane >> 3);
+    if ((lane & 7) == 0 && n < n1) rowpart[((int64_t)b * n1 + n) * ct + tilec] = key;
   }
 #pragma unroll
   for (int j = 0; j < 4; ++j)
@@ -2068,11 +2087,20 @@ int match_impl(const void* packed_weights, const float* desc2d, int64_t desc2d_b
     a.nprob = 2;
     a.p[0] = gemm_prob(x2r, 256, fw, 256, fw + 65536, p.f2, 256, n1, 256, 256, B);
     a.p[1] = gemm_prob(x3r, 256, fw, 256, fw + 65536, p.f3, 256, n3, 256, 256, B);
-    if ((rc = gemm_launch(EPI_BIAS, PRO_PLAIN, kTileFinal, a, st, K_FINAL, pm_out)) != ONEPOSE_OK)
-      return rc;
-    const int rows = B * (n1 + n3);
-    OP_LAUNCH(K_L2NORM, st, l2norm_kernel, dim3(ceil_div(rows, 4)), dim3(256), 0, st, p.f2, B * n1,
-                       p.f3, B * n3);
+    if (pm_out == PM_F32) {
+      // fp32: whole-row tiles normalise in the epilogue (l2norm_kernel's arithmetic, the same
+      // bits), one launch and one pass over f2 / f3 fewer; half the workgroups of 64 x 64,
+      // which leaves CUs to the other match stream
+      if ((rc = gemm_launch(EPI_BIAS_L2, PRO_PLAIN, kTileFinalL2, a, st, K_FINAL, pm_out)) !=
+          ONEPOSE_OK)
+        return rc;
+    } else {
+      if ((rc = gemm_launch(EPI_BIAS, PRO_PLAIN, kTileFinal, a, st, K_FINAL, pm_out)) != ONEPOSE_OK)
+        return rc;
+      const int rows = B * (n1 + n3);
+      OP_LAUNCH(K_L2NORM, st, l2norm_kernel, dim3(ceil_div(rows, 4)), dim3(256), 0, st, p.f2,
+                B * n1, p.f3, B * n3);
+    }
   }
   // score tile: 128 x 64 on 8 waves in fp32 (K = 256 is short; fewer operand loads per FLOP
   // than 64 x 64), 64 x 64 in the split mode (its LDS images are three bf16 planes)
