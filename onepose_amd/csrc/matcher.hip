@@ -256,6 +256,8 @@ struct TransArgs {
   unsigned* zero;   // the forward's in-launch arrival counters, zeroed here (first kernel)
   int nzero;
   int npl = 0;      // activation planes per dstp (0: none)
+  unsigned long long* zero64 = nullptr;   // the packed column winners (fused conf), zeroed here
+  int64_t nzero64 = 0;
 };
 __global__ __launch_bounds__(256) void transpose_in_kernel(TransArgs args, int batch) {
   __shared__ float tile[64][65];
@@ -265,6 +267,8 @@ __global__ __launch_bounds__(256) void transpose_in_kernel(TransArgs args, int b
   if (second) bid -= args.p[0].tiles * batch;
   for (int i = blockIdx.x * 256 + threadIdx.x; i < args.nzero; i += gridDim.x * 256)
     args.zero[i] = 0u;
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < args.nzero64; i += gridDim.x * 256)
+    args.zero64[i] = 0ull;
   const int b = bid / P.tiles, r = bid - b * P.tiles;
   const int n0 = (r >> 2) * 64, c0 = (r & 3) * 64, n = P.n;
   const float* s = P.src + b * P.bs;
@@ -960,6 +964,20 @@ __global__ __launch_bounds__(256) void l2norm_kernel(float* x2, int rows2, float
   *reinterpret_cast<float4*>(p + lane * 4) = v;
 }
 
+// One row's (or column's) softmax statistics from its nt per-tile (max, sum exp) partials at p:
+// lane l takes partials l, l + 64, ...; the max and the rescaled sum over the wave's lanes.
+// Every lane returns the totals.  (conf_kernel's fused form uses the same function, so the
+// statistics are the same bits.)
+__device__ __forceinline__ float2 softmax_stats_wave(const float* p, int nt, int lane) {
+  float mx = -INFINITY;
+  for (int i = lane; i < nt; i += 64) mx = fmaxf(mx, p[2 * i]);
+  mx = wave_max(mx);
+  float s = 0.f;
+  for (int i = lane; i < nt; i += 64) s += p[2 * i + 1] * expf(p[2 * i] - mx);
+  s = wave_sum(s);
+  return make_float2(mx, s);
+}
+
 // Combine the score GEMM's per-tile softmax partials: rows over N3 tiles (softmax dim 2),
 // columns over N1 tiles (softmax dim 1); one wave per row / column, partials across lanes.
 // Also resets the packed argmax words.
@@ -981,12 +999,8 @@ __global__ __launch_bounds__(256) void softmax_reduce_kernel(
   } else {
     return;
   }
-  float mx = -INFINITY;
-  for (int i = lane; i < nt; i += 64) mx = fmaxf(mx, p[2 * i]);
-  mx = wave_max(mx);
-  float s = 0.f;
-  for (int i = lane; i < nt; i += 64) s += p[2 * i + 1] * expf(p[2 * i] - mx);
-  s = wave_sum(s);
+  const float2 st = softmax_stats_wave(p, nt, lane);
+  const float mx = st.x, s = st.y;
   if (lane == 0) {
     if (idx < nr) {
       rowmax[idx] = mx;
@@ -1018,27 +1032,76 @@ __device__ __forceinline__ unsigned long long shfl_xor_u64(unsigned long long v,
 }
 
 // conf = softmax(S, dim=1) * softmax(S, dim=2) (GATs_SuperGlue.py:253) in place over S,
-// plus row/column max+argmax (:256).  Workgroup = 32 rows (2D) x 256 columns (3D); wave w owns
-// rows 8w..8w+7, lane l owns 4 columns (16-byte loads when n3 % 4 == 0), all loads issued
-// before any use.  Row winners: in-wave reduction, then lane i stores row i's winner over the
+// plus row/column max+argmax (:256).  Workgroup = 32 rows (2D) x 256 columns (3D) on 8 waves
+// (4 waves per SIMD at config 2, for the latency; 4 waves of 8 rows gave 2); wave w owns rows
+// 4w..4w+3, lane l owns 4 columns (16-byte loads when n3 % 4 == 0), all loads issued before
+// any use.  Row winners: in-wave reduction, then one lane per row stores its winner over the
 // workgroup's 256 columns to rowpart[b][row][column tile] (plain stores; the consumers take
 // the max over the ceil(n3 / 256) parts).  A 64-bit atomicMax per row and workgroup instead
 // cost ~3.5 of the kernel's 12.5 us alone (tools/conf_probe.hip: 16 workgroups meet at each
-// row's word).  Column winners: per thread over its rows, then over the four waves in LDS,
-// one atomicMax per column per workgroup (~0.5 us).
-template <bool VEC>
-__global__ __launch_bounds__(256) void conf_kernel(float* S, int n1, int n3,
+// row's word).  Column winners: per thread over its rows, then over the waves in LDS, one
+// atomicMax per column per workgroup (~0.5 us).
+// STATS (the whole-frame path): the workgroup derives the softmax statistics it needs from the
+// score GEMM's per-tile partials itself -- its 32 rows' (one wave per row, softmax_stats_wave)
+// and its 256 columns' (a thread per column, softmax_stats_wave's lane-0 sum tree restated
+// for nt <= kConfColTiles partials) -- instead of a softmax_reduce launch before it: the same
+// bits, one dependent launch fewer on the frame's chain.  The packed column winners must be
+// zero before the launch (transpose_in zeroes them).
+constexpr int kConfColTiles = 16;   // column partials (score M-tiles) the fused form takes
+constexpr int kConfWaves = 8, kConfRows = 4;   // 32 rows per workgroup: 8 waves x 4 rows
+template <bool VEC, bool STATS>
+__global__ __launch_bounds__(kConfWaves * 64) void conf_kernel(float* S, int n1, int n3,
                                                    const float* rowmax, const float* rowsum,
                                                    const float* colmax, const float* colsum,
                                                    unsigned long long* rowpart,
                                                    unsigned long long* colbest, int write_conf,
-                                                   int col_offset) {
-  __shared__ unsigned long long cb[4][256];
+                                                   int col_offset, const float* srow, int nt3,
+                                                   const float* scol, int mt1) {
+  constexpr int RW = kConfRows;
+  __shared__ unsigned long long cb[kConfWaves][256];
+  __shared__ float cst[2][STATS ? 256 : 1];
   const int ct = (n3 + 255) / 256;
   const int tilec = blockIdx.x % ct, tiler = blockIdx.x / ct;
   const int b = blockIdx.y;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   float* Sb = S + (int64_t)b * n1 * n3;
+  float rst[STATS ? RW : 1][2];   // STATS: the wave's rows' (max, 1 / sum)
+  if constexpr (STATS) {
+    {   // column tilec * 256 + t: lane 0's butterfly sum of softmax_stats_wave, nt <= 16
+      const int cg = tilec * 256 + threadIdx.x;
+      if (threadIdx.x < 256 && cg < n3) {
+        const float* p = scol + ((int64_t)b * n3 + cg) * mt1 * 2;
+        float pm[kConfColTiles], ps[kConfColTiles];
+#pragma unroll
+        for (int i = 0; i < kConfColTiles; ++i) {
+          pm[i] = i < mt1 ? p[2 * i] : -INFINITY;
+          ps[i] = i < mt1 ? p[2 * i + 1] : 0.f;
+        }
+        float mx = -INFINITY;
+#pragma unroll
+        for (int i = 0; i < kConfColTiles; ++i) mx = fmaxf(mx, pm[i]);
+        float v[kConfColTiles];
+#pragma unroll
+        for (int i = 0; i < kConfColTiles; ++i) v[i] = i < mt1 ? ps[i] * expf(pm[i] - mx) : 0.f;
+        // wave_sum's xor 32 / 16 steps add zeros (lanes >= 16 hold none); xor 8 .. 1 as lane 0
+        // sees them
+#pragma unroll
+        for (int o = kConfColTiles / 2; o >= 1; o >>= 1)
+#pragma unroll
+          for (int l = 0; l < o; ++l) v[l] = v[l] + v[l + o];
+        cst[0][threadIdx.x] = mx;
+        cst[1][threadIdx.x] = 1.0f / v[0];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < RW; ++i) {   // the wave's rows, one at a time (as softmax_reduce)
+      const int n = min(tiler * 32 + wave * RW + i, n1 - 1);
+      const float2 r = softmax_stats_wave(srow + ((int64_t)b * n1 + n) * nt3 * 2, nt3, lane);
+      rst[i][0] = r.x;
+      rst[i][1] = 1.0f / r.y;
+    }
+    __syncthreads();
+  }
   int col[4];
   bool cok[4];
   float cmx[4], cinv[4];
@@ -1046,13 +1109,19 @@ __global__ __launch_bounds__(256) void conf_kernel(float* S, int n1, int n3,
   for (int j = 0; j < 4; ++j) {
     col[j] = tilec * 256 + (VEC ? lane * 4 + j : lane + 64 * j);
     cok[j] = col[j] < n3;
-    cmx[j] = cok[j] ? colmax[(int64_t)b * n3 + col[j]] : 0.f;
-    cinv[j] = cok[j] ? 1.0f / colsum[(int64_t)b * n3 + col[j]] : 0.f;
+    if constexpr (STATS) {
+      const int cl = VEC ? lane * 4 + j : lane + 64 * j;
+      cmx[j] = cok[j] ? cst[0][cl] : 0.f;
+      cinv[j] = cok[j] ? cst[1][cl] : 0.f;
+    } else {
+      cmx[j] = cok[j] ? colmax[(int64_t)b * n3 + col[j]] : 0.f;
+      cinv[j] = cok[j] ? 1.0f / colsum[(int64_t)b * n3 + col[j]] : 0.f;
+    }
   }
-  float v[8][4];
+  float v[RW][4];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int n = min(tiler * 32 + wave * 8 + i, n1 - 1);
+  for (int i = 0; i < RW; ++i) {
+    const int n = min(tiler * 32 + wave * RW + i, n1 - 1);
     const float* ps = Sb + (int64_t)n * n3;
     if (VEC && cok[0]) {
       const float4 q = *reinterpret_cast<const float4*>(ps + col[0]);
@@ -1070,15 +1139,21 @@ __global__ __launch_bounds__(256) void conf_kernel(float* S, int n1, int n3,
   // (0 = none yet; bits + 1 does not wrap for any conf the kernel can produce).
   unsigned cbu[4] = {0u, 0u, 0u, 0u};
   int cbi[4] = {0, 0, 0, 0};
-  unsigned long long rk[8];   // this lane's best over its 4 columns, per row of the wave
+  unsigned long long rk[RW];   // this lane's best over its 4 columns, per row of the wave
 #pragma unroll
-  for (int i = 0; i < 8; ++i) rk[i] = 0ull;
+  for (int i = 0; i < RW; ++i) rk[i] = 0ull;
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int n = tiler * 32 + wave * 8 + i;
+  for (int i = 0; i < RW; ++i) {
+    const int n = tiler * 32 + wave * RW + i;
     if (n >= n1) break;   // wave-uniform
-    const float rmx = rowmax[(int64_t)b * n1 + n];
-    const float rinv = 1.0f / rowsum[(int64_t)b * n1 + n];
+    float rmx, rinv;
+    if constexpr (STATS) {
+      rmx = rst[i][0];
+      rinv = rst[i][1];
+    } else {
+      rmx = rowmax[(int64_t)b * n1 + n];
+      rinv = 1.0f / rowsum[(int64_t)b * n1 + n];
+    }
     unsigned ru = 0u;
     int ri = 0;
     float c[4];
@@ -1101,15 +1176,18 @@ __global__ __launch_bounds__(256) void conf_kernel(float* S, int n1, int n3,
     }
     rk[i] = ru ? pack_best(__uint_as_float(ru - 1u), ri + col_offset) : 0ull;
   }
-  // The 8 rows' maxima over the wave's 64 lanes, transposed: at the xor-32 step each lane keeps
-  // 4 of the rows (lanes 0-31 rows 0-3, lanes 32-63 rows 4-7) and trades the other 4 with its
-  // partner, at xor 16 2 rows, at xor 8 one; then xor 4, 2, 1 finish that row.  Lane l ends
-  // with row (l >> 3)'s maximum: 10 exchanges instead of 8 full butterflies (48).  A max over
-  // the same keys, so the same winner.
+  // The RW rows' maxima over the wave's 64 lanes, transposed: at the xor-32 step each lane keeps
+  // half of the rows (lanes 0-31 the first half, lanes 32-63 the second) and trades the other
+  // half with its partner, at xor 16 a quarter, ...; once one row is left, the remaining xor
+  // steps finish it.  Lane l ends with row (l >> (6 - log2 RW))'s maximum: RW - 1 + 6 - log2 RW
+  // exchanges instead of RW full butterflies (6 RW).  A max over the same keys, so the same
+  // winner.
   {
+    constexpr int LG = RW == 8 ? 3 : RW == 4 ? 2 : RW == 2 ? 1 : 0;
+    static_assert((1 << LG) == RW, "rows per wave: a power of two <= 8");
 #pragma unroll
-    for (int st = 0; st < 3; ++st) {
-      const int half = 4 >> st, o = 32 >> st;
+    for (int st = 0; st < LG; ++st) {
+      const int half = (RW / 2) >> st, o = 32 >> st;
       const bool hi = (lane & o) != 0;
 #pragma unroll
       for (int j = 0; j < half; ++j) {
@@ -1121,12 +1199,12 @@ __global__ __launch_bounds__(256) void conf_kernel(float* S, int n1, int n3,
     }
     unsigned long long key = rk[0];
 #pragma unroll
-    for (int o = 4; o >= 1; o >>= 1) {
+    for (int o = 32 >> LG; o >= 1; o >>= 1) {
       const unsigned long long other = shfl_xor_u64(key, o);
       key = other > key ? other : key;
     }
-    const int n = tiler * 32 + wave * 8 + (lane >> 3);
-    if ((lane & 7) == 0 && n < n1) rowpart[((int64_t)b * n1 + n) * ct + tilec] = key;
+    const int n = tiler * 32 + wave * RW + (lane >> (6 - LG));
+    if ((lane & ((64 >> LG) - 1)) == 0 && n < n1) rowpart[((int64_t)b * n1 + n) * ct + tilec] = key;
   }
 #pragma unroll
   for (int j = 0; j < 4; ++j)
@@ -1135,9 +1213,9 @@ __global__ __launch_bounds__(256) void conf_kernel(float* S, int n1, int n3,
   __syncthreads();
   {
     const int cc = threadIdx.x, cg = tilec * 256 + cc;
-    if (cg < n3) {
+    if (cc < 256 && cg < n3) {
       unsigned long long k = cb[0][cc];
-      for (int w = 1; w < 4; ++w) k = cb[w][cc] > k ? cb[w][cc] : k;
+      for (int w = 1; w < kConfWaves; ++w) k = cb[w][cc] > k ? cb[w][cc] : k;
       if (k != 0ull) atomicMax(colbest + (int64_t)b * n3 + cg, k);
     }
   }
@@ -1145,11 +1223,19 @@ __global__ __launch_bounds__(256) void conf_kernel(float* S, int n1, int n3,
 
 // Mutual nearest neighbour + threshold (GATs_SuperGlue.py:256-267).
 // A row's winner over all columns: the max of its conf_kernel parts (ct of them).
+// The parts' loads are issued 16 at a time (one round trip at config 2, ct = 16) instead of one
+// per loop iteration; the max of the same keys (all >= 0), so the same winner.
 __device__ __forceinline__ unsigned long long row_best(const unsigned long long* rowpart, int ct,
                                                        int64_t row) {
   const unsigned long long* q = rowpart + row * ct;
-  unsigned long long k = q[0];
-  for (int i = 1; i < ct; ++i) k = q[i] > k ? q[i] : k;
+  unsigned long long k = 0ull;
+  for (int i0 = 0; i0 < ct; i0 += 16) {
+    unsigned long long t[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) t[j] = i0 + j < ct ? q[i0 + j] : 0ull;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) k = t[j] > k ? t[j] : k;
+  }
   return k;
 }
 
@@ -1977,6 +2063,10 @@ int match_impl(const void* packed_weights, const float* desc2d, int64_t desc2d_b
   // planes (the token states x2 / x3, phi(q)), which those GEMMs then move by DMA
   const int npl = planes_of(pm);
   auto pl = [&](uint16_t* q) { return npl ? q : nullptr; };
+  // the dual softmax's statistics inside conf_kernel (whole frames, few score M-tiles): no
+  // softmax_reduce launch; the packed column winners are zeroed by the first kernel instead
+  const int score_mt = ceil_div(n1, pm_out == PM_F32 ? kScoreBM : 64);   // colpart per column
+  const bool conf_stats = !sh && score_mt <= kConfColTiles;
   {
     TransArgs ta;
     ta.p[0] = {desc2d, desc2d_bstride, n1, ceil_div(n1, 64) * 4, p.x2[0], pl(p.x2p[0])};
@@ -1985,6 +2075,10 @@ int match_impl(const void* packed_weights, const float* desc2d, int64_t desc2d_b
     ta.zero = p.cnt;
     ta.nzero = p.ncnt;
     ta.npl = npl;
+    if (conf_stats) {
+      ta.zero64 = p.colbest;
+      ta.nzero64 = (int64_t)B * n3;
+    }
     OP_LAUNCH(K_TRANSPOSE, st, transpose_in_kernel, dim3((ta.p[0].tiles + ta.p[1].tiles) * B),
               dim3(256), 0, st, ta, B);
   }
@@ -2105,7 +2199,6 @@ int match_impl(const void* packed_weights, const float* desc2d, int64_t desc2d_b
   // score tile: 128 x 64 on 8 waves in fp32 (K = 256 is short; fewer operand loads per FLOP
   // than 64 x 64), 64 x 64 in the split mode (its LDS images are three bf16 planes)
   const int score_tile = pm_out == PM_F32 ? kTileScore : TILE_64x64;
-  const int score_mt = ceil_div(n1, pm_out == PM_F32 ? kScoreBM : 64);   // colpart per column
   {  // S = D2^T D3 / scale_factor with softmax partials
     GemmArgs a;
     a.nprob = 1;
@@ -2119,9 +2212,10 @@ int match_impl(const void* packed_weights, const float* desc2d, int64_t desc2d_b
   }
   {
     const int64_t total = (int64_t)B * (n1 + n3);
-    OP_LAUNCH(K_SMX_REDUCE, st, softmax_reduce_kernel, dim3((unsigned)((total + 3) / 4)), dim3(256),
-                       0, st, p.rowpart, ch3, p.colpart, score_mt, B, n1, n3, p.rowmax, p.rowsum,
-                       p.colmax, p.colsum, p.rowbest, p.colbest);
+    if (!conf_stats)
+      OP_LAUNCH(K_SMX_REDUCE, st, softmax_reduce_kernel, dim3((unsigned)((total + 3) / 4)),
+                dim3(256), 0, st, p.rowpart, ch3, p.colpart, score_mt, B, n1, n3, p.rowmax,
+                p.rowsum, p.colmax, p.colsum, p.rowbest, p.colbest);
     const int64_t nr = (int64_t)B * n1;
     if (sh) {   // row softmax over every rank's columns
       OP_HIP(hipMemcpyAsync(sh->send, p.rowmax, nr * 4, hipMemcpyDeviceToDevice, st));
@@ -2133,12 +2227,19 @@ int match_impl(const void* packed_weights, const float* desc2d, int64_t desc2d_b
     }
     const int coff = sh ? sh->offset : 0;
     const dim3 cgrid(ceil_div(n1, 32) * ceil_div(n3, 256), B);
-    if (n3 % 4 == 0)
-      OP_LAUNCH(K_CONF, st, conf_kernel<true>, cgrid, dim3(256), 0, st, S, n1, n3, p.rowmax,
-                p.rowsum, p.colmax, p.colsum, p.rowwin, p.colbest, with_conf ? 1 : 0, coff);
-    else
-      OP_LAUNCH(K_CONF, st, conf_kernel<false>, cgrid, dim3(256), 0, st, S, n1, n3, p.rowmax,
-                p.rowsum, p.colmax, p.colsum, p.rowwin, p.colbest, with_conf ? 1 : 0, coff);
+#define CONF_LAUNCH(V, ST)                                                                   \
+  OP_LAUNCH(K_CONF, st, (conf_kernel<V, ST>), cgrid, dim3(kConfWaves * 64), 0, st, S, n1, n3,  \
+            p.rowmax,                                                                       \
+            p.rowsum, p.colmax, p.colsum, p.rowwin, p.colbest, with_conf ? 1 : 0, coff,     \
+            p.rowpart, ch3, p.colpart, score_mt)
+    if (n3 % 4 == 0) {
+      if (conf_stats) CONF_LAUNCH(true, true);
+      else CONF_LAUNCH(true, false);
+    } else {
+      if (conf_stats) CONF_LAUNCH(false, true);
+      else CONF_LAUNCH(false, false);
+    }
+#undef CONF_LAUNCH
     const unsigned long long* colbest = p.colbest;
     const unsigned long long* rowwin = p.rowwin;
     if (sh) {   // row winners over all columns; every rank's column winners at global columns
