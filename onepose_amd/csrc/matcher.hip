@@ -903,14 +903,15 @@ __global__ __launch_bounds__(256) void gat_tab_kernel(const float* __restrict__ 
   const int lane = threadIdx.x & 63;
   const float4 wh = reinterpret_cast<const float4*>(wa + 256)[lane];
   const float4 h = reinterpret_cast<const float4*>(x3 + ((int64_t)b * n3 + p) * kDim)[lane];
-  float s3 = gat_dot(h, wh);
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) s3 += __shfl_xor(s3, o, 64);
+  // the sorted logits load in the same round trip as h (they do not depend on s3)
   const int pu = __builtin_amdgcn_readfirstlane(p);
   const float* sp = slogs + (int64_t)pu * kLogitStride;
   float sv[MAXL];
 #pragma unroll
   for (int r = 0; r < MAXL; ++r) sv[r] = r < L ? sp[r] : 0.f;
+  float s3 = gat_dot(h, wh);
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) s3 += __shfl_xor(s3, o, 64);
   const float c = sv[0];
   float e0 = s3 + s3;
   e0 = e0 > 0.f ? e0 : e0 * 0.2f;
