@@ -96,12 +96,12 @@ def kernel_work(kind, B, n1, n3, L, cached=False):
         "qkv_gemm": (2 * 3 * C * C * Tq, "flop", "mfma"),      # [q | k v] = Wqkv x
         "mlp1_gemm": (2 * 2 * C * 2 * C * T1, "flop", "mfma"),   # [W1a | Mf] [x ; QZ]
         "mlp2_gemm": (2 * 2 * C * C * T, "flop", "mfma"),
-        "final_gemm": (2 * C * C * T, "flop", "mfma"),
+        "final_gemm": (2 * C * C * B * (n1 + n3), "flop", "mfma"),   # once per frame, all tokens
         "score_gemm": (2 * C * n1 * n3 * B, "flop", "mfma"),
         # GAT: leaves once + the 3D descriptors in and out (fp32)
         "gat": (4 * C * n3 * B * (L + 2), "byte", "hbm"),
-        # conf: read S, write conf (fp32)
-        "conf": (8 * n1 * n3 * B, "byte", "hbm"),
+        # conf: read S (fp32); the pipeline keeps no conf_matrix (the reference discards it)
+        "conf": (4 * n1 * n3 * B, "byte", "hbm"),
     }
     return table.get(kind)
 

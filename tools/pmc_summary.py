@@ -11,7 +11,7 @@ import sys
 
 # GEMM template instance <EPI, PRO, BN> -> kernel kind (gemm.h enums; one instance per kind)
 GEMM_KIND = {(1, 0): "qkv_gemm", (2, 2): "mlp1_gemm", (3, 1): "mlp2_gemm", (0, 0): "final_gemm",
-             (4, 0): "score_gemm"}
+             (6, 0): "final_gemm", (4, 0): "score_gemm"}
 
 
 def kind_of(name):
