@@ -78,25 +78,19 @@ struct GemmProb {
   const float* R;      // residual, [batch][M][ldr]
   int64_t r_bs;
   int ldr;
-  const float* pro_mean;   // [batch][K] (PRO_NORM_RELU), when pro_grp is null
+  const float* pro_mean;   // [batch][K] (PRO_NORM_RELU)
   const float* pro_rstd;
   int64_t pro_bs;
-  // PRO_NORM_RELU from the producing EPI_STATS launch's group partials instead: each workgroup
-  // merges the pro_ngroups (mean, M2) pairs of every K channel (groups of pro_grows rows, the
-  // M rows in all) into mean / rstd in its prologue -- the finalize's second level, moved out
-  // of the STATS launch's tail.  [batch][ngroups][2][K] doubles, pro_grp_bs per sample.
-  const double* pro_grp;
-  int64_t pro_grp_bs;
-  int pro_ngroups, pro_grows;
   float* stats;        // EPI_STATS: [batch][mtiles][2][N]  (mtiles = ceil(M / tile rows))
   unsigned* st_cnt;    // EPI_STATS: arrival counters, zero before the launch, st_cnt_bs per
-                       //   sample: [ntiles] column-block counters (unused since the second
-                       //   level moved to the consumer), then [ntiles][ngroups] group counters;
-                       //   null = partials only.  The last M-tile of each group
-                       //   (stats_group_size) merges the group into st_grp; the consumer
-                       //   (PRO_NORM_RELU with pro_grp) merges the groups
+                       //   sample: [ntiles] column-block counters, then [ntiles][ngroups] group
+                       //   counters; null = partials only.  Two levels (gemm.hip): the last
+                       //   M-tile of each group (stats_group_size) merges the group into
+                       //   st_grp, the last group merger the groups into st_mean / st_rstd
   int st_cnt_bs;
   double* st_grp;      // EPI_STATS with st_cnt: [batch][ngroups][2][N] group (mean, M2)
+  float* st_mean;
+  float* st_rstd;
   float* rowstat;      // EPI_SCORE: [batch][M][ntiles][2]
   float* colstat;      // EPI_SCORE: [batch][N][mtiles][2]
   float* kvpart;       // EPI_QKV: [batch][mtiles][4][64][64]

@@ -99,37 +99,6 @@ __device__ __forceinline__ int bsw(int row, int k) {
   else return row * 64 + ((((k >> 3) ^ (row >> 1)) & 7) << 3) + (k & 7);
 }
 
-// InstanceNorm statistics of one channel from the STATS launch's group partials (mean, M2 of
-// groups of `grows` rows, M rows in all), merged in group order shifted by group 0's mean:
-// S1 = sum n_g (mean_g - c), S2 = sum M2_g + n_g (mean_g - c)^2, double.  g2: the channel's
-// group-0 mean; the M2 of group g is at g2[(2 g + 1) * N], its mean at g2[2 g N].
-__device__ __forceinline__ float2 norm_stats_from_groups(const double* g2, int64_t N, int ngroups,
-                                                        int grows, int M) {
-  const double c = g2[0];
-  double S1 = 0.0, S2 = 0.0;
-  constexpr int GD = kStatsMaxGroups;   // every group's partials in flight at once
-  for (int q0 = 0; q0 < ngroups; q0 += GD) {
-    double mg[GD], m2g[GD];
-#pragma unroll
-    for (int u = 0; u < GD; ++u) {
-      const int g = min(q0 + u, ngroups - 1);
-      mg[u] = g2[(int64_t)g * 2 * N];
-      m2g[u] = g2[(int64_t)g * 2 * N + N];
-    }
-#pragma unroll
-    for (int u = 0; u < GD; ++u) {
-      const int g = q0 + u;
-      if (g < ngroups) {
-        const double ngr = (double)min(grows, M - g * grows), d = mg[u] - c;
-        S1 += ngr * d;
-        S2 += m2g[u] + ngr * d * d;
-      }
-    }
-  }
-  const double n = (double)M;
-  return make_float2((float)(c + S1 / n), (float)(1.0 / sqrt((S2 - S1 * S1 / n) / n + 1e-5)));
-}
-
 // Stage registers.  WPL: the W operand comes from NPL bf16 planes in HBM (pre-split weights /
 // folded message weights, gemm.h GemmProb::Wp): 8 B per plane and k-quad, copied to LDS as is.
 template <class T, bool WPL = false, int NPL = 1>
@@ -137,6 +106,7 @@ struct Stage {
   float4 a[T::A4];
   float4 w[WPL ? 1 : T::W4];
   uint2 wp[WPL ? T::W4 : 1][NPL];
+  float4 mean, rstd;
 };
 
 // Per-launch problem fields, selected field by field from the kernel arguments (a
@@ -165,6 +135,10 @@ __device__ __forceinline__ void load_stage(const Ctx& c, int m0, int n0, int k0,
   const int lda = first ? c.lda0 : c.lda1;
   const int ldw = first ? c.ldw0 : c.ldw1;
   const int kk = first ? (k0 + kq) : (k0 - c.ksplit + kq);
+  if (PRO == PRO_NORM_RELU) {
+    s.mean = *reinterpret_cast<const float4*>(c.mean + k0 + kq);
+    s.rstd = *reinterpret_cast<const float4*>(c.rstd + k0 + kq);
+  }
 #pragma unroll
   for (int i = 0; i < T::A4; ++i) {
     const int m = min(m0 + (t + T::NT * i) / T::KQ, c.M - 1);
@@ -257,27 +231,19 @@ __device__ __forceinline__ void store_quad_bf16(__bf16* b16, int off, float4 v) 
 
 // Stage registers -> LDS image at `base` ([BM + BN] rows: A then W), applying the prologue;
 // fp32 rows of PITCH floats, or swizzled bf16 images (Tile::STAGEB elements each).
-// PRO_NORM_RELU: the stage's K offset k0 and the channel statistics nst ([2][K] in LDS: mean,
-// then rstd) give the prologue's (mean, rstd).
 template <int PRO, class T, int PM, bool WPL = false, int NPL = 1, bool DOW = true>
-__device__ __forceinline__ void store_stage(float* base, Stage<T, WPL, NPL>& s, int k0 = 0,
-                                            const float* nst = nullptr, int K = 0) {
+__device__ __forceinline__ void store_stage(float* base, Stage<T, WPL, NPL>& s) {
   const int t = threadIdx.x;
   const int kq = (t % T::KQ) * 4;
   __bf16* b16 = reinterpret_cast<__bf16*>(base);
-  float4 mean = make_float4(0.f, 0.f, 0.f, 0.f), rstd = mean;
-  if (PRO == PRO_NORM_RELU) {
-    mean = *reinterpret_cast<const float4*>(nst + k0 + kq);
-    rstd = *reinterpret_cast<const float4*>(nst + K + k0 + kq);
-  }
 #pragma unroll
   for (int i = 0; i < T::A4; ++i) {
     float4 v = s.a[i];
     if (PRO == PRO_NORM_RELU) {
-      v.x = fmaxf((v.x - mean.x) * rstd.x, 0.f);
-      v.y = fmaxf((v.y - mean.y) * rstd.y, 0.f);
-      v.z = fmaxf((v.z - mean.z) * rstd.z, 0.f);
-      v.w = fmaxf((v.w - mean.w) * rstd.w, 0.f);
+      v.x = fmaxf((v.x - s.mean.x) * s.rstd.x, 0.f);
+      v.y = fmaxf((v.y - s.mean.y) * s.rstd.y, 0.f);
+      v.z = fmaxf((v.z - s.mean.z) * s.rstd.z, 0.f);
+      v.w = fmaxf((v.w - s.mean.w) * s.rstd.w, 0.f);
     }
     const int row = (t + T::NT * i) / T::KQ;
     if constexpr (PM == PM_F32)
@@ -324,7 +290,7 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
   constexpr int LDS0 = NBUF * STAGE > BM * TP ? NBUF * STAGE : BM * TP;
   constexpr int LDSF = LDS0 > QKVL ? LDS0 : QKVL;
   __shared__ __attribute__((aligned(16))) float lds[LDSF];
-  __shared__ float zrow[PRO == PRO_HEADZ ? 2 * BM : 1];
+  __shared__ float zrow[2 * BM];
   __shared__ float part[(EPI == EPI_STATS) ? T::NT * 2 : 1];
 
   // XCD-aware tile order: blocks are dealt round-robin over the 8 XCDs, so hand each XCD a
@@ -387,24 +353,6 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
   const int lane = t & 63;
   const int wave = t >> 6;
   const int ks = wave / (T::WM * T::WN);
-  // PRO_NORM_RELU: the K channels' (mean, rstd) in LDS, merged from the STATS launch's group
-  // partials (or copied from pro_mean / pro_rstd); computed while the first stages' loads are
-  // in flight, before the first stage is stored
-  __shared__ float nst[PRO == PRO_NORM_RELU ? 2 * 512 : 1];
-  auto norm_stats = [&]() __attribute__((always_inline)) {
-    if constexpr (PRO == PRO_NORM_RELU) {
-      const double* grp = F(pro_grp);
-      if (grp != nullptr) grp += b * F(pro_grp_bs);
-      const int ngr = F(pro_ngroups), grows = F(pro_grows);
-      for (int k = t; k < c.K; k += T::NT) {
-        const float2 r = grp != nullptr ? norm_stats_from_groups(grp + k, c.K, ngr, grows, c.M)
-                                        : make_float2(c.mean[k], c.rstd[k]);
-        nst[k] = r.x;
-        nst[c.K + k] = r.y;
-      }
-      __syncthreads();
-    }
-  };
   const int wm = (wave % (T::WM * T::WN)) / T::WN;
   const int wn = wave % T::WN;
 
@@ -635,6 +583,10 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
 #pragma unroll
       for (int i = 0; i < T::A4; ++i)
         sa.a[i] = *reinterpret_cast<const float4*>(base + (first ? aoff0[i] : aoff1[i]));
+      if (PRO == PRO_NORM_RELU) {
+        sa.mean = *reinterpret_cast<const float4*>(c.mean + k0 + kq);
+        sa.rstd = *reinterpret_cast<const float4*>(c.rstd + k0 + kq);
+      }
     };
     auto buf = [&](int st) __attribute__((always_inline)) { return lds + (st % NBUF) * STAGE; };
     // LA stages of loads in flight: stage kt's MFMAs run while stages kt + 1 .. kt + LA load;
@@ -681,10 +633,9 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
       dma_w(kt0 + 1);
     }
     tk = stamp_start(args.stamp, sl);
-    norm_stats();
     if (LA == 2 && kt0 + 1 < nk) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(OPS) : "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if constexpr (!ADMA) store_stage<PRO, T, PM, WPL, NPL, false>(buf(kt0), sa, kt0 * T::BKS, nst, c.K);
+    if constexpr (!ADMA) store_stage<PRO, T, PM, WPL, NPL, false>(buf(kt0), sa);
     raw_barrier();
     // @phase 1
     // one stage: kt's fragments into tg (zd: phi(q) stage, its Z partials; zf >= 0: the head's
@@ -703,8 +654,7 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
       if (zf >= 0) zfinal(zf);
       if (LA == 2 && more) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(OPS) : "memory");
       else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (!ADMA && more)
-        store_stage<PRO, T, PM, WPL, NPL, false>(buf(kt + 1), sa, (kt + 1) * T::BKS, nst, c.K);
+      if (!ADMA && more) store_stage<PRO, T, PM, WPL, NPL, false>(buf(kt + 1), sa);
       raw_barrier();
     };
     if (PRO != PRO_HEADZ) {
@@ -723,8 +673,7 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
   load_stage<PRO, T, WPL, NPL>(c, m0, n0, kt0 * T::BKS, s0);
   load_stage<PRO, T, WPL, NPL>(c, m0, n0, (kt0 + 1) * T::BKS, s1);
   tk = stamp_start(args.stamp, sl);
-  norm_stats();
-  store_stage<PRO, T, PM, WPL, NPL>(lds, s0, kt0 * T::BKS, nst, c.K);
+  store_stage<PRO, T, PM, WPL, NPL>(lds, s0);
   __syncthreads();
   // @phase 1
   read_frag(lds, f0);
@@ -737,8 +686,7 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
     mfma_kk(tg, cur, 0);
     ONEPOSE_SCHED_BARRIER();
     float* na = lds + ((kt + 1) & 1) * STAGE;
-    store_stage<PRO, T, PM, WPL, NPL>(na, next, (kt + 1) * T::BKS, nst, c.K);   // (unused after
-                                                                                 //  the last step)
+    store_stage<PRO, T, PM, WPL, NPL>(na, next);                // (unused after the last step)
     ONEPOSE_SCHED_BARRIER();
 #pragma unroll
     for (int kk = 1; kk < KKW - 1; ++kk) mfma_kk(tg, cur, kk);
@@ -1149,14 +1097,53 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
               }
             }
           }
-          if (n0 + t < N) {   // (read by the consumer's prologue, a later launch)
-            gp[(int64_t)g1 * 2 * N + n0 + t] = c + s1 / ng;
-            gp[(int64_t)g1 * 2 * N + N + n0 + t] = s2 - s1 * s1 / ng;
+          if (n0 + t < N) {
+            __hip_atomic_store(gp + (int64_t)g1 * 2 * N + n0 + t, c + s1 / ng, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(gp + (int64_t)g1 * 2 * N + N + n0 + t, s2 - s1 * s1 / ng,
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           }
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
-        // The second level -- the groups merged into mean / rstd -- is the consumer's prologue
-        // (norm_stats_from_groups): it kept two more round trips (a ticket and the group
-        // partials' loads) on this launch's last tile, the end of the frame's critical path.
+        __syncthreads();
+        if (t == 0) {
+          const unsigned t2 = __hip_atomic_fetch_add(cb + nt, 1u, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_AGENT);
+          last[1] = t2 == (unsigned)(ngroups - 1) ? 1 : 0;
+        }
+        __syncthreads();
+        if (last[1] && t < BN && n0 + t < N) {
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+          const double* g2 = gp + n0 + t;
+          auto ld2 = [&](int g, int half) __attribute__((always_inline)) {
+            return __hip_atomic_load(g2 + (int64_t)g * 2 * N + half * N, __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_AGENT);
+          };
+          const double c = ld2(0, 0);
+          double S1 = 0.0, S2 = 0.0;
+          constexpr int GD = kStatsMaxGroups;   // every group's partials in flight at once
+          for (int q0 = 0; q0 < ngroups; q0 += GD) {
+            double mg[GD], m2g[GD];
+#pragma unroll
+            for (int u = 0; u < GD; ++u) {
+              const int g = min(q0 + u, ngroups - 1);
+              mg[u] = ld2(g, 0);
+              m2g[u] = ld2(g, 1);
+            }
+#pragma unroll
+            for (int u = 0; u < GD; ++u) {
+              const int g = q0 + u;
+              if (g < ngroups) {
+                const double ngr = (double)min(G * BM, M - g * G * BM), d = mg[u] - c;
+                S1 += ngr * d;
+                S2 += m2g[u] + ngr * d * d;
+              }
+            }
+          }
+          const double n = (double)M;
+          F(st_mean)[(int64_t)b * N + n0 + t] = (float)(c + S1 / n);
+          F(st_rstd)[(int64_t)b * N + n0 + t] = (float)(1.0 / sqrt((S2 - S1 * S1 / n) / n + 1e-5));
+        }
       }
     }
   }
@@ -1215,9 +1202,7 @@ void gemm_kernel(GemmArgs args) {
 
 using T64x64 = Tile<64, 64, 1, 4, 32>;
 using T32x128 = Tile<32, 128, 1, 4, 32>;
-// (32-deep stages: with the InstanceNorm statistics in LDS (4 KB) a 64-deep stage's 52 KB
-// would leave two workgroups per CU instead of three)
-using T64x32K2 = Tile<64, 32, 2, 4, 32>;
+using T64x32K2 = Tile<64, 32, 2, 4, 64>;
 using T64x128 = Tile<64, 128, 1, 4, 32>;
 using T128x128 = Tile<128, 128, 1, 4, 32>;
 using T128x64W8 = Tile<128, 64, 1, 8, 32>;
@@ -1246,7 +1231,7 @@ TileDims tile_dims(int tile) {
   switch (tile) {
     case TILE_64x64: return {64, 64, 32};
     case TILE_32x128: return {32, 128, 32};
-    case TILE_64x32K2: return {64, 32, 32};
+    case TILE_64x32K2: return {64, 32, 64};
     case TILE_64x128: return {64, 128, 32};
     case TILE_128x128: return {128, 128, 32};
     case TILE_128x64W8: return {128, 64, 32};
@@ -1321,11 +1306,6 @@ int gemm_launch(int epi, int pro, int tile, GemmArgs& args, hipStream_t stream, 
     OP_REQUIRE((epi != EPI_BIAS && epi != EPI_STATS && epi != EPI_RESID) ||
                    (P.N % 4 == 0 && P.ldy % 4 == 0 && (epi != EPI_RESID || P.ldr % 4 == 0)),
                "gemm: row-stored epilogues need N, ldy (and ldr) multiples of 4");
-    OP_REQUIRE(pro != PRO_NORM_RELU ||
-                   (P.K <= 512 && (P.pro_grp != nullptr
-                                       ? P.pro_ngroups >= 1 && P.pro_grows >= 1
-                                       : P.pro_mean != nullptr && P.pro_rstd != nullptr)),
-               "gemm: NORM prologue needs K <= 512 and group partials or mean / rstd");
     OP_REQUIRE(pro != PRO_HEADZ || (P.ksplit % 64 == 0 && P.K - P.ksplit == 256 &&
                                     (td.bks == 32 || td.bks == 64) && P.ksum != nullptr),
                "gemm: HEADZ needs 4 heads x 64 after ksplit");

@@ -1967,6 +1967,8 @@ int attention_layer(const ApW& w, const Side* sd, int nside, int B, const Plan& 
       a.p[i].st_cnt = cnt + (size_t)i * B * p.cps;
       a.p[i].st_cnt_bs = p.cps;
       a.p[i].st_grp = s.stats == p.stats2 ? p.grp2 : p.grp3;
+      a.p[i].st_mean = p.mean + (size_t)i * B * 512;
+      a.p[i].st_rstd = p.rstd + (size_t)i * B * 512;
       a.p[i].ksum = p.ksum + (size_t)s.src * B * 256;
       a.p[i].ksum_bs = 256;
       a.p[i].ns = sd[s.src].len;
@@ -1998,9 +2000,8 @@ int attention_layer(const ApW& w, const Side* sd, int nside, int B, const Plan& 
     if ((rc = gemm_launch(EPI_STATS, PRO_HEADZ, mlp1_tile(pm), a, st, K_MLP1, pm)) != ONEPOSE_OK)
       return rc;
   }
-  // 5. InstanceNorm statistics: merged into groups inside MLP conv 1 by each group's last M-tile
-  //    (st_cnt), the groups merged in MLP conv 2's prologue; a sharded 3D side is re-merged
-  //    over the ranks' (n, mean, M2)
+  // 5. InstanceNorm statistics: finalized inside MLP conv 1 by each column block's last
+  //    M-tile (st_cnt); a sharded 3D side is re-merged over the ranks' (n, mean, M2)
   if (sh) {
     StatsArgs sa;
     const int str = gemm_tile_rows(kTileMLP1);
@@ -2029,17 +2030,9 @@ int attention_layer(const ApW& w, const Side* sd, int nside, int B, const Plan& 
       g.R = s.x;
       g.ldr = 256;
       g.r_bs = s.x_bs;
-      if (sh && i == 1) {   // a sharded 3D side: the statistics merged over the ranks
-        g.pro_mean = p.mean + (size_t)i * B * 512;
-        g.pro_rstd = p.rstd + (size_t)i * B * 512;
-        g.pro_bs = 512;
-      } else {              // MLP conv 1's group partials, merged in MLP conv 2's prologue
-        const int mt1 = ceil_div(s.n, gemm_tile_bm(kTileMLP1));   // = every mlp1_tile's rows
-        g.pro_grp = s.stats == p.stats2 ? p.grp2 : p.grp3;
-        g.pro_ngroups = stats_groups(s.n, gemm_tile_bm(kTileMLP1));
-        g.pro_grp_bs = (int64_t)g.pro_ngroups * 2 * 512;
-        g.pro_grows = stats_group_size(mt1) * gemm_tile_bm(kTileMLP1);
-      }
+      g.pro_mean = p.mean + (size_t)i * B * 512;
+      g.pro_rstd = p.rstd + (size_t)i * B * 512;
+      g.pro_bs = 512;
       if (pm != PM_F32) set_w_planes(g, w.w2_p, kPlW2);
       if (yp) set_y_planes(g, s.xop, s.n, B);
     }

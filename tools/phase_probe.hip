@@ -80,6 +80,8 @@ void run(const char* name, Bufs& B, int M, int N, int K, bool fin, int iters) {
   p.st_cnt = fin ? B.cnt : nullptr;
   p.st_cnt_bs = 1024;   // one sample: the whole counter buffer
   p.st_grp = B.grp;
+  p.st_mean = B.mean;
+  p.st_rstd = B.rstd;
   if (PRO == PRO_HEADZ) {   // K = [x (256) | phi(q) (256)] from the same A rows
     p.ksplit = K - 256;
     p.A1 = B.A + (K - 256);

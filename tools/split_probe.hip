@@ -456,6 +456,8 @@ float time_prod(float* A, const __bf16* Wp, int64_t wplane, float* bias, float* 
   p.wpl = wplane;
   p.stats = stats;
   p.st_cnt = cnt;
+  p.st_mean = mean;
+  p.st_rstd = rstd;
   if (PRO == PRO_HEADZ) {   // K = [x (256) | phi(q) (256)], the second range from the same A
     p.ksplit = 256;
     p.A1 = A + 256;
