@@ -1045,9 +1045,9 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
       //     partial stores drained; the group's last tile merges the group's partials in tile
       //     order (shifted by the group's first mean) into st_grp -- while the other groups'
       //     tiles still compute;
-      //  2. the groups are merged in group order (shifted by group 0's mean) into mean / rstd
-      //     by the consumer's prologue (PRO_NORM_RELU with pro_grp, a later launch).
-      // Deterministic: neither result depends on which tile arrives last.
+      //  2. that merger takes a ticket on the column block; the last one merges the groups in
+      //     group order (shifted by group 0's mean) into mean / rstd.
+      // Deterministic: neither result depends on which tile or group arrives last.
       static_assert(EPI != EPI_STATS || T::NT >= BN, "finalize threads");
       const int G = stats_group_size(mtiles);
       const int ngroups = (mtiles + G - 1) / G, g1 = mt / G;
