@@ -1319,7 +1319,10 @@ struct Plan {
 // global_load_lds; config 5 QKV 0.204 -> 0.181 ms per step, config 2 bf16 1801 -> 2422 frames/s
 // with the W planes); MLP conv 2 keeps 64 x 64
 constexpr int kTileBf16 = TILE_64x128;
-int mlp1_tile(int pm) { return pm == PM_BF16 ? kTileBf16 : kTileMLP1; }
+#ifndef ONEPOSE_BF16_MLP1_TILE   // (A/B builds only: tools/build_variant.sh)
+#define ONEPOSE_BF16_MLP1_TILE kTileBf16
+#endif
+int mlp1_tile(int pm) { return pm == PM_BF16 ? ONEPOSE_BF16_MLP1_TILE : kTileMLP1; }
 // make_plan sizes MLP conv 1's InstanceNorm partials (stats rows `str`), its arrival counters
 // (kCntPerSide column blocks) and group partials once for every precision: each precision's
 // MLP conv 1 tile must have those rows and at most that many column blocks over N = 512.

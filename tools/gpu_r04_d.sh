@@ -20,3 +20,14 @@ for r in 1 2; do
 done
 timeout -k 10 200 python bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline > $O/bench_20.json 2> $O/bench_20.err || exit $?
 python -c "import json; d=json.loads(open('$O/bench_20.json').read().strip().splitlines()[-1]); print('20 steps', d['value'], d['ms_per_step'], d['roofline']['frac'])"
+# bf16 MLP conv 1 on 64 x 64 DMA-2 tiles (tools/ab/lib_bf64.so) vs the 64 x 128 default
+for r in 1 2; do
+  for v in D V; do
+    if [ $v = V ]; then lib=$PWD/tools/ab/lib_bf64.so; else lib=""; fi
+    for cfg in c2 c5; do
+      if [ $cfg = c5 ]; then A="--n1 2048 --n3 8192"; else A=""; fi
+      ONEPOSE_LIB=$lib timeout -k 10 200 python bench.py --no-cpu-baseline --precision bf16 --steps 200 --warmup 5 $A > $O/bf_${cfg}_$v$r.json 2> $O/bf_${cfg}_$v$r.err || exit $?
+      python -c "import json; d=json.loads(open('$O/bf_${cfg}_$v$r.json').read().strip().splitlines()[-1]); k=d['kernel_ms_per_step']; print('bf16 $cfg $v$r', d['value'], d['roofline']['frac'], {x: k.get(x) for x in ('mlp1_gemm','qkv_gemm','mlp2_gemm')})"
+    done
+  done
+done
