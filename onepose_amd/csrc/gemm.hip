@@ -1329,8 +1329,7 @@ int gemm_launch(int epi, int pro, int tile, GemmArgs& args, hipStream_t stream, 
   // register-staged split loop needs 160+ VGPRs and spills).  bf16 mode: the DMA loop for the
   // 64 x 128 tiles (QKV, MLP conv 1), the register-staged loop for 64 x 64 (MLP conv 2, whose
   // two MFMAs per wave and stage leave a DMA loop nothing to hide behind).
-  const bool dma = pm == PM_SPLIT3 || (pm == PM_BF16 && (tile == TILE_64x128 ||
-                                                         args.p[0].Ap != nullptr));
+  const bool dma = pm == PM_SPLIT3 || (pm == PM_BF16 && tile == TILE_64x128);
   // A from activation planes (every problem of the launch, or none): the DMA loop's DMA-2 form
   const bool adma = args.p[0].Ap != nullptr;
   const bool yplanes = args.p[0].Yp != nullptr;

@@ -1318,11 +1318,10 @@ struct Plan {
 // bf16 mode: QKV and MLP conv 1 on 64 x 128 tiles (4 bf16 MFMAs per wave and stage, W planes by
 // global_load_lds; config 5 QKV 0.204 -> 0.181 ms per step, config 2 bf16 1801 -> 2422 frames/s
 // with the W planes); MLP conv 2 keeps 64 x 64
+// (bf16 MLP conv 1 on 64 x 64 DMA-2 tiles -- 640 workgroups, two stages ahead -- measured
+// slower: config 2 2962 -> 2828, config 5 1642 -> 1552 frames/s, profiles/r04/r04d/)
 constexpr int kTileBf16 = TILE_64x128;
-#ifndef ONEPOSE_BF16_MLP1_TILE   // (A/B builds only: tools/build_variant.sh)
-#define ONEPOSE_BF16_MLP1_TILE kTileBf16
-#endif
-int mlp1_tile(int pm) { return pm == PM_BF16 ? ONEPOSE_BF16_MLP1_TILE : kTileMLP1; }
+int mlp1_tile(int pm) { return pm == PM_BF16 ? kTileBf16 : kTileMLP1; }
 // make_plan sizes MLP conv 1's InstanceNorm partials (stats rows `str`), its arrival counters
 // (kCntPerSide column blocks) and group partials once for every precision: each precision's
 // MLP conv 1 tile must have those rows and at most that many column blocks over N = 512.
