@@ -908,9 +908,6 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
         } else {
           y = acc[j][i] + bias;
         }
-        if (EPI == EPI_SCORE) {
-          if (gm < M && col_ok) Y[(int64_t)gm * ldy + gn] = y;
-        }
         yv[i] = (gm < M) ? y : 0.f;
         if (kStage || kRowStore) tile[row * TP + col] = yv[i];
       }
@@ -1155,6 +1152,28 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
     static_assert(EPI != EPI_SCORE || (T::NT >= 4 * BM && T::NT >= 4 * BN && BM % 16 == 0 &&
                                        BN % 16 == 0 && BM <= 128 && BN <= 128), "score tile");
     const int cols = min(BN, N - n0);
+    // S from the staged tile by rows, four consecutive columns per thread (one 16-B store per
+    // thread and row instead of a 4-B store per accumulator element: the same values)
+    {
+      constexpr int C4 = BN / 4, PER = BM * C4 / T::NT;
+      static_assert(EPI != EPI_SCORE || BM * C4 % T::NT == 0, "score row pass");
+      const bool vec = (ldy & 3) == 0 && (n0 & 3) == 0;
+#pragma unroll
+      for (int p = 0; p < PER; ++p) {
+        const int idx = t + T::NT * p, r = idx / C4, cc = (idx % C4) * 4;
+        const int gm = m0 + r, gn = n0 + cc;
+        if (gm >= M) continue;
+        const float* tr = tile + r * TP + cc;   // (pitch BN + 1: scalar reads)
+        float* yr = Y + (int64_t)gm * ldy + gn;
+        if (vec && gn + 3 < N) {
+          *reinterpret_cast<float4*>(yr) = make_float4(tr[0], tr[1], tr[2], tr[3]);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (gn + e < N) yr[e] = tr[e];
+        }
+      }
+    }
     const int line = t >> 2, qtr = t & 3;
     // quarters of a row (column) of BN (BM) entries: 16 or 32 each
     const int lo_r = qtr * (BN / 4), lo_c = qtr * (BM / 4);

@@ -1,5 +1,5 @@
 #!/bin/bash
-# kv_fold with its whole C column in flight: bit identity against the round-start build, then a
+# kv_fold with its whole C column in flight, score S stored by rows: bit identity against the round-start build, then a
 # same-box A/B against the previous commit's build (tools/ab/lib_prev.so), fp32 300 steps.
 set -u
 export TMPDIR=/tmp
@@ -13,6 +13,6 @@ for r in 1 2 3; do
   for v in A B; do
     if [ $v = A ]; then lib=$PWD/tools/ab/lib_prev.so; else lib=""; fi
     ONEPOSE_LIB=$lib timeout -k 10 200 python bench.py --no-cpu-baseline --steps 300 --warmup 5 > $O/c2_$v$r.json 2> $O/c2_$v$r.err || exit $?
-    python -c "import json; d=json.loads(open('$O/c2_$v$r.json').read().strip().splitlines()[-1]); k=d['kernel_ms_per_step']; print('c2 $v$r', d['value'], d['roofline']['frac'], {x: k.get(x) for x in ('kv_reduce','mlp1_gemm','qkv_gemm')})"
+    python -c "import json; d=json.loads(open('$O/c2_$v$r.json').read().strip().splitlines()[-1]); k=d['kernel_ms_per_step']; print('c2 $v$r', d['value'], d['roofline']['frac'], {x: k.get(x) for x in ('kv_reduce','score_gemm','mlp1_gemm','qkv_gemm')})"
   done
 done
