@@ -29,7 +29,7 @@ struct WgRec {
   unsigned hwid, xcc, pad0, pad1;
 };
 
-template <int EPI, int PRO, class T, int PM, bool WPL, bool DMA>
+template <int EPI, int PRO, class T, int PM, bool WPL, int DMA>
 __global__ __launch_bounds__(T::NT) __attribute__((amdgpu_waves_per_eu(T::WPE)))
 void phase_kernel(GemmArgs args, WgRec* rec) {
   __shared__ StampLds sl;
@@ -60,12 +60,13 @@ struct Bufs {
   double* grp;   // InstanceNorm group partials (gemm.h st_grp)
   uint16_t* Wp;   // 3 bf16 planes of W ([N][K] each, MMAX-sized stride)
   uint16_t* Ab;   // bf16 copy of A ([MMAX][K], round to nearest even)
-  int64_t wpl;
+  uint16_t* Ap;   // 3 activation planes of A ([MMAX][K] each: the exact split; plane 0 = Ab)
+  int64_t wpl, apl;
   unsigned* cnt;
   WgRec* rec;
 };
 
-template <int EPI, int PRO, class T, int PM = PM_F32, bool DMA = false>
+template <int EPI, int PRO, class T, int PM = PM_F32, int DMA = 0>
 void run(const char* name, Bufs& B, int M, int N, int K, bool fin, int iters) {
   GemmArgs a;
   memset(&a, 0, sizeof(a));
@@ -75,6 +76,11 @@ void run(const char* name, Bufs& B, int M, int N, int K, bool fin, int iters) {
   if (PM != PM_F32) {
     p.Wp = B.Wp;
     p.wpl = B.wpl;
+  }
+  if (DMA == 2) {   // A planes by global_load_lds (the product's QKV / MLP conv 1 in bf16 modes)
+    p.Ap = B.Ap;
+    p.apl = B.apl;
+    p.ldap = K;
   }
   p.stats = B.stats;
   p.st_cnt = fin ? B.cnt : nullptr;
@@ -88,6 +94,11 @@ void run(const char* name, Bufs& B, int M, int N, int K, bool fin, int iters) {
     p.lda1 = K;
     p.ksum = B.ksum;
     p.ns = 4096.f;
+    if (DMA == 2) {
+      p.Ap1 = B.Ap + (K - 256);
+      p.apl1 = B.apl;
+      p.ldap1 = K;
+    }
   }
   if (EPI == EPI_QKV) {
     p.kvpart = B.stats;    // [mtiles][4][64][64]: 80 x 64 KB = 5 MB < 16 MB
@@ -230,7 +241,7 @@ static double maxdiff(const std::vector<float>& a, const std::vector<float>& b) 
   return d;
 }
 
-int main() {
+int main(int argc, char** argv) {
   const int MMAX = 16384, K = 512, N = 768;   // W rows: up to 768 (QKV)
   srand(1);
   std::vector<float> hA((size_t)MMAX * K), hW((size_t)N * K), hb(N), hk(256, 30.f), hm(N, 0.1f),
@@ -276,8 +287,19 @@ int main() {
       pl[(size_t)N * K + i] = m;
       pl[(size_t)2 * N * K + i] = bits(r - val(m));
     }
-    std::vector<uint16_t> ab(hA.size());
-    for (size_t i = 0; i < hA.size(); ++i) ab[i] = bits(hA[i]);
+    std::vector<uint16_t> ab(hA.size()), ap(3 * hA.size());
+    for (size_t i = 0; i < hA.size(); ++i) {
+      const float x = hA[i];
+      const uint16_t h = bits(x);
+      const float r = x - val(h);
+      const uint16_t m = bits(r);
+      ab[i] = ap[i] = h;
+      ap[hA.size() + i] = m;
+      ap[2 * hA.size() + i] = bits(r - val(m));
+    }
+    hipMalloc(&B.Ap, ap.size() * 2);
+    hipMemcpy(B.Ap, ap.data(), ap.size() * 2, hipMemcpyHostToDevice);
+    B.apl = (int64_t)hA.size();
     hipMalloc(&B.Ab, ab.size() * 2);
     hipMemcpy(B.Ab, ab.data(), ab.size() * 2, hipMemcpyHostToDevice);
     hipMalloc(&B.Wp, pl.size() * 2);
@@ -288,6 +310,22 @@ int main() {
   using T64x128 = Tile<64, 128, 1, 4, 32>;
   using T64x128B = Tile<64, 128, 1, 4, 64>;
   for (int r = 0; r < 2; ++r) run<EPI_STATS, PRO_HEADZ, T64x64>("warm", B, 5120, 512, 512, true, 200);
+  if (argc > 1 && !strcmp(argv[1], "dma")) {   // round 4: the DMA-2 loop (A and W planes)
+    for (int m : {5120, 10240}) {
+      printf("--- mlp1 STATS+HEADZ+fin, M %d (A planes by DMA) ---\n", m);
+      run<EPI_STATS, PRO_HEADZ, T64x64>("fp32 64x64 (production)", B, m, 512, 512, true, it);
+      run<EPI_STATS, PRO_HEADZ, T64x64, PM_SPLIT3, 2>("split 64x64 dma2", B, m, 512, 512, true, it);
+      run<EPI_STATS, PRO_HEADZ, T64x128, PM_SPLIT3, 2>("split 64x128 dma2", B, m, 512, 512, true, it);
+      run<EPI_STATS, PRO_HEADZ, T64x128, PM_BF16, 2>("bf16 64x128 dma2", B, m, 512, 512, true, it);
+      run<EPI_STATS, PRO_HEADZ, T64x128, PM_BF16, 1>("bf16 64x128 dma1", B, m, 512, 512, true, it);
+      printf("--- qkv, M %d N 768 K 256 ---\n", m);
+      run<EPI_QKV, PRO_PLAIN, T32x128>("fp32 32x128", B, m, 768, 256, false, it);
+      run<EPI_QKV, PRO_PLAIN, T32x128, PM_SPLIT3, 2>("split 32x128 dma2", B, m, 768, 256, false, it);
+      run<EPI_QKV, PRO_PLAIN, T64x128, PM_SPLIT3, 2>("split 64x128 dma2", B, m, 768, 256, false, it);
+      run<EPI_QKV, PRO_PLAIN, T64x128, PM_BF16, 2>("bf16 64x128 dma2", B, m, 768, 256, false, it);
+    }
+    return 0;
+  }
   printf("--- score GEMM (config 2: 1024 x 4096, K 256) ---\n");
   using T128x64W8 = Tile<128, 64, 1, 8, 32>;
   for (int r = 0; r < 2; ++r) {
