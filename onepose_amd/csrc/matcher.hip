@@ -484,14 +484,13 @@ __global__ __launch_bounds__(256) void kv_fold256_kernel(KvFoldArgs args, float*
 #pragma unroll
     for (int j = 0; j < KVF_DEPTH; ++j) { acc.x += v[j].x; acc.y += v[j].y; acc.z += v[j].z; acc.w += v[j].w; }
   }
-  // the fold's C column (independent of KV): all 64 values in flight across the reduction
-  // below -- one round trip instead of a quarter per round trip (the same values and FMAs)
+  // the fold's first quarter of C (independent of KV) is in flight across the reduction below
   const int o = os * 256 + t;   // Mf row o
   const float* ct = args.ct + (h * 64) * 512 + o;
-  float cv[64];
+  float cv[16];
   if (g != 64) {
 #pragma unroll
-    for (int i = 0; i < 64; ++i) cv[i] = ct[i * 512];
+    for (int i = 0; i < 16; ++i) cv[i] = *reinterpret_cast<const std::remove_reference_t<decltype(cv[0])>*>(ct + i * 512);
   }
   red[w][lane] = acc;
   __syncthreads();
@@ -515,7 +514,10 @@ __global__ __launch_bounds__(256) void kv_fold256_kernel(KvFoldArgs args, float*
   f2v y01, y23;
 #pragma unroll
   for (int qq = 0; qq < 4; ++qq) {
-    const float* cq = cv + qq * 16;
+    if (qq > 0) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) cv[i] = ct[(qq * 16 + i) * 512];
+    }
     f2v a01 = (f2v)(0.f), a23 = (f2v)(0.f);
 #pragma unroll
     for (int i = 0; i < 16; i += 4) {
@@ -523,14 +525,14 @@ __global__ __launch_bounds__(256) void kv_fold256_kernel(KvFoldArgs args, float*
       const float4 k1 = *reinterpret_cast<const float4*>(kvr + 1 * 64 + qq * 16 + i);
       const float4 k2 = *reinterpret_cast<const float4*>(kvr + 2 * 64 + qq * 16 + i);
       const float4 k3 = *reinterpret_cast<const float4*>(kvr + 3 * 64 + qq * 16 + i);
-      a01 = __builtin_elementwise_fma((f2v)(cq[i]), (f2v){k0.x, k1.x}, a01);
-      a23 = __builtin_elementwise_fma((f2v)(cq[i]), (f2v){k2.x, k3.x}, a23);
-      a01 = __builtin_elementwise_fma((f2v)(cq[i + 1]), (f2v){k0.y, k1.y}, a01);
-      a23 = __builtin_elementwise_fma((f2v)(cq[i + 1]), (f2v){k2.y, k3.y}, a23);
-      a01 = __builtin_elementwise_fma((f2v)(cq[i + 2]), (f2v){k0.z, k1.z}, a01);
-      a23 = __builtin_elementwise_fma((f2v)(cq[i + 2]), (f2v){k2.z, k3.z}, a23);
-      a01 = __builtin_elementwise_fma((f2v)(cq[i + 3]), (f2v){k0.w, k1.w}, a01);
-      a23 = __builtin_elementwise_fma((f2v)(cq[i + 3]), (f2v){k2.w, k3.w}, a23);
+      a01 = __builtin_elementwise_fma((f2v)(cv[i]), (f2v){k0.x, k1.x}, a01);
+      a23 = __builtin_elementwise_fma((f2v)(cv[i]), (f2v){k2.x, k3.x}, a23);
+      a01 = __builtin_elementwise_fma((f2v)(cv[i + 1]), (f2v){k0.y, k1.y}, a01);
+      a23 = __builtin_elementwise_fma((f2v)(cv[i + 1]), (f2v){k2.y, k3.y}, a23);
+      a01 = __builtin_elementwise_fma((f2v)(cv[i + 2]), (f2v){k0.z, k1.z}, a01);
+      a23 = __builtin_elementwise_fma((f2v)(cv[i + 2]), (f2v){k2.z, k3.z}, a23);
+      a01 = __builtin_elementwise_fma((f2v)(cv[i + 3]), (f2v){k0.w, k1.w}, a01);
+      a23 = __builtin_elementwise_fma((f2v)(cv[i + 3]), (f2v){k2.w, k3.w}, a23);
     }
     y01 = qq == 0 ? a01 : y01 + a01;
     y23 = qq == 0 ? a23 : y23 + a23;
