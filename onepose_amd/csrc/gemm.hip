@@ -1406,6 +1406,7 @@ int gemm_launch(int epi, int pro, int tile, GemmArgs& args, hipStream_t stream, 
   CASE(EPI_STATS, PRO_HEADZ, TILE_64x64, T64x64, PM_SPLIT3, true)
   CASE(EPI_STATS, PRO_HEADZ, TILE_64x128, T64x128, PM_SPLIT3, true)
   CASE(EPI_QKV, PRO_PLAIN, TILE_64x128, T64x128, PM_SPLIT3, true)
+  CASE(EPI_ACC, PRO_PLAIN, TILE_64x128, T64x128, PM_SPLIT3, true)
   CASE(EPI_RESID, PRO_NORM_RELU, TILE_64x64, T64x64, PM_SPLIT3, true)
   // final projection and score GEMM in the split mode (activations as W: VALU split)
   CASE(EPI_SCORE, PRO_PLAIN, TILE_64x64, T64x64, PM_SPLIT3, false)

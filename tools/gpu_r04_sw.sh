@@ -8,7 +8,7 @@ O=gpurun_out/r04sw
 mkdir -p $O
 SW=$PWD/tools/ab/lib_sw.so
 ONEPOSE_LIB=$SW timeout -k 10 400 python -u -m pytest tests/test_matcher_gpu.py tests/test_configs_gpu.py \
-  -m gpu -k "split" -x -q -s --timeout 200 --timeout-method thread > $O/tests_sw.log 2>&1 \
+  -m gpu -x -q -s --timeout 200 --timeout-method thread > $O/tests_sw.log 2>&1 \
   || { tail -30 $O/tests_sw.log; exit 1; }
 tail -1 $O/tests_sw.log
 for r in 1 2; do
