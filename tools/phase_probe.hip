@@ -310,6 +310,22 @@ int main(int argc, char** argv) {
   using T64x128 = Tile<64, 128, 1, 4, 32>;
   using T64x128B = Tile<64, 128, 1, 4, 64>;
   for (int r = 0; r < 2; ++r) run<EPI_STATS, PRO_HEADZ, T64x64>("warm", B, 5120, 512, 512, true, 200);
+  if (argc > 1 && !strcmp(argv[1], "big")) {   // round 4: wider split / bf16 tiles, 8 waves
+    using T128x128W8 = Tile<128, 128, 1, 8, 32>;
+    for (int m : {5120, 10240}) {
+      printf("--- mlp1 STATS+HEADZ+fin, M %d ---\n", m);
+      run<EPI_STATS, PRO_HEADZ, T64x64, PM_SPLIT3, 2>("split 64x64 dma2", B, m, 512, 512, true, it);
+      run<EPI_STATS, PRO_HEADZ, T128x128W8, PM_SPLIT3, 2>("split 128x128 w8 dma2", B, m, 512, 512, true, it);
+      run<EPI_STATS, PRO_HEADZ, T64x128, PM_BF16, 2>("bf16 64x128 dma2", B, m, 512, 512, true, it);
+      run<EPI_STATS, PRO_HEADZ, T128x128W8, PM_BF16, 2>("bf16 128x128 w8 dma2", B, m, 512, 512, true, it);
+      printf("--- qkv, M %d N 768 K 256 ---\n", m);
+      run<EPI_QKV, PRO_PLAIN, T64x128, PM_SPLIT3, 2>("split 64x128 dma2", B, m, 768, 256, false, it);
+      run<EPI_QKV, PRO_PLAIN, T128x128, PM_SPLIT3, 2>("split 128x128 dma2", B, m, 768, 256, false, it);
+      run<EPI_QKV, PRO_PLAIN, T64x128, PM_BF16, 2>("bf16 64x128 dma2", B, m, 768, 256, false, it);
+      run<EPI_QKV, PRO_PLAIN, T128x128, PM_BF16, 2>("bf16 128x128 dma2", B, m, 768, 256, false, it);
+    }
+    return 0;
+  }
   if (argc > 1 && !strcmp(argv[1], "dma")) {   // round 4: the DMA-2 loop (A and W planes)
     for (int m : {5120, 10240}) {
       printf("--- mlp1 STATS+HEADZ+fin, M %d (A planes by DMA) ---\n", m);
