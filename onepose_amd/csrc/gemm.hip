@@ -1408,9 +1408,7 @@ int gemm_launch(int epi, int pro, int tile, GemmArgs& args, hipStream_t stream, 
   CASE(EPI_RESID, PRO_NORM_RELU, TILE_32x64W2, T32x64W2, PM_SPLIT3, true)
   CASE(EPI_QKV, PRO_PLAIN, TILE_32x128, T32x128, PM_SPLIT3, true)
   CASE(EPI_STATS, PRO_HEADZ, TILE_64x64, T64x64, PM_SPLIT3, true)
-  CASE(EPI_STATS, PRO_HEADZ, TILE_64x128, T64x128, PM_SPLIT3, true)
   CASE(EPI_QKV, PRO_PLAIN, TILE_64x128, T64x128, PM_SPLIT3, true)
-  CASE(EPI_ACC, PRO_PLAIN, TILE_64x128, T64x128, PM_SPLIT3, true)
   CASE(EPI_RESID, PRO_NORM_RELU, TILE_64x64, T64x64, PM_SPLIT3, true)
   // final projection and score GEMM in the split mode (activations as W: VALU split)
   CASE(EPI_SCORE, PRO_PLAIN, TILE_64x64, T64x64, PM_SPLIT3, false)

@@ -1331,14 +1331,11 @@ struct Plan {
 // (bf16 MLP conv 1 on 64 x 64 DMA-2 tiles -- 640 workgroups, two stages ahead -- measured
 // slower: config 2 2962 -> 2828, config 5 1642 -> 1552 frames/s, profiles/r04/r04d/)
 constexpr int kTileBf16 = TILE_64x128;
-#ifdef ONEPOSE_SPLIT_WIDE
-constexpr bool kSplitWide = true;
-#else
-constexpr bool kSplitWide = false;
-#endif
-// the 64 x 128 DMA tile for QKV and MLP conv 1 (bf16; split mode under kSplitWide)
-bool wide_pm(int pm) { return pm == PM_BF16 || (kSplitWide && pm == PM_SPLIT3); }
-int mlp1_tile(int pm) { return wide_pm(pm) ? kTileBf16 : kTileMLP1; }
+// The split mode's QKV takes the same 64 x 128 DMA tile (round 4; config 2: QKV 0.210 -> 0.189
+// ms per frame, profiles/r04/sw/); its MLP conv 1 keeps 64 x 64 (64 x 128 gives 320 workgroups
+// at config 2: 0.273 -> 0.313 ms per frame; a DMA stage's time follows the bytes its workgroup
+// moves).
+int mlp1_tile(int pm) { return pm == PM_BF16 ? kTileBf16 : kTileMLP1; }
 // make_plan sizes MLP conv 1's InstanceNorm partials (stats rows `str`), its arrival counters
 // (kCntPerSide column blocks) and group partials once for every precision: each precision's
 // MLP conv 1 tile must have those rows and at most that many column blocks over N = 512.
@@ -1766,7 +1763,7 @@ int mlp2_tile_for(int64_t t64, int pm) {
 // Every side the same choices, from the launch as a whole (layers 4-11, sharded frames).
 LayerTiles layer_tiles(int qkv_n3, const Side* sd, int nside, int B, int pm, bool sharded) {
   LayerTiles t;
-  const int q = pm == PM_F32 ? qkv_tile_for(qkv_n3, B) : wide_pm(pm) ? kTileBf16 : kTileKV;
+  const int q = pm == PM_F32 ? qkv_tile_for(qkv_n3, B) : kTileBf16;
   // kv_fold re-reads the whole 128 KB C_h panel per workgroup (64 of them per side and
   // sample): one launch instead of two pays at small batches; at B = 32 the separate MFMA
   // m_fold (16 KB of C per workgroup) is cheaper (config 3: 1.68 vs 2.02 ms per step).
@@ -1790,8 +1787,8 @@ LayerTiles layer_tiles(int qkv_n3, const Side* sd, int nside, int B, int pm, boo
 // take the choice over both sides there.
 LayerTiles side_tiles(int n1, int n3, int B, int pm, bool cross) {
   LayerTiles t;
-  t.qkv[0] = pm == PM_F32 ? qkv_tile_for(n1, B) : wide_pm(pm) ? kTileBf16 : kTileKV;
-  t.qkv[1] = pm == PM_F32 ? qkv_tile_for(n3, 1) : wide_pm(pm) ? kTileBf16 : kTileKV;
+  t.qkv[0] = pm == PM_F32 ? qkv_tile_for(n1, B) : kTileBf16;
+  t.qkv[1] = pm == PM_F32 ? qkv_tile_for(n3, 1) : kTileBf16;
   t.fused_fold[0] = B <= kFusedFoldMaxBatch;
   t.fused_fold[1] = true;
   const int64_t t2 = (int64_t)ceil_div(n1, 64) * 4 * B, t3 = (int64_t)ceil_div(n3, 64) * 4;
