@@ -652,6 +652,10 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
 #pragma unroll
       for (int kk = 0; kk < KKW; ++kk) mfma_kk(tg, f0, kk);
       if (zf >= 0) zfinal(zf);
+      // keep the MFMAs above the wait: register-only, the scheduler would otherwise sink all but
+      // the first below the inline wait + barrier (measured so: the DMA's latency then runs
+      // alone, before the stage's MFMAs, instead of under them)
+      ONEPOSE_SCHED_BARRIER();
       if (LA == 2 && more) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(OPS) : "memory");
       else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if (!ADMA && more) store_stage<PRO, T, PM, WPL, NPL, false>(buf(kt + 1), sa);
