@@ -125,24 +125,23 @@ enum GemmTile {
                     //   (N = 256 gives 2x the 64x64 tile count: 640 tiles at config 2)
   TILE_64x128 = 3,  // qkv fp32 at large batches: 2 accumulators per wave, 64-row KV chunks
   TILE_128x128 = 4, // qkv fp32 at larger batches: 4 accumulators per wave, 128-row KV chunks
-  TILE_32x256 = 7,   // final projection + L2 normalisation (EPI_BIAS_L2): whole rows, 4 waves of
-                     //   32 x 64
   TILE_32x64W2 = 6,  // mlp2 in the split mode: 32 x 64 outputs on 2 waves (N = 256: 640 tiles
                      //   at config 2, where 64 x 64 gives 320 for 256 CUs)
   TILE_128x64W8 = 5, // score: 128 x 64 outputs on 8 waves of 32 x 32 (K = 256 is short: half
                      //   the operand loads per FLOP of 64 x 64)
-  TILE_32x256W8 = 8, // final projection + L2 on 8 waves of 32 x 32 (two waves per SIMD)
+  TILE_32x256W8 = 8, // final projection + L2 normalisation (EPI_BIAS_L2): whole rows on 8 waves
+                     //   of 32 x 32 (two per SIMD), 64-deep stages
 };
 // Output tile shape of each configuration, usable in constant expressions (the workspace
 // plan sizes per-tile partials and counters from these; tile_dims in gemm.hip agrees).
 constexpr int gemm_tile_bm(int t) {
-  return (t == TILE_32x128 || t == TILE_32x64W2 || t == TILE_32x256 || t == TILE_32x256W8) ? 32
+  return (t == TILE_32x128 || t == TILE_32x64W2 || t == TILE_32x256W8) ? 32
          : (t == TILE_128x128 || t == TILE_128x64W8) ? 128 : 64;
 }
 constexpr int gemm_tile_bn(int t) {
   return (t == TILE_32x128 || t == TILE_64x128 || t == TILE_128x128) ? 128
          : t == TILE_64x32K2                                        ? 32
-         : (t == TILE_32x256 || t == TILE_32x256W8)                  ? 256
+         : t == TILE_32x256W8                                       ? 256
                                                                     : 64;
 }
 // (STATS + HEADZ also compile for 64x32 / 2 waves and for 64x64 / 8 waves with K split in

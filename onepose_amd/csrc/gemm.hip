@@ -1230,7 +1230,6 @@ using T64x128 = Tile<64, 128, 1, 4, 32>;
 using T128x128 = Tile<128, 128, 1, 4, 32>;
 using T128x64W8 = Tile<128, 64, 1, 8, 32>;
 using T32x64W2 = Tile<32, 64, 1, 2, 32>;
-using T32x256 = Tile<32, 256, 1, 4, 32, 1>;
 using T32x256W8 = Tile<32, 256, 1, 8, 64, 1>;
 
 
@@ -1260,7 +1259,6 @@ TileDims tile_dims(int tile) {
     case TILE_128x128: return {128, 128, 32};
     case TILE_128x64W8: return {128, 64, 32};
     case TILE_32x64W2: return {32, 64, 32};
-    case TILE_32x256: return {32, 256, 32};
     case TILE_32x256W8: return {32, 256, 64};
 
     default: return {0, 0, 0};
@@ -1278,7 +1276,6 @@ static_assert(gemm_tile_bm(TILE_64x64) == 64 && gemm_tile_bn(TILE_64x64) == 64 &
                   gemm_tile_bm(TILE_128x128) == 128 && gemm_tile_bn(TILE_128x128) == 128 &&
                   gemm_tile_bm(TILE_128x64W8) == 128 && gemm_tile_bn(TILE_128x64W8) == 64 &&
                   gemm_tile_bm(TILE_32x64W2) == 32 && gemm_tile_bn(TILE_32x64W2) == 64 &&
-                  gemm_tile_bm(TILE_32x256) == 32 && gemm_tile_bn(TILE_32x256) == 256 &&
                   gemm_tile_bm(TILE_32x256W8) == 32 && gemm_tile_bn(TILE_32x256W8) == 256,
               "gemm.h tile shapes must match tile_dims");
 
@@ -1395,7 +1392,6 @@ int gemm_launch(int epi, int pro, int tile, GemmArgs& args, hipStream_t stream, 
   CASE(EPI_SCORE, PRO_PLAIN, TILE_64x64, T64x64, PM_F32, false)
   CASE(EPI_SCORE, PRO_PLAIN, TILE_128x64W8, T128x64W8, PM_F32, false)
   CASE(EPI_BIAS, PRO_PLAIN, TILE_64x64, T64x64, PM_F32, false)
-  CASE(EPI_BIAS_L2, PRO_PLAIN, TILE_32x256, T32x256, PM_F32, false)
   CASE(EPI_BIAS_L2, PRO_PLAIN, TILE_32x256W8, T32x256W8, PM_F32, false)
   CASE(EPI_ACC, PRO_PLAIN, TILE_64x64, T64x64, PM_F32, false)
   // attention-layer GEMMs in the bf16 modes: W from the packed bf16 planes (weights rounded /

@@ -43,16 +43,11 @@ namespace onepose {
 // GEMM tile per layer GEMM (gemm.h; measured per shape on config 2).
 constexpr int kTileKV = TILE_32x128, kTileMLP1 = TILE_64x64,
               kTileMLP2 = TILE_64x64, kTileMLP2F32 = TILE_64x32K2, kTileFinal = TILE_64x64;
-#ifdef ONEPOSE_FINAL_W8
+// fp32 final projection + L2: whole rows on 8 waves (two per SIMD; 160 workgroups at config 2).
+// Same-box A/B at config 2 (profiles/r04/final_proj/): 1718 / 1719 frames/s on 4 waves, 1727 /
+// 1732 on 8 (final 0.021 -> 0.019 ms per frame, bit-identical), 1700 / 1703 unfused (BIAS 64 x
+// 64 + l2norm_kernel)
 constexpr int kTileFinalL2 = TILE_32x256W8;
-#else
-constexpr int kTileFinalL2 = TILE_32x256;
-#endif
-#ifdef ONEPOSE_FINAL_UNFUSED
-constexpr bool kFinalL2Fused = false;
-#else
-constexpr bool kFinalL2Fused = true;
-#endif
 constexpr int kTileScore = TILE_128x64W8, kScoreBM = 128;
 // mlp2 in the split mode below 4 tiles per CU: 32 x 64 on 2 waves (config 2: 640 workgroups
 // instead of 320; 0.231 -> 0.213 ms per frame); the bf16 mode keeps 64 x 64 (32 x 64 measured
@@ -2198,7 +2193,7 @@ int match_impl(const void* packed_weights, const float* desc2d, int64_t desc2d_b
     a.nprob = 2;
     a.p[0] = gemm_prob(x2r, 256, fw, 256, fw + 65536, p.f2, 256, n1, 256, 256, B);
     a.p[1] = gemm_prob(x3r, 256, fw, 256, fw + 65536, p.f3, 256, n3, 256, 256, B);
-    if (pm_out == PM_F32 && kFinalL2Fused) {
+    if (pm_out == PM_F32) {
       // fp32: whole-row tiles normalise in the epilogue (l2norm_kernel's arithmetic, the same
       // bits), one launch and one pass over f2 / f3 fewer; half the workgroups of 64 x 64,
       // which leaves CUs to the other match stream
