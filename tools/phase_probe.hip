@@ -310,6 +310,21 @@ int main(int argc, char** argv) {
   using T64x128 = Tile<64, 128, 1, 4, 32>;
   using T64x128B = Tile<64, 128, 1, 4, 64>;
   for (int r = 0; r < 2; ++r) run<EPI_STATS, PRO_HEADZ, T64x64>("warm", B, 5120, 512, 512, true, 200);
+  if (argc > 1 && !strcmp(argv[1], "mlp2")) {   // round 4: fp32 MLP conv 2 tiles (RESID + NORM)
+    using T64x64K2W8 = Tile<64, 64, 2, 8, 64>;
+    using T128x32K2W8 = Tile<128, 32, 2, 8, 64>;
+    using T64x32K2W = Tile<64, 32, 2, 4, 64>;
+    for (int m : {5120, 10240}) {
+      printf("--- mlp2 RESID+NORM fp32, M %d N 256 K 512 ---\n", m);
+      for (int r = 0; r < 2; ++r) {
+        run<EPI_RESID, PRO_NORM_RELU, T64x32K2W>("fp32 64x32K2 (production)", B, m, 256, 512, false, it);
+        run<EPI_RESID, PRO_NORM_RELU, T64x64K2W8>("fp32 64x64K2 w8", B, m, 256, 512, false, it);
+        run<EPI_RESID, PRO_NORM_RELU, T128x32K2W8>("fp32 128x32K2 w8", B, m, 256, 512, false, it);
+        run<EPI_RESID, PRO_NORM_RELU, T64x64>("fp32 64x64", B, m, 256, 512, false, it);
+      }
+    }
+    return 0;
+  }
   if (argc > 1 && !strcmp(argv[1], "big")) {   // round 4: wider split / bf16 tiles, 8 waves
     using T128x128W8 = Tile<128, 128, 1, 8, 32>;
     for (int m : {5120, 10240}) {
