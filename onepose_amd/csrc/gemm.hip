@@ -285,8 +285,12 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
   // DMA-2 loop (two stages in flight: nothing is staged through registers there, and a bf16
   // stage is small -- 12 KB at 64 x 128 -- so the third buffer fits the epilogue's LDS anyway)
   // (the A pieces must deal evenly over the waves: every wave then waits for its own stage)
+#ifndef ONEPOSE_BF16_NBUF
+#define ONEPOSE_BF16_NBUF 3
+#endif
   constexpr int NBUF =
-      (DMA == 2 && PM == PM_BF16 && (NPL * BM / (512 / T::BKS)) % T::NW == 0) ? 3 : 2;
+      (DMA == 2 && PM == PM_BF16 && (NPL * BM / (512 / T::BKS)) % T::NW == 0) ? ONEPOSE_BF16_NBUF
+                                                                               : 2;
   constexpr int LDS0 = NBUF * STAGE > BM * TP ? NBUF * STAGE : BM * TP;
   constexpr int LDSF = LDS0 > QKVL ? LDS0 : QKVL;
   __shared__ __attribute__((aligned(16))) float lds[LDSF];
@@ -594,7 +598,7 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
     // order), so with LA = 2 a load has two stages' time to land instead of one
     constexpr int LA = NBUF - 1;
     constexpr int OPS = PPW + (ADMA ? APPW : 0);   // DMA instructions per wave and stage
-    static_assert(LA == 1 || (ADMA && APIECES % T::NW == 0 && OPS <= 63),
+    static_assert(LA == 1 || (ADMA && APIECES % T::NW == 0 && (LA - 1) * OPS <= 63),
                   "two stages ahead: A by DMA, the same instruction count on every wave");
     auto dma_w = [&](int st) __attribute__((always_inline)) {
       const int k0 = st * T::BKS;
@@ -628,12 +632,15 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
     };
     next_a(kt0);
     dma_w(kt0);
-    if (LA == 2 && kt0 + 1 < nk) {
-      next_a(kt0 + 1);
-      dma_w(kt0 + 1);
-    }
+#pragma unroll
+    for (int s = 1; s < LA; ++s)
+      if (kt0 + s < nk) {
+        next_a(kt0 + s);
+        dma_w(kt0 + s);
+      }
     tk = stamp_start(args.stamp, sl);
-    if (LA == 2 && kt0 + 1 < nk) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(OPS) : "memory");
+    if (LA >= 2 && kt0 + LA - 1 < nk)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"((LA - 1) * OPS) : "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if constexpr (!ADMA) store_stage<PRO, T, PM, WPL, NPL, false>(buf(kt0), sa);
     raw_barrier();
@@ -656,7 +663,7 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
       // the first below the inline wait + barrier (measured so: the DMA's latency then runs
       // alone, before the stage's MFMAs, instead of under them)
       ONEPOSE_SCHED_BARRIER();
-      if (LA == 2 && more) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(OPS) : "memory");
+      if (LA >= 2 && more) asm volatile("s_waitcnt vmcnt(%0)" ::"n"((LA - 1) * OPS) : "memory");
       else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if (!ADMA && more) store_stage<PRO, T, PM, WPL, NPL, false>(buf(kt + 1), sa);
       raw_barrier();
