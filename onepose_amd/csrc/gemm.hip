@@ -285,12 +285,10 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
   // DMA-2 loop (two stages in flight: nothing is staged through registers there, and a bf16
   // stage is small -- 12 KB at 64 x 128 -- so the third buffer fits the epilogue's LDS anyway)
   // (the A pieces must deal evenly over the waves: every wave then waits for its own stage)
-#ifndef ONEPOSE_BF16_NBUF
-#define ONEPOSE_BF16_NBUF 3
-#endif
+  // (four and five buffers measured slower: config 5 1644 -> 1619 / 1499 frames/s, config 2
+  // bf16 2906 -> 2901 / 2704; the loop is bound by the L2 -> LDS bytes)
   constexpr int NBUF =
-      (DMA == 2 && PM == PM_BF16 && (NPL * BM / (512 / T::BKS)) % T::NW == 0) ? ONEPOSE_BF16_NBUF
-                                                                               : 2;
+      (DMA == 2 && PM == PM_BF16 && (NPL * BM / (512 / T::BKS)) % T::NW == 0) ? 3 : 2;
   constexpr int LDS0 = NBUF * STAGE > BM * TP ? NBUF * STAGE : BM * TP;
   constexpr int LDSF = LDS0 > QKVL ? LDS0 : QKVL;
   __shared__ __attribute__((aligned(16))) float lds[LDSF];
