@@ -1072,7 +1072,43 @@ __global__ __launch_bounds__(kConfWaves * 64) void conf_kernel(float* S, int n1,
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   float* Sb = S + (int64_t)b * n1 * n3;
   float rst[STATS ? RW : 1][2];   // STATS: the wave's rows' (max, 1 / sum)
+  // The workgroup's S block first: its loads do not depend on the statistics, so they are in
+  // flight while the statistics' partials load and reduce (one round trip instead of three).
+  int col[4];
+  bool cok[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    col[j] = tilec * 256 + (VEC ? lane * 4 + j : lane + 64 * j);
+    cok[j] = col[j] < n3;
+  }
+  float v[RW][4];
+#pragma unroll
+  for (int i = 0; i < RW; ++i) {
+    const int n = min(tiler * 32 + wave * RW + i, n1 - 1);
+    const float* ps = Sb + (int64_t)n * n3;
+    if (VEC && cok[0]) {
+      const float4 q = *reinterpret_cast<const float4*>(ps + col[0]);
+      v[i][0] = q.x;
+      v[i][1] = q.y;
+      v[i][2] = q.z;
+      v[i][3] = q.w;
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[i][j] = cok[j] ? ps[col[j]] : 0.f;
+    }
+  }
   if constexpr (STATS) {
+    // the wave's rows' partials (nt3 <= 64: one per lane), all RW rows' loads issued together
+    float rpm[RW], rps[RW];
+    if (nt3 <= 64) {
+#pragma unroll
+      for (int i = 0; i < RW; ++i) {
+        const int n = min(tiler * 32 + wave * RW + i, n1 - 1);
+        const float* p = srow + ((int64_t)b * n1 + n) * nt3 * 2;
+        rpm[i] = lane < nt3 ? p[2 * lane] : -INFINITY;
+        rps[i] = lane < nt3 ? p[2 * lane + 1] : 0.f;
+      }
+    }
     {   // column tilec * 256 + t: lane 0's butterfly sum of softmax_stats_wave, nt <= 16
       const int cg = tilec * 256 + threadIdx.x;
       if (threadIdx.x < 256 && cg < n3) {
@@ -1099,22 +1135,30 @@ __global__ __launch_bounds__(kConfWaves * 64) void conf_kernel(float* S, int n1,
         cst[1][threadIdx.x] = 1.0f / v[0];
       }
     }
+    if (nt3 <= 64) {
+      // softmax_stats_wave's arithmetic with its one loop iteration per lane unrolled: the max
+      // from -inf, then 0 + the lane's rescaled sum, the same wave reductions -- the same bits
 #pragma unroll
-    for (int i = 0; i < RW; ++i) {   // the wave's rows, one at a time (as softmax_reduce)
-      const int n = min(tiler * 32 + wave * RW + i, n1 - 1);
-      const float2 r = softmax_stats_wave(srow + ((int64_t)b * n1 + n) * nt3 * 2, nt3, lane);
-      rst[i][0] = r.x;
-      rst[i][1] = 1.0f / r.y;
+      for (int i = 0; i < RW; ++i) {
+        const float mx = wave_max(lane < nt3 ? fmaxf(-INFINITY, rpm[i]) : -INFINITY);
+        const float s = wave_sum(lane < nt3 ? 0.f + rps[i] * expf(rpm[i] - mx) : 0.f);
+        rst[i][0] = mx;
+        rst[i][1] = 1.0f / s;
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < RW; ++i) {   // the wave's rows, one at a time (as softmax_reduce)
+        const int n = min(tiler * 32 + wave * RW + i, n1 - 1);
+        const float2 r = softmax_stats_wave(srow + ((int64_t)b * n1 + n) * nt3 * 2, nt3, lane);
+        rst[i][0] = r.x;
+        rst[i][1] = 1.0f / r.y;
+      }
     }
     __syncthreads();
   }
-  int col[4];
-  bool cok[4];
   float cmx[4], cinv[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    col[j] = tilec * 256 + (VEC ? lane * 4 + j : lane + 64 * j);
-    cok[j] = col[j] < n3;
     if constexpr (STATS) {
       const int cl = VEC ? lane * 4 + j : lane + 64 * j;
       cmx[j] = cok[j] ? cst[0][cl] : 0.f;
@@ -1122,22 +1166,6 @@ __global__ __launch_bounds__(kConfWaves * 64) void conf_kernel(float* S, int n1,
     } else {
       cmx[j] = cok[j] ? colmax[(int64_t)b * n3 + col[j]] : 0.f;
       cinv[j] = cok[j] ? 1.0f / colsum[(int64_t)b * n3 + col[j]] : 0.f;
-    }
-  }
-  float v[RW][4];
-#pragma unroll
-  for (int i = 0; i < RW; ++i) {
-    const int n = min(tiler * 32 + wave * RW + i, n1 - 1);
-    const float* ps = Sb + (int64_t)n * n3;
-    if (VEC && cok[0]) {
-      const float4 q = *reinterpret_cast<const float4*>(ps + col[0]);
-      v[i][0] = q.x;
-      v[i][1] = q.y;
-      v[i][2] = q.z;
-      v[i][3] = q.w;
-    } else {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) v[i][j] = cok[j] ? ps[col[j]] : 0.f;
     }
   }
   // Running winners as (conf bits + 1, index): conf >= 0 (or NaN), so 32-bit unsigned order of
