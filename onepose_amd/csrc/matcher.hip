@@ -477,25 +477,6 @@ __global__ __launch_bounds__(256) void kv_fold256_kernel(KvFoldArgs args, float*
       : reinterpret_cast<const float4*>(P.kspart + (int64_t)b * P.chunks * 256);
   const int stride = kvrow ? 4096 : 64;
   const int idx = kvrow ? e4 : e4 - 4096;
-  // C's first quarter (independent of KV) is loaded with the chunk partials, the other three
-  // right after the first barrier (a barrier keeps the compiler from hoisting them into the chunk
-  // loop, where their 48 VGPRs beside the 64 of the chunk loads would cost the co-resident GEMM
-  // workgroups their slots): two round trips instead of five, the same values and FMAs
-  const int o = os * 256 + t;   // Mf row o
-  // C_h's rows q = 0..63 at column o by buffer loads: one lane offset (VGPR) and the row offset
-  // in the scalar operand, so the 64 loads in flight hold no address VGPRs (64-bit addresses
-  // held 128 of them); the range ends with the head's last row
-  const __amdgpu_buffer_rsrc_t crs = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<float*>(args.ct + (h * 64) * 512 + os * 256), (short)0, (63 * 512 + 256) * 4,
-      0x00020000);
-  auto cload = [&](int q) __attribute__((always_inline)) {
-    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(crs, t * 4, q * 2048, 0));
-  };
-  float cv[4][16];
-  if (g != 64) {
-#pragma unroll
-    for (int i = 0; i < 16; ++i) cv[0][i] = cload(i);
-  }
   // Up to KVF_DEPTH chunk loads in flight per lane (config 2 at 16: one round for either
   // side; the predicated-off slots add nothing, and the adds keep kv_reduce's order: chunk w,
   // w + 4, ...)
@@ -508,14 +489,16 @@ __global__ __launch_bounds__(256) void kv_fold256_kernel(KvFoldArgs args, float*
 #pragma unroll
     for (int j = 0; j < KVF_DEPTH; ++j) { acc.x += v[j].x; acc.y += v[j].y; acc.z += v[j].z; acc.w += v[j].w; }
   }
-  red[w][lane] = acc;
-  __syncthreads();
+  // the fold's first quarter of C (independent of KV) is in flight across the reduction below
+  const int o = os * 256 + t;   // Mf row o
+  const float* ct = args.ct + (h * 64) * 512 + o;
+  float cv[16];
   if (g != 64) {
 #pragma unroll
-    for (int qq = 1; qq < 4; ++qq)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) cv[qq][i] = cload(qq * 16 + i);
+    for (int i = 0; i < 16; ++i) cv[i] = *reinterpret_cast<const std::remove_reference_t<decltype(cv[0])>*>(ct + i * 512);
   }
+  red[w][lane] = acc;
+  __syncthreads();
   if (w == 0) {
     float4 s = red[0][lane];
 #pragma unroll
@@ -533,34 +516,36 @@ __global__ __launch_bounds__(256) void kv_fold256_kernel(KvFoldArgs args, float*
   const float* kvr = reinterpret_cast<const float*>(&red[0][0]);
   // one Mf row per thread, its four d as two packed pairs (d0, d0 + 1), (d0 + 2, d0 + 3); q
   // quarters accumulated in q order, then added in quarter order
-  // (scalar FMAs: the packed form's broadcast operand takes an aligned register pair per C
-  // value, 128 VGPRs for the column in flight; v_pk_fma_f32 and v_fma_f32 round alike)
-  float y[4];
+  f2v y01, y23;
 #pragma unroll
   for (int qq = 0; qq < 4; ++qq) {
-    float a[4] = {0.f, 0.f, 0.f, 0.f};
+    if (qq > 0) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) cv[i] = ct[(qq * 16 + i) * 512];
+    }
+    f2v a01 = (f2v)(0.f), a23 = (f2v)(0.f);
 #pragma unroll
     for (int i = 0; i < 16; i += 4) {
       const float4 k0 = *reinterpret_cast<const float4*>(kvr + 0 * 64 + qq * 16 + i);
       const float4 k1 = *reinterpret_cast<const float4*>(kvr + 1 * 64 + qq * 16 + i);
       const float4 k2 = *reinterpret_cast<const float4*>(kvr + 2 * 64 + qq * 16 + i);
       const float4 k3 = *reinterpret_cast<const float4*>(kvr + 3 * 64 + qq * 16 + i);
-      const float* c = cv[qq] + i;
-      a[0] = fmaf(c[0], k0.x, a[0]); a[1] = fmaf(c[0], k1.x, a[1]);
-      a[2] = fmaf(c[0], k2.x, a[2]); a[3] = fmaf(c[0], k3.x, a[3]);
-      a[0] = fmaf(c[1], k0.y, a[0]); a[1] = fmaf(c[1], k1.y, a[1]);
-      a[2] = fmaf(c[1], k2.y, a[2]); a[3] = fmaf(c[1], k3.y, a[3]);
-      a[0] = fmaf(c[2], k0.z, a[0]); a[1] = fmaf(c[2], k1.z, a[1]);
-      a[2] = fmaf(c[2], k2.z, a[2]); a[3] = fmaf(c[2], k3.z, a[3]);
-      a[0] = fmaf(c[3], k0.w, a[0]); a[1] = fmaf(c[3], k1.w, a[1]);
-      a[2] = fmaf(c[3], k2.w, a[2]); a[3] = fmaf(c[3], k3.w, a[3]);
+      a01 = __builtin_elementwise_fma((f2v)(cv[i]), (f2v){k0.x, k1.x}, a01);
+      a23 = __builtin_elementwise_fma((f2v)(cv[i]), (f2v){k2.x, k3.x}, a23);
+      a01 = __builtin_elementwise_fma((f2v)(cv[i + 1]), (f2v){k0.y, k1.y}, a01);
+      a23 = __builtin_elementwise_fma((f2v)(cv[i + 1]), (f2v){k2.y, k3.y}, a23);
+      a01 = __builtin_elementwise_fma((f2v)(cv[i + 2]), (f2v){k0.z, k1.z}, a01);
+      a23 = __builtin_elementwise_fma((f2v)(cv[i + 2]), (f2v){k2.z, k3.z}, a23);
+      a01 = __builtin_elementwise_fma((f2v)(cv[i + 3]), (f2v){k0.w, k1.w}, a01);
+      a23 = __builtin_elementwise_fma((f2v)(cv[i + 3]), (f2v){k2.w, k3.w}, a23);
     }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) y[j] = qq == 0 ? a[j] : y[j] + a[j];
+    y01 = qq == 0 ? a01 : y01 + a01;
+    y23 = qq == 0 ? a23 : y23 + a23;
   }
   const int64_t e0 = (int64_t)o * 256 + h * 64 + d0;
   if (args.planes) {
     bf16x4 q0, q1, q2;
+    const float y[4] = {y01.x, y01.y, y23.x, y23.y};
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
       __bf16 h, m, l;
@@ -576,7 +561,7 @@ __global__ __launch_bounds__(256) void kv_fold256_kernel(KvFoldArgs args, float*
     return;
   }
   float* mf = (src ? args.mf[1] : args.mf[0]) + (int64_t)b * kMfFloats + e0;
-  *reinterpret_cast<float4*>(mf) = make_float4(y[0], y[1], y[2], y[3]);
+  *reinterpret_cast<float4*>(mf) = make_float4(y01.x, y01.y, y23.x, y23.y);
 }
 
 // InstanceNorm1d statistics (GATs_SuperGlue.py:145; biased variance, eps 1e-5): per-64-row-tile
