@@ -225,6 +225,9 @@ def main():
     ap.add_argument("--match-streams", type=int, default=2,
                     help="consecutive frames' matchers on this many concurrent streams "
                          "(default 2: one frame's kernels leave CUs idle; 1 = one at a time)")
+    ap.add_argument("--pose-streams", type=int, default=0,
+                    help="pose stages of consecutive steps on this many streams (default: one per "
+                         "matcher stream, so the last frames' pose stages run side by side)")
     ap.add_argument("--eager", action="store_true",
                     help="launch every kernel from the host each step instead of replaying "
                          "captured HIP graphs")
@@ -362,7 +365,8 @@ def main():
         if overlap:
             pipe.run_stream(k, graphs=stage_graphs,
                             marks=marks if record and args.stage_marks else None,
-                            match_streams=args.match_streams, pose=not args.diag_no_pose)
+                            match_streams=args.match_streams, pose=not args.diag_no_pose,
+                            pose_streams=args.pose_streams or args.match_streams)
             return pipe.slots[(k - 1) % len(pipe.slots)]
         for _ in range(k):
             if step_graph is not None:
@@ -535,7 +539,8 @@ def main():
         cfg_name += " (fp32 attention as 3-piece bf16 split)"
     if rank == 0:
         sched = (f"matchers of consecutive steps on {args.match_streams} concurrent stream(s), "
-                 "each step's pose stage on its own stream overlapping the next matchers"
+                 f"each step's pose stage on one of {args.pose_streams or args.match_streams} "
+                 "pose stream(s) overlapping the next matchers"
                  if overlap else "serial steps")
         sched += "; stages replayed as HIP graphs" if graphs_on else "; host-launched kernels"
         sched += ("; object prefix (GAT 0 + 3D half of self-attention 1) prepared once per object"

@@ -274,19 +274,30 @@ class FramePipeline:
         return out
 
     def run_stream(self, steps: int, match_stream=None, pose_stream=None, graphs=None,
-                   marks=None, match_streams: int = 1, pose: bool = True):
+                   marks=None, match_streams: int = 1, pose: bool = True,
+                   pose_streams: int = 1):
         """Enqueue `steps` frames (batches) with matcher(k+1) overlapping pose(k); with
         `graphs` (from ``capture_stages``) each stage is one graph replay.  With
         `match_streams` = m > 1, consecutive frames' matchers run on m streams concurrently
         (frame k on stream k % m; needs >= m + 1 buffer slots), filling the CUs that one
         frame's kernels leave idle.  Every frame still runs every kernel.  All streams are
-        joined into the first match stream at the end; the caller synchronises.  `marks`
-        (a list) receives per step (start, matcher done, pose done) timing events."""
+        joined into the first match stream at the end; the caller synchronises.  With
+        `pose_streams` = p > 1, frame k's pose stage runs on pose stream k % p (each stage reads
+        and writes only its slot's buffers), so two frames' pose stages that become ready
+        together -- the last frames of a batch -- run side by side instead of one after the
+        other.  `marks` (a list) receives per step (start, matcher done, pose done) timing
+        events."""
         ms0 = match_stream or torch.cuda.current_stream(self.device)
         ps = pose_stream or getattr(self, "_pose_stream", None)
         if ps is None:
             ps = self._pose_stream = torch.cuda.Stream(
                 self.device, priority=getattr(self, "pose_priority", 0))
+        pextra = getattr(self, "_pose_streams", [])
+        while len(pextra) < pose_streams - 1:
+            pextra.append(torch.cuda.Stream(self.device,
+                                            priority=getattr(self, "pose_priority", 0)))
+        self._pose_streams = pextra
+        pss = [ps] + pextra[:max(1, pose_streams) - 1]
         extra = getattr(self, "_match_streams", [])
         while len(extra) < match_streams - 1:
             extra.append(torch.cuda.Stream(self.device,
@@ -317,6 +328,7 @@ class FramePipeline:
                 matched[sl].record(ms)
                 if mk:
                     mk[1].record(ms)
+            ps = pss[k % len(pss)]
             with torch.cuda.stream(ps):
                 ps.wait_event(matched[sl])
                 if pose:   # (False: a diagnostic of the matcher streams alone, bench.py)
@@ -332,5 +344,6 @@ class FramePipeline:
                 marks.append(mk)
         for s in mss[1:]:
             ms0.wait_stream(s)
-        ms0.wait_stream(ps)
-        return ps
+        for s in pss:
+            ms0.wait_stream(s)
+        return pss[0]

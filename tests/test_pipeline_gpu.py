@@ -133,6 +133,22 @@ def test_two_concurrent_matcher_streams_match_eager(setup):
 
 
 @pytest.mark.gpu
+def test_two_pose_streams_match_eager(setup):
+    """Two matcher streams and two pose streams (the bench's default schedule): consecutive
+    frames' pose stages run side by side on their own slots' buffers -- same bits."""
+    pipe, batches = setup
+    pipe.set_frames(*batches[1])
+    pipe.enqueue(0)
+    torch.cuda.synchronize()
+    ref = _outputs(pipe.slots[0])
+    graphs = pipe.capture_stages()
+    pipe.run_stream(10, graphs=graphs, match_streams=2, pose_streams=2)
+    torch.cuda.synchronize()
+    for s in pipe.slots:
+        _assert_same(ref, _outputs(s))
+
+
+@pytest.mark.gpu
 def test_detector_pipeline_from_images():
     """Images -> SuperPoint -> matcher -> selection -> RANSAC-EPnP: the detector stage writes
     exactly what SuperPoint.detect_raw returns, the matcher stage equals the module forward on
