@@ -524,10 +524,11 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
     //  - the stage's LDS reads come before the next stages' loads in program order, and the
     //    barrier is a raw s_barrier after lgkmcnt(0): __syncthreads()' fence would drain every
     //    load and DMA in flight (vmcnt(0)) and undo the lookahead.
-    // A and W one stage ahead in two LDS buffers.  (Two stages ahead -- two A register sets,
-    // three LDS buffers -- measured no faster: the stage is bound by its own instruction
-    // latencies at 1-3 waves per SIMD)  Same images, fragments and MFMA
-    // order as the register-staged loop, so the same bits.
+    // A and W LA = NBUF - 1 stages ahead: one in two LDS buffers, two in three for the bf16
+    // DMA-2 loop (A staged through registers with two stages ahead -- two A register sets --
+    // measured no faster).  With the MFMAs under the loads (the scheduling barrier in `stage`),
+    // a stage's time follows the bytes its workgroup moves.  Same
+    // images, fragments and MFMA order as the register-staged loop, so the same bits.
     static_assert(WPL && PM != PM_F32, "DMA loop: bf16 images, W planes");
     // DMA 2: A from its activation planes too -- no VALU rounding / split, no LDS stores of A
     constexpr bool ADMA = DMA == 2;
