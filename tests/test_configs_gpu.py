@@ -106,12 +106,16 @@ def test_config3_batch32_1024x16384(device):
 
 
 @pytest.mark.timeout(300)
-def test_config4_batch32_1024x2500_ragged(device):
+@pytest.mark.parametrize("precision", [0, 2], ids=["fp32", "fp32_split"])
+def test_config4_batch32_1024x2500_ragged(device, precision):
+    """Config 4's per-GPU shard (B = 32, ragged n3 = 2500) through the cached path, frames 0
+    and 31 against the numpy oracle under the index contract -- in fp32 and in the split mode
+    (its batched launches: 64 x 128 QKV tiles, the separate m_fold with bf16 planes)."""
     from oracle import matcher_np as M
     n1, n3, L, seed = 1024, 2500, 8, 12
     sd = synthetic.make_state_dict(seed)
     data, d2 = batch_inputs(n1, n3, L, seed, 32)
-    cm = CachedMatcher(sd, data, device)
+    cm = CachedMatcher(sd, data, device, precision=precision)
     preds, conf = cm(d2, with_conf=True)
     for b in (0, 31):
         one = dict(data)
