@@ -84,13 +84,14 @@ class CachedMatcher:
 
 
 @pytest.mark.timeout(300)
-def test_config3_batch32_1024x16384(device):
+@pytest.mark.parametrize("precision", [0, 2], ids=["fp32", "fp32_split"])
+def test_config3_batch32_1024x16384(device, precision):
     g = golden("matcher_c3_idx")
     n1, n3, L, seed = [int(g[k]) for k in ("n1", "n3", "num_leaf", "seed")]
     assert (n1, n3, L) == (1024, 16384, 8)
     sd = synthetic.make_state_dict(seed, well_conditioned=bool(int(g["well_conditioned"])))
     data, d2 = batch_inputs(n1, n3, L, seed, 32)
-    cm = CachedMatcher(sd, data, device)
+    cm = CachedMatcher(sd, data, device, precision=precision)
     preds, _ = cm(d2)
     assert_pred_equal(preds[0], g, "config 3, frame 0 of 32 vs the reference")
     for b in (1, 17, 31):
