@@ -201,6 +201,39 @@ def cpu_baseline(sd, data, frames, obj, seconds=15.0, detector_image=None):
             "sample": sample}
 
 
+def summarize_pose(res, world, B, F, steps):
+    """cm/deg and inlier statistics over every timed frame, from the gathered result rows
+    (pose 12, R_err, t_err, cmd 1/3/5, inliers, status, global frame id; any row order).
+
+    With a frame bank of F steps (F > 0), row g is global frame g of one sequence: step j's
+    global batch is frames [j world B, (j + 1) world B) and step k of the timed region runs bank
+    entry k % F, so a row's weight is the number of timed steps that ran its entry.  Without a
+    bank (F = 0) the rows are the one batch every step replays, weight 1 each."""
+    res = res[np.argsort(res[:, 19], kind="stable")]
+    n_rows = world * B * (F or 1)
+    assert np.array_equal(res[:, 19], np.arange(n_rows)), "gathered frame order"
+    if F:
+        entry = (res[:, 19] // (world * B)).astype(np.int64)
+        w = np.bincount(np.arange(steps) % F, minlength=F)[entry].astype(np.float64)
+        assert w.sum() == world * B * steps
+    else:
+        w = np.ones(len(res))
+
+    def wmean(x):
+        return float((w * x).sum() / w.sum())
+    rep = np.repeat(np.arange(len(res)), w.astype(np.int64))
+    return {"frames": int(w.sum()), "distinct_frames": int((w > 0).sum()),
+            "cmd1": wmean(res[:, 14]), "cmd3": wmean(res[:, 15]), "cmd5": wmean(res[:, 16]),
+            "R_err_deg_mean": wmean(res[:, 12]), "t_err_cm_mean": wmean(res[:, 13]),
+            "R_err_deg_median": float(np.median(res[rep, 12])),
+            "t_err_cm_median": float(np.median(res[rep, 13])),
+            "n_inliers_mean": wmean(res[:, 17]),
+            "status_ok": wmean((res[:, 18] == 0).astype(np.float64)),
+            "source": (f"every timed frame: a bank of {F} steps x {B} frame(s) x {world} rank(s) "
+                       f"of distinct synthetic frames, step k runs entry k % {F}") if F
+                      else "the last step's frames (one batch replayed every step)"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -238,7 +271,12 @@ def main():
                     help="diagnostic: no device stamps in the timed region (roofline then "
                          "reports the serial profile pass)")
     ap.add_argument("--slots", type=int, default=0,
-                    help="frame buffer slots (default: match streams + 1)")
+                    help="frame buffer slots (default: the smallest count >= match streams + 1 "
+                         "that divides --frames)")
+    ap.add_argument("--frames", type=int, default=64,
+                    help="frame bank: this many steps' distinct query frames (x batch x ranks) are "
+                         "resident before timing and step k runs bank entry k %% frames; the pose "
+                         "summary covers every timed frame (0: one batch of frames replayed)")
     ap.add_argument("--precision", choices=["fp32", "bf16", "fp32_split"], default="fp32",
                     help="matcher attention-layer GEMMs: fp32 MFMA (the reference's numerics, "
                          "default) or bf16 MFMA with fp32 accumulation (BASELINE config 5)")
@@ -292,6 +330,13 @@ def main():
     n_global = world * B
     fs, fe = D.frame_shard(n_global, world, rank)
     data, obj, frames = synthetic.make_matcher_inputs(n1, n3, L, seed=0, frame_ids=range(fs, fe))
+    F = max(0, args.frames)
+    if args.e2e:
+        F = 0   # the detector path reads each slot's own images (no query-frame bank)
+    bank = synthetic.make_frame_bank(n1, n3, F, B, seed=0, world=world, rank=rank) if F else None
+    nslots = args.slots or max(2, args.match_streams + 1)
+    while F and not args.slots and F % nslots:
+        nslots += 1
     m = matcher.from_state_dict(sd, {**synthetic.DEFAULT_HPARAMS,
                                      "attention_precision": args.precision})
     detector, images = None, None
@@ -304,7 +349,7 @@ def main():
         images = np.stack([synthetic.superpoint_image(S, S, fs + i) for i in range(B)])
     pipe = FramePipeline(m, data["keypoints3d"][0], data["descriptors3d_db"][0],
                          data["descriptors2d_db"][0], B, n1, dev, scale=1000.0,
-                         slots=args.slots or max(2, args.match_streams + 1), detector=detector,
+                         slots=nslots, detector=detector,
                          image_hw=(args.image_size, args.image_size),
                          object_cache=not args.no_object_cache)
     pipe.fused_pose = not args.unfused_pose
@@ -315,6 +360,9 @@ def main():
                     np.stack([f.K for f in frames]), np.stack([f.pose_gt for f in frames]))
     if images is not None:
         pipe.set_images(images)
+    if bank is not None:
+        pipe.set_frame_bank(bank["descriptors2d_query"], bank["keypoints2d"], bank["K"],
+                            bank["pose_gt"])
 
     # setup: one eager pass (loads every kernel's code object) before the profile pass; the W
     # warm-up steps run right before the timed region, below
@@ -379,14 +427,23 @@ def main():
 
     def result_rows(slot):   # per-frame result row: pose, errors, cm/deg flags, inliers, status,
         # and the frame's index in the global batch (rank 0 checks the gathered order)
+        if bank is not None:   # every bank entry's frames (the results of its last run)
+            r = pipe.bank_results
+            gid = torch.as_tensor(bank["frame_id"], dtype=torch.float64, device=dev)
+            return torch.cat([r["pose"].reshape(F * B, 12), r["R_err"].reshape(-1, 1),
+                              r["t_err"].reshape(-1, 1), r["cmd"].reshape(-1, 3).double(),
+                              r["n_inliers"].reshape(-1, 1).double(),
+                              r["status"].reshape(-1, 1).double(), gid.reshape(-1, 1)], 1)
         return torch.cat([slot.pose.reshape(B, 12), slot.R_err[:, None], slot.t_err[:, None],
                           slot.cmd.double(), slot.n_inliers[:, None].double(),
                           slot.status[:, None].double(), frame_ids], 1)
 
+    n_rows = world * B * (F or 1)   # gathered result rows (global frames)
+
     # first replay of each graph (upload) and the first use of every torch kernel the timed
     # region launches (ROCm loads a kernel's code object lazily at its first launch, which
     # can take tens of ms) stay out of the timed region
-    D.gather_frames(result_rows(run_steps(max(2, len(pipe.slots)))), world * B)
+    D.gather_frames(result_rows(run_steps(max(2, len(pipe.slots), F))), n_rows)
     torch.cuda.synchronize()
     # settle + W warm-up steps of the timed schedule, back to back and immediately before the
     # timed region: the GPU leaves its idle power state within them (after >= 20 ms idle a
@@ -409,7 +466,7 @@ def main():
     ev_begin.record()
     last = run_steps(args.steps, record=True)
     host_enqueue = time.perf_counter() - t0   # host time to issue the K steps
-    result = D.gather_frames(result_rows(last), world * B)   # the only cross-rank exchange
+    result = D.gather_frames(result_rows(last), n_rows)   # the only cross-rank exchange
     ev_end.record()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
@@ -513,13 +570,10 @@ def main():
                                "note": "MFMA FLOPs the kernels execute (the Mf fold removes the "
                                        "merge conv and the attention apply)"}}
 
-    # the gathered rows are the global batch, in frame order (one object's frames over ranks)
-    assert np.array_equal(res[:, 19], np.arange(n_global)), "gathered frame order"
-    pose_summary = {"frames": int(n_global), "cmd1": float(res[:, 14].mean()), "cmd3": float(res[:, 15].mean()),
-                    "cmd5": float(res[:, 16].mean()), "R_err_deg_mean": float(res[:, 12].mean()),
-                    "t_err_cm_mean": float(res[:, 13].mean()),
-                    "n_inliers_mean": float(res[:, 17].mean()),
-                    "status_ok": float((res[:, 18] == 0).mean())}
+    # the gathered rows are the global frames (one object's sequence sharded over ranks); with
+    # a bank, step j's global batch is frames [j world B, (j + 1) world B), and a row's weight is
+    # the number of timed steps that ran its bank entry (step k runs entry k % F)
+    pose_summary = summarize_pose(res, world, B, F, args.steps)
     if args.e2e:
         # Random-weight SuperPoint descriptors barely discriminate (cosine 0.97 between random
         # keypoints of the synthetic images; trained weights are not available offline), so the
@@ -569,6 +623,8 @@ def main():
             "frame_roofline": frame_roof,
             **({"detector": det} if det else {}),
             "host_enqueue_ms_per_step": round(host_enqueue / args.steps * 1e3, 4),
+            "library": {"path": os.path.relpath(_lib.LIB_PATH, REPO),
+                        "overridden_by_ONEPOSE_LIB": bool(os.environ.get("ONEPOSE_LIB"))},
             **({"diagnostic": "pose stage skipped (--diag-no-pose): not the metric"}
                if args.diag_no_pose else {}),
             **({"stage_ms": stage_ms} if stage_ms else {}),

@@ -51,7 +51,8 @@ enum {
 
 /* Thread-local description of the last error ("" when none). */
 const char* onepose_last_error(void);
-/* ABI version, bumped on any signature change. */
+/* ABI version, bumped on any signature change or new entry point (4: the per-precision
+ * workspace and object-cache size queries). */
 int onepose_abi_version(void);
 
 /* ------------------------------------------------------------------------------------ *
@@ -82,6 +83,11 @@ int onepose_matcher_pack(const float* const* tensors, int n_tensors, void* packe
 /* Workspace bytes onepose_match needs for this shape.  with_conf=0 adds room for the
  * score matrix that would otherwise live in `conf`. */
 size_t onepose_match_workspace_bytes(int batch, int n1, int n3, int num_leaf, int with_conf);
+/* (ABI 4) The same for one precision: fp32 needs no bf16 activation planes, so its workspace
+ * is smaller (the query above is the largest over precisions and stays valid for all).  A
+ * match call checks `workspace_bytes` against its own precision's need. */
+size_t onepose_match_workspace_bytes_ex(int batch, int n1, int n3, int num_leaf, int with_conf,
+                                        int precision);
 
 /* One matcher forward over `batch` frames.
  *   desc2d  [batch, 256, n1]        descriptors2d_query  (device, fp32)
@@ -188,6 +194,10 @@ enum {
   ONEPOSE_OBJ_GAT_TABLES = 1    /* build / use the GAT prefix tables (num_leaf <= 8)          */
 };
 size_t onepose_object_cache_bytes(int n3, int num_leaf, int flags);
+/* (ABI 4) The cache bytes for one precision: the bf16 activation planes of the cached phi(q)
+ * (1.5 KB per point) only in the bf16 modes.  A cache sized by this query must be prepared and
+ * matched with that precision; onepose_object_cache_bytes fits every precision. */
+size_t onepose_object_cache_bytes_ex(int n3, int num_leaf, int flags, int precision);
 size_t onepose_object_prepare_workspace_bytes(int n3, int num_leaf);
 int onepose_object_prepare(const void* packed_weights, const float* desc3d,
                            const float* leaves_prepared, int n3, int num_leaf, int precision,

@@ -20,7 +20,7 @@ c_void_p, c_char_p = ctypes.c_void_p, ctypes.c_char_p
 
 # onepose_allgather_fn: int (*)(size_t bytes_per_rank, void* stream, void* user)
 ALLGATHER_FN = ctypes.CFUNCTYPE(c_int, c_size_t, c_void_p, c_void_p)
-ABI_VERSION = 3
+ABI_VERSION = 4
 OBJ_GAT_TABLES = 1   # ONEPOSE_OBJ_GAT_TABLES
 
 # name -> (restype, argtypes); mirrors include/onepose_hip.h
@@ -33,6 +33,7 @@ PROTOTYPES = {
     "onepose_matcher_packed_bytes": (c_size_t, []),
     "onepose_matcher_pack": (c_int, [ctypes.POINTER(c_void_p), c_int, c_void_p]),
     "onepose_match_workspace_bytes": (c_size_t, [c_int, c_int, c_int, c_int, c_int]),
+    "onepose_match_workspace_bytes_ex": (c_size_t, [c_int, c_int, c_int, c_int, c_int, c_int]),
     "onepose_match": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64,
                               c_int, c_int, c_int, c_int, c_float, c_float,
                               c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
@@ -50,6 +51,7 @@ PROTOTYPES = {
                                           c_float, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                                           c_void_p, c_void_p, c_size_t, c_void_p]),
     "onepose_object_cache_bytes": (c_size_t, [c_int, c_int, c_int]),
+    "onepose_object_cache_bytes_ex": (c_size_t, [c_int, c_int, c_int, c_int]),
     "onepose_object_prepare_workspace_bytes": (c_size_t, [c_int, c_int]),
     "onepose_object_prepare": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
                                        c_int, c_void_p, c_void_p, c_size_t, c_void_p]),
@@ -122,15 +124,34 @@ def load():
                 f"{LIB_PATH} is missing: build it with `python -m onepose_amd.build` "
                 "(onepose_amd has no CPU fallback)")
         lib = ctypes.CDLL(LIB_PATH)
+        # A/B measurement only: an older build named by ONEPOSE_LIB may predate the newest
+        # entry points (ABI >= 3); callers fall back where one is missing (size_query)
+        ab = bool(os.environ.get("ONEPOSE_LIB"))
         for name, (res, args) in PROTOTYPES.items():
+            if ab and not hasattr(lib, name):
+                continue
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args
-        if lib.onepose_abi_version() != ABI_VERSION:
+        if lib.onepose_abi_version() != ABI_VERSION and not (ab and lib.onepose_abi_version() >= 3):
             raise OnePoseError(f"{LIB_PATH}: ABI version {lib.onepose_abi_version()}, "
                                f"expected {ABI_VERSION}: rebuild with `python -m onepose_amd.build`")
         _lib = lib
     return _lib
+
+
+def workspace_bytes(lib, B, n1, n3, L, with_conf, precision) -> int:
+    """onepose_match_workspace_bytes_ex (this precision's need), or the every-precision query
+    on an older A/B build without it."""
+    if hasattr(lib, "onepose_match_workspace_bytes_ex"):
+        return lib.onepose_match_workspace_bytes_ex(B, n1, n3, L, int(with_conf), int(precision))
+    return lib.onepose_match_workspace_bytes(B, n1, n3, L, int(with_conf))
+
+
+def object_cache_bytes(lib, n3, L, flags, precision) -> int:
+    if hasattr(lib, "onepose_object_cache_bytes_ex"):
+        return lib.onepose_object_cache_bytes_ex(n3, L, flags, int(precision))
+    return lib.onepose_object_cache_bytes(n3, L, flags)
 
 
 def check(rc: int, what: str = "") -> None:

@@ -1373,7 +1373,14 @@ int qkv_tile_for(int n3, int B) {
   return t64 >= kQkvWiderTiles ? TILE_128x128 : t64 >= kQkvWideTiles ? TILE_64x128 : kTileKV;
 }
 
-Plan make_plan(void* ws, int B, int n1, int n3, int L, bool with_conf) {
+bool valid_precision(int p) {
+  return p == ONEPOSE_PREC_FP32 || p == ONEPOSE_PREC_BF16_ATTN || p == ONEPOSE_PREC_FP32_SPLIT;
+}
+
+// `planes`: carve the bf16 modes' activation planes (kPlanesMax per tensor); fp32 never reads
+// them (match_impl's pl() is null there), so an fp32 plan leaves them out (+75% of
+// the per-token footprint otherwise).
+Plan make_plan(void* ws, int B, int n1, int n3, int L, bool with_conf, bool planes = true) {
   Carve c(ws);
   Plan p;
   const size_t t2 = (size_t)B * n1, t3 = (size_t)B * n3;
@@ -1394,12 +1401,13 @@ Plan make_plan(void* ws, int B, int n1, int n3, int L, bool with_conf) {
   p.phiq3 = c.take<float>(t3 * 256);
   p.y12 = c.take<float>(t2 * 512);
   p.y13 = c.take<float>(t3 * 512);
+  const size_t npl = planes ? kPlanesMax : 0;
   for (int i = 0; i < 2; ++i) {
-    p.x2p[i] = c.take<uint16_t>(t2 * 256 * kPlanesMax);
-    p.x3p[i] = c.take<uint16_t>(t3 * 256 * kPlanesMax);
+    p.x2p[i] = planes ? c.take<uint16_t>(t2 * 256 * npl) : nullptr;
+    p.x3p[i] = planes ? c.take<uint16_t>(t3 * 256 * npl) : nullptr;
   }
-  p.phiq2p = c.take<uint16_t>(t2 * 256 * kPlanesMax);
-  p.phiq3p = c.take<uint16_t>(t3 * 256 * kPlanesMax);
+  p.phiq2p = planes ? c.take<uint16_t>(t2 * 256 * npl) : nullptr;
+  p.phiq3p = planes ? c.take<uint16_t>(t3 * 256 * npl) : nullptr;
   p.stats2 = c.take<float>((size_t)B * ceil_div(n1, str) * 1024);
   p.stats3 = c.take<float>((size_t)B * ceil_div(n3, str) * 1024);
   p.mean = c.take<float>((size_t)2 * B * 512);
@@ -1437,7 +1445,7 @@ using namespace onepose;
 extern "C" {
 
 const char* onepose_last_error(void) { return g_last_error.c_str(); }
-int onepose_abi_version(void) { return 3; }
+int onepose_abi_version(void) { return 4; }
 
 int onepose_profile_begin(uint64_t kind_mask, int capacity) {
   clear_error();
@@ -1647,7 +1655,16 @@ size_t onepose_match_workspace_bytes(int batch, int n1, int n3, int num_leaf, in
   clear_error();
   if (batch <= 0 || n1 <= 0 || n3 <= 0) return 0;
   OP_REQUIRE(num_leaf >= 1 && num_leaf <= 16, "workspace: num_leaf=%d", num_leaf);
-  return make_plan(nullptr, batch, n1, n3, num_leaf, with_conf != 0).bytes;
+  return make_plan(nullptr, batch, n1, n3, num_leaf, with_conf != 0).bytes;   // every precision
+}
+
+size_t onepose_match_workspace_bytes_ex(int batch, int n1, int n3, int num_leaf, int with_conf,
+                                        int precision) {
+  clear_error();
+  if (batch <= 0 || n1 <= 0 || n3 <= 0 || !valid_precision(precision)) return 0;
+  OP_REQUIRE(num_leaf >= 1 && num_leaf <= 16, "workspace: num_leaf=%d", num_leaf);
+  return make_plan(nullptr, batch, n1, n3, num_leaf, with_conf != 0,
+                   precision != ONEPOSE_PREC_FP32).bytes;
 }
 
 }  // extern "C"
@@ -1699,9 +1716,6 @@ int shard_exchange(const ShardCtx& sh, size_t bytes, hipStream_t st) {
   return ONEPOSE_OK;
 }
 
-bool valid_precision(int p) {
-  return p == ONEPOSE_PREC_FP32 || p == ONEPOSE_PREC_BF16_ATTN || p == ONEPOSE_PREC_FP32_SPLIT;
-}
 int attention_pm(int precision) {
   return precision == ONEPOSE_PREC_BF16_ATTN ? PM_BF16
          : precision == ONEPOSE_PREC_FP32_SPLIT ? PM_SPLIT3 : PM_F32;
@@ -1831,7 +1845,7 @@ struct ObjLayout {
   int64_t logits, phiq, acc, ksum, mf, phiqp, slogs, tab, total;
   bool tables;
 };
-ObjLayout obj_layout(int n3, int num_leaf, int flags) {
+ObjLayout obj_layout(int n3, int num_leaf, int flags, bool planes) {
   ObjLayout L;
   L.tables = obj_tables(num_leaf, flags);
   L.logits = (int64_t)n3 * 256;
@@ -1839,10 +1853,10 @@ ObjLayout obj_layout(int n3, int num_leaf, int flags) {
   L.acc = L.phiq + (int64_t)n3 * 256;
   L.ksum = L.acc + (int64_t)ceil_div(n3, 64) * 64 * 512;   // TILE_64x64 tiles of N = 512
   L.mf = L.ksum + 256;
-  // phi(q)'s activation planes [kPlanesMax][n3][256] uint16 (bf16 modes; reserved in every
-  // precision, so the size query needs none)
+  // phi(q)'s activation planes [kPlanesMax][n3][256] uint16 (bf16 modes only: onepose_
+  // object_cache_bytes reserves them in every precision, _ex only for the bf16 ones)
   L.phiqp = L.mf + kMfFloats;
-  L.slogs = L.phiqp + (int64_t)kPlanesMax * n3 * 256 / 2;
+  L.slogs = L.phiqp + (planes ? (int64_t)kPlanesMax * n3 * 256 / 2 : 0);
   L.tab = L.slogs + (L.tables ? (int64_t)3 * n3 * kLogitStride : 0);
   L.total = L.tab + (L.tables ? (int64_t)3 * n3 * 2 * num_leaf * 256 : 0);
   return L;
@@ -2144,7 +2158,7 @@ int match_impl(const void* packed_weights, const float* desc2d, int64_t desc2d_b
                                 ? obj_cache + (int64_t)n3 * 256 +
                                       (int64_t)(gat - 1) * n3 * kLogitStride
                                 : nullptr;
-        const ObjLayout OL = obj_layout(n3, num_leaf, obj_flags);
+        const ObjLayout OL = obj_layout(n3, num_leaf, obj_flags, npl != 0);
         uint16_t* yp = pl(p.x3p[c3 ^ 1]);
         if (slog != nullptr && OL.tables) {
           OP_LAUNCH(K_GAT, st, gat_tab_kernel, ggrid, dim3(256), 0, st, x3r, gat_weights(wbase, gat),
@@ -2194,7 +2208,7 @@ int match_impl(const void* packed_weights, const float* desc2d, int64_t desc2d_b
       rc = attention_layer(w, sd, 1, B, p, lcnt, st, pm, sh, tl);
     } else if (obj_cache && layer == 2 && !sh) {
       // cross-attention 1: the 3D side's frame-independent half from the object cache
-      const ObjLayout L = obj_layout(n3, num_leaf, obj_flags);
+      const ObjLayout L = obj_layout(n3, num_leaf, obj_flags, npl != 0);
       const SideCache xc = {obj_cache + L.phiq, obj_cache + L.acc, obj_cache + L.ksum,
                             obj_cache + L.mf,
                             npl ? reinterpret_cast<const uint16_t*>(obj_cache + L.phiqp) : nullptr};
@@ -2339,7 +2353,7 @@ int object_prepare_impl(const void* packed_weights, const float* desc3d, const f
               gat_weights(wbase, 0), nolog, p.x3[1], n3, num_leaf, 1, pl(p.x3p[1]), npl);
     OP_LAUNCH(K_GAT, st, gat_logits_kernel<8>, ggrid, dim3(256), 0, st, leaves_pm,
               gat_weights(wbase, 1), slog, n3, num_leaf);
-    const ObjLayout OL = obj_layout(n3, num_leaf, flags);
+    const ObjLayout OL = obj_layout(n3, num_leaf, flags, npl != 0);
     if (OL.tables)
       OP_LAUNCH(K_GAT, st, gat_table_kernel, ggrid, dim3(256), 0, st, leaves_pm,
                 gat_weights(wbase, 1), cache + OL.slogs, cache + OL.tab, n3, num_leaf);
@@ -2362,7 +2376,7 @@ int object_prepare_impl(const void* packed_weights, const float* desc3d, const f
   // Cross-attention 1 (layer 2), the 3D side's frame-independent half, with the choices a
   // cached forward's layer 2 makes (batch <= kFusedFoldMaxBatch: QKV tile from n3 alone, one
   // kv_fold launch), so that its bits are the ones the uncached forward computes in place.
-  const ObjLayout L = obj_layout(n3, num_leaf, flags);
+  const ObjLayout L = obj_layout(n3, num_leaf, flags, npl != 0);
   const ApW w = ap_weights(wbase, 1);
   const Side x3 = {cache, 0, nullptr, cache + L.phiq, p.kvpart3, p.kspart3, nullptr, nullptr, n3,
                    (float)n3, 0, n3};
@@ -2459,13 +2473,14 @@ int onepose_match_ex(const void* packed_weights, const float* desc2d, int64_t de
   int rc = check_match_args(packed_weights, desc2d, desc3d, leaves, batch, n1, n3, num_leaf,
                             scale_factor, matches0, matches1, mscores0, mscores1, workspace);
   if (rc != ONEPOSE_OK) return rc;
-  const Plan need = make_plan(nullptr, batch, n1, n3, num_leaf, conf != nullptr);
+  const bool planes = precision != ONEPOSE_PREC_FP32;
+  const Plan need = make_plan(nullptr, batch, n1, n3, num_leaf, conf != nullptr, planes);
   if (workspace_bytes < need.bytes) {
     set_error("match: workspace %zu < %zu bytes", workspace_bytes, need.bytes);
     return ONEPOSE_ERR_WORKSPACE;
   }
   hipStream_t st = static_cast<hipStream_t>(stream_);
-  const Plan p = make_plan(workspace, batch, n1, n3, num_leaf, conf != nullptr);
+  const Plan p = make_plan(workspace, batch, n1, n3, num_leaf, conf != nullptr, planes);
   // reference layout [*, 256, n3*L] -> point-major copy in the workspace
   const int lb = leaves_bstride == 0 ? 1 : batch;
   if ((rc = onepose_prepare_leaves(leaves, leaves_bstride, lb, n3, num_leaf, p.leaves_pm,
@@ -2503,12 +2518,13 @@ int onepose_match_prepared_ex(const void* packed_weights, const float* desc2d,
                             num_leaf, scale_factor, matches0, matches1, mscores0, mscores1,
                             workspace);
   if (rc != ONEPOSE_OK) return rc;
-  const Plan need = make_plan(nullptr, batch, n1, n3, num_leaf, conf != nullptr);
+  const bool planes = precision != ONEPOSE_PREC_FP32;
+  const Plan need = make_plan(nullptr, batch, n1, n3, num_leaf, conf != nullptr, planes);
   if (workspace_bytes < need.bytes) {
     set_error("match: workspace %zu < %zu bytes", workspace_bytes, need.bytes);
     return ONEPOSE_ERR_WORKSPACE;
   }
-  const Plan p = make_plan(workspace, batch, n1, n3, num_leaf, conf != nullptr);
+  const Plan p = make_plan(workspace, batch, n1, n3, num_leaf, conf != nullptr, planes);
   return match_impl(packed_weights, desc2d, desc2d_bstride, desc3d, desc3d_bstride,
                     leaves_prepared, prepared_bstride, batch, n1, n3, num_leaf, scale_factor,
                     match_threshold, matches0, matches1, mscores0, mscores1, conf, p,
@@ -2532,7 +2548,14 @@ int onepose_match_prepared(const void* packed_weights, const float* desc2d,
 size_t onepose_object_cache_bytes(int n3, int num_leaf, int flags) {
   if (n3 <= 0 || num_leaf < 1 || num_leaf > 16) return 0;
   if ((flags & ~ONEPOSE_OBJ_GAT_TABLES) != 0) return 0;   // the flags prepare / match refuse
-  return (size_t)obj_layout(n3, num_leaf, flags).total * sizeof(float);
+  return (size_t)obj_layout(n3, num_leaf, flags, true).total * sizeof(float);   // any precision
+}
+
+size_t onepose_object_cache_bytes_ex(int n3, int num_leaf, int flags, int precision) {
+  if (n3 <= 0 || num_leaf < 1 || num_leaf > 16 || !valid_precision(precision)) return 0;
+  if ((flags & ~ONEPOSE_OBJ_GAT_TABLES) != 0) return 0;
+  return (size_t)obj_layout(n3, num_leaf, flags, precision != ONEPOSE_PREC_FP32).total *
+         sizeof(float);
 }
 
 size_t onepose_object_prepare_workspace_bytes(int n3, int num_leaf) {
@@ -2625,12 +2648,13 @@ int onepose_match_cached(const void* packed_weights, const float* desc2d, int64_
                "called with n3=%d num_leaf=%d precision=%d flags=%d",
                c.n3, c.num_leaf, c.precision, c.flags, n3, num_leaf, precision, object_flags);
   }
-  const Plan need = make_plan(nullptr, batch, n1, n3, num_leaf, conf != nullptr);
+  const bool planes = precision != ONEPOSE_PREC_FP32;
+  const Plan need = make_plan(nullptr, batch, n1, n3, num_leaf, conf != nullptr, planes);
   if (workspace_bytes < need.bytes) {
     set_error("match_cached: workspace %zu < %zu bytes", workspace_bytes, need.bytes);
     return ONEPOSE_ERR_WORKSPACE;
   }
-  const Plan p = make_plan(workspace, batch, n1, n3, num_leaf, conf != nullptr);
+  const Plan p = make_plan(workspace, batch, n1, n3, num_leaf, conf != nullptr, planes);
   return match_impl(packed_weights, desc2d, desc2d_bstride, object_cache, 0, leaves_prepared,
                     prepared_bstride, batch, n1, n3, num_leaf, scale_factor, match_threshold,
                     matches0, matches1, mscores0, mscores1, conf, p,

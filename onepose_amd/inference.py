@@ -366,9 +366,16 @@ def inference_core(cfg, data_root, seq_dir, sfm_model_dir):
     return eval_result
 
 
-def inference(cfg):
+def inference(cfg, seed: bool = True):
     """``inference.py:185-198``: every ``"<data_root> <seq> ..."`` entry of
-    ``cfg.input.data_dirs`` against the matching ``cfg.input.sfm_model_dirs`` entry."""
+    ``cfg.input.data_dirs`` against the matching ``cfg.input.sfm_model_dirs`` entry.
+
+    The reference seeds numpy / torch once, when ``inference.py`` is imported
+    (``seed_everything(12345)``, :14), and the 3D padding and leaf sampling of every sequence
+    draw from that stream; so this entry seeds the same way before its first sequence (pass
+    ``seed=False`` to keep the caller's stream, e.g. to continue one across calls)."""
+    if seed:
+        seed_reference_stream()
     data_dirs = cfg.input.data_dirs
     sfm_model_dirs = cfg.input.sfm_model_dirs
     if isinstance(data_dirs, str) and isinstance(sfm_model_dirs, str):

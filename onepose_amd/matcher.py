@@ -206,7 +206,7 @@ class GATsSuperGlue(nn.Module):
             ms0 = torch.empty(B, n1, dtype=torch.float32, device=dev)
             ms1 = torch.empty(B, n3, dtype=torch.float32, device=dev)
             conf = torch.empty(B, n1, n3, dtype=torch.float32, device=dev)
-            ws_bytes = lib.onepose_match_workspace_bytes(B, n1, n3, nleaf, 1)
+            ws_bytes = _lib.workspace_bytes(lib, B, n1, n3, nleaf, True, self.precision)
             ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
             rc = lib.onepose_match_ex(
                 w.data_ptr(), d2.data_ptr(), s2, d3.data_ptr(), s3, db.data_ptr(), sl,

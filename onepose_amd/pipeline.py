@@ -40,7 +40,7 @@ from .matcher import GATsSuperGlue
 
 
 class _Slot:
-    def __init__(self, B, n1, n3, dev, with_conf, lib, L, iters, image_hw=None):
+    def __init__(self, B, n1, n3, dev, with_conf, lib, L, iters, image_hw=None, precision=0):
         f32 = dict(dtype=torch.float32, device=dev)
         if image_hw is not None:   # detector inputs / outputs (the matcher reads the latter)
             h, w = image_hw
@@ -66,7 +66,7 @@ class _Slot:
         self.R_err = torch.empty(B, dtype=torch.float64, device=dev)
         self.t_err = torch.empty(B, dtype=torch.float64, device=dev)
         self.cmd = torch.empty(B, 3, dtype=torch.uint8, device=dev)
-        self.ws_match_bytes = lib.onepose_match_workspace_bytes(B, n1, n3, L, int(with_conf))
+        self.ws_match_bytes = _lib.workspace_bytes(lib, B, n1, n3, L, with_conf, precision)
         self.ws_match = torch.empty(self.ws_match_bytes, dtype=torch.uint8, device=dev)
         self.ws_pnp_bytes = lib.onepose_pnp_workspace_bytes(B, n1, iters)
         self.ws_pnp = torch.empty(self.ws_pnp_bytes, dtype=torch.uint8, device=dev)
@@ -108,7 +108,8 @@ class FramePipeline:
         self.object_cache = None
         self.object_flags = _lib.OBJ_GAT_TABLES if gat_tables else 0
         if object_cache:
-            nbytes = self.lib.onepose_object_cache_bytes(self.n3, self.L, self.object_flags)
+            nbytes = _lib.object_cache_bytes(self.lib, self.n3, self.L, self.object_flags,
+                                             self.precision)
             self.object_cache = torch.empty(nbytes // 4, **f32)
             wsb = self.lib.onepose_object_prepare_workspace_bytes(self.n3, self.L)
             ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
@@ -133,7 +134,7 @@ class FramePipeline:
             self.det_weights = detector.to(dev).packed_weights()
         self.image_hw = tuple(image_hw) if detector is not None else None
         self.slots = [_Slot(B, n1, self.n3, dev, with_conf, self.lib, self.L, self.iters,
-                            self.image_hw) for _ in range(max(1, slots))]
+                            self.image_hw, self.precision) for _ in range(max(1, slots))]
 
     def __del__(self):
         # drop the library's record of this object cache before its memory goes back to the
@@ -160,6 +161,37 @@ class FramePipeline:
         self.pose_gt.copy_(torch.as_tensor(np.asarray(pose_gt), dtype=torch.float64)[..., :3, :]
                            .expand_as(self.pose_gt))
 
+    def set_frame_bank(self, desc2d, kpts2d, K, pose_gt):
+        """A bank of F steps' inputs ([F, B, ...]: F * B distinct frames) made resident once;
+        step k of ``run_stream`` then reads bank entry k % F (F must be a multiple of the slot
+        count: entry j always runs in slot j % slots, so its captured graphs stay bound to one
+        slot's buffers).  Each entry also gets its own result rows (pose, errors, cm/deg flags,
+        inliers, status: ``bank_results``), written by the pose stage of the entry's last run."""
+        F = int(np.asarray(desc2d).shape[0]) if not torch.is_tensor(desc2d) else desc2d.shape[0]
+        if F % len(self.slots) != 0:
+            raise ValueError(f"frame bank of {F} steps is not a multiple of {len(self.slots)} slots")
+        dev, B = self.device, self.B
+
+        def dev_t(x, dt, shape):
+            return torch.as_tensor(np.asarray(x) if not torch.is_tensor(x) else x,
+                                   dtype=dt).reshape(shape).to(dev).contiguous()
+        f64 = torch.float64
+        self.bank = {"desc2d": dev_t(desc2d, torch.float32, (F, B, 256, self.n1)),
+                     "kpts2d": dev_t(kpts2d, torch.float32, (F, B, self.n1, 2)),
+                     "K": dev_t(K, f64, (F, B, 3, 3)),
+                     "pose_gt": dev_t(np.asarray(pose_gt)[..., :3, :] if not torch.is_tensor(pose_gt)
+                                      else pose_gt[..., :3, :], f64, (F, B, 3, 4))}
+        self.bank_results = {"pose": torch.zeros(F, B, 3, 4, dtype=f64, device=dev),
+                             "R_err": torch.zeros(F, B, dtype=f64, device=dev),
+                             "t_err": torch.zeros(F, B, dtype=f64, device=dev),
+                             "cmd": torch.zeros(F, B, 3, dtype=torch.uint8, device=dev),
+                             "n_inliers": torch.zeros(F, B, dtype=torch.int32, device=dev),
+                             "status": torch.full((F, B), -1, dtype=torch.int32, device=dev)}
+
+    @property
+    def bank_size(self) -> int:
+        return self.bank["desc2d"].shape[0] if getattr(self, "bank", None) is not None else 0
+
     def set_images(self, images, slot=None):
         """Copy B images ([B, H, W] or [B, 1, H, W], float in [0, 1]) into one slot's image
         buffer, or into every slot when slot is None."""
@@ -168,8 +200,12 @@ class FramePipeline:
         for o in (self.slots if slot is None else [self.slots[slot]]):
             o.image.copy_(img)
 
-    def _inputs(self, o):
-        return (o.desc2d, o.kpts2d) if self.detector is not None else (self.desc2d, self.kpts2d)
+    def _inputs(self, o, frame=None):
+        if self.detector is not None:
+            return o.desc2d, o.kpts2d
+        if frame is not None:
+            return self.bank["desc2d"][frame], self.bank["kpts2d"][frame]
+        return self.desc2d, self.kpts2d
 
     def enqueue_detect(self, slot: int = 0):
         """SuperPoint on the slot's images into the slot's matcher inputs."""
@@ -184,16 +220,17 @@ class FramePipeline:
             o.desc2d.data_ptr(), o.det_counts.data_ptr(), 0, 0, o.ws_det.data_ptr(),
             o.ws_det_bytes, _lib.stream_ptr(self.device)), "onepose_superpoint")
 
-    def enqueue_front(self, slot: int = 0):
-        """The stage that runs on a match stream: [detector ->] matcher."""
+    def enqueue_front(self, slot: int = 0, frame=None):
+        """The stage that runs on a match stream: [detector ->] matcher (on frame-bank entry
+        `frame` when given)."""
         if self.detector is not None:
             self.enqueue_detect(slot)
-        self.enqueue_match(slot)
+        self.enqueue_match(slot, frame)
 
-    def enqueue_match(self, slot: int = 0):
+    def enqueue_match(self, slot: int = 0, frame=None):
         o = self.slots[slot]
         s = _lib.stream_ptr(self.device)
-        desc2d, _ = self._inputs(o)
+        desc2d, _ = self._inputs(o, frame)
         if self.object_cache is not None:
             _lib.check(self.lib.onepose_match_cached(
                 self.weights.data_ptr(), desc2d.data_ptr(), 256 * self.n1,
@@ -213,24 +250,35 @@ class FramePipeline:
 
     fused_pose = True   # enqueue_pose's default: onepose_pose_stage (two launches)
 
-    def enqueue_pose(self, slot: int = 0, fused: bool | None = None):
+    def enqueue_pose(self, slot: int = 0, fused: bool | None = None, frame=None):
         """Selection -> RANSAC-EPnP -> cm/deg errors for the slot's frames: two launches
-        (onepose_pose_stage), or the three separate entry points (fused=False)."""
+        (onepose_pose_stage), or the three separate entry points (fused=False).  With `frame`
+        (a frame-bank entry) the entry's K and ground truth are read and its result rows
+        written (``bank_results``)."""
         fused = self.fused_pose if fused is None else fused
         o = self.slots[slot]
         s = _lib.stream_ptr(self.device)
         lib = self.lib
-        _, kpts2d = self._inputs(o)
+        _, kpts2d = self._inputs(o, frame)
+        if frame is not None:
+            K, pose_gt = self.bank["K"][frame], self.bank["pose_gt"][frame]
+            r = {k: v[frame] for k, v in self.bank_results.items()}
+        else:
+            K, pose_gt = self.K, self.pose_gt
+            r = {"pose": o.pose, "R_err": o.R_err, "t_err": o.t_err, "cmd": o.cmd,
+                 "n_inliers": o.n_inliers, "status": o.status}
         if fused:
             _lib.check(lib.onepose_pose_stage(
                 o.matches0.data_ptr(), kpts2d.data_ptr(), self.n1 * 2, self.kp3.data_ptr(), 0,
-                self.B, self.n1, self.n3, self.scale, self.K.data_ptr(), 9, self.reproj,
-                self.iters, self.conf_level, self.pose_gt.data_ptr(), 12, o.pts2d.data_ptr(),
-                o.pts3d.data_ptr(), o.counts.data_ptr(), o.pose.data_ptr(),
-                o.inlier_mask.data_ptr(), o.n_inliers.data_ptr(), o.status.data_ptr(),
-                o.R_err.data_ptr(), o.t_err.data_ptr(), o.cmd.data_ptr(), o.ws_pnp.data_ptr(),
-                o.ws_pnp_bytes, s), "pose_stage")
+                self.B, self.n1, self.n3, self.scale, K.data_ptr(), 9, self.reproj,
+                self.iters, self.conf_level, pose_gt.data_ptr(), 12, o.pts2d.data_ptr(),
+                o.pts3d.data_ptr(), o.counts.data_ptr(), r["pose"].data_ptr(),
+                o.inlier_mask.data_ptr(), r["n_inliers"].data_ptr(), r["status"].data_ptr(),
+                r["R_err"].data_ptr(), r["t_err"].data_ptr(), r["cmd"].data_ptr(),
+                o.ws_pnp.data_ptr(), o.ws_pnp_bytes, s), "pose_stage")
             return
+        if frame is not None:
+            raise ValueError("frame-bank entries run the fused pose stage")
         _lib.check(lib.onepose_select_correspondences(
             o.matches0.data_ptr(), kpts2d.data_ptr(), self.n1 * 2, self.kp3.data_ptr(), 0,
             self.B, self.n1, self.n3, self.scale, o.pts2d.data_ptr(), o.pts3d.data_ptr(),
@@ -262,14 +310,17 @@ class FramePipeline:
 
     def capture_stages(self, pool=None):
         """Capture, per buffer slot, the front stage ([detector ->] matcher) and the pose stage
-        as two HIP graphs (for ``run_stream(graphs=...)``)."""
+        as two HIP graphs (for ``run_stream(graphs=...)``).  With a frame bank, one pair per
+        bank entry j instead (slot j % slots, the entry's inputs and result rows)."""
         out = []
-        for sl in range(len(self.slots)):
+        F = self.bank_size
+        for j in range(F or len(self.slots)):
+            sl, fr = j % len(self.slots), (j if F else None)
             gm, gp = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
             with torch.cuda.graph(gm, pool=pool):
-                self.enqueue_front(sl)
+                self.enqueue_front(sl, fr)
             with torch.cuda.graph(gp, pool=pool):
-                self.enqueue_pose(sl)
+                self.enqueue_pose(sl, frame=fr)
             out.append((gm, gp))
         return out
 
@@ -286,8 +337,10 @@ class FramePipeline:
         and writes only its slot's buffers), so two frames' pose stages that become ready
         together -- the last frames of a batch -- run side by side instead of one after the
         other.  `marks` (a list) receives per step (start, matcher done, pose done) timing
-        events."""
+        events.  With a frame bank (``set_frame_bank``), step k runs bank entry k % F; `graphs`
+        then holds one pair per entry (``capture_stages``)."""
         ms0 = match_stream or torch.cuda.current_stream(self.device)
+        F = self.bank_size
         ps = pose_stream or getattr(self, "_pose_stream", None)
         if ps is None:
             ps = self._pose_stream = torch.cuda.Stream(
@@ -322,9 +375,9 @@ class FramePipeline:
                 if mk:
                     mk[0].record(ms)
                 if graphs:
-                    graphs[sl][0].replay()
+                    graphs[k % len(graphs)][0].replay()
                 else:
-                    self.enqueue_front(sl)
+                    self.enqueue_front(sl, k % F if F else None)
                 matched[sl].record(ms)
                 if mk:
                     mk[1].record(ms)
@@ -333,9 +386,9 @@ class FramePipeline:
                 ps.wait_event(matched[sl])
                 if pose:   # (False: a diagnostic of the matcher streams alone, bench.py)
                     if graphs:
-                        graphs[sl][1].replay()
+                        graphs[k % len(graphs)][1].replay()
                     else:
-                        self.enqueue_pose(sl)
+                        self.enqueue_pose(sl, frame=k % F if F else None)
                 posed[sl].record(ps)
                 if mk:
                     mk[2].record(ps)

@@ -234,6 +234,29 @@ def make_matcher_inputs(n1: int, n3: int, num_leaf: int = 8, seed: int = 0, batc
     }, obj, frames
 
 
+
+def make_frame_bank(n1: int, n3: int, steps: int, batch: int = 1, seed: int = 0, world: int = 1,
+                    rank: int = 0):
+    """Per-step query inputs of one object's sequence, for a bank of ``steps`` steps of
+    ``batch`` frames on this rank: arrays [steps, batch, ...] (keypoints2d, descriptors2d_query
+    in the reference's [256, n1] layout, K, pose_gt) and the global frame ids [steps, batch].
+    Step j of the sequence holds global frames [j * world * batch, (j + 1) * world * batch),
+    sharded contiguously over ranks (distributed.frame_shard), so rank r's frame (j, i) is
+    global frame (j * world + r) * batch + i -- frame g is ``make_frame(obj, n1, seed * 131 +
+    g)``, the same frames make_matcher_inputs(frame_ids=...) builds.  The object itself is not
+    copied per frame (make_matcher_inputs broadcasts it over the batch)."""
+    obj = make_object(n3, seed)
+    gid = np.array([[(j * world + rank) * batch + i for i in range(batch)] for j in range(steps)],
+                   np.int64)
+    frames = [[make_frame(obj, n1, seed * 131 + int(g)) for g in row] for row in gid]
+    return {
+        "keypoints2d": np.stack([np.stack([f.keypoints2d for f in r]) for r in frames]),
+        "descriptors2d_query": np.stack([np.stack([f.descriptors2d for f in r]) for r in frames]),
+        "K": np.stack([np.stack([f.K for f in r]) for r in frames]),
+        "pose_gt": np.stack([np.stack([f.pose_gt for f in r]) for r in frames]),
+        "frame_id": gid,
+    }
+
 # ------------------------------------------------------------------ SuperPoint
 SUPERPOINT_LAYERS = [   # (name, c_in, c_out, kernel)  superpoint.py:147-162
     ("conv1a", 1, 64, 3), ("conv1b", 64, 64, 3), ("conv2a", 64, 64, 3), ("conv2b", 64, 64, 3),

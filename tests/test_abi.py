@@ -30,7 +30,7 @@ def test_library_exports_every_header_symbol():
     missing = [s for s in header_symbols() if not hasattr(lib, s)]
     assert not missing, missing
     assert set(header_symbols()) == set(_lib.PROTOTYPES), "ctypes prototypes out of sync"
-    assert lib.onepose_abi_version() == _lib.ABI_VERSION == 3
+    assert lib.onepose_abi_version() == _lib.ABI_VERSION == 4
 
 
 def test_object_cache_size_follows_its_flags():
@@ -166,6 +166,30 @@ def test_workspace_sizes():
     b = lib.onepose_match_workspace_bytes(1, 1024, 4096, 8, 0)
     assert a > 0 and b - a >= 1024 * 4096 * 4
     assert lib.onepose_match_workspace_bytes(0, 1, 1, 8, 1) == 0
+    # ABI 4: per precision -- fp32 carves no bf16 activation planes (x2 / x3 ping-pong and
+    # phi(q), 3 planes of 512 B per token each: 6 KB per 2D + 3D token pair ... per token)
+    from onepose_amd.matcher import PRECISIONS
+    for B, n1, n3 in ((1, 1024, 4096), (3, 200, 330)):
+        full = lib.onepose_match_workspace_bytes(B, n1, n3, 8, 1)
+        f32 = lib.onepose_match_workspace_bytes_ex(B, n1, n3, 8, 1, PRECISIONS["fp32"])
+        assert lib.onepose_match_workspace_bytes_ex(B, n1, n3, 8, 1, PRECISIONS["bf16"]) == full
+        assert lib.onepose_match_workspace_bytes_ex(B, n1, n3, 8, 1, PRECISIONS["fp32_split"]) == full
+        planes = 3 * 3 * 256 * 2 * B * (n1 + n3)   # (x ping, x pong, phi(q)) x 3 planes x bf16
+        assert 0 <= full - f32 - planes < 3 * 256 * 8
+    assert lib.onepose_match_workspace_bytes_ex(1, 8, 8, 8, 1, 7) == 0
+
+
+def test_object_cache_size_per_precision():
+    from onepose_amd import _lib
+    from onepose_amd.matcher import PRECISIONS
+    lib = _lib.load()
+    for flags in (0, _lib.OBJ_GAT_TABLES):
+        for n3 in (77, 4096):
+            full = lib.onepose_object_cache_bytes(n3, 8, flags)
+            assert lib.onepose_object_cache_bytes_ex(n3, 8, flags, PRECISIONS["bf16"]) == full
+            assert lib.onepose_object_cache_bytes_ex(n3, 8, flags, PRECISIONS["fp32_split"]) == full
+            assert full - lib.onepose_object_cache_bytes_ex(n3, 8, flags, PRECISIONS["fp32"]) == 1536 * n3
+    assert lib.onepose_object_cache_bytes_ex(16, 8, 0, 9) == 0
     assert lib.onepose_pnp_workspace_bytes(2, 1024, 10000) >= 2 * 1024 * 4
 
 

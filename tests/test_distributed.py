@@ -138,3 +138,48 @@ def test_two_rank_bench_shards_one_objects_batch(tmp_path):
         np.testing.assert_array_equal(got[:, -1], np.arange(N_GLOBAL))
     assert (ref[:, 16] > 20).all()                       # every frame has correspondences
     assert len({tuple(np.round(r[:12], 6)) for r in ref.numpy()}) == N_GLOBAL
+
+
+# ---- the bench's frame bank: F steps of distinct frames, step k runs entry k % F ----
+def test_frame_bank_shards_one_sequence():
+    """Rank r's bank entry (j, i) is global frame (j world + r) B + i: the ranks' banks together
+    are the world-1 bank of batch world * B, frame for frame."""
+    from onepose_amd import synthetic as S
+    world, B, F = 2, 2, 3
+    one = S.make_frame_bank(N1, N3, F, world * B, seed=0)
+    for r in range(world):
+        bank = S.make_frame_bank(N1, N3, F, B, seed=0, world=world, rank=r)
+        for j in range(F):
+            for i in range(B):
+                g = bank["frame_id"][j, i]
+                assert g == (j * world + r) * B + i
+                jj, ii = divmod(int(g), world * B)
+                assert one["frame_id"][jj, ii] == g
+                np.testing.assert_array_equal(bank["keypoints2d"][j, i], one["keypoints2d"][jj, ii])
+                np.testing.assert_array_equal(bank["descriptors2d_query"][j, i],
+                                              one["descriptors2d_query"][jj, ii])
+                np.testing.assert_array_equal(bank["pose_gt"][j, i], one["pose_gt"][jj, ii])
+    # distinct frames
+    assert len({tuple(np.round(p.reshape(-1), 6)) for p in one["pose_gt"].reshape(-1, 3, 4)}) == F * world * B
+
+
+def test_bench_pose_summary_weights_every_timed_frame():
+    """summarize_pose: a row counts once per timed step that ran its bank entry; rows may come
+    in any order (the gather is in rank order, not frame order)."""
+    import bench
+    world, B, F, steps = 2, 2, 4, 10
+    n = world * B * F
+    res = np.zeros((n, 20))
+    res[:, 19] = np.arange(n)
+    res[:, 12] = np.arange(n)          # R_err = global frame id
+    res[:, 14] = (np.arange(n) % 2)    # cmd1
+    res[:, 18] = 0
+    perm = np.random.RandomState(0).permutation(n)
+    s = bench.summarize_pose(res[perm], world, B, F, steps)
+    w = np.bincount(np.arange(steps) % F, minlength=F)[np.arange(n) // (world * B)]
+    assert s["frames"] == world * B * steps == w.sum()
+    assert s["distinct_frames"] == n
+    assert abs(s["R_err_deg_mean"] - (w * np.arange(n)).sum() / w.sum()) < 1e-12
+    assert abs(s["cmd1"] - (w * (np.arange(n) % 2)).sum() / w.sum()) < 1e-12
+    s1 = bench.summarize_pose(res[:world * B], world, B, 0, steps)   # no bank: one batch
+    assert s1["frames"] == world * B

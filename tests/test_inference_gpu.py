@@ -161,6 +161,11 @@ def test_inference_cfg_entry_and_reference_call_sequence(tmp_path, device, monke
     out_file = tmp_path / "runs" / "eval" / "GATsSPG" / "objseq-1.txt"
     assert out_file.read_text() == "cmd1: 1.0\ncmd3: 1.0\ncmd5: 1.0\n"
     assert list(res.values())[0] == {"cmd1": 1.0, "cmd3": 1.0, "cmd5": 1.0}
+    # inference(cfg) seeds the reference's stream itself (inference.py:14 at import): the
+    # caller's RNG state does not change the result
+    np.random.seed(7)
+    torch.manual_seed(7)
+    assert I.inference(cfg) == res and out_file.read_text() == "cmd1: 1.0\ncmd3: 1.0\ncmd5: 1.0\n"
 
     # frame 1 through the reference call sequence, over the same leaves (same numpy stream)
     I.seed_reference_stream()

@@ -149,6 +149,50 @@ def test_two_pose_streams_match_eager(setup):
 
 
 @pytest.mark.gpu
+def test_frame_bank_runs_each_entry_like_eager():
+    """A frame bank of F steps (bench.py --frames): step k runs entry k % F through its own
+    captured graphs on slot k % slots; every entry's result rows equal an eager run of the
+    same frames through the static inputs, bit for bit, under the bench's two-stream
+    schedule."""
+    dev = torch.device("cuda", 0)
+    F = 3
+    sd = synthetic.make_state_dict(0)
+    data, obj, frames = synthetic.make_matcher_inputs(N1, N3, L, seed=5, batch=F * B)
+    m = matcher.from_state_dict(sd)
+    pipe = FramePipeline(m, data["keypoints3d"][0], data["descriptors3d_db"][0],
+                         data["descriptors2d_db"][0], B, N1, dev, scale=1000.0, slots=3)
+    Ks = np.stack([f.K for f in frames]).reshape(F, B, 3, 3)
+    gts = np.stack([f.pose_gt for f in frames]).reshape(F, B, 3, 4)
+    d2 = data["descriptors2d_query"].reshape(F, B, 256, N1)
+    k2 = data["keypoints2d"].reshape(F, B, N1, 2)
+    ref = []
+    for j in range(F):
+        pipe.set_frames(d2[j], k2[j], Ks[j], gts[j])
+        pipe.enqueue(0)
+        torch.cuda.synchronize()
+        ref.append(_outputs(pipe.slots[0]))
+    pipe.set_frame_bank(d2, k2, Ks, gts)
+    with pytest.raises(ValueError):
+        FramePipeline.set_frame_bank(pipe, d2[:2], k2[:2], Ks[:2], gts[:2])   # 2 % 3 slots
+    graphs = pipe.capture_stages()
+    assert len(graphs) == F
+    pipe.run_stream(7, graphs=graphs, match_streams=2, pose_streams=2)
+    torch.cuda.synchronize()
+    r = pipe.bank_results
+    for j in range(F):
+        for k in ("pose", "R_err", "t_err", "cmd", "n_inliers", "status"):
+            np.testing.assert_array_equal(r[k][j].cpu().numpy(), ref[j][k], err_msg=f"{k} {j}")
+    assert len({tuple(np.round(x.reshape(-1), 6)) for x in r["pose"].cpu().numpy().reshape(-1, 12)}) == F * B
+    # eager steps over the bank too
+    for v in r.values():
+        v.zero_()
+    pipe.run_stream(F, match_streams=2)
+    torch.cuda.synchronize()
+    for j in range(F):
+        np.testing.assert_array_equal(r["pose"][j].cpu().numpy(), ref[j]["pose"])
+
+
+@pytest.mark.gpu
 def test_detector_pipeline_from_images():
     """Images -> SuperPoint -> matcher -> selection -> RANSAC-EPnP: the detector stage writes
     exactly what SuperPoint.detect_raw returns, the matcher stage equals the module forward on
