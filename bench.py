@@ -280,6 +280,10 @@ def main():
     ap.add_argument("--precision", choices=["fp32", "bf16", "fp32_split"], default="fp32",
                     help="matcher attention-layer GEMMs: fp32 MFMA (the reference's numerics, "
                          "default) or bf16 MFMA with fp32 accumulation (BASELINE config 5)")
+    ap.add_argument("--desc-dtype", choices=["fp32", "fp16"], default="fp32",
+                    help="the object's and the query frames' descriptors as held in HBM (fp16: "
+                         "BASELINE config 5's 'fp16 desc'; the kernels convert them as they load "
+                         "them, the reference's .float() upcast)")
     ap.add_argument("--no-object-cache", action="store_true",
                     help="run GAT 0 and the 3D half of self-attention 1 every frame instead of "
                          "once per object (onepose_match_prepared_ex instead of _cached)")
@@ -351,7 +355,7 @@ def main():
                          data["descriptors2d_db"][0], B, n1, dev, scale=1000.0,
                          slots=nslots, detector=detector,
                          image_hw=(args.image_size, args.image_size),
-                         object_cache=not args.no_object_cache)
+                         object_cache=not args.no_object_cache, desc_dtype=args.desc_dtype)
     pipe.fused_pose = not args.unfused_pose
     pipe.pose_priority = args.pose_priority
     pipe.match_priority = args.match_priority
@@ -589,6 +593,8 @@ def main():
                 (2048, 8192): "config 5"}.get((n1, n3), "custom")
     if args.precision == "bf16":
         cfg_name += " (bf16-MFMA attention)"
+    if args.desc_dtype == "fp16":
+        cfg_name += " (fp16 desc)"
     elif args.precision == "fp32_split":
         cfg_name += " (fp32 attention as 3-piece bf16 split)"
     if rank == 0:
@@ -607,7 +613,9 @@ def main():
             "dtype": {"fp32": "fp32",
                       "fp32_split": "fp32 (attention GEMMs as the exact 3-piece bf16 split on "
                                     "bf16 MFMA, fp32 accumulation)",
-                      "bf16": "bf16 attention GEMMs, fp32 rest"}[args.precision],
+                      "bf16": "bf16 attention GEMMs, fp32 rest"}[args.precision]
+                     + ("; descriptors fp16 in HBM (converted on load)"
+                        if args.desc_dtype == "fp16" else ""),
             "data": "synthetic",
             "config": {"workload": (f"{cfg_name}: {n1} kpts x {n3} 3D pts, L={L}, {B} frame(s) per "
                                     f"GPU per step; "

@@ -49,6 +49,12 @@ enum {
                                    fp32-accurate (the dropped terms are < 2^-22 |a b|)  */
 };
 
+/* Descriptor element types of the _dt entry points (ABI 4).  The reference upcasts every
+ * descriptor input with .float() (GATs_SuperGlue.py:219-221); an fp16 input is converted as it
+ * is loaded, so the results are those of the fp32 path on the upcast inputs, bit for bit, and
+ * the inputs (the object's leaves above all) take half the bytes in HBM. */
+enum { ONEPOSE_DT_F32 = 0, ONEPOSE_DT_F16 = 1 };
+
 /* Thread-local description of the last error ("" when none). */
 const char* onepose_last_error(void);
 /* ABI version, bumped on any signature change or new entry point (4: the per-precision
@@ -119,12 +125,25 @@ int onepose_match(const void* packed_weights,
 size_t onepose_leaves_prepared_bytes(int batch, int n3, int num_leaf);
 int onepose_prepare_leaves(const float* leaves, int64_t leaves_bstride, int batch, int n3,
                            int num_leaf, float* out, void* stream);
+/* (ABI 4) leaves of `dtype` (ONEPOSE_DT_*); the prepared copy is fp32. */
+int onepose_prepare_leaves_dt(const void* leaves, int dtype, int64_t leaves_bstride, int batch,
+                              int n3, int num_leaf, float* out, void* stream);
 /* The same two calls with a precision mode (ONEPOSE_PREC_*); the plain forms are
  * ONEPOSE_PREC_FP32. */
 int onepose_match_ex(const void* packed_weights,
                      const float* desc2d, int64_t desc2d_bstride,
                      const float* desc3d, int64_t desc3d_bstride,
                      const float* leaves, int64_t leaves_bstride,
+                     int batch, int n1, int n3, int num_leaf,
+                     float scale_factor, float match_threshold, int precision,
+                     int64_t* matches0, int64_t* matches1,
+                     float* mscores0, float* mscores1, float* conf,
+                     void* workspace, size_t workspace_bytes, void* stream);
+/* (ABI 4) onepose_match_ex with desc2d, desc3d and leaves of `desc_dtype` (ONEPOSE_DT_*). */
+int onepose_match_dt(const void* packed_weights,
+                     const void* desc2d, int64_t desc2d_bstride,
+                     const void* desc3d, int64_t desc3d_bstride,
+                     const void* leaves, int64_t leaves_bstride, int desc_dtype,
                      int batch, int n1, int n3, int num_leaf,
                      float scale_factor, float match_threshold, int precision,
                      int64_t* matches0, int64_t* matches1,
@@ -203,6 +222,11 @@ int onepose_object_prepare(const void* packed_weights, const float* desc3d,
                            const float* leaves_prepared, int n3, int num_leaf, int precision,
                            int flags, float* cache, void* workspace, size_t workspace_bytes,
                            void* stream);
+/* (ABI 4) desc3d [256, n3] of `desc_dtype` (ONEPOSE_DT_*). */
+int onepose_object_prepare_dt(const void* packed_weights, const void* desc3d, int desc_dtype,
+                              const float* leaves_prepared, int n3, int num_leaf, int precision,
+                              int flags, float* cache, void* workspace, size_t workspace_bytes,
+                              void* stream);
 void onepose_object_release(const float* cache);
 /* Workspace: onepose_match_workspace_bytes(batch, n1, n3, num_leaf, conf != NULL). */
 int onepose_match_cached(const void* packed_weights,
@@ -215,6 +239,17 @@ int onepose_match_cached(const void* packed_weights,
                          int64_t* matches0, int64_t* matches1,
                          float* mscores0, float* mscores1, float* conf,
                          void* workspace, size_t workspace_bytes, void* stream);
+/* (ABI 4) desc2d [batch, 256, n1] of `desc_dtype` (ONEPOSE_DT_*). */
+int onepose_match_cached_dt(const void* packed_weights,
+                            const void* desc2d, int desc_dtype, int64_t desc2d_bstride,
+                            const float* object_cache,
+                            const float* leaves_prepared, int64_t prepared_bstride,
+                            int batch, int n1, int n3, int num_leaf,
+                            float scale_factor, float match_threshold, int precision,
+                            int object_flags,
+                            int64_t* matches0, int64_t* matches1,
+                            float* mscores0, float* mscores1, float* conf,
+                            void* workspace, size_t workspace_bytes, void* stream);
 
 /* ------------------------------------------------------------------------------------ *
  * N3-sharded single frame (SURVEY.md §8e optional / §8f rank 4): one frame's 3D points split

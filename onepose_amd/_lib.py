@@ -22,6 +22,7 @@ c_void_p, c_char_p = ctypes.c_void_p, ctypes.c_char_p
 ALLGATHER_FN = ctypes.CFUNCTYPE(c_int, c_size_t, c_void_p, c_void_p)
 ABI_VERSION = 4
 OBJ_GAT_TABLES = 1   # ONEPOSE_OBJ_GAT_TABLES
+DT_F32, DT_F16 = 0, 1   # ONEPOSE_DT_*
 
 # name -> (restype, argtypes); mirrors include/onepose_hip.h
 PROTOTYPES = {
@@ -34,6 +35,18 @@ PROTOTYPES = {
     "onepose_matcher_pack": (c_int, [ctypes.POINTER(c_void_p), c_int, c_void_p]),
     "onepose_match_workspace_bytes": (c_size_t, [c_int, c_int, c_int, c_int, c_int]),
     "onepose_match_workspace_bytes_ex": (c_size_t, [c_int, c_int, c_int, c_int, c_int, c_int]),
+    "onepose_prepare_leaves_dt": (c_int, [c_void_p, c_int, c_int64, c_int, c_int, c_int, c_void_p,
+                                          c_void_p]),
+    "onepose_match_dt": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64,
+                                 c_int, c_int, c_int, c_int, c_int, c_float, c_float, c_int,
+                                 c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                 c_void_p, c_size_t, c_void_p]),
+    "onepose_object_prepare_dt": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_int, c_int, c_int,
+                                          c_int, c_void_p, c_void_p, c_size_t, c_void_p]),
+    "onepose_match_cached_dt": (c_int, [c_void_p, c_void_p, c_int, c_int64, c_void_p, c_void_p,
+                                        c_int64, c_int, c_int, c_int, c_int, c_float, c_float,
+                                        c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
+                                        c_void_p, c_void_p, c_size_t, c_void_p]),
     "onepose_match": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64,
                               c_int, c_int, c_int, c_int, c_float, c_float,
                               c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,

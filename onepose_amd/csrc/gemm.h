@@ -173,6 +173,73 @@ inline int stats_groups(int M, int rows) {
   return (mtiles + g - 1) / g;
 }
 
+// gemm_bal.hip: MLP conv 1 (EPI_STATS + PRO_HEADZ, fp32, N = K = 512) on the tile-balanced
+// kernel (64 x 32 strips dealt evenly to one 8-wave workgroup per CU, the same bits as the
+// 64 x 64 tile) when the 64 x 64 grid would load CUs unevenly (at most 3 tiles per CU).
+// Returns false, launching nothing, when it does not apply; otherwise *rc is the launch status.
+// Its in-launch finalize counts per 32-column block: st_cnt_bs >= gemm_bal_counters_per_sample.
+bool gemm_bal_try(GemmArgs& args, hipStream_t stream, int kind, int* rc);
+int gemm_bal_counters_per_sample(int M);
+
+// PRO_HEADZ arithmetic, shared by the two MLP conv 1 kernels for the same reason as the merges
+// below: one stage's 8-term piece of phi(q)_row . ksum_h (products rounded, summed left to
+// right) added to the running dot, and the head fold acc + Z*Ns * acc_h as one fma.
+__device__ __forceinline__ float headz_dot8(float zp, float4 a0, float4 a1, float4 k0, float4 k1) {
+#pragma clang fp contract(off)
+  return zp + (a0.x * k0.x + a0.y * k0.y + a0.z * k0.z + a0.w * k0.w + a1.x * k1.x +
+               a1.y * k1.y + a1.z * k1.z + a1.w * k1.w);
+}
+__device__ __forceinline__ float headz_fold(float acc, float z, float acc_h) {
+  return fmaf(z, acc_h, acc);
+}
+
+// InstanceNorm merges of MLP conv 1's in-launch finalize, shared by gemm.hip's 64 x 64 tile and
+// gemm_bal.hip so that both round every operation alike: each statement exactly as written
+// (contraction off -- left to itself the compiler fused some of these in one kernel and not in
+// the other), with fma() where the merge takes one.
+// (count, mean, M2) of a 32-row block into the running column statistics (Chan et al.)
+__device__ __forceinline__ void in_merge_block(float& n, float& mean, float& M2, float nb, float mb,
+                                               float m2b) {
+#pragma clang fp contract(off)
+  const float nn = n + nb, delta = mb - mean;
+  mean += delta * (nb / nn);
+  M2 += m2b + delta * delta * (n * nb / nn);
+  n = nn;
+}
+// one M-tile's (mean mv, M2 qv) of nb rows into a group's shifted sums (shift c)
+__device__ __forceinline__ void in_merge_tile(double& s1, double& s2, double& ng, double nb, float mv,
+                                              float qv, double c) {
+#pragma clang fp contract(off)
+  const double d = (double)mv - c;
+  s1 = fma(nb, d, s1);
+  s2 = s2 + fma(nb * d, d, (double)qv);
+  ng = ng + nb;
+}
+// one group's (mean mg, M2 m2g) of ngr rows into the column's shifted sums (shift c)
+__device__ __forceinline__ void in_merge_group(double& S1, double& S2, double ngr, double mg,
+                                               double m2g, double c) {
+#pragma clang fp contract(off)
+  const double d = mg - c;
+  S1 = fma(ngr, d, S1);
+  S2 = S2 + fma(ngr * d, d, m2g);
+}
+__device__ __forceinline__ double in_group_mean(double c, double s1, double ng) {
+#pragma clang fp contract(off)
+  return c + s1 / ng;
+}
+__device__ __forceinline__ double in_group_m2(double s1, double s2, double ng) {
+#pragma clang fp contract(off)
+  return s2 - s1 * s1 / ng;
+}
+__device__ __forceinline__ float in_final_mean(double c, double S1, double n) {
+#pragma clang fp contract(off)
+  return (float)(c + S1 / n);
+}
+__device__ __forceinline__ float in_final_rstd(double S1, double S2, double n) {
+#pragma clang fp contract(off)
+  return (float)(1.0 / sqrt((S2 - S1 * S1 / n) / n + 1e-5));
+}
+
 // Zero-initialised problem with the common fields set.
 GemmProb gemm_prob(const float* A, int lda, const float* W, int ldw, const float* bias,
                    float* Y, int ldy, int M, int N, int K, int batch);

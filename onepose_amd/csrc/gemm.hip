@@ -482,8 +482,7 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
         }
         const float4 k0 = *reinterpret_cast<const float4*>(kp);
         const float4 k1 = *reinterpret_cast<const float4*>(kp + 4);
-        zp += a0.x * k0.x + a0.y * k0.y + a0.z * k0.z + a0.w * k0.w + a1.x * k1.x +
-              a1.y * k1.y + a1.z * k1.z + a1.w * k1.w;
+        zp = headz_dot8(zp, a0, a1, k0, k1);
       }
     }
   };
@@ -499,7 +498,7 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const int row = wm * 32 + (i & 3) + 8 * (i >> 2) + 4 * (lane >> 5);
-        acc[j][i] += zrow[par * BM + row] * acc_h[j][i];
+        acc[j][i] = headz_fold(acc[j][i], zrow[par * BM + row], acc_h[j][i]);
         acc_h[j][i] = 0.f;
       }
   };
@@ -1020,10 +1019,7 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
         const float nb = (float)max(min(g * RG + RG, rows) - g * RG, 0);
         if (nb == 0.f) continue;
         const float mb = part[(g * BN + t) * 2], m2b = part[(g * BN + t) * 2 + 1];
-        const float nn = n + nb, delta = mb - mean;
-        mean += delta * (nb / nn);
-        M2 += m2b + delta * delta * (n * nb / nn);
-        n = nn;
+        in_merge_block(n, mean, M2, nb, mb, m2b);
       }
       float* st_out = F(stats) + ((int64_t)b * mtiles + mt) * 2 * N;
       if (F(st_cnt) != nullptr) {   // handed to this launch's last tile: write-through (sc1)
@@ -1096,18 +1092,14 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
             }
 #pragma unroll
             for (int u = 0; u < UD; ++u) {
-              if (u0 + u < gsz) {
-                const double nb = (double)min(BM, M - (gt0 + u0 + u) * BM), d = (double)mv[u] - c;
-                s1 += nb * d;
-                s2 += (double)qv[u] + nb * d * d;
-                ng += nb;
-              }
+              if (u0 + u < gsz)
+                in_merge_tile(s1, s2, ng, (double)min(BM, M - (gt0 + u0 + u) * BM), mv[u], qv[u], c);
             }
           }
           if (n0 + t < N) {
-            __hip_atomic_store(gp + (int64_t)g1 * 2 * N + n0 + t, c + s1 / ng, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(gp + (int64_t)g1 * 2 * N + N + n0 + t, s2 - s1 * s1 / ng,
+            __hip_atomic_store(gp + (int64_t)g1 * 2 * N + n0 + t, in_group_mean(c, s1, ng),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(gp + (int64_t)g1 * 2 * N + N + n0 + t, in_group_m2(s1, s2, ng),
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           }
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1140,16 +1132,13 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
 #pragma unroll
             for (int u = 0; u < GD; ++u) {
               const int g = q0 + u;
-              if (g < ngroups) {
-                const double ngr = (double)min(G * BM, M - g * G * BM), d = mg[u] - c;
-                S1 += ngr * d;
-                S2 += m2g[u] + ngr * d * d;
-              }
+              if (g < ngroups)
+                in_merge_group(S1, S2, (double)min(G * BM, M - g * G * BM), mg[u], m2g[u], c);
             }
           }
           const double n = (double)M;
-          F(st_mean)[(int64_t)b * N + n0 + t] = (float)(c + S1 / n);
-          F(st_rstd)[(int64_t)b * N + n0 + t] = (float)(1.0 / sqrt((S2 - S1 * S1 / n) / n + 1e-5));
+          F(st_mean)[(int64_t)b * N + n0 + t] = in_final_mean(c, S1, n);
+          F(st_rstd)[(int64_t)b * N + n0 + t] = in_final_rstd(S1, S2, n);
         }
       }
     }
@@ -1311,6 +1300,13 @@ GemmProb gemm_prob(const float* A, int lda, const float* W, int ldw, const float
 
 int gemm_launch(int epi, int pro, int tile, GemmArgs& args, hipStream_t stream, int kind,
                 int pm) {
+#if defined(ONEPOSE_BAL) && !defined(ONEPOSE_NO_BAL)   // (under evaluation: A/B builds)
+  if (epi == EPI_STATS && pro == PRO_HEADZ && tile == TILE_64x64 && pm == PM_F32 &&
+      args.p[0].Wp == nullptr) {
+    int rc = ONEPOSE_OK;
+    if (gemm_bal_try(args, stream, kind, &rc)) return rc;
+  }
+#endif
   const TileDims td = tile_dims(tile);
   OP_REQUIRE(td.bm > 0, "gemm: unknown tile %d", tile);
   int grid = 0;

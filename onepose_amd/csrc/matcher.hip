@@ -250,11 +250,12 @@ const std::vector<TensorSpec>& tensor_specs() {
 // [B][n][256], both inputs in one launch.  64 tokens x 64 channels per workgroup through a
 // padded LDS tile; 16-byte loads along tokens when n % 4 == 0, 16-byte stores along channels.
 struct TransProb {
-  const float* src;
+  const void* src;   // fp32, or fp16 with f16 (the reference's .float() upcast, exact)
   int64_t bs;
   int n, tiles;   // tokens, workgroups per sample (ceil(n/64) * 4)
   float* dst;
   uint16_t* dstp = nullptr;   // bf16 modes: dst's activation planes ([B][3][n][256]; npl of them)
+  int f16 = 0;
 };
 struct TransArgs {
   TransProb p[2];
@@ -276,9 +277,29 @@ __global__ __launch_bounds__(256) void transpose_in_kernel(TransArgs args, int b
     args.zero64[i] = 0ull;
   const int b = bid / P.tiles, r = bid - b * P.tiles;
   const int n0 = (r >> 2) * 64, c0 = (r & 3) * 64, n = P.n;
-  const float* s = P.src + b * P.bs;
+  const float* s = static_cast<const float*>(P.src) + b * P.bs;
+  const _Float16* sh = static_cast<const _Float16*>(P.src) + b * P.bs;
   const int t = threadIdx.x;
-  if ((n & 3) == 0) {
+  if (P.f16) {   // descriptors in fp16: converted as loaded (GATs_SuperGlue.py:219-221 .float())
+    if ((n & 3) == 0) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int e = t + 256 * i, ch = e >> 4, tq = (e & 15) * 4;
+        typedef _Float16 half4 __attribute__((ext_vector_type(4)));
+        half4 v = {0, 0, 0, 0};
+        if (n0 + tq < n) v = *reinterpret_cast<const half4*>(sh + (int64_t)(c0 + ch) * n + n0 + tq);
+        tile[ch][tq] = (float)v[0];
+        tile[ch][tq + 1] = (float)v[1];
+        tile[ch][tq + 2] = (float)v[2];
+        tile[ch][tq + 3] = (float)v[3];
+      }
+    } else {
+      for (int i = 0; i < 16; ++i) {
+        const int ch = (t >> 6) + 4 * i, tk = t & 63;
+        tile[ch][tk] = (n0 + tk < n) ? (float)sh[(int64_t)(c0 + ch) * n + n0 + tk] : 0.f;
+      }
+    }
+  } else if ((n & 3) == 0) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {   // 64 channels x 16 float4 of tokens
       const int e = t + 256 * i, ch = e >> 4, tq = (e & 15) * 4;
@@ -1319,7 +1340,9 @@ __global__ __launch_bounds__(256) void mutual_kernel(const unsigned long long* r
 // ------------------------------------------------------------------------------------
 namespace {
 
-constexpr int kCntPerSide = 512 / 64;   // mlp1 column blocks (TILE_64x64, N = 512)
+// MLP conv 1's finalize counters per sample: column blocks of 32 (gemm_bal.hip's strips; the
+// 64 x 64 tile uses the first 512 / 64 of them), then that many per stats group
+constexpr int kCntPerSide = 512 / 32;
 
 struct Plan {
   float *x2[2], *x3[2];
@@ -2096,13 +2119,14 @@ int attention_layer(const ApW& w, const Side* sd, int nside, int B, const Plan& 
 // The matcher forward on point-major leaves [*, n3*L, 256] (leaves_pm_bs elements per sample).
 // obj_cache (onepose_match_cached): the 3D side entering layer 2, [n3][256] shared by the
 // batch (onepose_object_prepare) -- GAT 0 and the 3D half of self-attention 1 are skipped.
-int match_impl(const void* packed_weights, const float* desc2d, int64_t desc2d_bstride,
-               const float* desc3d, int64_t desc3d_bstride, const float* leaves_pm,
+// desc_dt (ONEPOSE_DT_*): the element type of desc2d and of an uncached desc3d.
+int match_impl(const void* packed_weights, const void* desc2d, int64_t desc2d_bstride,
+               const void* desc3d, int64_t desc3d_bstride, const float* leaves_pm,
                int64_t leaves_pm_bs, int batch, int n1, int n3, int num_leaf, float scale_factor,
                float match_threshold, int64_t* matches0, int64_t* matches1, float* mscores0,
                float* mscores1, float* conf, const Plan& p, hipStream_t st, int precision,
                const ShardCtx* sh = nullptr, const float* obj_cache = nullptr,
-               int obj_flags = 0) {
+               int obj_flags = 0, int desc_dt = ONEPOSE_DT_F32) {
   const bool with_conf = conf != nullptr;
   const int n3g = sh ? sh->n3_total : n3;   // the 3D side's full length (softmax / attention)
   const int pm = attention_pm(precision);   // attention-layer GEMM operand mode
@@ -2126,6 +2150,8 @@ int match_impl(const void* packed_weights, const float* desc2d, int64_t desc2d_b
     ta.p[0] = {desc2d, desc2d_bstride, n1, ceil_div(n1, 64) * 4, p.x2[0], pl(p.x2p[0])};
     ta.p[1] = {desc3d, desc3d_bstride, n3, obj_cache ? 0 : ceil_div(n3, 64) * 4, p.x3[0],
                pl(p.x3p[0])};
+    ta.p[0].f16 = desc_dt == ONEPOSE_DT_F16;
+    ta.p[1].f16 = !obj_cache && desc_dt == ONEPOSE_DT_F16;
     ta.zero = p.cnt;
     ta.nzero = p.ncnt;
     ta.npl = npl;
@@ -2330,9 +2356,9 @@ int match_impl(const void* packed_weights, const float* desc2d, int64_t desc2d_b
 // side attends only to itself there) -> cache [n3][256], the state entering layer 2.
 // The same kernels and tiles as the grouped forward, so the cached state is bit-identical
 // to what onepose_match computes in place.
-int object_prepare_impl(const void* packed_weights, const float* desc3d, const float* leaves_pm,
-                        int n3, int num_leaf, int precision, int flags, float* cache,
-                        const Plan& p, hipStream_t st) {
+int object_prepare_impl(const void* packed_weights, const void* desc3d, int desc_dt,
+                        const float* leaves_pm, int n3, int num_leaf, int precision, int flags,
+                        float* cache, const Plan& p, hipStream_t st) {
   const float* wbase = static_cast<const float*>(packed_weights);
   const int pm = attention_pm(precision);
   const int npl = planes_of(pm);   // activation planes (bf16 modes), as in match_impl
@@ -2341,6 +2367,7 @@ int object_prepare_impl(const void* packed_weights, const float* desc3d, const f
     TransArgs ta;
     ta.p[0] = {desc3d, 0, n3, ceil_div(n3, 64) * 4, p.x3[0]};
     ta.p[1] = {desc3d, 0, n3, 0, p.x3[0]};
+    ta.p[0].f16 = desc_dt == ONEPOSE_DT_F16;
     ta.zero = p.cnt;
     ta.nzero = p.ncnt;
     OP_LAUNCH(K_TRANSPOSE, st, transpose_in_kernel, dim3(ta.p[0].tiles), dim3(256), 0, st, ta, 1);
@@ -2420,8 +2447,8 @@ int object_prepare_impl(const void* packed_weights, const float* desc3d, const f
   return ONEPOSE_OK;
 }
 
-int check_match_args(const void* packed_weights, const float* desc2d, const float* desc3d,
-                     const float* leaves, int batch, int n1, int n3, int num_leaf,
+int check_match_args(const void* packed_weights, const void* desc2d, const void* desc3d,
+                     const void* leaves, int batch, int n1, int n3, int num_leaf,
                      float scale_factor, const int64_t* matches0, const int64_t* matches1,
                      const float* mscores0, const float* mscores1, const void* workspace) {
   OP_REQUIRE(packed_weights && desc2d && desc3d && leaves, "match: null input");
@@ -2445,8 +2472,15 @@ size_t onepose_leaves_prepared_bytes(int batch, int n3, int num_leaf) {
 
 int onepose_prepare_leaves(const float* leaves, int64_t leaves_bstride, int batch, int n3,
                            int num_leaf, float* out, void* stream_) {
+  return onepose_prepare_leaves_dt(leaves, ONEPOSE_DT_F32, leaves_bstride, batch, n3, num_leaf,
+                                   out, stream_);
+}
+
+int onepose_prepare_leaves_dt(const void* leaves, int dtype, int64_t leaves_bstride, int batch,
+                              int n3, int num_leaf, float* out, void* stream_) {
   clear_error();
   OP_REQUIRE(leaves && out, "prepare_leaves: null pointer");
+  OP_REQUIRE(dtype == ONEPOSE_DT_F32 || dtype == ONEPOSE_DT_F16, "prepare_leaves: dtype %d", dtype);
   OP_REQUIRE(batch >= 1 && n3 >= 1 && num_leaf >= 1 && num_leaf <= 16,
              "prepare_leaves: batch=%d n3=%d num_leaf=%d", batch, n3, num_leaf);
   hipStream_t st = static_cast<hipStream_t>(stream_);
@@ -2454,6 +2488,7 @@ int onepose_prepare_leaves(const float* leaves, int64_t leaves_bstride, int batc
   TransArgs ta;
   ta.p[0] = {leaves, leaves_bstride, ncol, ceil_div(ncol, 64) * 4, out};
   ta.p[1] = {leaves, 0, 1, 0, out};
+  ta.p[0].f16 = dtype == ONEPOSE_DT_F16;
   ta.zero = nullptr;
   ta.nzero = 0;
   OP_LAUNCH(K_TRANSPOSE, st, transpose_in_kernel, dim3(ta.p[0].tiles * batch), dim3(256), 0, st,
@@ -2467,9 +2502,23 @@ int onepose_match_ex(const void* packed_weights, const float* desc2d, int64_t de
                      float scale_factor, float match_threshold, int precision,
                      int64_t* matches0, int64_t* matches1, float* mscores0, float* mscores1,
                      float* conf, void* workspace, size_t workspace_bytes, void* stream_) {
+  return onepose_match_dt(packed_weights, desc2d, desc2d_bstride, desc3d, desc3d_bstride, leaves,
+                          leaves_bstride, ONEPOSE_DT_F32, batch, n1, n3, num_leaf, scale_factor,
+                          match_threshold, precision, matches0, matches1, mscores0, mscores1,
+                          conf, workspace, workspace_bytes, stream_);
+}
+
+int onepose_match_dt(const void* packed_weights, const void* desc2d, int64_t desc2d_bstride,
+                     const void* desc3d, int64_t desc3d_bstride, const void* leaves,
+                     int64_t leaves_bstride, int desc_dtype, int batch, int n1, int n3,
+                     int num_leaf, float scale_factor, float match_threshold, int precision,
+                     int64_t* matches0, int64_t* matches1, float* mscores0, float* mscores1,
+                     float* conf, void* workspace, size_t workspace_bytes, void* stream_) {
   clear_error();
   OP_REQUIRE(valid_precision(precision),
              "match: precision %d", precision);
+  OP_REQUIRE(desc_dtype == ONEPOSE_DT_F32 || desc_dtype == ONEPOSE_DT_F16, "match: dtype %d",
+             desc_dtype);
   int rc = check_match_args(packed_weights, desc2d, desc3d, leaves, batch, n1, n3, num_leaf,
                             scale_factor, matches0, matches1, mscores0, mscores1, workspace);
   if (rc != ONEPOSE_OK) return rc;
@@ -2483,13 +2532,14 @@ int onepose_match_ex(const void* packed_weights, const float* desc2d, int64_t de
   const Plan p = make_plan(workspace, batch, n1, n3, num_leaf, conf != nullptr, planes);
   // reference layout [*, 256, n3*L] -> point-major copy in the workspace
   const int lb = leaves_bstride == 0 ? 1 : batch;
-  if ((rc = onepose_prepare_leaves(leaves, leaves_bstride, lb, n3, num_leaf, p.leaves_pm,
-                                   stream_)) != ONEPOSE_OK)
+  if ((rc = onepose_prepare_leaves_dt(leaves, desc_dtype, leaves_bstride, lb, n3, num_leaf,
+                                      p.leaves_pm, stream_)) != ONEPOSE_OK)
     return rc;
   const int64_t pm_bs = leaves_bstride == 0 ? 0 : (int64_t)n3 * num_leaf * 256;
   return match_impl(packed_weights, desc2d, desc2d_bstride, desc3d, desc3d_bstride, p.leaves_pm,
                     pm_bs, batch, n1, n3, num_leaf, scale_factor, match_threshold, matches0,
-                    matches1, mscores0, mscores1, conf, p, st, precision);
+                    matches1, mscores0, mscores1, conf, p, st, precision, nullptr, nullptr, 0,
+                    desc_dtype);
 }
 
 int onepose_match(const void* packed_weights, const float* desc2d, int64_t desc2d_bstride,
@@ -2587,7 +2637,18 @@ int onepose_object_prepare(const void* packed_weights, const float* desc3d,
                            const float* leaves_prepared, int n3, int num_leaf, int precision,
                            int flags, float* cache, void* workspace, size_t workspace_bytes,
                            void* stream_) {
+  return onepose_object_prepare_dt(packed_weights, desc3d, ONEPOSE_DT_F32, leaves_prepared, n3,
+                                   num_leaf, precision, flags, cache, workspace, workspace_bytes,
+                                   stream_);
+}
+
+int onepose_object_prepare_dt(const void* packed_weights, const void* desc3d, int desc_dtype,
+                              const float* leaves_prepared, int n3, int num_leaf, int precision,
+                              int flags, float* cache, void* workspace, size_t workspace_bytes,
+                              void* stream_) {
   clear_error();
+  OP_REQUIRE(desc_dtype == ONEPOSE_DT_F32 || desc_dtype == ONEPOSE_DT_F16,
+             "object_prepare: dtype %d", desc_dtype);
   OP_REQUIRE(packed_weights && desc3d && leaves_prepared && cache, "object_prepare: null pointer");
   OP_REQUIRE(valid_precision(precision),
              "object_prepare: precision %d", precision);
@@ -2605,8 +2666,9 @@ int onepose_object_prepare(const void* packed_weights, const float* desc3d,
     std::lock_guard<std::mutex> lk(g_cache_mu);
     g_caches.erase(cache);   // whatever it held before is gone from here on
   }
-  const int rc = object_prepare_impl(packed_weights, desc3d, leaves_prepared, n3, num_leaf,
-                                     precision, flags, cache, p, static_cast<hipStream_t>(stream_));
+  const int rc = object_prepare_impl(packed_weights, desc3d, desc_dtype, leaves_prepared, n3,
+                                     num_leaf, precision, flags, cache, p,
+                                     static_cast<hipStream_t>(stream_));
   if (rc == ONEPOSE_OK) {
     std::lock_guard<std::mutex> lk(g_cache_mu);
     g_caches[cache] = {n3, num_leaf, precision, flags};
@@ -2626,7 +2688,24 @@ int onepose_match_cached(const void* packed_weights, const float* desc2d, int64_
                          int object_flags, int64_t* matches0, int64_t* matches1, float* mscores0,
                          float* mscores1, float* conf, void* workspace, size_t workspace_bytes,
                          void* stream_) {
+  return onepose_match_cached_dt(packed_weights, desc2d, ONEPOSE_DT_F32, desc2d_bstride,
+                                 object_cache, leaves_prepared, prepared_bstride, batch, n1, n3,
+                                 num_leaf, scale_factor, match_threshold, precision, object_flags,
+                                 matches0, matches1, mscores0, mscores1, conf, workspace,
+                                 workspace_bytes, stream_);
+}
+
+int onepose_match_cached_dt(const void* packed_weights, const void* desc2d, int desc_dtype,
+                            int64_t desc2d_bstride, const float* object_cache,
+                            const float* leaves_prepared, int64_t prepared_bstride, int batch,
+                            int n1, int n3, int num_leaf, float scale_factor,
+                            float match_threshold, int precision, int object_flags,
+                            int64_t* matches0, int64_t* matches1, float* mscores0,
+                            float* mscores1, float* conf, void* workspace, size_t workspace_bytes,
+                            void* stream_) {
   clear_error();
+  OP_REQUIRE(desc_dtype == ONEPOSE_DT_F32 || desc_dtype == ONEPOSE_DT_F16,
+             "match_cached: dtype %d", desc_dtype);
   OP_REQUIRE(valid_precision(precision),
              "match_cached: precision %d", precision);
   OP_REQUIRE((object_flags & ~ONEPOSE_OBJ_GAT_TABLES) == 0, "match_cached: flags %d",
@@ -2659,7 +2738,7 @@ int onepose_match_cached(const void* packed_weights, const float* desc2d, int64_
                     prepared_bstride, batch, n1, n3, num_leaf, scale_factor, match_threshold,
                     matches0, matches1, mscores0, mscores1, conf, p,
                     static_cast<hipStream_t>(stream_), precision, nullptr, object_cache,
-                    object_flags);
+                    object_flags, desc_dtype);
 }
 
 void onepose_shard_range(int n3_total, int world, int rank, int* start, int* count) {

@@ -161,9 +161,10 @@ class GATsSuperGlue(nn.Module):
 
     # ---------------------------------------------------------------- forward
     @staticmethod
-    def _operand(x):
-        """[B, C, N] float32 with contiguous (C, N); batch stride may be 0 (expanded)."""
-        x = x.float()
+    def _operand(x, keep_half=False):
+        """[B, C, N] float32 (or float16 with keep_half) with contiguous (C, N); batch stride may
+        be 0 (expanded)."""
+        x = x if (keep_half and x.dtype == torch.float16) else x.float()
         if x.stride(2) != 1 or x.stride(1) != x.shape[2]:
             x = x.contiguous()
         bstride = x.stride(0) if x.shape[0] > 1 else x.shape[1] * x.shape[2]
@@ -182,9 +183,14 @@ class GATsSuperGlue(nn.Module):
             }
         if self.match_type != "softmax":
             raise NotImplementedError
-        d2, s2 = self._operand(data["descriptors2d_query"])
-        d3, s3 = self._operand(data["descriptors3d_db"])
-        db, sl = self._operand(data["descriptors2d_db"])
+        # GATs_SuperGlue.py:219-221 upcasts every descriptor with .float(); fp16 descriptors
+        # (all three) go to the library as they are and are converted as its kernels load
+        # them (onepose_match_dt): the same bits as upcasting first, half the input bytes
+        half = all(data[k].dtype == torch.float16
+                   for k in ("descriptors2d_query", "descriptors3d_db", "descriptors2d_db"))
+        d2, s2 = self._operand(data["descriptors2d_query"], half)
+        d3, s3 = self._operand(data["descriptors3d_db"], half)
+        db, sl = self._operand(data["descriptors2d_db"], half)
         if d2.device.type != "cuda":
             raise RuntimeError("onepose_amd.GATsSuperGlue runs on a ROCm GPU only; "
                                "move the inputs with .cuda()")
@@ -208,8 +214,12 @@ class GATsSuperGlue(nn.Module):
             conf = torch.empty(B, n1, n3, dtype=torch.float32, device=dev)
             ws_bytes = _lib.workspace_bytes(lib, B, n1, n3, nleaf, True, self.precision)
             ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
-            rc = lib.onepose_match_ex(
-                w.data_ptr(), d2.data_ptr(), s2, d3.data_ptr(), s3, db.data_ptr(), sl,
+            dt = _lib.DT_F16 if d2.dtype == torch.float16 else _lib.DT_F32
+            # (an older A/B build named by ONEPOSE_LIB has only the fp32 entry point)
+            call = (lib.onepose_match_dt if hasattr(lib, "onepose_match_dt")
+                    else lambda *a: lib.onepose_match_ex(*a[:7], *a[8:]))
+            rc = call(
+                w.data_ptr(), d2.data_ptr(), s2, d3.data_ptr(), s3, db.data_ptr(), sl, dt,
                 B, n1, n3, nleaf, float(_hp(self.hparams, "scale_factor")),
                 float(_hp(self.hparams, "match_threshold")), self.precision,
                 m0.data_ptr(), m1.data_ptr(), ms0.data_ptr(), ms1.data_ptr(), conf.data_ptr(),

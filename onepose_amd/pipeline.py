@@ -77,7 +77,11 @@ class FramePipeline:
                  device, scale: float = 1000.0, reprojection_error: float = 5.0,
                  iterations_count: int = 10000, confidence: float = 0.99, with_conf=False,
                  slots: int = 2, detector=None, image_hw=(512, 512), object_cache: bool = True,
-                 gat_tables: bool = True):
+                 gat_tables: bool = True, desc_dtype: str = "fp32"):
+        """desc_dtype "fp16": the object's descriptors / leaves and the query descriptors are held
+        in fp16 on the device (BASELINE config 5's "fp16 desc"); the kernels convert them as they
+        load them, which is the reference's .float() upcast (GATs_SuperGlue.py:219-221), so the
+        results are those of the fp32 pipeline on the fp16-rounded inputs, bit for bit."""
         self.lib = _lib.load()
         self.device = torch.device(device)
         self.B, self.n1 = int(batch), int(n1)
@@ -89,17 +93,26 @@ class FramePipeline:
         self.threshold = float(hp["match_threshold"] if isinstance(hp, dict) else hp.match_threshold)
         dev = self.device
         f32 = dict(dtype=torch.float32, device=dev)
+        if desc_dtype not in ("fp32", "fp16"):
+            raise ValueError(f"desc_dtype {desc_dtype!r}")
+        self.desc_dt = _lib.DT_F16 if desc_dtype == "fp16" else _lib.DT_F32
+        fdesc = dict(dtype=torch.float16 if desc_dtype == "fp16" else torch.float32, device=dev)
+        if desc_dtype == "fp16" and (not object_cache or detector is not None):
+            raise ValueError("fp16 descriptors: the object-cached pipeline without a detector")
         self.weights = matcher.packed_weights(dev)
         self.kp3 = torch.as_tensor(np.asarray(keypoints3d), **f32).reshape(-1, 3).contiguous()
-        self.desc3d = torch.as_tensor(np.asarray(desc3d), **f32).reshape(256, -1).contiguous()
+        def as_desc(x):
+            x = x if torch.is_tensor(x) else torch.as_tensor(np.asarray(x))
+            return x.to(**fdesc).reshape(256, -1).contiguous()
+        self.desc3d = as_desc(desc3d)
         self.n3 = self.desc3d.shape[1]
-        self.leaves = torch.as_tensor(np.asarray(leaves), **f32).reshape(256, -1).contiguous()
+        self.leaves = as_desc(leaves)
         self.L = self.leaves.shape[1] // self.n3
         assert self.L * self.n3 == self.leaves.shape[1] and self.kp3.shape[0] == self.n3
         # the object's leaves, transposed once to the point-major layout the GAT layers read
         self.leaves_pm = torch.empty(self.n3 * self.L * 256, **f32)
-        _lib.check(self.lib.onepose_prepare_leaves(
-            self.leaves.data_ptr(), 0, 1, self.n3, self.L, self.leaves_pm.data_ptr(),
+        _lib.check(self.lib.onepose_prepare_leaves_dt(
+            self.leaves.data_ptr(), self.desc_dt, 0, 1, self.n3, self.L, self.leaves_pm.data_ptr(),
             _lib.stream_ptr(dev)), "prepare_leaves")
         # the object-only prefix of the forward (GAT 0 + the 3D half of self-attention 1) and,
         # with gat_tables, the GAT prefix tables, computed once: every frame starts from it
@@ -113,8 +126,9 @@ class FramePipeline:
             self.object_cache = torch.empty(nbytes // 4, **f32)
             wsb = self.lib.onepose_object_prepare_workspace_bytes(self.n3, self.L)
             ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
-            _lib.check(self.lib.onepose_object_prepare(
-                self.weights.data_ptr(), self.desc3d.data_ptr(), self.leaves_pm.data_ptr(),
+            _lib.check(self.lib.onepose_object_prepare_dt(
+                self.weights.data_ptr(), self.desc3d.data_ptr(), self.desc_dt,
+                self.leaves_pm.data_ptr(),
                 self.n3, self.L, self.precision, self.object_flags, self.object_cache.data_ptr(),
                 ws.data_ptr(), wsb,
                 _lib.stream_ptr(dev)), "object_prepare")
@@ -122,7 +136,7 @@ class FramePipeline:
             del ws
         B = self.B
         # per-frame inputs (filled by the caller)
-        self.desc2d = torch.zeros(B, 256, n1, **f32)
+        self.desc2d = torch.zeros(B, 256, n1, **fdesc)
         self.kpts2d = torch.zeros(B, n1, 2, **f32)
         self.K = torch.zeros(B, 3, 3, dtype=torch.float64, device=dev)
         self.pose_gt = torch.zeros(B, 3, 4, dtype=torch.float64, device=dev)
@@ -155,7 +169,7 @@ class FramePipeline:
 
     def set_frames(self, desc2d, kpts2d, K, pose_gt):
         """Copy B frames' inputs into the static buffers (host or device arrays)."""
-        self.desc2d.copy_(torch.as_tensor(np.asarray(desc2d), dtype=torch.float32))
+        self.desc2d.copy_(torch.as_tensor(np.asarray(desc2d)).to(self.desc2d.dtype))
         self.kpts2d.copy_(torch.as_tensor(np.asarray(kpts2d), dtype=torch.float32))
         self.K.copy_(torch.as_tensor(np.asarray(K), dtype=torch.float64).expand_as(self.K))
         self.pose_gt.copy_(torch.as_tensor(np.asarray(pose_gt), dtype=torch.float64)[..., :3, :]
@@ -176,7 +190,7 @@ class FramePipeline:
             return torch.as_tensor(np.asarray(x) if not torch.is_tensor(x) else x,
                                    dtype=dt).reshape(shape).to(dev).contiguous()
         f64 = torch.float64
-        self.bank = {"desc2d": dev_t(desc2d, torch.float32, (F, B, 256, self.n1)),
+        self.bank = {"desc2d": dev_t(desc2d, self.desc2d.dtype, (F, B, 256, self.n1)),
                      "kpts2d": dev_t(kpts2d, torch.float32, (F, B, self.n1, 2)),
                      "K": dev_t(K, f64, (F, B, 3, 3)),
                      "pose_gt": dev_t(np.asarray(pose_gt)[..., :3, :] if not torch.is_tensor(pose_gt)
@@ -232,8 +246,8 @@ class FramePipeline:
         s = _lib.stream_ptr(self.device)
         desc2d, _ = self._inputs(o, frame)
         if self.object_cache is not None:
-            _lib.check(self.lib.onepose_match_cached(
-                self.weights.data_ptr(), desc2d.data_ptr(), 256 * self.n1,
+            _lib.check(self.lib.onepose_match_cached_dt(
+                self.weights.data_ptr(), desc2d.data_ptr(), self.desc_dt, 256 * self.n1,
                 self.object_cache.data_ptr(), self.leaves_pm.data_ptr(), 0,
                 self.B, self.n1, self.n3, self.L, self.scale_factor, self.threshold,
                 self.precision, self.object_flags, o.matches0.data_ptr(), o.matches1.data_ptr(),

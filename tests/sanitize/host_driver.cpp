@@ -18,7 +18,7 @@ float frand() {
 }  // namespace
 
 int main() {
-  if (onepose_abi_version() != 3) return 1;
+  if (onepose_abi_version() != 4) return 1;
   // matcher packer
   {
     const int n = onepose_matcher_num_tensors();
@@ -67,6 +67,10 @@ int main() {
     acc += onepose_leaves_prepared_bytes(B, n3, L);
     acc += onepose_object_cache_bytes(n3, L, 0) + onepose_object_cache_bytes(n3, L, ONEPOSE_OBJ_GAT_TABLES);
     acc += onepose_object_prepare_workspace_bytes(n3, L);
+    for (int prec = 0; prec <= 3; ++prec) {   // (3: refused, 0 bytes)
+      acc += onepose_match_workspace_bytes_ex(B, n1, n3, L, 1, prec);
+      acc += onepose_object_cache_bytes_ex(n3, L, ONEPOSE_OBJ_GAT_TABLES, prec);
+    }
     for (int world = 1; world <= 3; ++world) {
       acc += onepose_match_sharded_xchg_bytes(B, n1, n3, world);
       for (int r = 0; r < world; ++r) acc += onepose_match_sharded_workspace_bytes(B, n1, n3, world, r, L, 1);

@@ -34,9 +34,13 @@ def batch_inputs(n1, n3, L, seed, B):
 class CachedMatcher:
     """onepose_object_prepare once + onepose_match_cached per call (the FramePipeline path)."""
 
-    def __init__(self, sd, data, device, flags=_lib.OBJ_GAT_TABLES, precision=0):
+    def __init__(self, sd, data, device, flags=_lib.OBJ_GAT_TABLES, precision=0, fp16=False):
+        """fp16: the object's descriptors and leaves and every query's descriptors go to the
+        library as fp16 (the _dt entry points)."""
         self.lib = lib = _lib.load()
         self.device, self.flags, self.precision = device, flags, precision
+        self.dt = _lib.DT_F16 if fp16 else _lib.DT_F32
+        ddt = np.float16 if fp16 else np.float32
         m = matcher.from_state_dict(sd)
         self.sf = float(m.hparams["scale_factor"])
         self.thr = float(m.hparams["match_threshold"])
@@ -44,19 +48,26 @@ class CachedMatcher:
         f32 = dict(dtype=torch.float32, device=device)
         self.n3 = n3 = data["descriptors3d_db"].shape[2]
         self.L = L = data["descriptors2d_db"].shape[2] // n3
-        d3 = torch.from_numpy(data["descriptors3d_db"][0]).to(device).contiguous()
-        lv = torch.from_numpy(data["descriptors2d_db"][0]).to(device).contiguous()
+        d3 = torch.from_numpy(data["descriptors3d_db"][0].astype(ddt)).to(device).contiguous()
+        lv = torch.from_numpy(data["descriptors2d_db"][0].astype(ddt)).to(device).contiguous()
         s = _lib.stream_ptr(device)
         self.pm = torch.empty(lib.onepose_leaves_prepared_bytes(1, n3, L) // 4, **f32)
-        _lib.check(lib.onepose_prepare_leaves(lv.data_ptr(), 0, 1, n3, L, self.pm.data_ptr(), s),
-                   "leaves")
-        self.cache = torch.empty(lib.onepose_object_cache_bytes(n3, L, flags) // 4, **f32)
+        _lib.check(lib.onepose_prepare_leaves_dt(lv.data_ptr(), self.dt, 0, 1, n3, L,
+                                                 self.pm.data_ptr(), s), "leaves")
+        self.cache = torch.empty(
+            _lib.object_cache_bytes(lib, n3, L, flags, precision) // 4, **f32)
         wsb = lib.onepose_object_prepare_workspace_bytes(n3, L)
         ws = torch.empty(wsb, dtype=torch.uint8, device=device)
-        _lib.check(lib.onepose_object_prepare(self.w.data_ptr(), d3.data_ptr(), self.pm.data_ptr(),
-                                              n3, L, precision, flags, self.cache.data_ptr(),
-                                              ws.data_ptr(), wsb, s), "prepare")
+        _lib.check(lib.onepose_object_prepare_dt(self.w.data_ptr(), d3.data_ptr(), self.dt,
+                                                 self.pm.data_ptr(), n3, L, precision, flags,
+                                                 self.cache.data_ptr(), ws.data_ptr(), wsb, s),
+                   "prepare")
         torch.cuda.synchronize()
+
+    def __del__(self):   # drop the library's record of the cache with its memory
+        cache = self.__dict__.get("cache")
+        if cache is not None:
+            self.lib.onepose_object_release(cache.data_ptr())
 
     def __call__(self, d2, with_conf=False):
         """d2 [B, 256, n1] numpy -> per-frame pred dicts (and conf [B, n1, n3] if asked)."""
@@ -64,15 +75,17 @@ class CachedMatcher:
         B, _, n1 = d2.shape
         n3 = self.n3
         f32 = dict(dtype=torch.float32, device=dev)
-        t = torch.from_numpy(np.ascontiguousarray(d2)).to(dev)
+        t = torch.from_numpy(np.ascontiguousarray(
+            d2.astype(np.float16 if self.dt == _lib.DT_F16 else np.float32))).to(dev)
         o = dict(m0=torch.empty(B, n1, dtype=torch.int64, device=dev),
                  m1=torch.empty(B, n3, dtype=torch.int64, device=dev),
                  s0=torch.empty(B, n1, **f32), s1=torch.empty(B, n3, **f32))
         conf = torch.empty(B, n1, n3, **f32) if with_conf else None
-        wsb = lib.onepose_match_workspace_bytes(B, n1, n3, self.L, int(with_conf))
+        wsb = _lib.workspace_bytes(lib, B, n1, n3, self.L, with_conf, self.precision)
         ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
-        _lib.check(lib.onepose_match_cached(
-            self.w.data_ptr(), t.data_ptr(), 256 * n1, self.cache.data_ptr(), self.pm.data_ptr(),
+        _lib.check(lib.onepose_match_cached_dt(
+            self.w.data_ptr(), t.data_ptr(), self.dt, 256 * n1, self.cache.data_ptr(),
+            self.pm.data_ptr(),
             0, B, n1, n3, self.L, self.sf, self.thr, self.precision, self.flags,
             o["m0"].data_ptr(), o["m1"].data_ptr(), o["s0"].data_ptr(), o["s1"].data_ptr(),
             _lib.ptr(conf), ws.data_ptr(), wsb, _lib.stream_ptr(dev)), "match_cached")
@@ -157,3 +170,62 @@ def test_config5_2048x8192_vs_oracle(device):
     assert dconf <= 2e-3
     assert (m16[conf_rows] == om0[conf_rows]).all()
     assert agree >= 0.99
+
+
+def _fp16_rounded(data):
+    """The matcher inputs with every descriptor rounded to fp16, as fp16 and upcast to fp32."""
+    keys = ("descriptors2d_query", "descriptors3d_db", "descriptors2d_db")
+    h = {k: (v.astype(np.float16) if k in keys else v) for k, v in data.items()}
+    up = {k: (v.astype(np.float32) if k in keys else v) for k, v in h.items()}
+    return h, up
+
+
+@pytest.mark.parametrize("precision", [0, 1, 2])
+def test_fp16_descriptors_equal_the_upcast_fp32_path(precision, device):
+    """fp16 descriptors (BASELINE config 5's "fp16 desc"), converted by the kernels as they load
+    them, give the bits of the fp32 path on the upcast inputs (GATs_SuperGlue.py:219-221 .float()):
+    the cached path (object prepare + match_cached) and the module forward, every precision."""
+    sd = synthetic.make_state_dict(0)
+    data, _, _ = synthetic.make_matcher_inputs(300, 1000, 8, seed=4, batch=2)
+    h, up = _fp16_rounded(data)
+    p16, c16 = CachedMatcher(sd, data, device, precision=precision, fp16=True)(
+        data["descriptors2d_query"], with_conf=True)
+    p32, c32 = CachedMatcher(sd, up, device, precision=precision)(
+        up["descriptors2d_query"], with_conf=True)
+    np.testing.assert_array_equal(c16, c32)
+    for a, b in zip(p16, p32):
+        for k in a:
+            np.testing.assert_array_equal(a[k], b[k], err_msg=k)
+    prec = {0: "fp32", 1: "bf16", 2: "fp32_split"}[precision]
+    m = matcher.from_state_dict(sd, {**synthetic.DEFAULT_HPARAMS, "attention_precision": prec})
+    m = m.to(device)
+    with torch.no_grad():
+        th = {k: torch.from_numpy(v).to(device) for k, v in h.items()}
+        tu = {k: torch.from_numpy(v).to(device) for k, v in up.items()}
+        assert th["descriptors2d_db"].dtype == torch.float16
+        ph, ch = m(th)
+        pu, cu = m(tu)
+    np.testing.assert_array_equal(ch.cpu().numpy(), cu.cpu().numpy())
+    for k in ph:
+        np.testing.assert_array_equal(ph[k].cpu().numpy(), pu[k].cpu().numpy(), err_msg=k)
+
+
+def test_config5_fp16_descriptors_vs_oracle(device):
+    """BASELINE config 5 as named: 2048 x 8192, fp16 descriptors.  fp32 attention: indices
+    exact and conf within 2e-5 against the numpy oracle on the upcast inputs; MFMA-bf16
+    attention: bit-identical to the bf16 mode on the upcast fp32 inputs."""
+    from oracle import matcher_np as M
+    n1, n3, L, seed = 2048, 8192, 8, 11
+    sd = synthetic.make_state_dict(0)
+    data, _, _ = synthetic.make_matcher_inputs(n1, n3, L, seed=seed, batch=1)
+    _, up = _fp16_rounded(data)
+    opred, oconf = M.forward(sd, up)
+    p16, c16 = CachedMatcher(sd, data, device, precision=0, fp16=True)(
+        data["descriptors2d_query"], with_conf=True)
+    np.testing.assert_allclose(c16[0], oconf[0], rtol=0, atol=ATOL)
+    assert_pred_equal(p16[0], opred, "config 5 fp16 desc, fp32 vs oracle")
+    b16, bc16 = CachedMatcher(sd, data, device, precision=1, fp16=True)(
+        data["descriptors2d_query"], with_conf=True)
+    b32, bc32 = CachedMatcher(sd, up, device, precision=1)(up["descriptors2d_query"], with_conf=True)
+    np.testing.assert_array_equal(bc16, bc32)
+    np.testing.assert_array_equal(b16[0]["matches0"], b32[0]["matches0"])

@@ -1,0 +1,161 @@
+"""Throughput of the drop-in entry (not the headline): ``onepose_amd.inference.inference(cfg)``
+over an on-disk synthetic sequence, exactly the reference's per-frame call sequence
+(inference.py:98-198: image read -> extractor -> .cpu().numpy() -> pack_data -> matcher ->
+.cpu() -> ransac_PnP -> Evaluator), with the real checkpoint loaders (LitModelGATsSPG from a
+.ckpt, SuperPoint from a .pth).
+
+    python tools/entry_bench.py --frames 64 --n3 4096 --out profiles/r05/entry/entry.json
+
+Two runs:
+  "superpoint": the real extractor (random weights: its descriptors never match the synthetic
+                object, so the pose stage runs on ~0 correspondences; the frame rate is what
+                counts here);
+  "detections": the extractor replaced by the synthetic frames' own detections (keyed by the
+                image's first pixel), so matcher + RANSAC-EPnP + cm/deg run on real
+                correspondences (ragged n1 = 1024 - (37 i mod 97)).
+Then one more "detections" pass with every stage bracketed by torch.cuda.synchronize to say
+where the time goes (host round trips and copies vs the library's kernels)."""
+import argparse
+import json
+import os
+import sys
+import tempfile
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, "tests"))
+
+import numpy as np
+import torch
+
+
+def build_sequence(tmp, n3, frames, size):
+    from PIL import Image
+    from onepose_amd import data_utils as DU
+    from onepose_amd import inference as I
+    from onepose_amd import synthetic as S
+    obj = S.make_object(n3, seed=8)
+    root, sfm = os.path.join(tmp, "root"), os.path.join(tmp, "sfm", "obj")
+    seq = os.path.join(root, "seq-1")
+    for d in ("color", "intrin_ba", "poses_ba"):
+        os.makedirs(os.path.join(seq, d))
+    _, paths = I.default_paths(seq, sfm)
+    DU.save_object_annotations(paths["anno_dir"], obj.keypoints3d, obj.clt_descriptors,
+                               obj.clt_scores, obj.idxs)
+    fr = [S.make_frame(obj, 1024 - (37 * i) % 97, seed=400 + i) for i in range(frames)]
+    for i, f in enumerate(fr):
+        im = (S.superpoint_image(size, size, 20 + i) * 255).round().astype(np.uint8)
+        im[0, 0] = i   # the frame's index, for the "detections" extractor
+        Image.fromarray(im, mode="L").save(os.path.join(seq, "color", f"{i:04d}.png"))
+        np.savetxt(os.path.join(seq, "intrin_ba", f"{i:04d}.txt"), f.K)
+        np.savetxt(os.path.join(seq, "poses_ba", f"{i:04d}.txt"),
+                   np.concatenate([f.pose_gt, [[0, 0, 0, 1]]]))
+    ckpt = {"state_dict": {"matcher." + k: torch.from_numpy(v)
+                           for k, v in S.make_state_dict(0).items()},
+            "hyper_parameters": dict(S.DEFAULT_HPARAMS)}
+    torch.save(ckpt, os.path.join(tmp, "GATsSPG.ckpt"))
+    torch.save({k: torch.from_numpy(v) for k, v in S.superpoint_state_dict(0).items()},
+               os.path.join(tmp, "superpoint_v1.pth"))
+    from types import SimpleNamespace as N
+    cfg = N(type="inference", num_leaf=8, object_detect_mode="GT_box", save_wis3d=False,
+            model=N(onepose_model_path=os.path.join(tmp, "GATsSPG.ckpt"),
+                    extractor_model_path=os.path.join(tmp, "superpoint_v1.pth")),
+            network=N(detection="superpoint", matching="superglue"),
+            input=N(data_dirs=f"{root} seq-1", sfm_model_dirs=sfm),
+            output=N(eval_dir=os.path.join(tmp, "eval")))
+    return cfg, fr
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--frames", type=int, default=64)
+    ap.add_argument("--n3", type=int, default=4096)
+    ap.add_argument("--size", type=int, default=512)
+    ap.add_argument("--out", default="")
+    a = ap.parse_args()
+    from onepose_amd import inference as I
+    res = {"what": "inference(cfg) over an on-disk sequence: the reference's per-frame call "
+                   "sequence (host round trips, eager launches, uncached matcher per frame)",
+           "frames": a.frames, "n3": a.n3, "image": [a.size, a.size],
+           "n1": "1024 - (37 i mod 97), ragged"}
+    with tempfile.TemporaryDirectory() as tmp:
+        cfg, fr = build_sequence(tmp, a.n3, a.frames, a.size)
+        real_loader = I.load_extractor_model
+
+        def detections_loader(cfg_, model_path):
+            real_loader(cfg_, model_path)   # the real weights file is still read
+
+            def extract(img):
+                f = fr[int(round(float(img.flatten()[0]) * 255))]
+                return {"keypoints": [torch.from_numpy(f.keypoints2d).cuda()],
+                        "descriptors": [torch.from_numpy(f.descriptors2d).cuda()],
+                        "scores": [torch.ones(len(f.keypoints2d), device="cuda")]}
+            return extract
+
+        # warm-up: one pass loads every kernel's code object
+        I.load_extractor_model = detections_loader
+        I.inference(cfg)
+        for mode in ("superpoint", "detections"):
+            I.load_extractor_model = real_loader if mode == "superpoint" else detections_loader
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            out = I.inference(cfg)
+            torch.cuda.synchronize()
+            dt = time.perf_counter() - t0
+            summ = list(out.values())[0]
+            res[mode] = {"seconds": round(dt, 3), "frames_per_s": round(a.frames / dt, 2),
+                         "ms_per_frame": round(dt / a.frames * 1e3, 3), "cm_deg": summ,
+                         "includes": "model + object loading once per sequence (as the "
+                                     "reference's inference_core does)"}
+            print(mode, res[mode], flush=True)
+
+        # where the time goes: the same "detections" loop with synchronised stage brackets
+        times = {}
+
+        def timed(name, fn):
+            def w(*args, **kw):
+                torch.cuda.synchronize()
+                t = time.perf_counter()
+                r = fn(*args, **kw)
+                torch.cuda.synchronize()
+                times[name] = times.get(name, 0.0) + time.perf_counter() - t
+                return r
+            return w
+        from onepose_amd import pose
+        from onepose_amd.matcher import GATsSuperGlue
+        saved = (I.load_model, I.load_object, I.NormalizedDataset.__getitem__, I.pack_data,
+                 GATsSuperGlue._run, pose.ransac_PnP, pose.Evaluator.evaluate)
+        I.load_extractor_model = detections_loader
+        I.load_model = timed("load_model (ckpt + SuperPoint weights, once)", I.load_model)
+        I.load_object = timed("load_object (annotations, padding, leaves; once)", I.load_object)
+        I.NormalizedDataset.__getitem__ = timed("image read (PIL, /255)",
+                                                I.NormalizedDataset.__getitem__)
+        I.pack_data = timed("pack_data (host tensors -> device)", I.pack_data)
+        GATsSuperGlue._run = timed("matcher kernels (onepose_match_dt, incl. leaves transpose "
+                                   "and the uncached object prefix)", GATsSuperGlue._run)
+        pose.ransac_PnP = timed("ransac_PnP (H2D, RANSAC-EPnP + refit kernels, D2H)",
+                                pose.ransac_PnP)
+        pose.Evaluator.evaluate = timed("Evaluator", pose.Evaluator.evaluate)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        I.inference(cfg)
+        torch.cuda.synchronize()
+        tot = time.perf_counter() - t0
+        (I.load_model, I.load_object, I.NormalizedDataset.__getitem__, I.pack_data,
+         GATsSuperGlue._run, pose.ransac_PnP, pose.Evaluator.evaluate) = saved
+        I.load_extractor_model = real_loader
+        res["breakdown_ms_per_frame"] = {k: round(v / a.frames * 1e3, 3) for k, v in times.items()}
+        res["breakdown_ms_per_frame"]["total (synchronised pass)"] = round(tot / a.frames * 1e3, 3)
+        res["breakdown_ms_per_frame"]["rest (extractor lookup, .cpu() of matches / 3D points, "
+                                      "masking, Python)"] = round(
+            (tot - sum(times.values())) / a.frames * 1e3, 3)
+    print(json.dumps(res))
+    if a.out:
+        os.makedirs(os.path.dirname(a.out), exist_ok=True)
+        with open(a.out, "w") as f:
+            json.dump(res, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
