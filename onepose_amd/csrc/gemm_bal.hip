@@ -28,12 +28,15 @@ namespace onepose {
 namespace {
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));
+#define ONEPOSE_BAL_SCHED_BARRIER() __builtin_amdgcn_sched_barrier(0)
 
-constexpr int kBalS = 6;          // strips per workgroup, at most (host-checked)
+constexpr int kBalS = 5;          // strips per workgroup, at most (host-checked)
 constexpr int kBalNT = 512;       // 8 waves, two per SIMD
 constexpr int kBalRG = 2;         // 64-row M-tiles (row groups) per workgroup, at most
 constexpr int kBalRowF = 32;      // floats per LDS row: one 32-deep stage, no padding
-constexpr int kBalARows = kBalRG * 64, kBalRows = kBalARows + kBalS * 32;
+// (W rows for an even number of strips: the last W slot of an odd strip count writes a copy of
+// its last strip into the next strip's rows)
+constexpr int kBalARows = kBalRG * 64, kBalRows = kBalARows + (kBalS + 1) / 2 * 2 * 32;
 constexpr int kBalStage = kBalRows * kBalRowF;   // 10240 floats = 40 KB per stage buffer
 constexpr int kBalTP = 36;        // epilogue tile pitch: 32 columns + 4
 constexpr int kBalNS = 16;        // 32-column strips of N = 512
@@ -75,11 +78,11 @@ __device__ __forceinline__ void bal_body(const GemmArgs& args, int64_t i0, int64
   int s_rg[NS], s_cs[NS], s_k0[NS], s_q[NS], s_b[NS], s_mt[NS];
 #pragma unroll
   for (int s = 0; s < NS; ++s) {
-    const int64_t i = i0 + s;
-    const int q = i >= S0 ? 1 : 0;
-    const int64_t j = i - (q ? S0 : 0);
+    const int i = (int)i0 + s;   // (strip counts are far below 2^31: host-checked grid)
+    const int q = i >= (int)S0 ? 1 : 0;
+    const int j = i - (q ? (int)S0 : 0);
     const int per = PF(q, mtiles) * kBalNS;
-    const int b = (int)(j / per), r = (int)(j - (int64_t)b * per);
+    const int b = j / per, r = j - b * per;
     s_q[s] = q;
     s_b[s] = b;
     s_mt[s] = r / kBalNS;
@@ -249,47 +252,86 @@ __device__ __forceinline__ void bal_body(const GemmArgs& args, int64_t i0, int64
         acc_h[s][v] = 0.f;
       }
   };
-  // one stage's MFMAs from `buf` into tg (x range: the strips not from acc0)
-  auto mfmas = [&](const float* buf, floatx4 (&tg)[NS], bool xr) __attribute__((always_inline)) {
+  // fragments of one half stage (k groups 2h, 2h + 1) of every strip, and its MFMAs: part 0 the
+  // first k group (.x, .y: MFMA pair a, b), part 1 the second (.z, .w); x range: the strips
+  // not from acc0.  Per accumulator the k order is the 32x32x2 chain's.
+  // (A fragments once per row group -- a strip takes its row group's by a select -- W per strip)
+  struct Frag {
+    float4 a[kBalRG], w[NS];
+  };
+  auto read_half = [&](const float* buf, int h, Frag& F) __attribute__((always_inline)) {
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      float4 a[NS], w[NS];
+    for (int rg = 0; rg < kBalRG; ++rg)
+      F.a[rg] = *reinterpret_cast<const float4*>(buf + rg * 64 * kBalRowF + (h ? fa1 : fa0));
 #pragma unroll
-      for (int s = 0; s < NS; ++s) {
-        a[s] = *reinterpret_cast<const float4*>(buf + s_rg[s] * 64 * kBalRowF + (h ? fa1 : fa0));
-        w[s] = *reinterpret_cast<const float4*>(buf + s * 32 * kBalRowF + (h ? fw1 : fw0));
+    for (int s = 0; s < NS; ++s)
+      F.w[s] = *reinterpret_cast<const float4*>(buf + s * 32 * kBalRowF + (h ? fw1 : fw0));
+  };
+  auto mfma_part = [&](const Frag& F, floatx4 (&tg)[NS], bool xr, int part)
+      __attribute__((always_inline)) {
+#ifdef BAL_PROBE_NOMFMA
+    return;
+#endif
+    // (the pair's two MFMAs of a strip are dependent: issue the first of every strip, then the
+    // second, so consecutive MFMAs are independent)
+#pragma unroll
+    for (int s = 0; s < NS; ++s)
+      if (!MIX || !xr || s_k0[s] == 0) {
+        const float4 a = s_rg[s] ? F.a[1] : F.a[0];
+        tg[s] = __builtin_amdgcn_mfma_f32_16x16x4f32(part ? a.z : a.x, part ? F.w[s].z : F.w[s].x,
+                                                      tg[s], 0, 0, 0);
       }
 #pragma unroll
-      for (int s = 0; s < NS; ++s)
-        if (!MIX || !xr || s_k0[s] == 0) {
-          tg[s] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s].x, w[s].x, tg[s], 0, 0, 0);
-          tg[s] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s].y, w[s].y, tg[s], 0, 0, 0);
-        }
-#pragma unroll
-      for (int s = 0; s < NS; ++s)
-        if (!MIX || !xr || s_k0[s] == 0) {
-          tg[s] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s].z, w[s].z, tg[s], 0, 0, 0);
-          tg[s] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s].w, w[s].w, tg[s], 0, 0, 0);
-        }
-    }
+    for (int s = 0; s < NS; ++s)
+      if (!MIX || !xr || s_k0[s] == 0) {
+        const float4 a = s_rg[s] ? F.a[1] : F.a[0];
+        tg[s] = __builtin_amdgcn_mfma_f32_16x16x4f32(part ? a.w : a.y, part ? F.w[s].w : F.w[s].y,
+                                                      tg[s], 0, 0, 0);
+      }
   };
 
-  // ---- main loop: stage kt in LDS buffer kt & 1; stage kt + 2 loads under its MFMAs (register
-  // set kt & 1), stage kt + 1 (set (kt + 1) & 1) goes to LDS at its end ----
+  // ---- main loop, software-pipelined across the stage barrier: stage kt is in LDS buffer
+  // kt & 1 and its first half's fragments in F0 when step kt starts; then
+  //   global loads of stage kt + 2 | read half 1 -> F1 | MFMAs of F0 | store stage kt + 1 to
+  //   the other buffer | MFMAs of F1's first group | barrier | read stage kt + 1's half 0 -> F0
+  //   | MFMAs of F1's second group (hiding that read)
+  // so the matrix pipe is fed across the store / barrier / read phases.  Stage kt + 2's global
+  // loads (register set kt & 1) have two stages to land. ----
   StampTick tk = stamp_start(args.stamp, sl);
+#ifdef BAL_PROBE_SETUPONLY
+  if (fa0 == -1 && acc[0][0] == 1.f) PF(0, Y)[threadIdx.x] = 0.f;
+  return;
+#endif
   load(kt0, r0);
   load(kt0 + 1, r1);
   store(lds + (kt0 & 1) * kBalStage, r0);
   __syncthreads();   // (also publishes zks)
+  Frag F0, F1;
+  read_half(lds + (kt0 & 1) * kBalStage, 0, F0);
   auto step = [&](int kt, Regs& cur, Regs& nxt, floatx4 (&tg)[NS]) __attribute__((always_inline)) {
+    // (kt < kBalXs: the x range into acc; kt >= kBalXs: one phi(q) head per two stages into acc_h)
     const float* buf = lds + (kt & 1) * kBalStage;
+    float* nbuf = lds + ((kt + 1) & 1) * kBalStage;
+    const bool xr = kt < kBalXs, more = kt + 1 < kBalStages;
+    const bool head_end = !xr && ((kt - kBalXs) & 1) == 1;
+#ifndef BAL_PROBE_NOLOAD
     if (kt + 2 < kBalStages) load(kt + 2, cur);
-    if (kt >= kBalXs) zdot(buf, kt);
-    mfmas(buf, tg, kt < kBalXs);
-    const bool head_end = kt >= kBalXs && ((kt - kBalXs) & 1) == 1;
+#endif
+    read_half(buf, 1, F1);
+    if (!xr) zdot(buf, kt);
+    mfma_part(F0, tg, xr, 0);
+    mfma_part(F0, tg, xr, 1);
+    ONEPOSE_BAL_SCHED_BARRIER();
+#ifndef BAL_PROBE_NOSTORE
+    if (more) store(nbuf, nxt);
+#endif
+    ONEPOSE_BAL_SCHED_BARRIER();
+    mfma_part(F1, tg, xr, 0);
     if (head_end) zfinal(((kt - kBalXs) >> 1) & 1);
-    if (kt + 1 < kBalStages) store(lds + ((kt + 1) & 1) * kBalStage, nxt);
     __syncthreads();
+    if (more) read_half(nbuf, 0, F0);
+    ONEPOSE_BAL_SCHED_BARRIER();
+    mfma_part(F1, tg, xr, 1);
     if (head_end) fold(((kt - kBalXs) >> 1) & 1);   // every row's Z is in zrow now
   };
   for (int kt = kt0; kt < kBalXs; kt += 2) {   // kt0 is 0 or kBalXs: even
@@ -302,6 +344,10 @@ __device__ __forceinline__ void bal_body(const GemmArgs& args, int64_t i0, int64
     step(kt + 1, r1, r0, acc_h);
   }
   stamp_ticket(args.stamp, tk);
+#ifdef BAL_PROBE_NOEPI
+  if (acc[0][0] == 12345.f) PF(0, Y)[threadIdx.x] = acc[NS - 1][1] + acc_h[0][2];   // (keep acc)
+  return;
+#endif
 
   // ---- epilogue: y = acc + bias staged per strip [64][kBalTP] (invalid rows hold 0) ----
   float* tile = lds;
@@ -319,6 +365,9 @@ __device__ __forceinline__ void bal_body(const GemmArgs& args, int64_t i0, int64
     }
   }
   __syncthreads();
+#ifdef BAL_PROBE_EPI_TILE
+  return;
+#endif
 
   // InstanceNorm (mean, M2) partials of strip `wave`'s 32 columns over its M-tile: per 32-row
   // block the sums gemm.hip takes from a wave's registers (a lane's 16 rows in register order,
@@ -378,7 +427,11 @@ __device__ __forceinline__ void bal_body(const GemmArgs& args, int64_t i0, int64
       __hip_atomic_store(st_out + f_N, M2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's partial stores drained
+#ifdef BAL_PROBE_EPI_NOFIN
+    if (false) {
+#else
     if (lane == 0) {
+#endif
       const int G1 = stats_group_size(f_mtiles);
       const int ngroups = (f_mtiles + G1 - 1) / G1;
       unsigned* cb = f_cnt + (int64_t)f_b * PF(f_q, st_cnt_bs);
@@ -401,7 +454,11 @@ __device__ __forceinline__ void bal_body(const GemmArgs& args, int64_t i0, int64
 
   // two-level finalize (gemm.hip's, per 32-column block): the group's last M-tile merges the
   // group's partials, the last group merger the groups -> mean, rstd
+#ifdef BAL_PROBE_EPI_NOFIN
+  if (false) {
+#else
   if (ws < NS) {
+#endif
     const int G1 = stats_group_size(f_mtiles);
     const int ngroups = (f_mtiles + G1 - 1) / G1, g1 = f_mt / G1;
     const int gt0 = g1 * G1, gsz = min(G1, f_mtiles - gt0);
@@ -500,7 +557,7 @@ void gemm_mlp1_bal_kernel(GemmArgs args) {
     case 3: bal_body<3, MIX>(args, i0, S0, lds, sh, &sl); break;
     case 4: bal_body<4, MIX>(args, i0, S0, lds, sh, &sl); break;
     case 5: bal_body<5, MIX>(args, i0, S0, lds, sh, &sl); break;
-    default: bal_body<6, MIX>(args, i0, S0, lds, sh, &sl); break;
+    default: bal_body<5, MIX>(args, i0, S0, lds, sh, &sl); break;
   }
 }
 
