@@ -131,15 +131,23 @@ enum GemmTile {
                      //   the operand loads per FLOP of 64 x 64)
   TILE_32x256W8 = 8, // final projection + L2 normalisation (EPI_BIAS_L2): whole rows on 8 waves
                      //   of 32 x 32 (two per SIMD), 64-deep stages
+  TILE_256x128W8 = 9, // bf16 MLP conv 1 (STATS + HEADZ, DMA 2): 256 x 128 outputs on 8 waves of
+                      //   32 x 128, one workgroup per CU; a stage's W rows are fetched once per 256
+                      //   output rows instead of 64.  Its InstanceNorm partials, tickets and acc0
+                      //   are the 64 x 128 tile's (gemm_tile_stat_rows = 64): same workspace, same bits
 };
 // Output tile shape of each configuration, usable in constant expressions (the workspace
 // plan sizes per-tile partials and counters from these; tile_dims in gemm.hip agrees).
 constexpr int gemm_tile_bm(int t) {
   return (t == TILE_32x128 || t == TILE_32x64W2 || t == TILE_32x256W8) ? 32
-         : (t == TILE_128x128 || t == TILE_128x64W8) ? 128 : 64;
+         : (t == TILE_128x128 || t == TILE_128x64W8) ? 128
+         : t == TILE_256x128W8                       ? 256
+                                                     : 64;
 }
+// rows per EPI_STATS partial (and per acc0 tile): the tile's, or its stand-in tile's
+constexpr int gemm_tile_stat_rows(int t) { return t == TILE_256x128W8 ? 64 : gemm_tile_bm(t); }
 constexpr int gemm_tile_bn(int t) {
-  return (t == TILE_32x128 || t == TILE_64x128 || t == TILE_128x128) ? 128
+  return (t == TILE_32x128 || t == TILE_64x128 || t == TILE_128x128 || t == TILE_256x128W8) ? 128
          : t == TILE_64x32K2                                        ? 32
          : t == TILE_32x256W8                                       ? 256
                                                                     : 64;

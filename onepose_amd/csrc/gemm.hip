@@ -20,6 +20,7 @@
 
 #include <cstdlib>
 #include <cstring>
+#include <type_traits>
 
 // Pins the pipeline's phase order (the compiler's own schedule measured within +-2%,
 // DESIGN.md §3d).
@@ -64,10 +65,17 @@ struct FragT<PM_SPLIT3, KKW, FN> {   // hi / mid / lo pieces
 
 constexpr int kScoreGroup = 8;   // N-tiles per column group of the score grid
 
-template <int BM_, int BN_, int KS_, int NW_, int BKS_, int WPE_ = 3>
+constexpr int kDma3Bufs = 3;   // DMA-3 loop: LDS buffers (stages of loads in flight + 1)
+
+template <int BM_, int BN_, int KS_, int NW_, int BKS_, int WPE_ = 3, int SUB_ = BM_>
 struct Tile {
   static constexpr int BM = BM_, BN = BN_, KS = KS_, NW = NW_, BKS = BKS_;
   static constexpr int WPE = WPE_;              // amdgpu_waves_per_eu hint
+  // SUB < BM: the tile stands in for BM / SUB tiles of SUB rows -- its InstanceNorm partials,
+  // finalize tickets (EPI_STATS) and acc0 (PRO_HEADZ) are those of the SUB x BN tile, so the
+  // workspace layout and every result bit are the smaller tile's
+  static constexpr int SUB = SUB_;
+  static constexpr int NSUB = BM / SUB;
   static constexpr int NT = 64 * NW;            // threads
   static constexpr int WM = BM / 32;            // waves along M
   static constexpr int WN = NW / (WM * KS);     // waves along N
@@ -287,13 +295,18 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
   // (the A pieces must deal evenly over the waves: every wave then waits for its own stage)
   // (four and five buffers measured slower: config 5 1644 -> 1619 / 1499 frames/s, config 2
   // bf16 2906 -> 2901 / 2704; the loop is bound by the L2 -> LDS bytes)
+  // (a tile that stands in for several -- one workgroup per CU -- has no other workgroup to
+  // cover its DMA latency, and its staging tile is larger than five stages: four in flight)
   constexpr int NBUF =
-      (DMA == 2 && PM == PM_BF16 && (NPL * BM / (512 / T::BKS)) % T::NW == 0) ? 3 : 2;
+      DMA == 3 ? kDma3Bufs
+      : (DMA == 2 && PM == PM_BF16 && (NPL * BM / (512 / T::BKS)) % T::NW == 0)
+          ? (T::NSUB > 1 ? 5 : 3)
+          : 2;
   constexpr int LDS0 = NBUF * STAGE > BM * TP ? NBUF * STAGE : BM * TP;
   constexpr int LDSF = LDS0 > QKVL ? LDS0 : QKVL;
   __shared__ __attribute__((aligned(16))) float lds[LDSF];
   __shared__ float zrow[2 * BM];
-  __shared__ float part[(EPI == EPI_STATS) ? T::NT * 2 : 1];
+  __shared__ float part[(EPI == EPI_STATS) ? (T::NT > T::WM * BN ? T::NT : T::WM * BN) * 2 : 1];
 
   // XCD-aware tile order: blocks are dealt round-robin over the 8 XCDs, so hand each XCD a
   // contiguous run of logical tiles -- the N-tiles of one M-tile then share that XCD's L2.
@@ -341,7 +354,7 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
     c.wp1 = wp1 ? wp1 + b * F(wp1_bs) : c.wp0 + c.ksplit;
     c.wpl1 = wp1 ? F(wpl1) : c.wpl0;
   }
-  if constexpr (DMA == 2) {   // A planes (range 1: its own planes, or range 0's continuing)
+  if constexpr (DMA >= 2) {   // A planes (range 1: its own planes, or range 0's continuing)
     const uint16_t* ap1 = F(Ap1);
     c.ap0 = F(Ap) + b * F(ap_bs);
     c.apl0 = F(apl);
@@ -447,7 +460,15 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
   for (int j = 0; j < FN; ++j)
 #pragma unroll
     for (int i = 0; i < 16; ++i) acc_h[j][i] = 0.f;
-  float zp = 0.f;
+  // one running dot per 8-wide chunk: the head's Z is ((c0 + c1) + (c2 + c3)) over the four
+  // chunks of each 32-deep stage whatever the threads per row (TPR 4: one chunk per thread and
+  // a two-step butterfly; TPR 2: two chunks added, then one step)
+  constexpr int ZC = ZK >= 8 ? ZK / 8 : 1;   // (tiles without HEADZ: unused)
+  static_assert(PRO != PRO_HEADZ || (T::BKS == 32 ? ZK / 8 * TPR == 4 : TPR == 4),
+                "Z's chunk tree (32-deep stages: four chunks per row)");
+  float zp[ZC];
+#pragma unroll
+  for (int cc = 0; cc < ZC; ++cc) zp[cc] = 0.f;
   const int zr = t / TPR, zq = t % TPR;
   __shared__ float zks[(PRO == PRO_HEADZ) ? 256 : 1];   // sum phi(k) of the source
   if (PRO == PRO_HEADZ)
@@ -482,15 +503,19 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
         }
         const float4 k0 = *reinterpret_cast<const float4*>(kp);
         const float4 k1 = *reinterpret_cast<const float4*>(kp + 4);
-        zp = headz_dot8(zp, a0, a1, k0, k1);
+        zp[cc] = headz_dot8(zp[cc], a0, a1, k0, k1);
       }
     }
   };
   auto zfinal = [&](int par) __attribute__((always_inline)) {   // the head's partials are in zp
+    float z = zp[0];
+    if constexpr (ZC == 2) z = zp[0] + zp[1];
+    if constexpr (ZC == 4) z = (zp[0] + zp[1]) + (zp[2] + zp[3]);
 #pragma unroll
-    for (int o = 1; o < TPR; o <<= 1) zp += __shfl_xor(zp, o, 64);
-    if (zq == 0) zrow[par * BM + zr] = (1.0f / (zp + 1e-6f)) * zns;
-    zp = 0.f;
+    for (int o = 1; o < TPR; o <<= 1) z += __shfl_xor(z, o, 64);
+    if (zq == 0) zrow[par * BM + zr] = (1.0f / (z + 1e-6f)) * zns;
+#pragma unroll
+    for (int cc = 0; cc < ZC; ++cc) zp[cc] = 0.f;
   };
   auto fold = [&](int par) __attribute__((always_inline)) {     // acc += Z*Ns (per row) * acc_h
 #pragma unroll
@@ -507,14 +532,152 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
   // MFMA sequence); start from them at stage xs (even, so it sits in LDS buffer 0 like stage 0)
   const float* acc0 = PRO == PRO_HEADZ ? F(acc0) : nullptr;
   const int kt0 = acc0 != nullptr ? xs : 0;
-  if (acc0 != nullptr) {
+  if (acc0 != nullptr && T::NSUB == 1) {
     const float* a0p = acc0 + b * F(acc0_bs) + ((int64_t)(mt * ntiles + nt) * T::NW + wave) * FN * 1024 + lane;
 #pragma unroll
     for (int j = 0; j < FN; ++j)
 #pragma unroll
       for (int i = 0; i < 16; ++i) acc[j][i] = a0p[j * 1024 + i * 64];
+  } else if (acc0 != nullptr) {
+    // acc0 as the 64 x 128 four-wave tile stored it (2 x 2 waves of 32 x 64, FN 2): this wave's
+    // 32 rows are sub-tile wm / 2's wave row wm % 2, its 32-column block j that tile's wave
+    // column j / 2, accumulator j % 2 (sub-tiles past M hold nothing and are never stored)
+    static_assert(T::NSUB == 1 || (T::SUB == 64 && BN == 128 && T::WN == 1 && T::KS == 1),
+                  "acc0 of 64 x 128 sub-tiles");
+    const int st = mt * T::NSUB + wm / 2;
+    if (st * 64 < c.M) {
+      const float* a0p = acc0 + b * F(acc0_bs) + lane +
+                         ((int64_t)(st * ntiles + nt) * 4 + (wm % 2) * 2) * 2 * 1024;
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) acc[j][i] = a0p[((j / 2) * 2 + (j % 2)) * 1024 + i * 64];
+    }
   }
-  if constexpr (DMA >= 1) {
+  if constexpr (DMA == 3) {
+    // DMA 3 (bf16, W and A planes; the 256-row stand-in tile): only W goes through LDS, by
+    // global_load_lds, one 1-KB piece per wave and stage.  Each wave's A rows are its own (WN
+    // = 1), so A is loaded from its planes straight into the MFMA fragment registers (lane half
+    // h holds k = 16 kk + 8 h .. + 7 of row lane & 31: one 16-B load per fragment) -- no LDS
+    // stores or reads of A, and 1 DMA piece instead of 3 per wave and stage (a piece costs the
+    // issuing wave ~60-180 cycles).  LA = 4 stages of loads in flight, in a ring of A registers
+    // indexed at compile time (the loops are unrolled by LA).  Same images, fragments, MFMA
+    // order and Z arithmetic as the DMA-2 loop: the same bits.
+    static_assert(WPL && PM == PM_BF16 && T::WN == 1 && T::KS == 1 && T::BKS == 32, "DMA 3 tiling");
+    constexpr int LA = NBUF - 1;
+    constexpr int CPR = T::BKS / 8, RP = 64 / CPR;
+    constexpr int PIECES = T::BN / RP, PPW = PIECES / T::NW;
+    static_assert(T::BN % RP == 0 && PIECES % T::NW == 0, "W pieces");
+    constexpr int OPS = PPW + KKW;   // vm instructions per wave and stage
+    static_assert((LA - 1) * OPS <= 63, "vmcnt");
+    unsigned woff0[PPW], woff1[PPW];
+    int wdst[PPW];
+#pragma unroll
+    for (int i = 0; i < PPW; ++i) {
+      const int p = wave + T::NW * i;
+      const int rb = p * RP;
+      const int row = T::BM + rb + lane / CPR;
+      const int chunk = bsw<T>(row, (lane % CPR) * 8) - row * T::BKS;
+      const int o = min(n0 + rb + lane / CPR, c.N - 1);
+      woff0[i] = (unsigned)(((int64_t)o * c.ldw0 + chunk) * 2);
+      woff1[i] = (unsigned)(((int64_t)o * c.ldw1 + chunk) * 2);
+      wdst[i] = (T::BM + rb) * T::BKS * 2;
+    }
+    const int arow = min(m0 + wm * 32 + (lane & 31), c.M - 1);
+    const unsigned aoff0 = (unsigned)(((int64_t)arow * c.ldap0 + (lane >> 5) * 8) * 2);
+    const unsigned aoff1 = (unsigned)(((int64_t)arow * c.ldap1 + (lane >> 5) * 8) * 2);
+    bf16x8 ar[LA][KKW];
+    auto buf = [&](int st) __attribute__((always_inline)) { return lds + (st % NBUF) * STAGE; };
+    auto issue = [&](int st, auto slot) __attribute__((always_inline)) {
+      const int k0 = st * T::BKS;
+      const bool first = PRO != PRO_HEADZ || k0 < c.ksplit;
+      const char* wb = reinterpret_cast<const char*>(first ? c.wp0 + k0 : c.wp1 + (k0 - c.ksplit));
+      char* dst = reinterpret_cast<char*>(buf(st));
+#pragma unroll
+      for (int i = 0; i < PPW; ++i) dma16(wb + (first ? woff0[i] : woff1[i]), dst + wdst[i]);
+      const char* ab = reinterpret_cast<const char*>(first ? c.ap0 + k0 : c.ap1 + (k0 - c.ksplit));
+      const unsigned ao = first ? aoff0 : aoff1;
+#pragma unroll
+      for (int kk = 0; kk < KKW; ++kk)
+        ar[decltype(slot)::value][kk] = *reinterpret_cast<const bf16x8*>(ab + ao + kk * KG * 2);
+    };
+    auto raw_barrier = [&]() __attribute__((always_inline)) {
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    };
+    // Z from the fragments: lane half h holds chunk 2 kk + h of the stage (the TPR-4 thread zq's
+    // chunk), so ((c0 + c1) + (c2 + c3)) is (zp0 + its partner's) + (zp1 + its partner's)
+    float zr2[KKW];
+#pragma unroll
+    for (int kk = 0; kk < KKW; ++kk) zr2[kk] = 0.f;
+    auto zdot3 = [&](const Frag& f, int sg) __attribute__((always_inline)) {
+#pragma unroll
+      for (int kk = 0; kk < KKW; ++kk) {
+        const float* kp = zks + (sg * T::BKS - c.ksplit) + kk * KG + (lane >> 5) * 8;
+        const bf16x8 q = f.a[kk];
+        const float4 a0 = make_float4((float)q[0], (float)q[1], (float)q[2], (float)q[3]);
+        const float4 a1 = make_float4((float)q[4], (float)q[5], (float)q[6], (float)q[7]);
+        zr2[kk] = headz_dot8(zr2[kk], a0, a1, *reinterpret_cast<const float4*>(kp),
+                             *reinterpret_cast<const float4*>(kp + 4));
+      }
+    };
+    auto zfinal3 = [&](int par) __attribute__((always_inline)) {
+      static_assert(KKW == 2, "four chunks per stage");
+      const float z = (zr2[0] + __shfl_xor(zr2[0], 32, 64)) + (zr2[1] + __shfl_xor(zr2[1], 32, 64));
+      if (lane < 32) zrow[par * BM + wm * 32 + lane] = (1.0f / (z + 1e-6f)) * zns;
+      zr2[0] = zr2[1] = 0.f;
+    };
+    auto stage = [&](int kt, auto slot, floatx16 (&tg)[FN], bool zd, int zf)
+        __attribute__((always_inline)) {
+      const float* cur = buf(kt);
+      const __bf16* b16 = reinterpret_cast<const __bf16*>(cur);
+#pragma unroll
+      for (int kk = 0; kk < KKW; ++kk) {
+        f0.a[kk] = ar[decltype(slot)::value][kk];
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          f0.w[kk][j] = *reinterpret_cast<const bf16x8*>(b16 + bsw<T>(w_row + j * 32, kofs + kk * KG));
+      }
+      if (zd) zdot3(f0, kt);
+      const bool more = kt + LA < nk;
+      if (more) issue(kt + LA, slot);
+#pragma unroll
+      for (int kk = 0; kk < KKW; ++kk) mfma_kk(tg, f0, kk);
+      if (zf >= 0) zfinal3(zf);
+      ONEPOSE_SCHED_BARRIER();
+      if (more) asm volatile("s_waitcnt vmcnt(%0)" ::"n"((LA - 1) * OPS) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      raw_barrier();
+    };
+    using S0 = std::integral_constant<int, 0>;
+    using S1 = std::integral_constant<int, 1>;
+    static_assert(LA == 2, "the loops below are unrolled by two");
+    // stage st's A sits in slot st % 2 (kt0 is 0 or xs = 8)
+    issue(kt0, S0{});
+    if (kt0 + 1 < nk) issue(kt0 + 1, S1{});
+    tk = stamp_start(args.stamp, sl);
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"((LA - 1) * OPS) : "memory");
+    raw_barrier();
+    // @phase 1
+    if (PRO != PRO_HEADZ) {
+      for (int kt = kt0; kt < nk; kt += 2) {
+        stage(kt, S0{}, acc, false, -1);
+        stage(kt + 1, S1{}, acc, false, -1);
+      }
+    } else {
+      for (int kt = kt0; kt < xs; kt += 2) {
+        stage(kt, S0{}, acc, false, -1);
+        stage(kt + 1, S1{}, acc, false, -1);
+      }
+#pragma unroll 1
+      for (int h = 0; h < 4; ++h) {   // one head per two stages: slots 0, 1
+        const int k = xs + 2 * h;
+        stage(k, S0{}, acc_h, true, -1);
+        stage(k + 1, S1{}, acc_h, true, h & 1);
+        fold(h & 1);
+      }
+    }
+    // @phase 2
+  } else if constexpr (DMA >= 1) {
     // The lean DMA loop.  A bf16 stage is only 4-12 MFMAs per wave, so the loop is bound by the
     // instructions around them and by load latency, not by the matrix pipe:
     //  - row / piece offsets are computed once (32-bit, added to a wave-uniform base per stage);
@@ -899,6 +1062,10 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
     }
     return;
   }
+  // STATS on a stand-in tile: Y is stored from the registers (2 rows x 128 B per instruction)
+  // instead of through a 256-row LDS staging tile
+  constexpr bool kDirect = false;   // (EPI == EPI_STATS && T::NSUB > 1: measured no faster)
+  float ydir[kDirect ? FN : 1][16];
   if (ks == 0) {
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
@@ -918,7 +1085,8 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
           y = acc[j][i] + bias;
         }
         yv[i] = (gm < M) ? y : 0.f;
-        if (kStage || kRowStore) tile[row * TP + col] = yv[i];
+        if constexpr (kDirect) ydir[j][i] = yv[i];
+        else if (kStage || kRowStore) tile[row * TP + col] = yv[i];
       }
       if (EPI == EPI_STATS) {
         // the column's (mean, M2) over this wave's 32 rows, from the registers: each lane's 16
@@ -953,6 +1121,18 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
   if (yp != nullptr) yp += b * F(yp_bs);
   const int64_t ypl = F(ypl);
   auto row_store = [&]() __attribute__((always_inline)) {
+    if constexpr (kDirect) {
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int col = wn * FN * 32 + j * 32 + (lane & 31);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int gm = m0 + wm * 32 + (i & 3) + 8 * (i >> 2) + 4 * (lane >> 5);
+          if (gm < M) Y[(int64_t)gm * ldy + n0 + col] = ydir[j][i];
+        }
+      }
+      return;
+    }
     constexpr int C4 = BN / 4, PER = BM * C4 / T::NT;   // float4 per row, per thread
     static_assert(BM * C4 % T::NT == 0, "row-store pass");
     float4 rv[EPI == EPI_RESID ? PER : 1];
@@ -1008,26 +1188,32 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
   }
 
   if (EPI == EPI_STATS) {
-    // per column: the WM wave-row blocks' (mean, M2 about the block mean) (staged in `part`
-    // before the barrier above), Chan-merged in order
-    static_assert(EPI != EPI_STATS || (T::KS == 1 && T::NT >= BN && T::WM * BN <= T::NT),
+    // per column and SUB-row sub-tile: its wave-row blocks' (mean, M2 about the block mean)
+    // (staged in `part` before the barrier above), Chan-merged in order.  SUB = BM but for the
+    // tiles that stand in for several 64-row tiles (Tile::SUB): their partials, tickets and
+    // merges are those tiles', sub-tile by sub-tile.
+    constexpr int SUB = T::SUB, NSUB = T::NSUB, RG = 32, NRG = SUB / RG;
+    static_assert(EPI != EPI_STATS || (T::KS == 1 && T::WN * T::WM == T::NW && NSUB * BN <= T::NT &&
+                                       BM % SUB == 0 && SUB % RG == 0),
                   "stats tile");
-    constexpr int NRG = T::WM, RG = 32;
-    if (t < BN && n0 + t < N) {
+    const int mtiles_s = NSUB == 1 ? mtiles : (M + SUB - 1) / SUB;
+    const int tc = t % BN, ts = t / BN;   // merging thread: column, sub-tile
+    const int mt_s = mt * NSUB + ts;
+    if (t < NSUB * BN && n0 + tc < N && ts * SUB < rows) {
       float n = 0.f, mean = 0.f, M2 = 0.f;
-      for (int g = 0; g < NRG; ++g) {
+      for (int g = ts * NRG; g < ts * NRG + NRG; ++g) {
         const float nb = (float)max(min(g * RG + RG, rows) - g * RG, 0);
         if (nb == 0.f) continue;
-        const float mb = part[(g * BN + t) * 2], m2b = part[(g * BN + t) * 2 + 1];
+        const float mb = part[(g * BN + tc) * 2], m2b = part[(g * BN + tc) * 2 + 1];
         in_merge_block(n, mean, M2, nb, mb, m2b);
       }
-      float* st_out = F(stats) + ((int64_t)b * mtiles + mt) * 2 * N;
+      float* st_out = F(stats) + ((int64_t)b * mtiles_s + mt_s) * 2 * N;
       if (F(st_cnt) != nullptr) {   // handed to this launch's last tile: write-through (sc1)
-        __hip_atomic_store(st_out + n0 + t, mean, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(st_out + N + n0 + t, M2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(st_out + n0 + tc, mean, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(st_out + N + n0 + tc, M2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       } else {
-        st_out[n0 + t] = mean;
-        st_out[N + n0 + t] = M2;
+        st_out[n0 + tc] = mean;
+        st_out[N + n0 + tc] = M2;
       }
     }
     // InstanceNorm finalize in-launch (replaces a separate reduction launch): every M-tile of
@@ -1050,31 +1236,37 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
       //     tiles still compute;
       //  2. that merger takes a ticket on the column block; the last one merges the groups in
       //     group order (shifted by group 0's mean) into mean / rstd.
-      // Deterministic: neither result depends on which tile or group arrives last.
+      // Deterministic: neither result depends on which tile or group arrives last.  (A tile of
+      // several sub-tiles takes one ticket per sub-tile, and may close two groups.)
       static_assert(EPI != EPI_STATS || T::NT >= BN, "finalize threads");
-      const int G = stats_group_size(mtiles);
-      const int ngroups = (mtiles + G - 1) / G, g1 = mt / G;
+      const int G = stats_group_size(mtiles_s);
+      const int ngroups = (mtiles_s + G - 1) / G;
       unsigned* cb = tickets + (int64_t)b * F(st_cnt_bs);   // [ntiles] then [ntiles][ngroups]
       double* gp = F(st_grp) + (int64_t)b * ngroups * 2 * N;
       const int col = min(n0 + t, N - 1);
-      if (t < BN) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the storing wave drains
+      if (t < NSUB * BN) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // storing waves drain
       __syncthreads();   // partial stores drained; `part` no longer read
       // @phase 5
-      int* last = reinterpret_cast<int*>(part);
+      int* last = reinterpret_cast<int*>(part);   // [NSUB] group closed by sub-tile s, then [NSUB]
       unsigned ticket = 0u;
-      if (t == 0)
-        ticket = __hip_atomic_fetch_add(cb + ntiles + nt * ngroups + g1, 1u, __ATOMIC_RELAXED,
-                                        __HIP_MEMORY_SCOPE_AGENT);
-      row_store();   // the tile's Y rows, while the ticket is in flight
-      const int gt0 = g1 * G, gsz = min(G, mtiles - gt0);
-      if (t == 0) last[0] = ticket == (unsigned)(gsz - 1) ? 1 : 0;
+      const bool tk_thread = t % BN == 0 && ts < NSUB && ts * SUB < rows;
+      if (tk_thread)
+        ticket = __hip_atomic_fetch_add(cb + ntiles + nt * ngroups + mt_s / G, 1u,
+                                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      row_store();   // the tile's Y rows, while the tickets are in flight
+      if (t % BN == 0 && ts < NSUB) {
+        const int gt0 = (mt_s / G) * G, gsz = min(G, mtiles_s - gt0);
+        last[ts] = tk_thread && ticket == (unsigned)(gsz - 1) ? 1 : 0;
+      }
       __syncthreads();
       // @phase 6
-      if (last[0]) {
+      for (int s = 0; s < NSUB; ++s) {
+        if (!last[s]) continue;
+        const int g1 = (mt * NSUB + s) / G, gt0 = g1 * G, gsz = min(G, mtiles_s - gt0);
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // (no instruction: keeps the
                                                                  // loads below the ticket)
         if (t < BN) {
-          const float* sp = F(stats) + (int64_t)b * mtiles * 2 * N + col;
+          const float* sp = F(stats) + (int64_t)b * mtiles_s * 2 * N + col;
           auto ld = [&](int ti, int half) __attribute__((always_inline)) {
             return __hip_atomic_load(sp + (int64_t)ti * 2 * N + half * N, __ATOMIC_RELAXED,
                                      __HIP_MEMORY_SCOPE_AGENT);
@@ -1093,7 +1285,7 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
 #pragma unroll
             for (int u = 0; u < UD; ++u) {
               if (u0 + u < gsz)
-                in_merge_tile(s1, s2, ng, (double)min(BM, M - (gt0 + u0 + u) * BM), mv[u], qv[u], c);
+                in_merge_tile(s1, s2, ng, (double)min(SUB, M - (gt0 + u0 + u) * SUB), mv[u], qv[u], c);
             }
           }
           if (n0 + t < N) {
@@ -1108,10 +1300,10 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
         if (t == 0) {
           const unsigned t2 = __hip_atomic_fetch_add(cb + nt, 1u, __ATOMIC_RELAXED,
                                                      __HIP_MEMORY_SCOPE_AGENT);
-          last[1] = t2 == (unsigned)(ngroups - 1) ? 1 : 0;
+          last[NSUB] = t2 == (unsigned)(ngroups - 1) ? 1 : 0;
         }
         __syncthreads();
-        if (last[1] && t < BN && n0 + t < N) {
+        if (last[NSUB] && t < BN && n0 + t < N) {
           __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
           const double* g2 = gp + n0 + t;
           auto ld2 = [&](int g, int half) __attribute__((always_inline)) {
@@ -1133,7 +1325,7 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
             for (int u = 0; u < GD; ++u) {
               const int g = q0 + u;
               if (g < ngroups)
-                in_merge_group(S1, S2, (double)min(G * BM, M - g * G * BM), mg[u], m2g[u], c);
+                in_merge_group(S1, S2, (double)min(G * SUB, M - g * G * SUB), mg[u], m2g[u], c);
             }
           }
           const double n = (double)M;
@@ -1226,6 +1418,7 @@ using T128x128 = Tile<128, 128, 1, 4, 32>;
 using T128x64W8 = Tile<128, 64, 1, 8, 32>;
 using T32x64W2 = Tile<32, 64, 1, 2, 32>;
 using T32x256W8 = Tile<32, 256, 1, 8, 64, 1>;
+using T256x128W8 = Tile<256, 128, 1, 8, 32, 2, 64>;
 
 
 template <int EPI, int PRO, class T, int PM, bool WPL = false, int DMA = 0>
@@ -1239,7 +1432,7 @@ void launch_one(GemmArgs& args, int grid, hipStream_t stream) {
 template <int EPI, int PRO, class T, int PM>
 void launch_adma(GemmArgs& args, int grid, hipStream_t stream) {
   if constexpr (PRO != PRO_NORM_RELU && (EPI == EPI_QKV || EPI == EPI_STATS))
-    launch_one<EPI, PRO, T, PM, true, 2>(args, grid, stream);
+    launch_one<EPI, PRO, T, PM, true, (T::NSUB > 1 && PM == PM_BF16) ? 3 : 2>(args, grid, stream);
 }
 
 struct TileDims {
@@ -1255,6 +1448,7 @@ TileDims tile_dims(int tile) {
     case TILE_128x64W8: return {128, 64, 32};
     case TILE_32x64W2: return {32, 64, 32};
     case TILE_32x256W8: return {32, 256, 64};
+    case TILE_256x128W8: return {256, 128, 32};
 
     default: return {0, 0, 0};
   }
@@ -1271,7 +1465,8 @@ static_assert(gemm_tile_bm(TILE_64x64) == 64 && gemm_tile_bn(TILE_64x64) == 64 &
                   gemm_tile_bm(TILE_128x128) == 128 && gemm_tile_bn(TILE_128x128) == 128 &&
                   gemm_tile_bm(TILE_128x64W8) == 128 && gemm_tile_bn(TILE_128x64W8) == 64 &&
                   gemm_tile_bm(TILE_32x64W2) == 32 && gemm_tile_bn(TILE_32x64W2) == 64 &&
-                  gemm_tile_bm(TILE_32x256W8) == 32 && gemm_tile_bn(TILE_32x256W8) == 256,
+                  gemm_tile_bm(TILE_32x256W8) == 32 && gemm_tile_bn(TILE_32x256W8) == 256 &&
+                  gemm_tile_bm(TILE_256x128W8) == 256 && gemm_tile_bn(TILE_256x128W8) == 128,
               "gemm.h tile shapes must match tile_dims");
 
 GemmProb gemm_prob(const float* A, int lda, const float* W, int ldw, const float* bias,
@@ -1321,11 +1516,15 @@ int gemm_launch(int epi, int pro, int tile, GemmArgs& args, hipStream_t stream, 
     OP_REQUIRE(P.ksplit % td.bks == 0, "gemm: ksplit=%d", P.ksplit);
     OP_REQUIRE(P.lda0 % 4 == 0 && P.ldw % 4 == 0, "gemm: unaligned leading dimension");
     OP_REQUIRE(epi != EPI_QKV || (td.bn == 128 && P.N == 768), "gemm: QKV tiling");
+    const int srows = gemm_tile_stat_rows(tile);
     OP_REQUIRE(epi != EPI_STATS || P.st_cnt == nullptr ||
                    (P.st_grp != nullptr &&
-                    P.st_cnt_bs >= ceil_div(P.N, td.bn) * (1 + stats_groups(P.M, td.bm))),
+                    P.st_cnt_bs >= ceil_div(P.N, td.bn) * (1 + stats_groups(P.M, srows))),
                "gemm: STATS finalize needs group partials and %d counters per sample",
-               ceil_div(P.N, td.bn) * (1 + stats_groups(P.M, td.bm)));
+               ceil_div(P.N, td.bn) * (1 + stats_groups(P.M, srows)));
+    OP_REQUIRE(tile != TILE_256x128W8 || (epi == EPI_STATS && pro == PRO_HEADZ && pm == PM_BF16 &&
+                                          P.N == 512 && P.ksplit == 256),
+               "gemm: the 256 x 128 tile is bf16 MLP conv 1's");
     OP_REQUIRE(epi != EPI_BIAS_L2 || (td.bn == 256 && P.N == 256 && P.ldy % 4 == 0),
                "gemm: BIAS_L2 tiles hold whole 256-column rows");
     OP_REQUIRE((epi != EPI_BIAS && epi != EPI_STATS && epi != EPI_RESID) ||
@@ -1354,7 +1553,8 @@ int gemm_launch(int epi, int pro, int tile, GemmArgs& args, hipStream_t stream, 
   // register-staged split loop needs 160+ VGPRs and spills).  bf16 mode: the DMA loop for the
   // 64 x 128 tiles (QKV, MLP conv 1), the register-staged loop for 64 x 64 (MLP conv 2, whose
   // two MFMAs per wave and stage leave a DMA loop nothing to hide behind).
-  const bool dma = pm == PM_SPLIT3 || (pm == PM_BF16 && tile == TILE_64x128);
+  const bool dma =
+      pm == PM_SPLIT3 || (pm == PM_BF16 && (tile == TILE_64x128 || tile == TILE_256x128W8));
   // A from activation planes (every problem of the launch, or none): the DMA loop's DMA-2 form
   const bool adma = args.p[0].Ap != nullptr;
   const bool yplanes = args.p[0].Yp != nullptr;
@@ -1405,6 +1605,7 @@ int gemm_launch(int epi, int pro, int tile, GemmArgs& args, hipStream_t stream, 
   CASE(EPI_RESID, PRO_NORM_RELU, TILE_64x64, T64x64, PM_BF16, true)
   CASE(EPI_QKV, PRO_PLAIN, TILE_64x128, T64x128, PM_BF16, true)
   CASE(EPI_STATS, PRO_HEADZ, TILE_64x128, T64x128, PM_BF16, true)
+  CASE(EPI_STATS, PRO_HEADZ, TILE_256x128W8, T256x128W8, PM_BF16, true)
   CASE(EPI_RESID, PRO_NORM_RELU, TILE_64x128, T64x128, PM_BF16, true)
   CASE(EPI_ACC, PRO_PLAIN, TILE_64x128, T64x128, PM_BF16, true)
   CASE(EPI_RESID, PRO_NORM_RELU, TILE_32x64W2, T32x64W2, PM_SPLIT3, true)

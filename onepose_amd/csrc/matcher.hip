@@ -1381,14 +1381,26 @@ constexpr int kTileBf16 = TILE_64x128;
 // ms per frame, profiles/r04/sw/); its MLP conv 1 keeps 64 x 64 (64 x 128 gives 320 workgroups
 // at config 2: 0.273 -> 0.313 ms per frame; a DMA stage's time follows the bytes its workgroup
 // moves).
-int mlp1_tile(int pm) { return pm == PM_BF16 ? kTileBf16 : kTileMLP1; }
+// The bf16 MLP conv 1 itself runs on the 256 x 128 eight-wave tile (gemm.h TILE_256x128W8: the
+// 64 x 128 tile's partials, tickets, acc0 and bits, with a stage's W rows fetched once per 256
+// rows and A loaded straight into the MFMA registers); its acc0 (object cache) is still written
+// by the 64 x 128 EPI_ACC launch.  (Under evaluation: -DONEPOSE_MLP1_WIDE selects it.)
+#ifdef ONEPOSE_MLP1_WIDE
+constexpr int kTileBf16Mlp1 = TILE_256x128W8;
+#else
+constexpr int kTileBf16Mlp1 = kTileBf16;
+#endif
+int mlp1_tile(int pm) { return pm == PM_BF16 ? kTileBf16Mlp1 : kTileMLP1; }
+int mlp1_acc_tile(int pm) { return pm == PM_BF16 ? kTileBf16 : kTileMLP1; }
 // make_plan sizes MLP conv 1's InstanceNorm partials (stats rows `str`), its arrival counters
 // (kCntPerSide column blocks) and group partials once for every precision: each precision's
 // MLP conv 1 tile must have those rows and at most that many column blocks over N = 512.
-static_assert(gemm_tile_bm(kTileBf16) == gemm_tile_bm(kTileMLP1),
-              "MLP conv 1 tiles of all precisions must share their row count");
+static_assert(gemm_tile_stat_rows(kTileBf16) == gemm_tile_bm(kTileMLP1) &&
+                  gemm_tile_stat_rows(kTileBf16Mlp1) == gemm_tile_bm(kTileMLP1),
+              "MLP conv 1 tiles of all precisions must share their partials' row count");
 static_assert(512 / gemm_tile_bn(kTileMLP1) <= kCntPerSide &&
-                  512 / gemm_tile_bn(kTileBf16) <= kCntPerSide,
+                  512 / gemm_tile_bn(kTileBf16) <= kCntPerSide &&
+                  512 / gemm_tile_bn(kTileBf16Mlp1) <= kCntPerSide,
               "MLP conv 1 column blocks exceed the plan's counters");
 
 int qkv_tile_for(int n3, int B) {
@@ -2073,7 +2085,9 @@ int attention_layer(const ApW& w, const Side* sd, int nside, int B, const Plan& 
         a.p[i].ldap1 = 256;
       }
     }
-    if ((rc = gemm_launch(EPI_STATS, PRO_HEADZ, mlp1_tile(pm), a, st, K_MLP1, pm)) != ONEPOSE_OK)
+    // (the 256-row tile's loop reads A from its planes: without them, the 64 x 128 DMA-1 tile)
+    if ((rc = gemm_launch(EPI_STATS, PRO_HEADZ, ap ? mlp1_tile(pm) : mlp1_acc_tile(pm), a, st,
+                          K_MLP1, pm)) != ONEPOSE_OK)
       return rc;
   }
   // 5. InstanceNorm statistics: finalized inside MLP conv 1 by each column block's last
@@ -2441,7 +2455,7 @@ int object_prepare_impl(const void* packed_weights, const void* desc3d, int desc
     a.nprob = 1;
     a.p[0] = gemm_prob(cache, 256, w.w1a, 256, nullptr, cache + L.acc, 512, n3, 512, 256, 1);
     if (pm != PM_F32) set_w_planes(a.p[0], w.w1a_p, kPlW1a);
-    if ((rc = gemm_launch(EPI_ACC, PRO_PLAIN, mlp1_tile(pm), a, st, K_MLP1, pm)) != ONEPOSE_OK)
+    if ((rc = gemm_launch(EPI_ACC, PRO_PLAIN, mlp1_acc_tile(pm), a, st, K_MLP1, pm)) != ONEPOSE_OK)
       return rc;
   }
   return ONEPOSE_OK;

@@ -341,6 +341,18 @@ int main(int argc, char** argv) {
     }
     return 0;
   }
+  if (argc > 1 && !strcmp(argv[1], "ws")) {   // round 5: bf16 MLP conv 1 on 256 x 128, 8 waves
+    using T256x128W8 = Tile<256, 128, 1, 8, 32, 2, 64>;
+    for (int m : {5120, 10240}) {
+      printf("--- bf16 mlp1 STATS+HEADZ+fin, M %d (A planes by DMA) ---\n", m);
+      for (int r = 0; r < 2; ++r) {
+        run<EPI_STATS, PRO_HEADZ, T64x128, PM_BF16, 2>("bf16 64x128 dma2", B, m, 512, 512, true, it);
+        run<EPI_STATS, PRO_HEADZ, T256x128W8, PM_BF16, 2>("bf16 256x128 w8 dma2", B, m, 512, 512, true, it);
+        run<EPI_STATS, PRO_HEADZ, T256x128W8, PM_BF16, 2>("bf16 256x128 w8 (no fin)", B, m, 512, 512, false, it);
+      }
+    }
+    return 0;
+  }
   if (argc > 1 && !strcmp(argv[1], "dma")) {   // round 4: the DMA-2 loop (A and W planes)
     for (int m : {5120, 10240}) {
       printf("--- mlp1 STATS+HEADZ+fin, M %d (A planes by DMA) ---\n", m);
