@@ -201,9 +201,66 @@ class GATsSuperGlue(nn.Module):
             raise ValueError(f"bad matcher input shapes {tuple(d2.shape)} {tuple(d3.shape)} "
                              f"{tuple(db.shape)}")
         dev = d2.device
-        return self._run(d2, s2, d3, s3, db, sl, B, n1, n3, nleaf, dev)
+        obj = None
+        if self.resident_object and B == 1:
+            obj = self._resident(data["descriptors3d_db"], data["descriptors2d_db"], d3, db, n3,
+                                 nleaf, half, dev)
+        return self._run(d2, s2, d3, s3, db, sl, B, n1, n3, nleaf, dev, obj)
 
-    def _run(self, d2, s2, d3, s3, db, sl, B, n1, n3, nleaf, dev):
+    # The reference's driver calls forward() once per frame with the same object tensors
+    # (inference.py:98-182: load_object once, pack_data per frame).  With resident_object, the
+    # object-only prefix of the forward (GAT layer 0, the 3D half of self-attention 1) and the
+    # leaves' point-major copy are computed once per object (onepose_object_prepare, flags 0)
+    # and every later frame starts from them (onepose_match_cached): the same bits as the
+    # uncached forward (tests/test_matcher_gpu.py::test_object_cache_is_bit_identical).  The
+    # object is recognised by its two descriptor tensors' storage, layout and version counters
+    # (an in-place write bumps the version) and the packed weights; the module holds references
+    # to them, so their memory cannot be handed to other tensors while cached.
+    resident_object = True
+
+    def _resident(self, t3, tl, d3, db, n3, nleaf, half, dev):
+        w = self.packed_weights(dev)
+        def ident(t):
+            return (t.untyped_storage().data_ptr(), t.storage_offset(), tuple(t.shape),
+                    tuple(t.stride()), t.dtype, t._version)
+        key = (str(dev), self.precision, half, n3, nleaf, ident(t3), ident(tl), w.data_ptr(),
+               self._packed_key)
+        cur = self.__dict__.get("_obj")
+        if cur is not None and cur["key"] == key:
+            return cur
+        self._release_resident()
+        lib = _lib.load()
+        dt = _lib.DT_F16 if half else _lib.DT_F32
+        f32 = dict(dtype=torch.float32, device=dev)
+        s = _lib.stream_ptr(dev)
+        with torch.cuda.device(dev):
+            pm = torch.empty(n3 * nleaf * 256, **f32)
+            _lib.check(lib.onepose_prepare_leaves_dt(db.data_ptr(), dt, 0, 1, n3, nleaf,
+                                                     pm.data_ptr(), s), "prepare_leaves")
+            cache = torch.empty(_lib.object_cache_bytes(lib, n3, nleaf, 0, self.precision) // 4,
+                                **f32)
+            wsb = lib.onepose_object_prepare_workspace_bytes(n3, nleaf)
+            ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
+            _lib.check(lib.onepose_object_prepare_dt(w.data_ptr(), d3.data_ptr(), dt, pm.data_ptr(),
+                                                     n3, nleaf, self.precision, 0,
+                                                     cache.data_ptr(), ws.data_ptr(), wsb, s),
+                       "object_prepare")
+        del ws   # (stream-ordered: the allocator hands it out only behind the prepare)
+        self._obj = {"key": key, "refs": (t3, tl, d3, db), "pm": pm, "cache": cache}
+        return self._obj
+
+    def _release_resident(self):
+        cur = self.__dict__.pop("_obj", None)
+        if cur is not None:
+            try:
+                _lib.load().onepose_object_release(cur["cache"].data_ptr())
+            except Exception:
+                pass
+
+    def __del__(self):
+        self._release_resident()
+
+    def _run(self, d2, s2, d3, s3, db, sl, B, n1, n3, nleaf, dev, obj=None):
         lib = _lib.load()
         with torch.cuda.device(dev):
             w = self.packed_weights(dev)
@@ -215,6 +272,17 @@ class GATsSuperGlue(nn.Module):
             ws_bytes = _lib.workspace_bytes(lib, B, n1, n3, nleaf, True, self.precision)
             ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
             dt = _lib.DT_F16 if d2.dtype == torch.float16 else _lib.DT_F32
+            if obj is not None:
+                rc = lib.onepose_match_cached_dt(
+                    w.data_ptr(), d2.data_ptr(), dt, s2, obj["cache"].data_ptr(),
+                    obj["pm"].data_ptr(), 0, B, n1, n3, nleaf,
+                    float(_hp(self.hparams, "scale_factor")),
+                    float(_hp(self.hparams, "match_threshold")), self.precision, 0,
+                    m0.data_ptr(), m1.data_ptr(), ms0.data_ptr(), ms1.data_ptr(), conf.data_ptr(),
+                    ws.data_ptr(), ws_bytes, _lib.stream_ptr(dev))
+                _lib.check(rc, "onepose_match_cached")
+                return ({"matches0": m0[0], "matches1": m1[0],
+                         "matching_scores0": ms0[0], "matching_scores1": ms1[0]}, conf)
             # (an older A/B build named by ONEPOSE_LIB has only the fp32 entry point)
             call = (lib.onepose_match_dt if hasattr(lib, "onepose_match_dt")
                     else lambda *a: lib.onepose_match_ex(*a[:7], *a[8:]))

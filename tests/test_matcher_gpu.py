@@ -224,6 +224,46 @@ def test_object_cache_is_bit_identical(device, n1, n3, L, B, prec):
         assert (outs[1]["m0"] > -1).sum() > 100
 
 
+@pytest.mark.parametrize("precision", ["fp32", "bf16", "fp32_split"])
+def test_resident_object_forward(precision, device):
+    """The drop-in forward keeps the object resident (GATsSuperGlue.resident_object): frames
+    after the first start from the object's cached prefix.  Each frame's outputs equal the
+    uncached forward's bit for bit; an in-place write to the object's descriptors (a version
+    bump) and a new object tensor are both re-prepared."""
+    sd = synthetic.make_state_dict(3)
+    hp = {**synthetic.DEFAULT_HPARAMS, "attention_precision": precision}
+    res = matcher.from_state_dict(sd, hp).to(device)
+    unc = matcher.from_state_dict(sd, hp).to(device)
+    unc.resident_object = False
+    data, _, _ = synthetic.make_matcher_inputs(300, 1000, 8, seed=9)
+    t = {k: torch.from_numpy(v).to(device) for k, v in data.items()}
+
+    def same(tag):
+        with torch.no_grad():
+            p1, c1 = res(t)
+            p2, c2 = unc(t)
+        torch.cuda.synchronize()
+        for k in p1:
+            np.testing.assert_array_equal(p1[k].cpu().numpy(), p2[k].cpu().numpy(), err_msg=f"{tag} {k}")
+        np.testing.assert_array_equal(c1.cpu().numpy(), c2.cpu().numpy(), err_msg=tag)
+        return p1
+
+    first = same("frame 0")
+    key0 = res._obj["key"]
+    g = torch.Generator().manual_seed(4)
+    for f in range(1, 3):   # new frames against the same object: the cache is reused
+        t["descriptors2d_query"] = torch.nn.functional.normalize(
+            torch.randn(t["descriptors2d_query"].shape, generator=g), dim=1).to(device)
+        same(f"frame {f}")
+        assert res._obj["key"] == key0
+    t["descriptors3d_db"].mul_(1.5)   # in place: the version counter moves
+    same("object written in place")
+    assert res._obj["key"] != key0
+    t["descriptors2d_db"] = t["descriptors2d_db"].clone()   # a new leaves tensor
+    same("new leaves tensor")
+    assert (first["matches0"] > -1).sum() > 10
+
+
 def cached_and_uncached(lib, device, n1, n3, L, B, prec, seed, sd_seed=0, modes=(False, True),
                         flags=0):
     """Outputs of onepose_match_prepared_ex (False) / onepose_object_prepare +
