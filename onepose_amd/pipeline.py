@@ -55,7 +55,7 @@ class _Slot:
         self.matches1 = torch.empty(B, n3, dtype=torch.int64, device=dev)
         self.mscores0 = torch.empty(B, n1, **f32)
         self.mscores1 = torch.empty(B, n3, **f32)
-        self.conf = torch.empty(B, n1, n3, **f32) if with_conf else None
+        self._conf = torch.empty(B, n1, n3, **f32) if with_conf else None
         self.pts2d = torch.empty(B, n1, 2, **f32)
         self.pts3d = torch.empty(B, n1, 3, **f32)
         self.counts = torch.empty(B, dtype=torch.int32, device=dev)
@@ -70,6 +70,16 @@ class _Slot:
         self.ws_match = torch.empty(self.ws_match_bytes, dtype=torch.uint8, device=dev)
         self.ws_pnp_bytes = lib.onepose_pnp_workspace_bytes(B, n1, iters)
         self.ws_pnp = torch.empty(self.ws_pnp_bytes, dtype=torch.uint8, device=dev)
+
+
+    @property
+    def conf(self):
+        """The frame's conf_matrix [B, n1, n3] (only with FramePipeline(with_conf=True); the
+        default since round 4 is False, as the reference driver discards it)."""
+        if self._conf is None:
+            raise RuntimeError("conf_matrix is not kept: build FramePipeline(with_conf=True) to "
+                               "read it (the default, like the reference driver, discards it)")
+        return self._conf
 
 
 class FramePipeline:
@@ -251,7 +261,7 @@ class FramePipeline:
                 self.object_cache.data_ptr(), self.leaves_pm.data_ptr(), 0,
                 self.B, self.n1, self.n3, self.L, self.scale_factor, self.threshold,
                 self.precision, self.object_flags, o.matches0.data_ptr(), o.matches1.data_ptr(),
-                o.mscores0.data_ptr(), o.mscores1.data_ptr(), _lib.ptr(o.conf),
+                o.mscores0.data_ptr(), o.mscores1.data_ptr(), _lib.ptr(o._conf),
                 o.ws_match.data_ptr(), o.ws_match_bytes, s), "onepose_match_cached")
             return
         _lib.check(self.lib.onepose_match_prepared_ex(
@@ -259,7 +269,7 @@ class FramePipeline:
             self.desc3d.data_ptr(), 0, self.leaves_pm.data_ptr(), 0,
             self.B, self.n1, self.n3, self.L, self.scale_factor, self.threshold, self.precision,
             o.matches0.data_ptr(), o.matches1.data_ptr(), o.mscores0.data_ptr(),
-            o.mscores1.data_ptr(), _lib.ptr(o.conf), o.ws_match.data_ptr(),
+            o.mscores1.data_ptr(), _lib.ptr(o._conf), o.ws_match.data_ptr(),
             o.ws_match_bytes, s), "onepose_match_prepared")
 
     fused_pose = True   # enqueue_pose's default: onepose_pose_stage (two launches)

@@ -62,6 +62,14 @@ def test_graph_replay_matches_eager(setup):
 
 
 @pytest.mark.gpu
+def test_conf_needs_with_conf(setup):
+    """with_conf=False (the default): conf_matrix is not kept, and reading it says so."""
+    pipe, _ = setup
+    with pytest.raises(RuntimeError, match="with_conf=True"):
+        pipe.conf
+
+
+@pytest.mark.gpu
 def test_fused_pose_stage_matches_separate_calls(setup):
     """onepose_pose_stage (selection in the RANSAC kernel, errors in the refit kernel) gives
     the bits of onepose_select_correspondences + onepose_pnp_ransac + onepose_pose_errors."""
