@@ -20,7 +20,6 @@
 
 #include <cstdlib>
 #include <cstring>
-#include <type_traits>
 
 // Pins the pipeline's phase order (the compiler's own schedule measured within +-2%,
 // DESIGN.md §3d).
@@ -64,8 +63,6 @@ struct FragT<PM_SPLIT3, KKW, FN> {   // hi / mid / lo pieces
 
 
 constexpr int kScoreGroup = 8;   // N-tiles per column group of the score grid
-
-constexpr int kDma3Bufs = 3;   // DMA-3 loop: LDS buffers (stages of loads in flight + 1)
 
 template <int BM_, int BN_, int KS_, int NW_, int BKS_, int WPE_ = 3, int SUB_ = BM_>
 struct Tile {
@@ -298,8 +295,7 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
   // (a tile that stands in for several -- one workgroup per CU -- has no other workgroup to
   // cover its DMA latency, and its staging tile is larger than five stages: four in flight)
   constexpr int NBUF =
-      DMA == 3 ? kDma3Bufs
-      : (DMA == 2 && PM == PM_BF16 && (NPL * BM / (512 / T::BKS)) % T::NW == 0)
+      (DMA == 2 && PM == PM_BF16 && (NPL * BM / (512 / T::BKS)) % T::NW == 0)
           ? (T::NSUB > 1 ? 5 : 3)
           : 2;
   constexpr int LDS0 = NBUF * STAGE > BM * TP ? NBUF * STAGE : BM * TP;
@@ -354,7 +350,7 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
     c.wp1 = wp1 ? wp1 + b * F(wp1_bs) : c.wp0 + c.ksplit;
     c.wpl1 = wp1 ? F(wpl1) : c.wpl0;
   }
-  if constexpr (DMA >= 2) {   // A planes (range 1: its own planes, or range 0's continuing)
+  if constexpr (DMA == 2) {   // A planes (range 1: its own planes, or range 0's continuing)
     const uint16_t* ap1 = F(Ap1);
     c.ap0 = F(Ap) + b * F(ap_bs);
     c.apl0 = F(apl);
@@ -554,130 +550,7 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
         for (int i = 0; i < 16; ++i) acc[j][i] = a0p[((j / 2) * 2 + (j % 2)) * 1024 + i * 64];
     }
   }
-  if constexpr (DMA == 3) {
-    // DMA 3 (bf16, W and A planes; the 256-row stand-in tile): only W goes through LDS, by
-    // global_load_lds, one 1-KB piece per wave and stage.  Each wave's A rows are its own (WN
-    // = 1), so A is loaded from its planes straight into the MFMA fragment registers (lane half
-    // h holds k = 16 kk + 8 h .. + 7 of row lane & 31: one 16-B load per fragment) -- no LDS
-    // stores or reads of A, and 1 DMA piece instead of 3 per wave and stage (a piece costs the
-    // issuing wave ~60-180 cycles).  LA = 4 stages of loads in flight, in a ring of A registers
-    // indexed at compile time (the loops are unrolled by LA).  Same images, fragments, MFMA
-    // order and Z arithmetic as the DMA-2 loop: the same bits.
-    static_assert(WPL && PM == PM_BF16 && T::WN == 1 && T::KS == 1 && T::BKS == 32, "DMA 3 tiling");
-    constexpr int LA = NBUF - 1;
-    constexpr int CPR = T::BKS / 8, RP = 64 / CPR;
-    constexpr int PIECES = T::BN / RP, PPW = PIECES / T::NW;
-    static_assert(T::BN % RP == 0 && PIECES % T::NW == 0, "W pieces");
-    constexpr int OPS = PPW + KKW;   // vm instructions per wave and stage
-    static_assert((LA - 1) * OPS <= 63, "vmcnt");
-    unsigned woff0[PPW], woff1[PPW];
-    int wdst[PPW];
-#pragma unroll
-    for (int i = 0; i < PPW; ++i) {
-      const int p = wave + T::NW * i;
-      const int rb = p * RP;
-      const int row = T::BM + rb + lane / CPR;
-      const int chunk = bsw<T>(row, (lane % CPR) * 8) - row * T::BKS;
-      const int o = min(n0 + rb + lane / CPR, c.N - 1);
-      woff0[i] = (unsigned)(((int64_t)o * c.ldw0 + chunk) * 2);
-      woff1[i] = (unsigned)(((int64_t)o * c.ldw1 + chunk) * 2);
-      wdst[i] = (T::BM + rb) * T::BKS * 2;
-    }
-    const int arow = min(m0 + wm * 32 + (lane & 31), c.M - 1);
-    const unsigned aoff0 = (unsigned)(((int64_t)arow * c.ldap0 + (lane >> 5) * 8) * 2);
-    const unsigned aoff1 = (unsigned)(((int64_t)arow * c.ldap1 + (lane >> 5) * 8) * 2);
-    bf16x8 ar[LA][KKW];
-    auto buf = [&](int st) __attribute__((always_inline)) { return lds + (st % NBUF) * STAGE; };
-    auto issue = [&](int st, auto slot) __attribute__((always_inline)) {
-      const int k0 = st * T::BKS;
-      const bool first = PRO != PRO_HEADZ || k0 < c.ksplit;
-      const char* wb = reinterpret_cast<const char*>(first ? c.wp0 + k0 : c.wp1 + (k0 - c.ksplit));
-      char* dst = reinterpret_cast<char*>(buf(st));
-#pragma unroll
-      for (int i = 0; i < PPW; ++i) dma16(wb + (first ? woff0[i] : woff1[i]), dst + wdst[i]);
-      const char* ab = reinterpret_cast<const char*>(first ? c.ap0 + k0 : c.ap1 + (k0 - c.ksplit));
-      const unsigned ao = first ? aoff0 : aoff1;
-#pragma unroll
-      for (int kk = 0; kk < KKW; ++kk)
-        ar[decltype(slot)::value][kk] = *reinterpret_cast<const bf16x8*>(ab + ao + kk * KG * 2);
-    };
-    auto raw_barrier = [&]() __attribute__((always_inline)) {
-      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    };
-    // Z from the fragments: lane half h holds chunk 2 kk + h of the stage (the TPR-4 thread zq's
-    // chunk), so ((c0 + c1) + (c2 + c3)) is (zp0 + its partner's) + (zp1 + its partner's)
-    float zr2[KKW];
-#pragma unroll
-    for (int kk = 0; kk < KKW; ++kk) zr2[kk] = 0.f;
-    auto zdot3 = [&](const Frag& f, int sg) __attribute__((always_inline)) {
-#pragma unroll
-      for (int kk = 0; kk < KKW; ++kk) {
-        const float* kp = zks + (sg * T::BKS - c.ksplit) + kk * KG + (lane >> 5) * 8;
-        const bf16x8 q = f.a[kk];
-        const float4 a0 = make_float4((float)q[0], (float)q[1], (float)q[2], (float)q[3]);
-        const float4 a1 = make_float4((float)q[4], (float)q[5], (float)q[6], (float)q[7]);
-        zr2[kk] = headz_dot8(zr2[kk], a0, a1, *reinterpret_cast<const float4*>(kp),
-                             *reinterpret_cast<const float4*>(kp + 4));
-      }
-    };
-    auto zfinal3 = [&](int par) __attribute__((always_inline)) {
-      static_assert(KKW == 2, "four chunks per stage");
-      const float z = (zr2[0] + __shfl_xor(zr2[0], 32, 64)) + (zr2[1] + __shfl_xor(zr2[1], 32, 64));
-      if (lane < 32) zrow[par * BM + wm * 32 + lane] = (1.0f / (z + 1e-6f)) * zns;
-      zr2[0] = zr2[1] = 0.f;
-    };
-    auto stage = [&](int kt, auto slot, floatx16 (&tg)[FN], bool zd, int zf)
-        __attribute__((always_inline)) {
-      const float* cur = buf(kt);
-      const __bf16* b16 = reinterpret_cast<const __bf16*>(cur);
-#pragma unroll
-      for (int kk = 0; kk < KKW; ++kk) {
-        f0.a[kk] = ar[decltype(slot)::value][kk];
-#pragma unroll
-        for (int j = 0; j < FN; ++j)
-          f0.w[kk][j] = *reinterpret_cast<const bf16x8*>(b16 + bsw<T>(w_row + j * 32, kofs + kk * KG));
-      }
-      if (zd) zdot3(f0, kt);
-      const bool more = kt + LA < nk;
-      if (more) issue(kt + LA, slot);
-#pragma unroll
-      for (int kk = 0; kk < KKW; ++kk) mfma_kk(tg, f0, kk);
-      if (zf >= 0) zfinal3(zf);
-      ONEPOSE_SCHED_BARRIER();
-      if (more) asm volatile("s_waitcnt vmcnt(%0)" ::"n"((LA - 1) * OPS) : "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      raw_barrier();
-    };
-    using S0 = std::integral_constant<int, 0>;
-    using S1 = std::integral_constant<int, 1>;
-    static_assert(LA == 2, "the loops below are unrolled by two");
-    // stage st's A sits in slot st % 2 (kt0 is 0 or xs = 8)
-    issue(kt0, S0{});
-    if (kt0 + 1 < nk) issue(kt0 + 1, S1{});
-    tk = stamp_start(args.stamp, sl);
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"((LA - 1) * OPS) : "memory");
-    raw_barrier();
-    // @phase 1
-    if (PRO != PRO_HEADZ) {
-      for (int kt = kt0; kt < nk; kt += 2) {
-        stage(kt, S0{}, acc, false, -1);
-        stage(kt + 1, S1{}, acc, false, -1);
-      }
-    } else {
-      for (int kt = kt0; kt < xs; kt += 2) {
-        stage(kt, S0{}, acc, false, -1);
-        stage(kt + 1, S1{}, acc, false, -1);
-      }
-#pragma unroll 1
-      for (int h = 0; h < 4; ++h) {   // one head per two stages: slots 0, 1
-        const int k = xs + 2 * h;
-        stage(k, S0{}, acc_h, true, -1);
-        stage(k + 1, S1{}, acc_h, true, h & 1);
-        fold(h & 1);
-      }
-    }
-    // @phase 2
-  } else if constexpr (DMA >= 1) {
+  if constexpr (DMA >= 1) {
     // The lean DMA loop.  A bf16 stage is only 4-12 MFMAs per wave, so the loop is bound by the
     // instructions around them and by load latency, not by the matrix pipe:
     //  - row / piece offsets are computed once (32-bit, added to a wave-uniform base per stage);
@@ -1432,7 +1305,7 @@ void launch_one(GemmArgs& args, int grid, hipStream_t stream) {
 template <int EPI, int PRO, class T, int PM>
 void launch_adma(GemmArgs& args, int grid, hipStream_t stream) {
   if constexpr (PRO != PRO_NORM_RELU && (EPI == EPI_QKV || EPI == EPI_STATS))
-    launch_one<EPI, PRO, T, PM, true, (T::NSUB > 1 && PM == PM_BF16) ? 3 : 2>(args, grid, stream);
+    launch_one<EPI, PRO, T, PM, true, 2>(args, grid, stream);
 }
 
 struct TileDims {

@@ -314,7 +314,11 @@ def load_object(paths, num_leaf):
         avg_data["descriptors3d"], avg_data["scores3d"], num_3d)
     clt_descriptors, _ = data_utils.build_features3d_leaves(
         clt_data["descriptors3d"], clt_data["scores3d"], idxs, num_3d, num_leaf)
-    return keypoints3d, avg_descriptors3d, clt_descriptors
+    # The reference keeps the two descriptor tensors on the host and re-uploads them in every
+    # frame's pack_data (inference.py:89-90).  Here they move to the GPU once: pack_data's
+    # .cuda() is then a no-op, and the matcher sees the same object tensors every frame and keeps
+    # the object resident (GATsSuperGlue.resident_object).  Same values, same results.
+    return keypoints3d, avg_descriptors3d.cuda(), clt_descriptors.cuda()
 
 
 def frame_step(matching_model, extractor_model, data, K_crop, keypoints3d, avg_descriptors3d,

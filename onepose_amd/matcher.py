@@ -202,7 +202,7 @@ class GATsSuperGlue(nn.Module):
                              f"{tuple(db.shape)}")
         dev = d2.device
         obj = None
-        if self.resident_object and B == 1:
+        if self.resident_object and B == 1 and hasattr(_lib.load(), "onepose_match_cached_dt"):
             obj = self._resident(data["descriptors3d_db"], data["descriptors2d_db"], d3, db, n3,
                                  nleaf, half, dev)
         return self._run(d2, s2, d3, s3, db, sl, B, n1, n3, nleaf, dev, obj)

@@ -181,7 +181,7 @@ def test_inference_cfg_entry_and_reference_call_sequence(tmp_path, device, monke
     mk2, mk3 = det["keypoints"][valid], inp["keypoints3d"][0].detach().cpu().numpy()[matches[valid]]
     pose_ref, pose_homo, inliers = pose.ransac_PnP(f.K, mk2, mk3, scale=1000)
 
-    pipe = FramePipeline(matching_model.matcher, kp3.cpu().numpy(), avg.numpy(), clt.numpy(), 1,
+    pipe = FramePipeline(matching_model.matcher, kp3.cpu().numpy(), avg.cpu().numpy(), clt.cpu().numpy(), 1,
                          len(f.keypoints2d), device, gat_tables=False)
     pipe.set_frames(f.descriptors2d[None], f.keypoints2d[None], f.K, f.pose_gt)
     pipe.enqueue(0)

@@ -11,9 +11,11 @@ B=$PWD/tools/ab/lib_ws.so
 R04=$PWD/tools/ab/lib_r04.so
 timeout -k 10 120 ./tools/ws_probe > $O/ws_probe.txt 2>&1 || { cat $O/ws_probe.txt; exit 1; }
 grep -A2 timed $O/ws_probe.txt; tail -1 $O/ws_probe.txt
+if [ -z "${NOPHASE:-}" ]; then
 timeout -k 10 180 ./tools/phase_probe ws > $O/phase_ws.txt 2>&1 || { tail -5 $O/phase_ws.txt; exit 1; }
 grep -B1 "^bf16" $O/phase_ws.txt | tail -12
-dump() { ONEPOSE_LIB=$2 timeout -k 10 300 python tools/bitcmp.py dump $O/$1.npz > $O/dump_$1.log 2>&1 || { tail -20 $O/dump_$1.log; exit 1; }; }
+fi
+dump() { ONEPOSE_LIB=$2 timeout -k 10 300 python tools/bitcmp.py dump $O/$1.npz > $O/dump_$1.log 2>&1 || { tail -20 $O/dump_$1.log; rm -f $O/*.npz; exit 1; }; }
 dump m64 $A
 dump ws $B
 dump r04 $R04
