@@ -1655,18 +1655,30 @@ int onepose_matcher_pack(const float* const* tensors, int n_tensors, void* packe
         bkv[128 * h + d] = pb[1][cr];
         bkv[128 * h + 64 + d] = pb[2][cr];
       }
-    // MLP conv 1 split: x part as is; message part folded with the merge conv
+    // MLP conv 1 split: x part as is; message part folded with the merge conv.  Each output is
+    // one double chain over j in ascending order; the merge weight is read through a
+    // transposed double copy (packed column order) and eight chains run side by side, so the
+    // fold is not bound by strided loads and one dependent chain (1.09 -> 0.19 s per model on
+    // this container's CPU; the same chains, the same bits).
+    std::vector<double> mwt((size_t)256 * 256);   // [cp][j] = merge[j][cr(cp)]
+    for (int cp = 0; cp < 256; ++cp) {   // merge input channel q*4+h -> packed h*64+q
+      const int h = cp / 64, q = cp % 64, cr = q * 4 + h;
+      for (int j = 0; j < 256; ++j) mwt[(size_t)cp * 256 + j] = (double)mw[(int64_t)j * 256 + cr];
+    }
     for (int o = 0; o < 512; ++o) {
       memcpy(w1a + (int64_t)o * 256, m0w + (int64_t)o * 512, 256 * sizeof(float));
+      const float* mo = m0w + (int64_t)o * 512 + 256;
       double bacc = (double)m0b[o];
-      for (int j = 0; j < 256; ++j) bacc += (double)m0w[(int64_t)o * 512 + 256 + j] * mb[j];
+      for (int j = 0; j < 256; ++j) bacc += (double)mo[j] * mb[j];
       b1[o] = (float)bacc;
-      for (int cp = 0; cp < 256; ++cp) {   // merge input channel q*4+h -> packed h*64+q
-        const int h = cp / 64, q = cp % 64, cr = q * 4 + h;
-        double acc = 0.0;
+      double arow[256];
+      for (int j = 0; j < 256; ++j) arow[j] = (double)mo[j];
+      for (int cp0 = 0; cp0 < 256; cp0 += 8) {
+        double acc[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+        const double* wt = mwt.data() + (size_t)cp0 * 256;
         for (int j = 0; j < 256; ++j)
-          acc += (double)m0w[(int64_t)o * 512 + 256 + j] * (double)mw[(int64_t)j * 256 + cr];
-        cw[(int64_t)o * 256 + cp] = (float)acc;
+          for (int k = 0; k < 8; ++k) acc[k] += arow[j] * wt[(size_t)k * 256 + j];
+        for (int k = 0; k < 8; ++k) cw[(int64_t)o * 256 + cp0 + k] = (float)acc[k];
       }
     }
     memcpy(w2, m3w, kApW2 * sizeof(float));

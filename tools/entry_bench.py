@@ -112,7 +112,7 @@ def main():
             print(mode, res[mode], flush=True)
 
         # where the time goes: the same "detections" loop with synchronised stage brackets
-        times = {}
+        times, calls = {}, {}
 
         def timed(name, fn):
             def w(*args, **kw):
@@ -120,7 +120,9 @@ def main():
                 t = time.perf_counter()
                 r = fn(*args, **kw)
                 torch.cuda.synchronize()
-                times[name] = times.get(name, 0.0) + time.perf_counter() - t
+                dt = time.perf_counter() - t
+                times[name] = times.get(name, 0.0) + dt
+                calls.setdefault(name, []).append(dt)
                 return r
             return w
         from onepose_amd import pose
@@ -151,6 +153,11 @@ def main():
         res["breakdown_ms_per_frame"]["rest (extractor lookup, .cpu() of matches / 3D points, "
                                       "masking, Python)"] = round(
             (tot - sum(times.values())) / a.frames * 1e3, 3)
+        # per call: the first call of a stage against a freshly loaded model pays the one-time
+        # work (weight packing, the object's resident prefix); the median is the steady state
+        res["per_call_ms"] = {k: {"first": round(v[0] * 1e3, 3),
+                                  "median": round(float(np.median(v)) * 1e3, 3), "calls": len(v)}
+                              for k, v in calls.items()}
     print(json.dumps(res))
     if a.out:
         os.makedirs(os.path.dirname(a.out), exist_ok=True)
