@@ -92,7 +92,8 @@ struct GemmProb {
   float* st_mean;
   float* st_rstd;
   float* rowstat;      // EPI_SCORE: [batch][M][ntiles][2]
-  float* colstat;      // EPI_SCORE: [batch][N][mtiles][2]
+  float* colstat;      // EPI_SCORE: [batch][mtiles][N][2] (tile-major: a tile's columns
+                       //   contiguous, so a reader's lanes over columns load 8 B each, coalesced)
   float* kvpart;       // EPI_QKV: [batch][mtiles][4][64][64]
   float* kspart;       // EPI_QKV: [batch][mtiles][256]
   const float* ksum;   // PRO_HEADZ: [batch][256] sum phi(k) of the attention source

@@ -1265,7 +1265,7 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
     if (line < BN) {   // column `line` over this tile's rows
       const float2 r = partial(tile + line, TP, rows, lo_c, BM / 4);
       if (qtr == 0 && line < cols) {
-        float* o = F(colstat) + (((int64_t)b * N + n0 + line) * mtiles + mt) * 2;
+        float* o = F(colstat) + (((int64_t)b * mtiles + mt) * N + n0 + line) * 2;
         o[0] = r.x;
         o[1] = r.y;
       }

@@ -995,12 +995,14 @@ __global__ __launch_bounds__(256) void l2norm_kernel(float* x2, int rows2, float
 // lane l takes partials l, l + 64, ...; the max and the rescaled sum over the wave's lanes.
 // Every lane returns the totals.  (conf_kernel's fused form uses the same function, so the
 // statistics are the same bits.)
-__device__ __forceinline__ float2 softmax_stats_wave(const float* p, int nt, int lane) {
+// (tile i's (max, sum exp) at p[i * stride], p[i * stride + 1])
+__device__ __forceinline__ float2 softmax_stats_wave(const float* p, int nt, int lane,
+                                                     int64_t stride = 2) {
   float mx = -INFINITY;
-  for (int i = lane; i < nt; i += 64) mx = fmaxf(mx, p[2 * i]);
+  for (int i = lane; i < nt; i += 64) mx = fmaxf(mx, p[stride * i]);
   mx = wave_max(mx);
   float s = 0.f;
-  for (int i = lane; i < nt; i += 64) s += p[2 * i + 1] * expf(p[2 * i] - mx);
+  for (int i = lane; i < nt; i += 64) s += p[stride * i + 1] * expf(p[stride * i] - mx);
   s = wave_sum(s);
   return make_float2(mx, s);
 }
@@ -1017,16 +1019,19 @@ __global__ __launch_bounds__(256) void softmax_reduce_kernel(
   const int64_t nr = (int64_t)batch * n1, nc = (int64_t)batch * n3;
   const float* p;
   int nt;
+  int64_t stride = 2;
   if (idx < nr) {
     p = rowpart + idx * ntiles3 * 2;
     nt = ntiles3;
-  } else if (idx < nr + nc) {
-    p = colpart + (idx - nr) * mtiles1 * 2;
+  } else if (idx < nr + nc) {   // colpart is tile-major: [b][mtiles1][n3][2]
+    const int64_t b = (idx - nr) / n3, c = (idx - nr) % n3;
+    p = colpart + (b * mtiles1 * n3 + c) * 2;
     nt = mtiles1;
+    stride = (int64_t)n3 * 2;
   } else {
     return;
   }
-  const float2 st = softmax_stats_wave(p, nt, lane);
+  const float2 st = softmax_stats_wave(p, nt, lane, stride);
   const float mx = st.x, s = st.y;
   if (lane == 0) {
     if (idx < nr) {
@@ -1133,12 +1138,14 @@ __global__ __launch_bounds__(kConfWaves * 64) void conf_kernel(float* S, int n1,
     {   // column tilec * 256 + t: lane 0's butterfly sum of softmax_stats_wave, nt <= 16
       const int cg = tilec * 256 + threadIdx.x;
       if (threadIdx.x < 256 && cg < n3) {
-        const float* p = scol + ((int64_t)b * n3 + cg) * mt1 * 2;
+        // (tile-major partials: one 8-B load per tile, a wave's 64 columns contiguous)
+        const float2* p = reinterpret_cast<const float2*>(scol) + (int64_t)b * mt1 * n3 + cg;
         float pm[kConfColTiles], ps[kConfColTiles];
 #pragma unroll
         for (int i = 0; i < kConfColTiles; ++i) {
-          pm[i] = i < mt1 ? p[2 * i] : -INFINITY;
-          ps[i] = i < mt1 ? p[2 * i + 1] : 0.f;
+          const float2 q = i < mt1 ? p[(int64_t)i * n3] : make_float2(-INFINITY, 0.f);
+          pm[i] = q.x;
+          ps[i] = q.y;
         }
         float mx = -INFINITY;
 #pragma unroll
