@@ -224,12 +224,14 @@ def test_object_cache_is_bit_identical(device, n1, n3, L, B, prec):
         assert (outs[1]["m0"] > -1).sum() > 100
 
 
-@pytest.mark.parametrize("precision", ["fp32", "bf16", "fp32_split"])
-def test_resident_object_forward(precision, device):
+@pytest.mark.parametrize("precision,half", [("fp32", False), ("bf16", False),
+                                            ("fp32_split", False), ("fp32", True)])
+def test_resident_object_forward(precision, half, device):
     """The drop-in forward keeps the object resident (GATsSuperGlue.resident_object): frames
     after the first start from the object's cached prefix.  Each frame's outputs equal the
     uncached forward's bit for bit; an in-place write to the object's descriptors (a version
-    bump) and a new object tensor are both re-prepared."""
+    bump) and a new object tensor are both re-prepared.  half: fp16 descriptors (config 5's
+    "fp16 desc"), converted by the kernels on both paths."""
     sd = synthetic.make_state_dict(3)
     hp = {**synthetic.DEFAULT_HPARAMS, "attention_precision": precision}
     res = matcher.from_state_dict(sd, hp).to(device)
@@ -237,6 +239,9 @@ def test_resident_object_forward(precision, device):
     unc.resident_object = False
     data, _, _ = synthetic.make_matcher_inputs(300, 1000, 8, seed=9)
     t = {k: torch.from_numpy(v).to(device) for k, v in data.items()}
+    if half:
+        for k in ("descriptors2d_query", "descriptors3d_db", "descriptors2d_db"):
+            t[k] = t[k].half()
 
     def same(tag):
         with torch.no_grad():
@@ -253,7 +258,8 @@ def test_resident_object_forward(precision, device):
     g = torch.Generator().manual_seed(4)
     for f in range(1, 3):   # new frames against the same object: the cache is reused
         t["descriptors2d_query"] = torch.nn.functional.normalize(
-            torch.randn(t["descriptors2d_query"].shape, generator=g), dim=1).to(device)
+            torch.randn(t["descriptors2d_query"].shape, generator=g), dim=1).to(
+                device, t["descriptors2d_query"].dtype)
         same(f"frame {f}")
         assert res._obj["key"] == key0
     t["descriptors3d_db"].mul_(1.5)   # in place: the version counter moves
