@@ -275,7 +275,8 @@ __device__ __forceinline__ void store_stage(float* base, Stage<T, WPL, NPL>& s) 
 // DMA: 0 = register-staged loop; 1 = the lean loop, W planes by global_load_lds and A through
 // registers; 2 = the lean loop with A from activation planes by global_load_lds as well.
 template <int EPI, int PRO, class T, int PM, bool WPL, int DMA = 0>
-__device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, StampLds* sl) {
+__device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, StampLds* sl,
+                                          int vtile = -1) {
   constexpr int BM = T::BM, BN = T::BN, FN = T::FN, PITCH = T::PITCH;
   constexpr bool BF = PM != PM_F32;   // bf16 LDS images and MFMAs
   constexpr int NPL = PM == PM_SPLIT3 ? 3 : 1;   // bf16 images per operand
@@ -306,7 +307,9 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
 
   // XCD-aware tile order: blocks are dealt round-robin over the 8 XCDs, so hand each XCD a
   // contiguous run of logical tiles -- the N-tiles of one M-tile then share that XCD's L2.
-  int bid = xcd_contiguous(blockIdx.x, gridDim.x);
+  // (vtile >= 0: the logical tile given by a caller that loops over tiles -- tools/phase_probe's
+  // persistent form; the library's kernels pass none)
+  int bid = vtile >= 0 ? vtile : xcd_contiguous(blockIdx.x, gridDim.x);
   const bool second = bid >= args.p[0].tiles;
 #define F(x) (second ? args.p[1].x : args.p[0].x)
   if (second) bid -= args.p[0].tiles;

@@ -53,6 +53,20 @@ void phase_kernel(GemmArgs args, WgRec* rec) {
   }
 }
 
+// The verdict-r04 persistent form: a grid of `gridDim.x` resident workgroups, each taking the
+// logical tiles blockIdx.x, blockIdx.x + gridDim.x, ... in turn (the production gemm_body per
+// tile; its InstanceNorm tickets are per tile, so any tile order gives the same bits).
+template <int EPI, int PRO, class T, int PM, bool WPL, int DMA>
+__global__ __launch_bounds__(T::NT) __attribute__((amdgpu_waves_per_eu(T::WPE)))
+void persist_kernel(GemmArgs args, int tiles) {
+  __shared__ StampLds sl;
+  StampTick tk{0ull, 0ull};
+  for (int t = blockIdx.x; t < tiles; t += gridDim.x) {
+    gemm_body<EPI, PRO, T, PM, WPL, DMA>(args, tk, &sl, t);
+    __syncthreads();
+  }
+}
+
 static std::vector<float> g_lastY;   // Y of the last run (first M x N)
 
 struct Bufs {
@@ -235,6 +249,54 @@ void run(const char* name, Bufs& B, int M, int N, int K, bool fin, int iters) {
   g_lastY.resize((size_t)M * N);
   hipMemcpy(g_lastY.data(), B.Y, g_lastY.size() * 4, hipMemcpyDeviceToHost);
 }
+// event time of the persistent form over `grid` workgroups; its Y against the one-shot run's
+template <int EPI, int PRO, class T, int PM = PM_F32, int DMA = 0>
+void persist_run(Bufs& B, int M, int N, int K, int grid, int iters) {
+  std::vector<float> ref = g_lastY;
+  GemmArgs a;
+  memset(&a, 0, sizeof(a));
+  a.nprob = 1;
+  GemmProb& p = a.p[0];
+  p = gemm_prob(B.A, K, B.W, K, B.b, B.Y, N, M, N, K, 1);
+  p.stats = B.stats;
+  p.st_cnt = B.cnt;
+  p.st_cnt_bs = 1024;
+  p.st_grp = B.grp;
+  p.st_mean = B.mean;
+  p.st_rstd = B.rstd;
+  p.ksplit = K - 256;
+  p.A1 = B.A + (K - 256);
+  p.lda1 = K;
+  p.ksum = B.ksum;
+  p.ns = 4096.f;
+  p.mtiles = (M + T::BM - 1) / T::BM;
+  p.ntiles = (N + T::BN - 1) / T::BN;
+  p.tiles = p.mtiles * p.ntiles;
+  hipEvent_t e0, e1;
+  hipEventCreate(&e0);
+  hipEventCreate(&e1);
+  double sum = 0;
+  for (int it = -3; it < iters; ++it) {
+    hipMemsetAsync(B.cnt, 0, 4096);
+    hipEventRecord(e0);
+    hipLaunchKernelGGL((persist_kernel<EPI, PRO, T, PM, PM != PM_F32, DMA>), dim3(grid), dim3(T::NT), 0,
+                       0, a, p.tiles);
+    hipEventRecord(e1);
+    hipEventSynchronize(e1);
+    float ms;
+    hipEventElapsedTime(&ms, e0, e1);
+    if (it >= 0) sum += ms * 1e3;
+  }
+  std::vector<float> y((size_t)M * N);
+  hipMemcpy(y.data(), B.Y, y.size() * 4, hipMemcpyDeviceToHost);
+  size_t bad = 0;
+  for (size_t i = 0; i < y.size() && i < ref.size(); ++i) bad += memcmp(&y[i], &ref[i], 4) != 0;
+  printf("persistent grid %4d: tiles %d | event %6.2f us | Y vs one-shot: %zu of %zu differ\n", grid,
+         p.tiles, sum / iters, bad, y.size());
+  hipEventDestroy(e0);
+  hipEventDestroy(e1);
+}
+
 static double maxdiff(const std::vector<float>& a, const std::vector<float>& b) {
   double d = 0;
   for (size_t i = 0; i < a.size() && i < b.size(); ++i) d = std::max(d, (double)std::fabs(a[i] - b[i]));
@@ -338,6 +400,16 @@ int main(int argc, char** argv) {
       run<EPI_QKV, PRO_PLAIN, T128x128, PM_SPLIT3, 2>("split 128x128 dma2", B, m, 768, 256, false, it);
       run<EPI_QKV, PRO_PLAIN, T64x128, PM_BF16, 2>("bf16 64x128 dma2", B, m, 768, 256, false, it);
       run<EPI_QKV, PRO_PLAIN, T128x128, PM_BF16, 2>("bf16 128x128 dma2", B, m, 768, 256, false, it);
+    }
+    return 0;
+  }
+  if (argc > 1 && !strcmp(argv[1], "persist")) {   // round 5: the persistent form of fp32 MLP conv 1
+    for (int m : {5120, 10240}) {
+      printf("--- fp32 mlp1 STATS+HEADZ+fin, M %d: one-shot grid vs persistent grids ---\n", m);
+      for (int r = 0; r < 2; ++r) {
+        run<EPI_STATS, PRO_HEADZ, T64x64>("fp32 64x64 one-shot", B, m, 512, 512, true, it);
+        for (int g : {256, 512, 768}) persist_run<EPI_STATS, PRO_HEADZ, T64x64>(B, m, 512, 512, g, it);
+      }
     }
     return 0;
   }
