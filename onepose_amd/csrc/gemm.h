@@ -182,7 +182,8 @@ inline int stats_groups(int M, int rows) {
   return (mtiles + g - 1) / g;
 }
 
-// gemm_bal.hip: MLP conv 1 (EPI_STATS + PRO_HEADZ, fp32, N = K = 512) on the tile-balanced
+// tools/experiments/gemm_bal.hip (an evaluated alternative, not in the library: DESIGN.md §8b;
+// linked only into -DONEPOSE_BAL builds): MLP conv 1 (EPI_STATS + PRO_HEADZ, fp32, N = K = 512) on the tile-balanced
 // kernel (64 x 32 strips dealt evenly to one 8-wave workgroup per CU, the same bits as the
 // 64 x 64 tile) when the 64 x 64 grid would load CUs unevenly (at most 3 tiles per CU).
 // Returns false, launching nothing, when it does not apply; otherwise *rc is the launch status.
@@ -203,7 +204,7 @@ __device__ __forceinline__ float headz_fold(float acc, float z, float acc_h) {
 }
 
 // InstanceNorm merges of MLP conv 1's in-launch finalize, shared by gemm.hip's 64 x 64 tile and
-// gemm_bal.hip so that both round every operation alike: each statement exactly as written
+// tools/experiments/gemm_bal.hip so that both round every operation alike: each statement exactly as written
 // (contraction off -- left to itself the compiler fused some of these in one kernel and not in
 // the other), with fma() where the merge takes one.
 // (count, mean, M2) of a 32-row block into the running column statistics (Chan et al.)

@@ -1347,7 +1347,7 @@ __global__ __launch_bounds__(256) void mutual_kernel(const unsigned long long* r
 // ------------------------------------------------------------------------------------
 namespace {
 
-// MLP conv 1's finalize counters per sample: column blocks of 32 (gemm_bal.hip's strips; the
+// MLP conv 1's finalize counters per sample: column blocks of 32 (tools/experiments/gemm_bal.hip's strips; the
 // 64 x 64 tile uses the first 512 / 64 of them), then that many per stats group
 constexpr int kCntPerSide = 512 / 32;
 

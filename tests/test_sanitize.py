@@ -34,7 +34,7 @@ def test_oracle_under_asan_ubsan(tmp_path):
     assert report.count("status") == 12
 
 
-SRCS = ("matcher", "gemm", "gemm_bal", "pnp", "frame_ops", "superpoint")
+SRCS = ("matcher", "gemm", "pnp", "frame_ops", "superpoint")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
 

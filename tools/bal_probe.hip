@@ -3,7 +3,7 @@
 // Y, the per-M-tile (mean, M2) partials, the group partials, mean, rstd.  Reports the first
 // mismatches by (problem, sample, row, column).
 //   hipcc -O3 --offload-arch=gfx950 -std=c++17 -w -DONEPOSE_BAL -Ionepose_amd/csrc tools/bal_probe.hip \
-//     onepose_amd/csrc/gemm.hip onepose_amd/csrc/gemm_bal.hip -o tools/bal_probe
+//     onepose_amd/csrc/gemm.hip tools/experiments/gemm_bal.hip -o tools/bal_probe
 #include <hip/hip_runtime.h>
 #include <cstdarg>
 #include <cstdio>
