@@ -293,13 +293,54 @@ class NormalizedDataset:
     def __len__(self):
         return len(self.img_lists)
 
-    def batches(self):
-        """What ``DataLoader(dataset, num_workers=1)`` yields: each item collated into a
-        batch of one (``path`` a list, ``image`` [1,...] and ``size`` [1,2] tensors)."""
-        for i in range(len(self)):
-            d = self[i]
-            yield {"path": [d["path"]], "image": torch.from_numpy(d["image"])[None],
-                   "size": torch.from_numpy(d["size"])[None]}
+    def batches(self, prefetch: int = 2):
+        """What ``DataLoader(dataset, num_workers=1)`` (inference.py:108) yields: each item
+        collated into a batch of one (``path`` a list, ``image`` [1,...] and ``size`` [1,2]
+        tensors), in order.  As with that loader's one worker (default prefetch_factor 2), the
+        items are read ahead by one background worker -- a thread here: the image decode
+        releases the GIL -- so reading frame k + 1 overlaps frame k's GPU work.  A worker
+        error is raised to the consumer at the item it belongs to."""
+        import queue
+        import threading
+        q = queue.Queue(maxsize=max(1, prefetch))
+        done = object()
+        stop = threading.Event()
+
+        def put(x):
+            while not stop.is_set():
+                try:
+                    q.put(x, timeout=0.1)
+                    return True
+                except queue.Full:
+                    pass
+            return False
+
+        def work():
+            try:
+                for i in range(len(self)):
+                    d = self[i]
+                    item = {"path": [d["path"]], "image": torch.from_numpy(d["image"])[None],
+                            "size": torch.from_numpy(d["size"])[None]}
+                    if not put(item):
+                        return
+            except BaseException as e:   # handed to the consumer
+                put(e)
+                return
+            put(done)
+
+        th = threading.Thread(target=work, name="onepose-image-reader", daemon=True)
+        th.start()
+        try:
+            while True:
+                item = q.get()
+                if item is done:
+                    break
+                if isinstance(item, BaseException):
+                    raise item
+                yield item
+        finally:
+            stop.set()
+            th.join()
 
 
 def load_object(paths, num_leaf):

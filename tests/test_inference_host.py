@@ -147,6 +147,22 @@ def test_normalized_dataset_batches(tmp_path):
     np.testing.assert_array_equal(b["image"][0, 0].numpy(), a.astype(np.float32) / 255.0)
     with pytest.raises(ValueError):
         I.NormalizedDataset([], {})
+    # several images: read ahead by the worker, yielded in order; a bad file raises at its item;
+    # a consumer that stops early does not leave the worker behind
+    for i in (1, 2, 3):
+        Image.fromarray((a + i).astype(np.uint8), mode="L").save(tmp_path / f"{i}.png")
+    files = [str(tmp_path / f"{i}.png") for i in range(4)]
+    ds = I.NormalizedDataset(files, confs["superpoint"]["preprocessing"])
+    got = [b["path"][0] for b in ds.batches()]
+    assert got == files
+    bad = I.NormalizedDataset(files[:2] + [str(tmp_path / "missing.png")], {})
+    it = bad.batches()
+    assert next(it)["path"] == [files[0]] and next(it)["path"] == [files[1]]
+    with pytest.raises(Exception):
+        next(it)
+    it = ds.batches()
+    next(it)
+    it.close()
 
 
 def test_extractor_conf_threshold_typo():
