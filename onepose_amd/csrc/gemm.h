@@ -136,6 +136,8 @@ enum GemmTile {
                       //   32 x 128, one workgroup per CU; a stage's W rows are fetched once per 256
                       //   output rows instead of 64.  Its InstanceNorm partials, tickets and acc0
                       //   are the 64 x 128 tile's (gemm_tile_stat_rows = 64): same workspace, same bits
+  TILE_128x128W8 = 10, // split-mode MLP conv 1 (STATS + HEADZ, DMA 2): 128 x 128 on 8 waves of
+                       //   32 x 64, standing in for 64 x 64 tiles the same way (acc0 included)
 };
 // Output tile shape of each configuration, usable in constant expressions (the workspace
 // plan sizes per-tile partials and counters from these; tile_dims in gemm.hip agrees).
@@ -143,12 +145,17 @@ constexpr int gemm_tile_bm(int t) {
   return (t == TILE_32x128 || t == TILE_32x64W2 || t == TILE_32x256W8) ? 32
          : (t == TILE_128x128 || t == TILE_128x64W8) ? 128
          : t == TILE_256x128W8                       ? 256
+         : t == TILE_128x128W8                       ? 128
                                                      : 64;
 }
 // rows per EPI_STATS partial (and per acc0 tile): the tile's, or its stand-in tile's
-constexpr int gemm_tile_stat_rows(int t) { return t == TILE_256x128W8 ? 64 : gemm_tile_bm(t); }
+constexpr int gemm_tile_stat_rows(int t) {
+  return (t == TILE_256x128W8 || t == TILE_128x128W8) ? 64 : gemm_tile_bm(t);
+}
 constexpr int gemm_tile_bn(int t) {
-  return (t == TILE_32x128 || t == TILE_64x128 || t == TILE_128x128 || t == TILE_256x128W8) ? 128
+  return (t == TILE_32x128 || t == TILE_64x128 || t == TILE_128x128 || t == TILE_256x128W8 ||
+          t == TILE_128x128W8)
+             ? 128
          : t == TILE_64x32K2                                        ? 32
          : t == TILE_32x256W8                                       ? 256
                                                                     : 64;

@@ -64,7 +64,8 @@ struct FragT<PM_SPLIT3, KKW, FN> {   // hi / mid / lo pieces
 
 constexpr int kScoreGroup = 8;   // N-tiles per column group of the score grid
 
-template <int BM_, int BN_, int KS_, int NW_, int BKS_, int WPE_ = 3, int SUB_ = BM_>
+template <int BM_, int BN_, int KS_, int NW_, int BKS_, int WPE_ = 3, int SUB_ = BM_,
+          int SUBN_ = BN_>
 struct Tile {
   static constexpr int BM = BM_, BN = BN_, KS = KS_, NW = NW_, BKS = BKS_;
   static constexpr int WPE = WPE_;              // amdgpu_waves_per_eu hint
@@ -73,6 +74,7 @@ struct Tile {
   // workspace layout and every result bit are the smaller tile's
   static constexpr int SUB = SUB_;
   static constexpr int NSUB = BM / SUB;
+  static constexpr int SUBN = SUBN_;   // columns of the stand-in tile (its acc0 layout)
   static constexpr int NT = 64 * NW;            // threads
   static constexpr int WM = BM / 32;            // waves along M
   static constexpr int WN = NW / (WM * KS);     // waves along N
@@ -538,19 +540,27 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
 #pragma unroll
       for (int i = 0; i < 16; ++i) acc[j][i] = a0p[j * 1024 + i * 64];
   } else if (acc0 != nullptr) {
-    // acc0 as the 64 x 128 four-wave tile stored it (2 x 2 waves of 32 x 64, FN 2): this wave's
-    // 32 rows are sub-tile wm / 2's wave row wm % 2, its 32-column block j that tile's wave
-    // column j / 2, accumulator j % 2 (sub-tiles past M hold nothing and are never stored)
-    static_assert(T::NSUB == 1 || (T::SUB == 64 && BN == 128 && T::WN == 1 && T::KS == 1),
-                  "acc0 of 64 x 128 sub-tiles");
+    // acc0 as the 64 x SUBN four-wave tile stored it (2 x 2 waves of 32 x SUBN / 2, FNp
+    // accumulators each): this wave's 32 rows are sub-tile wm / 2's wave row wm % 2; its
+    // 32-column block cb (global column n0 + 32 cb) is that tile's column tile (n0 + 32 cb) /
+    // SUBN, wave column cbp / FNp, accumulator cbp % FNp for cbp = its block within that tile
+    // (sub-tiles past M hold nothing and are never stored)
+    constexpr int SN = T::SUBN, FNP = SN / 64;
+    static_assert(T::NSUB == 1 || (T::SUB == 64 && T::KS == 1 && (SN == 64 || SN == 128) &&
+                                   (BN % SN == 0 || SN % BN == 0)),
+                  "acc0 of 64-row sub-tiles");
     const int st = mt * T::NSUB + wm / 2;
+    const int ntp = c.N / SN;   // the stand-in grid's column tiles
     if (st * 64 < c.M) {
-      const float* a0p = acc0 + b * F(acc0_bs) + lane +
-                         ((int64_t)(st * ntiles + nt) * 4 + (wm % 2) * 2) * 2 * 1024;
+      const float* a0b = acc0 + b * F(acc0_bs) + lane;
 #pragma unroll
-      for (int j = 0; j < FN; ++j)
+      for (int j = 0; j < FN; ++j) {
+        const int gc = n0 + (wn * FN + j) * 32, cbp = (gc % SN) / 32;
+        const float* a0p = a0b + ((int64_t)(st * ntp + gc / SN) * 4 + (wm % 2) * 2 + cbp / FNP) *
+                                     FNP * 1024 + (cbp % FNP) * 1024;
 #pragma unroll
-        for (int i = 0; i < 16; ++i) acc[j][i] = a0p[((j / 2) * 2 + (j % 2)) * 1024 + i * 64];
+        for (int i = 0; i < 16; ++i) acc[j][i] = a0p[i * 64];
+      }
     }
   }
   if constexpr (DMA >= 1) {
@@ -938,10 +948,6 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
     }
     return;
   }
-  // STATS on a stand-in tile: Y is stored from the registers (2 rows x 128 B per instruction)
-  // instead of through a 256-row LDS staging tile
-  constexpr bool kDirect = false;   // (EPI == EPI_STATS && T::NSUB > 1: measured no faster)
-  float ydir[kDirect ? FN : 1][16];
   if (ks == 0) {
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
@@ -961,8 +967,7 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
           y = acc[j][i] + bias;
         }
         yv[i] = (gm < M) ? y : 0.f;
-        if constexpr (kDirect) ydir[j][i] = yv[i];
-        else if (kStage || kRowStore) tile[row * TP + col] = yv[i];
+        if (kStage || kRowStore) tile[row * TP + col] = yv[i];
       }
       if (EPI == EPI_STATS) {
         // the column's (mean, M2) over this wave's 32 rows, from the registers: each lane's 16
@@ -997,18 +1002,6 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
   if (yp != nullptr) yp += b * F(yp_bs);
   const int64_t ypl = F(ypl);
   auto row_store = [&]() __attribute__((always_inline)) {
-    if constexpr (kDirect) {
-#pragma unroll
-      for (int j = 0; j < FN; ++j) {
-        const int col = wn * FN * 32 + j * 32 + (lane & 31);
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const int gm = m0 + wm * 32 + (i & 3) + 8 * (i >> 2) + 4 * (lane >> 5);
-          if (gm < M) Y[(int64_t)gm * ldy + n0 + col] = ydir[j][i];
-        }
-      }
-      return;
-    }
     constexpr int C4 = BN / 4, PER = BM * C4 / T::NT;   // float4 per row, per thread
     static_assert(BM * C4 % T::NT == 0, "row-store pass");
     float4 rv[EPI == EPI_RESID ? PER : 1];
@@ -1295,6 +1288,7 @@ using T128x64W8 = Tile<128, 64, 1, 8, 32>;
 using T32x64W2 = Tile<32, 64, 1, 2, 32>;
 using T32x256W8 = Tile<32, 256, 1, 8, 64, 1>;
 using T256x128W8 = Tile<256, 128, 1, 8, 32, 2, 64>;
+using T128x128W8S = Tile<128, 128, 1, 8, 32, 2, 64, 64>;   // split MLP conv 1 for the 64 x 64 tile
 
 
 template <int EPI, int PRO, class T, int PM, bool WPL = false, int DMA = 0>
@@ -1325,6 +1319,7 @@ TileDims tile_dims(int tile) {
     case TILE_32x64W2: return {32, 64, 32};
     case TILE_32x256W8: return {32, 256, 64};
     case TILE_256x128W8: return {256, 128, 32};
+    case TILE_128x128W8: return {128, 128, 32};
 
     default: return {0, 0, 0};
   }
@@ -1342,7 +1337,8 @@ static_assert(gemm_tile_bm(TILE_64x64) == 64 && gemm_tile_bn(TILE_64x64) == 64 &
                   gemm_tile_bm(TILE_128x64W8) == 128 && gemm_tile_bn(TILE_128x64W8) == 64 &&
                   gemm_tile_bm(TILE_32x64W2) == 32 && gemm_tile_bn(TILE_32x64W2) == 64 &&
                   gemm_tile_bm(TILE_32x256W8) == 32 && gemm_tile_bn(TILE_32x256W8) == 256 &&
-                  gemm_tile_bm(TILE_256x128W8) == 256 && gemm_tile_bn(TILE_256x128W8) == 128,
+                  gemm_tile_bm(TILE_256x128W8) == 256 && gemm_tile_bn(TILE_256x128W8) == 128 &&
+                  gemm_tile_bm(TILE_128x128W8) == 128 && gemm_tile_bn(TILE_128x128W8) == 128,
               "gemm.h tile shapes must match tile_dims");
 
 GemmProb gemm_prob(const float* A, int lda, const float* W, int ldw, const float* bias,
@@ -1401,6 +1397,9 @@ int gemm_launch(int epi, int pro, int tile, GemmArgs& args, hipStream_t stream, 
     OP_REQUIRE(tile != TILE_256x128W8 || (epi == EPI_STATS && pro == PRO_HEADZ && pm == PM_BF16 &&
                                           P.N == 512 && P.ksplit == 256),
                "gemm: the 256 x 128 tile is bf16 MLP conv 1's");
+    OP_REQUIRE(tile != TILE_128x128W8 || (epi == EPI_STATS && pro == PRO_HEADZ && pm == PM_SPLIT3 &&
+                                          P.N == 512 && P.ksplit == 256),
+               "gemm: the 128 x 128 eight-wave tile is the split mode's MLP conv 1");
     OP_REQUIRE(epi != EPI_BIAS_L2 || (td.bn == 256 && P.N == 256 && P.ldy % 4 == 0),
                "gemm: BIAS_L2 tiles hold whole 256-column rows");
     OP_REQUIRE((epi != EPI_BIAS && epi != EPI_STATS && epi != EPI_RESID) ||
@@ -1487,6 +1486,7 @@ int gemm_launch(int epi, int pro, int tile, GemmArgs& args, hipStream_t stream, 
   CASE(EPI_RESID, PRO_NORM_RELU, TILE_32x64W2, T32x64W2, PM_SPLIT3, true)
   CASE(EPI_QKV, PRO_PLAIN, TILE_32x128, T32x128, PM_SPLIT3, true)
   CASE(EPI_STATS, PRO_HEADZ, TILE_64x64, T64x64, PM_SPLIT3, true)
+  CASE(EPI_STATS, PRO_HEADZ, TILE_128x128W8, T128x128W8S, PM_SPLIT3, true)
   CASE(EPI_QKV, PRO_PLAIN, TILE_64x128, T64x128, PM_SPLIT3, true)
   CASE(EPI_RESID, PRO_NORM_RELU, TILE_64x64, T64x64, PM_SPLIT3, true)
   // final projection and score GEMM in the split mode (activations as W: VALU split)

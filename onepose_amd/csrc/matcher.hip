@@ -1397,17 +1397,33 @@ constexpr int kTileBf16Mlp1 = TILE_256x128W8;
 #else
 constexpr int kTileBf16Mlp1 = kTileBf16;
 #endif
-int mlp1_tile(int pm) { return pm == PM_BF16 ? kTileBf16Mlp1 : kTileMLP1; }
+// The split mode's MLP conv 1 runs on the 8-wave 128 x 128 tile (TILE_128x128W8), standing in
+// for its 64 x 64 tiles (the same partials, tickets, acc0 and bits): 160 workgroups at config 2,
+// one per CU, leave the other CUs to the other frame's kernels -- split line 1767 / 1772 ->
+// 1878 / 1882 frames/s, same box (profiles/r05/wsplit/).  The fp32 MLP
+// conv 1 measured slower on it (1699 / 1701 -> 1602 / 1609: its loop is MFMA-bound, so fewer
+// CUs cost time; profiles/r05/wf32/) and keeps 64 x 64.  (-DONEPOSE_MLP1_SPLIT_64: the 64 x 64
+// split tile, for A/B builds.)
+#ifdef ONEPOSE_MLP1_SPLIT_64
+constexpr int kTileSplitMlp1 = kTileMLP1;
+#else
+constexpr int kTileSplitMlp1 = TILE_128x128W8;
+#endif
+int mlp1_tile(int pm) {
+  return pm == PM_BF16 ? kTileBf16Mlp1 : pm == PM_SPLIT3 ? kTileSplitMlp1 : kTileMLP1;
+}
 int mlp1_acc_tile(int pm) { return pm == PM_BF16 ? kTileBf16 : kTileMLP1; }
 // make_plan sizes MLP conv 1's InstanceNorm partials (stats rows `str`), its arrival counters
 // (kCntPerSide column blocks) and group partials once for every precision: each precision's
 // MLP conv 1 tile must have those rows and at most that many column blocks over N = 512.
 static_assert(gemm_tile_stat_rows(kTileBf16) == gemm_tile_bm(kTileMLP1) &&
-                  gemm_tile_stat_rows(kTileBf16Mlp1) == gemm_tile_bm(kTileMLP1),
+                  gemm_tile_stat_rows(kTileBf16Mlp1) == gemm_tile_bm(kTileMLP1) &&
+                  gemm_tile_stat_rows(kTileSplitMlp1) == gemm_tile_bm(kTileMLP1),
               "MLP conv 1 tiles of all precisions must share their partials' row count");
 static_assert(512 / gemm_tile_bn(kTileMLP1) <= kCntPerSide &&
                   512 / gemm_tile_bn(kTileBf16) <= kCntPerSide &&
-                  512 / gemm_tile_bn(kTileBf16Mlp1) <= kCntPerSide,
+                  512 / gemm_tile_bn(kTileBf16Mlp1) <= kCntPerSide &&
+                  512 / gemm_tile_bn(kTileSplitMlp1) <= kCntPerSide,
               "MLP conv 1 column blocks exceed the plan's counters");
 
 int qkv_tile_for(int n3, int B) {
@@ -2104,9 +2120,10 @@ int attention_layer(const ApW& w, const Side* sd, int nside, int B, const Plan& 
         a.p[i].ldap1 = 256;
       }
     }
-    // (the 256-row tile's loop reads A from its planes: without them, the 64 x 128 DMA-1 tile)
-    if ((rc = gemm_launch(EPI_STATS, PRO_HEADZ, ap ? mlp1_tile(pm) : mlp1_acc_tile(pm), a, st,
-                          K_MLP1, pm)) != ONEPOSE_OK)
+    // (the bf16 / split modes' wide tiles read A from its planes: without them, the tile of
+    // the EPI_ACC launch)
+    const int t1 = (pm != PM_F32 && !ap) ? mlp1_acc_tile(pm) : mlp1_tile(pm);
+    if ((rc = gemm_launch(EPI_STATS, PRO_HEADZ, t1, a, st, K_MLP1, pm)) != ONEPOSE_OK)
       return rc;
   }
   // 5. InstanceNorm statistics: finalized inside MLP conv 1 by each column block's last
