@@ -845,7 +845,10 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
     // 2m + 1 from lane halves 0, 1) read their operands as float4 runs of one column, and the
     // phi(k) column sums run down the column in row order: the same sums, in the same order, as
     // a row-major staging.
-    static_assert(BN == 128 && T::NW == 4 && T::KS == 1, "QKV tile is [k_h | v_h]");
+    // (a stand-in tile, SUB = 64 < BM, writes its 64-row sub-tiles' partials: the same chunks,
+    // sums and bits as the 64-row tile; four waves per sub-tile)
+    static_assert(BN == 128 && T::NW == 4 * T::NSUB && T::KS == 1 && (T::NSUB == 1 || T::SUB == 64),
+                  "QKV tile is [k_h | v_h]");
     constexpr int PT = BM + 4;
     const bool q_tile = n0 < 256;
     constexpr int HALF = BM / 2;
@@ -907,11 +910,15 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
       return;
     }
     const int h = (n0 - 256) / 128;
-    if (t < 64) {   // sum phi(k) over the tile's rows, in row order (invalid rows hold 0)
-      const float* cp = tileT + t * PT;
+    constexpr int SH = HALF / T::NSUB;   // a sub-tile's rows per half
+    const int mtiles_s = T::NSUB == 1 ? mtiles : (M + 63) / 64;
+    if (t < 64 * T::NSUB && (t / 64) * (BM / T::NSUB) < rows) {
+      // sum phi(k) over the (sub-)tile's rows, in row order (invalid rows hold 0)
+      const int sb = t / 64, tc = t % 64;
+      const float* cp = tileT + tc * PT + sb * SH;
       float s = 0.f;
 #pragma unroll
-      for (int q = 0; q < HALF; q += 4) {
+      for (int q = 0; q < SH; q += 4) {
         const float4 ev = *reinterpret_cast<const float4*>(cp + q);
         const float4 od = *reinterpret_cast<const float4*>(cp + HALF + q);
         s += ev.x;
@@ -923,16 +930,18 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
         s += ev.w;
         s += od.w;
       }
-      F(kspart)[((int64_t)b * mtiles + mt) * 256 + h * 64 + t] = s;
+      F(kspart)[((int64_t)b * mtiles_s + mt * T::NSUB + sb) * 256 + h * 64 + tc] = s;
     }
-    const int wd = wave >> 1, wq = wave & 1;
+    const int sbw = wave / 4, wv = wave % 4;   // the wave's sub-tile
+    if (sbw * (BM / T::NSUB) >= rows) return;   // (a sub-tile past M: no chunk)
+    const int wd = wv >> 1, wq = wv & 1;
     floatx16 kv;
 #pragma unroll
     for (int i = 0; i < 16; ++i) kv[i] = 0.f;
-    const float* ka = tileT + (wd * 32 + (lane & 31)) * PT + HALF * (lane >> 5);
-    const float* vb = tileT + (64 + wq * 32 + (lane & 31)) * PT + HALF * (lane >> 5);
+    const float* ka = tileT + (wd * 32 + (lane & 31)) * PT + HALF * (lane >> 5) + sbw * SH;
+    const float* vb = tileT + (64 + wq * 32 + (lane & 31)) * PT + HALF * (lane >> 5) + sbw * SH;
 #pragma unroll
-    for (int q = 0; q < HALF; q += 4) {   // MFMAs m = q .. q + 3: rows 2m + lane half
+    for (int q = 0; q < SH; q += 4) {   // MFMAs m = q .. q + 3: rows 2m + lane half
       const float4 a4 = *reinterpret_cast<const float4*>(ka + q);
       const float4 b4 = *reinterpret_cast<const float4*>(vb + q);
       kv = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.x, b4.x, kv, 0, 0, 0);
@@ -940,7 +949,7 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
       kv = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.z, b4.z, kv, 0, 0, 0);
       kv = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.w, b4.w, kv, 0, 0, 0);
     }
-    float* out = F(kvpart) + (((int64_t)b * mtiles + mt) * 4 + h) * 4096;
+    float* out = F(kvpart) + (((int64_t)b * mtiles_s + mt * T::NSUB + sbw) * 4 + h) * 4096;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const int d = wd * 32 + (i & 3) + 8 * (i >> 2) + 4 * (lane >> 5);
@@ -1398,8 +1407,9 @@ int gemm_launch(int epi, int pro, int tile, GemmArgs& args, hipStream_t stream, 
                                           P.N == 512 && P.ksplit == 256),
                "gemm: the 256 x 128 tile is bf16 MLP conv 1's");
     OP_REQUIRE(tile != TILE_128x128W8 || (epi == EPI_STATS && pro == PRO_HEADZ && pm == PM_SPLIT3 &&
-                                          P.N == 512 && P.ksplit == 256),
-               "gemm: the 128 x 128 eight-wave tile is the split mode's MLP conv 1");
+                                          P.N == 512 && P.ksplit == 256) ||
+                   (epi == EPI_QKV && pm == PM_F32),
+               "gemm: the 128 x 128 eight-wave tile is the split mode's MLP conv 1 and fp32 QKV's");
     OP_REQUIRE(epi != EPI_BIAS_L2 || (td.bn == 256 && P.N == 256 && P.ldy % 4 == 0),
                "gemm: BIAS_L2 tiles hold whole 256-column rows");
     OP_REQUIRE((epi != EPI_BIAS && epi != EPI_STATS && epi != EPI_RESID) ||
@@ -1462,6 +1472,7 @@ int gemm_launch(int epi, int pro, int tile, GemmArgs& args, hipStream_t stream, 
   }
   CASE(EPI_QKV, PRO_PLAIN, TILE_32x128, T32x128, PM_F32, false)
   CASE(EPI_QKV, PRO_PLAIN, TILE_64x128, T64x128, PM_F32, false)
+  CASE(EPI_QKV, PRO_PLAIN, TILE_128x128W8, T128x128W8S, PM_F32, false)
   CASE(EPI_QKV, PRO_PLAIN, TILE_128x128, T128x128, PM_F32, false)
   CASE(EPI_STATS, PRO_HEADZ, TILE_64x64, T64x64, PM_F32, false)
   CASE(EPI_RESID, PRO_NORM_RELU, TILE_64x64, T64x64, PM_F32, false)

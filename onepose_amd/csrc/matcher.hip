@@ -1426,9 +1426,21 @@ static_assert(512 / gemm_tile_bn(kTileMLP1) <= kCntPerSide &&
                   512 / gemm_tile_bn(kTileSplitMlp1) <= kCntPerSide,
               "MLP conv 1 column blocks exceed the plan's counters");
 
+// the bf16 / split modes' QKV tile (the split mode on the 128 x 128 stand-in measured no faster:
+// 1874 / 1847 -> 1838 / 1855 frames/s, profiles/r05/qwide/)
+int qkv_tile_planes(int pm) { (void)pm; return kTileBf16; }
+
 int qkv_tile_for(int n3, int B) {
   const int64_t t64 = (int64_t)ceil_div(n3, 64) * 6 * (B > kFusedFoldMaxBatch ? B : 1);
+  // (64 x 128 from kQkvWideTiles on through round 5; the 8-wave 128 x 128 stand-in -- 64-row KV
+  // chunks, the same bits -- measured +1.1 / +1.4% frames/s at config 2 in profiles/r05/qwide/, and
+  // +0.3% at 300 steps / level at 20 on the confirming run, profiles/r05/qconf/: a marginal gain;
+  // -DONEPOSE_QKV_NARROW: the 64 x 128 tile, for A/B builds)
+#ifdef ONEPOSE_QKV_NARROW
   return t64 >= kQkvWiderTiles ? TILE_128x128 : t64 >= kQkvWideTiles ? TILE_64x128 : kTileKV;
+#else
+  return t64 >= kQkvWiderTiles ? TILE_128x128 : t64 >= kQkvWideTiles ? TILE_128x128W8 : kTileKV;
+#endif
 }
 
 bool valid_precision(int p) {
@@ -1870,7 +1882,7 @@ int mlp2_tile_for(int64_t t64, int pm) {
 // Every side the same choices, from the launch as a whole (layers 4-11, sharded frames).
 LayerTiles layer_tiles(int qkv_n3, const Side* sd, int nside, int B, int pm, bool sharded) {
   LayerTiles t;
-  const int q = pm == PM_F32 ? qkv_tile_for(qkv_n3, B) : kTileBf16;
+  const int q = pm == PM_F32 ? qkv_tile_for(qkv_n3, B) : qkv_tile_planes(pm);
   // kv_fold re-reads the whole 128 KB C_h panel per workgroup (64 of them per side and
   // sample): one launch instead of two pays at small batches; at B = 32 the separate MFMA
   // m_fold (16 KB of C per workgroup) is cheaper (config 3: 1.68 vs 2.02 ms per step).
@@ -1894,8 +1906,8 @@ LayerTiles layer_tiles(int qkv_n3, const Side* sd, int nside, int B, int pm, boo
 // take the choice over both sides there.
 LayerTiles side_tiles(int n1, int n3, int B, int pm, bool cross) {
   LayerTiles t;
-  t.qkv[0] = pm == PM_F32 ? qkv_tile_for(n1, B) : kTileBf16;
-  t.qkv[1] = pm == PM_F32 ? qkv_tile_for(n3, 1) : kTileBf16;
+  t.qkv[0] = pm == PM_F32 ? qkv_tile_for(n1, B) : qkv_tile_planes(pm);
+  t.qkv[1] = pm == PM_F32 ? qkv_tile_for(n3, 1) : qkv_tile_planes(pm);
   t.fused_fold[0] = B <= kFusedFoldMaxBatch;
   t.fused_fold[1] = true;
   const int64_t t2 = (int64_t)ceil_div(n1, 64) * 4 * B, t3 = (int64_t)ceil_div(n3, 64) * 4;
@@ -2014,7 +2026,7 @@ int attention_layer(const ApW& w, const Side* sd, int nside, int B, const Plan& 
   auto mf_of = [&](int side) { return p.mf + (size_t)side * B * kMfFloats; };
   // bf16 modes: W operands as bf16 planes (gemm.h GemmProb::Wp)
   const bool planes = pm != PM_F32;
-  auto chunks = [&](int i) { return ceil_div(sd[i].n, gemm_tile_rows(tl.qkv[i])); };
+  auto chunks = [&](int i) { return ceil_div(sd[i].n, gemm_tile_stat_rows(tl.qkv[i])); };
   rc = groups(nsrc, [&](int a, int b) { return tl.fused_fold[a] == tl.fused_fold[b]; },
               [&](int i0, int i1) -> int {
     float* kv = p.kv + (size_t)i0 * B * 16384;
@@ -2478,7 +2490,7 @@ int object_prepare_impl(const void* packed_weights, const void* desc3d, int desc
     KvFoldArgs ka;
     ka.ct = w.ct;
     ka.planes = pm != PM_F32 ? 1 : 0;
-    ka.p[0] = {p.kvpart3, p.kspart3, ceil_div(n3, gemm_tile_rows(tl.qkv[0]))};
+    ka.p[0] = {p.kvpart3, p.kspart3, ceil_div(n3, gemm_tile_stat_rows(tl.qkv[0]))};
     ka.mf[0] = cache + L.mf;
     ka.mf[1] = nullptr;
     prof_pre(K_KV_REDUCE, st);
