@@ -71,6 +71,30 @@ def test_matcher_deterministic(precision, device):
     np.testing.assert_array_equal(a[0]["matches0"], b[0]["matches0"])
 
 
+_ORACLE_4100 = {}
+
+
+@pytest.mark.parametrize("precision", ["fp32", "fp32_split"])
+@pytest.mark.parametrize("n1", [900, 1000])
+def test_stand_in_tiles_ragged_vs_oracle(n1, precision, device):
+    """The 8-wave 128-row tiles that stand in for 64-row tiles (fp32 QKV from 256 64-row tiles
+    of the 3D side, the split mode's MLP conv 1) on ragged sides: n3 = 4100 (65 64-row tiles)
+    puts both sides' QKV on the 128-row tile; its last tile holds 4 rows of the 3D side and, for
+    n1 = 900, 4 rows of the 2D side (the second 64-row sub-tile past M: no KV chunk, no
+    InstanceNorm partial), for n1 = 1000 40 rows in the second sub-tile.  Against the oracle
+    under the exact-index contract."""
+    from oracle import matcher_np as M
+    sd = synthetic.make_state_dict(12)
+    data, _, _ = synthetic.make_matcher_inputs(n1, 4100, 8, seed=12)
+    pred, conf = run_matcher(sd, data, device, precision=precision)
+    if n1 not in _ORACLE_4100:   # (~10 s each; shared by the two precisions)
+        _ORACLE_4100[n1] = M.forward(sd, data)
+    opred, oconf = _ORACLE_4100[n1]
+    np.testing.assert_allclose(conf, oconf, atol=ATOL)
+    assert_pred_equal(pred, opred, f"{precision} n1={n1} n3=4100")
+    assert (pred["matches0"] > -1).sum() > 100
+
+
 @pytest.mark.parametrize("n1,n3,L,seed", [(256, 512, 8, 0), (1024, 4096, 8, 1)])
 def test_split_precision_is_fp32_accurate(n1, n3, L, seed, device):
     """ONEPOSE_PREC_FP32_SPLIT (every GEMM on three bf16 pieces per operand, six products)
