@@ -1080,6 +1080,7 @@ __device__ __forceinline__ unsigned long long shfl_xor_u64(unsigned long long v,
 // bits, one dependent launch fewer on the frame's chain.  The packed column winners must be
 // zero before the launch (transpose_in zeroes them).
 constexpr int kConfColTiles = 16;   // column partials (score M-tiles) the fused form takes
+constexpr int kConfRowTiles = 64;   // row partials (score N-tiles) the fused form takes
 constexpr int kConfWaves = 8, kConfRows = 4;   // 32 rows per workgroup: 8 waves x 4 rows
 template <bool VEC, bool STATS>
 __global__ __launch_bounds__(kConfWaves * 64) void conf_kernel(float* S, int n1, int n3,
@@ -2203,10 +2204,15 @@ int match_impl(const void* packed_weights, const void* desc2d, int64_t desc2d_bs
   // planes (the token states x2 / x3, phi(q)), which those GEMMs then move by DMA
   const int npl = planes_of(pm);
   auto pl = [&](uint16_t* q) { return npl ? q : nullptr; };
-  // the dual softmax's statistics inside conf_kernel (whole frames, few score M-tiles): no
-  // softmax_reduce launch; the packed column winners are zeroed by the first kernel instead
+  // the dual softmax's statistics inside conf_kernel (whole frames, few score M-tiles, at most
+  // kConfRowTiles score tiles per row): no softmax_reduce launch; the packed column winners are
+  // zeroed by the first kernel instead.  Every conf workgroup re-derives its rows' statistics
+  // from all of the row's partials, so above 64 score tiles per row (configs 3 and 5) those
+  // re-reads (n3 / 256 times each) cost more than the separate softmax_reduce launch: config 5
+  // conf 55.7 -> 36.4 + 7.6 us, config 3 1.91 -> 0.76 ms per step, the same bits
+  // (profiles/r05/conf_rpl/, profiles/r05/smx/)
   const int score_mt = ceil_div(n1, pm_out == PM_F32 ? kScoreBM : 64);   // colpart per column
-  const bool conf_stats = !sh && score_mt <= kConfColTiles;
+  const bool conf_stats = !sh && score_mt <= kConfColTiles && ceil_div(n3, 64) <= kConfRowTiles;
   {
     TransArgs ta;
     ta.p[0] = {desc2d, desc2d_bstride, n1, ceil_div(n1, 64) * 4, p.x2[0], pl(p.x2p[0])};

@@ -5,7 +5,10 @@ compared bit for bit.  Each build runs in its own process (ONEPOSE_LIB selects t
     python tools/bitcmp.py cmp /tmp/a.npz /tmp/b.npz
 Cases: the uncached forward (onepose_match_ex, conf) and the cached bench path
 (onepose_object_prepare + onepose_match_cached, with and without GAT tables) in fp32, bf16 and
-fp32_split, on ragged and batched shapes."""
+fp32_split, on ragged and batched shapes.  BITCMP_BIG=1 adds configs 5 and 3's shapes (2048 x
+8192, 1024 x 16384: more than 64 score tiles per row); their conf matrices are compared by
+SHA-256 digest."""
+import hashlib
 import os
 import sys
 
@@ -15,6 +18,15 @@ import torch
 
 CASES = [(1024, 4096, 8, 1), (200, 777, 8, 2), (96, 300, 3, 1), (256, 1024, 12, 3)]
 PRECS = ["fp32", "bf16", "fp32_split"]
+if os.environ.get("BITCMP_BIG") == "1":
+    CASES += [(2048, 8192, 8, 1), (1024, 16384, 8, 1)]
+
+
+def _conf(c):
+    x = c.cpu().numpy()
+    if x.size > 8 << 20:   # (a digest: the bits, not the values, are compared)
+        return np.frombuffer(hashlib.sha256(x.tobytes()).digest(), np.uint8).copy()
+    return x
 
 
 def dump(path):
@@ -33,7 +45,7 @@ def dump(path):
             key = f"u_{n1}_{n3}_{L}_{B}_{prec}"
             for k, v in pred.items():
                 out[f"{key}_{k}"] = v.cpu().numpy()
-            out[f"{key}_conf"] = conf.cpu().numpy()
+            out[f"{key}_conf"] = _conf(conf)
             # cached path (object = sample 0's object, all frames of the batch)
             w = m.packed_weights(dev)
             f32 = dict(dtype=torch.float32, device=dev)
@@ -66,7 +78,7 @@ def dump(path):
                 ck = f"c{flags}_{n1}_{n3}_{L}_{B}_{prec}"
                 for nm, x in zip(("m0", "m1", "s0", "s1"), o):
                     out[f"{ck}_{nm}"] = x.cpu().numpy()
-                out[f"{ck}_conf"] = cf.cpu().numpy()
+                out[f"{ck}_conf"] = _conf(cf)
     np.savez(path, **out)
     print("dumped", len(out), "arrays to", path)
 

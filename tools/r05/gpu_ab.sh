@@ -4,11 +4,11 @@
 # ran in this shape (the variant built by tools/build_variant.sh with its -D flag):
 #   A_LIB   build A (default tools/ab/lib_prev.so: the build before the change)
 #   B_LIB   build B (default the product build)
-#   LINES   which lines: any of f32 (20 / 300 steps, two pairs each), split, bf16, c5
+#   LINES   which lines: any of f32 (20 / 300 steps, two pairs each), split, bf16, c5, c3
 #           (default "f32 split c5")
 #   PAIRS   pairs per fp32 line (default 2); TESTS=1 runs the GPU suite on B
 #   KEYS    kernel_ms_per_step entries to print (default the layer GEMMs)
-#   OUT     gpurun_out/ subdirectory (default r05ab)
+#   OUT     gpurun_out/ subdirectory (default r05ab); BITCMP_BIG=1 adds configs 5 / 3 to the bits
 set -u
 export TMPDIR=/tmp
 O=gpurun_out/${OUT:-r05ab}
@@ -48,5 +48,8 @@ for L in ${LINES:-f32 split c5}; do
     c5)
       line c5_A $A "--steps 100 --warmup 5 $C5"
       line c5_B $B "--steps 100 --warmup 5 $C5" ;;
+    c3)
+      line c3_A $A "--n3 16384 --batch 32 --steps 10 --warmup 2"
+      line c3_B $B "--n3 16384 --batch 32 --steps 10 --warmup 2" ;;
   esac
 done
