@@ -1,6 +1,7 @@
 #!/bin/bash
 # Pose streams on their own CUs (hipExtStreamCreateWithCUMask): default against '8' (pose on 8
 # CUs spread over the XCDs, matchers on the other 248) and '8p' (pose masked only), alternated.
+# (The --diag-cu-mask bench flag this script used was removed after the measurement: DESIGN.md §8b.)
 set -u
 export TMPDIR=/tmp
 O=gpurun_out/${OUT:-r05cumask}
