@@ -593,10 +593,10 @@ def main():
                 (2048, 8192): "config 5"}.get((n1, n3), "custom")
     if args.precision == "bf16":
         cfg_name += " (bf16-MFMA attention)"
-    if args.desc_dtype == "fp16":
-        cfg_name += " (fp16 desc)"
     elif args.precision == "fp32_split":
         cfg_name += " (fp32 attention as 3-piece bf16 split)"
+    if args.desc_dtype == "fp16":
+        cfg_name += " (fp16 desc)"
     if rank == 0:
         sched = (f"matchers of consecutive steps on {args.match_streams} concurrent stream(s), "
                  f"each step's pose stage on one of {args.pose_streams or args.match_streams} "
@@ -624,6 +624,9 @@ def main():
                                     + f"matcher + RANSAC-EPnP + cm/deg; {sched}"),
                        "n1": n1, "n3": n3, "num_leaf": L, "batch_per_gpu": B,
                        "global_batch": n_global,
+                       # frame buffer slots of the pipeline (a pipeline setting: rounds 1-4 ran 3,
+                       # the 64-frame bank since round 5 gives 4 with two match streams)
+                       "slots": nslots, "frame_bank": F,
                        "parallelism": f"frame-dp{world} (one object; global batch of "
                                       f"{n_global} frames sharded contiguously over ranks)"},
             "pose": pose_summary,

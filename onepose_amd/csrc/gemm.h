@@ -132,10 +132,7 @@ enum GemmTile {
                      //   the operand loads per FLOP of 64 x 64)
   TILE_32x256W8 = 8, // final projection + L2 normalisation (EPI_BIAS_L2): whole rows on 8 waves
                      //   of 32 x 32 (two per SIMD), 64-deep stages
-  TILE_256x128W8 = 9, // bf16 MLP conv 1 (STATS + HEADZ, DMA 2): 256 x 128 outputs on 8 waves of
-                      //   32 x 128, one workgroup per CU; a stage's W rows are fetched once per 256
-                      //   output rows instead of 64.  Its InstanceNorm partials, tickets and acc0
-                      //   are the 64 x 128 tile's (gemm_tile_stat_rows = 64): same workspace, same bits
+  // (9: a 256 x 128 eight-wave bf16 MLP conv 1 tile, measured slower; removed, tag r05-lab)
   TILE_128x128W8 = 10, // split-mode MLP conv 1 (STATS + HEADZ, DMA 2): 128 x 128 on 8 waves of
                        //   32 x 64, standing in for 64 x 64 tiles the same way (acc0 included)
 };
@@ -144,17 +141,15 @@ enum GemmTile {
 constexpr int gemm_tile_bm(int t) {
   return (t == TILE_32x128 || t == TILE_32x64W2 || t == TILE_32x256W8) ? 32
          : (t == TILE_128x128 || t == TILE_128x64W8) ? 128
-         : t == TILE_256x128W8                       ? 256
          : t == TILE_128x128W8                       ? 128
                                                      : 64;
 }
 // rows per EPI_STATS partial (and per acc0 tile): the tile's, or its stand-in tile's
 constexpr int gemm_tile_stat_rows(int t) {
-  return (t == TILE_256x128W8 || t == TILE_128x128W8) ? 64 : gemm_tile_bm(t);
+  return t == TILE_128x128W8 ? 64 : gemm_tile_bm(t);
 }
 constexpr int gemm_tile_bn(int t) {
-  return (t == TILE_32x128 || t == TILE_64x128 || t == TILE_128x128 || t == TILE_256x128W8 ||
-          t == TILE_128x128W8)
+  return (t == TILE_32x128 || t == TILE_64x128 || t == TILE_128x128 || t == TILE_128x128W8)
              ? 128
          : t == TILE_64x32K2                                        ? 32
          : t == TILE_32x256W8                                       ? 256
@@ -189,17 +184,8 @@ inline int stats_groups(int M, int rows) {
   return (mtiles + g - 1) / g;
 }
 
-// tools/experiments/gemm_bal.hip (an evaluated alternative, not in the library: DESIGN.md §8b;
-// linked only into -DONEPOSE_BAL builds): MLP conv 1 (EPI_STATS + PRO_HEADZ, fp32, N = K = 512) on the tile-balanced
-// kernel (64 x 32 strips dealt evenly to one 8-wave workgroup per CU, the same bits as the
-// 64 x 64 tile) when the 64 x 64 grid would load CUs unevenly (at most 3 tiles per CU).
-// Returns false, launching nothing, when it does not apply; otherwise *rc is the launch status.
-// Its in-launch finalize counts per 32-column block: st_cnt_bs >= gemm_bal_counters_per_sample.
-bool gemm_bal_try(GemmArgs& args, hipStream_t stream, int kind, int* rc);
-int gemm_bal_counters_per_sample(int M);
-
-// PRO_HEADZ arithmetic, shared by the two MLP conv 1 kernels for the same reason as the merges
-// below: one stage's 8-term piece of phi(q)_row . ksum_h (products rounded, summed left to
+// PRO_HEADZ arithmetic, shared by every MLP conv 1 kernel variant (tools/experiments/gemm_bal.hip
+// at tag r05-lab too) for the same reason as the merges below: one stage's 8-term piece of phi(q)_row . ksum_h (products rounded, summed left to
 // right) added to the running dot, and the head fold acc + Z*Ns * acc_h as one fma.
 __device__ __forceinline__ float headz_dot8(float zp, float4 a0, float4 a1, float4 k0, float4 k1) {
 #pragma clang fp contract(off)
@@ -210,8 +196,8 @@ __device__ __forceinline__ float headz_fold(float acc, float z, float acc_h) {
   return fmaf(z, acc_h, acc);
 }
 
-// InstanceNorm merges of MLP conv 1's in-launch finalize, shared by gemm.hip's 64 x 64 tile and
-// tools/experiments/gemm_bal.hip so that both round every operation alike: each statement exactly as written
+// InstanceNorm merges of MLP conv 1's in-launch finalize, shared by gemm.hip's tiles (and the
+// experimental kernels at tag r05-lab) so that all round every operation alike: each statement exactly as written
 // (contraction off -- left to itself the compiler fused some of these in one kernel and not in
 // the other), with fma() where the merge takes one.
 // (count, mean, M2) of a 32-row block into the running column statistics (Chan et al.)

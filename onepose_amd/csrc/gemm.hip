@@ -295,12 +295,7 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
   // (the A pieces must deal evenly over the waves: every wave then waits for its own stage)
   // (four and five buffers measured slower: config 5 1644 -> 1619 / 1499 frames/s, config 2
   // bf16 2906 -> 2901 / 2704; the loop is bound by the L2 -> LDS bytes)
-  // (a tile that stands in for several -- one workgroup per CU -- has no other workgroup to
-  // cover its DMA latency, and its staging tile is larger than five stages: four in flight)
-  constexpr int NBUF =
-      (DMA == 2 && PM == PM_BF16 && (NPL * BM / (512 / T::BKS)) % T::NW == 0)
-          ? (T::NSUB > 1 ? 5 : 3)
-          : 2;
+  constexpr int NBUF = (DMA == 2 && PM == PM_BF16 && (NPL * BM / (512 / T::BKS)) % T::NW == 0) ? 3 : 2;
   constexpr int LDS0 = NBUF * STAGE > BM * TP ? NBUF * STAGE : BM * TP;
   constexpr int LDSF = LDS0 > QKVL ? LDS0 : QKVL;
   __shared__ __attribute__((aligned(16))) float lds[LDSF];
@@ -1296,7 +1291,6 @@ using T128x128 = Tile<128, 128, 1, 4, 32>;
 using T128x64W8 = Tile<128, 64, 1, 8, 32>;
 using T32x64W2 = Tile<32, 64, 1, 2, 32>;
 using T32x256W8 = Tile<32, 256, 1, 8, 64, 1>;
-using T256x128W8 = Tile<256, 128, 1, 8, 32, 2, 64>;
 using T128x128W8S = Tile<128, 128, 1, 8, 32, 2, 64, 64>;   // split MLP conv 1 for the 64 x 64 tile
 
 
@@ -1327,7 +1321,6 @@ TileDims tile_dims(int tile) {
     case TILE_128x64W8: return {128, 64, 32};
     case TILE_32x64W2: return {32, 64, 32};
     case TILE_32x256W8: return {32, 256, 64};
-    case TILE_256x128W8: return {256, 128, 32};
     case TILE_128x128W8: return {128, 128, 32};
 
     default: return {0, 0, 0};
@@ -1346,7 +1339,6 @@ static_assert(gemm_tile_bm(TILE_64x64) == 64 && gemm_tile_bn(TILE_64x64) == 64 &
                   gemm_tile_bm(TILE_128x64W8) == 128 && gemm_tile_bn(TILE_128x64W8) == 64 &&
                   gemm_tile_bm(TILE_32x64W2) == 32 && gemm_tile_bn(TILE_32x64W2) == 64 &&
                   gemm_tile_bm(TILE_32x256W8) == 32 && gemm_tile_bn(TILE_32x256W8) == 256 &&
-                  gemm_tile_bm(TILE_256x128W8) == 256 && gemm_tile_bn(TILE_256x128W8) == 128 &&
                   gemm_tile_bm(TILE_128x128W8) == 128 && gemm_tile_bn(TILE_128x128W8) == 128,
               "gemm.h tile shapes must match tile_dims");
 
@@ -1376,13 +1368,6 @@ GemmProb gemm_prob(const float* A, int lda, const float* W, int ldw, const float
 
 int gemm_launch(int epi, int pro, int tile, GemmArgs& args, hipStream_t stream, int kind,
                 int pm) {
-#if defined(ONEPOSE_BAL) && !defined(ONEPOSE_NO_BAL)   // (under evaluation: A/B builds)
-  if (epi == EPI_STATS && pro == PRO_HEADZ && tile == TILE_64x64 && pm == PM_F32 &&
-      args.p[0].Wp == nullptr) {
-    int rc = ONEPOSE_OK;
-    if (gemm_bal_try(args, stream, kind, &rc)) return rc;
-  }
-#endif
   const TileDims td = tile_dims(tile);
   OP_REQUIRE(td.bm > 0, "gemm: unknown tile %d", tile);
   int grid = 0;
@@ -1403,9 +1388,6 @@ int gemm_launch(int epi, int pro, int tile, GemmArgs& args, hipStream_t stream, 
                     P.st_cnt_bs >= ceil_div(P.N, td.bn) * (1 + stats_groups(P.M, srows))),
                "gemm: STATS finalize needs group partials and %d counters per sample",
                ceil_div(P.N, td.bn) * (1 + stats_groups(P.M, srows)));
-    OP_REQUIRE(tile != TILE_256x128W8 || (epi == EPI_STATS && pro == PRO_HEADZ && pm == PM_BF16 &&
-                                          P.N == 512 && P.ksplit == 256),
-               "gemm: the 256 x 128 tile is bf16 MLP conv 1's");
     OP_REQUIRE(tile != TILE_128x128W8 || (epi == EPI_STATS && pro == PRO_HEADZ && pm == PM_SPLIT3 &&
                                           P.N == 512 && P.ksplit == 256) ||
                    (epi == EPI_QKV && pm == PM_F32),
@@ -1439,7 +1421,7 @@ int gemm_launch(int epi, int pro, int tile, GemmArgs& args, hipStream_t stream, 
   // 64 x 128 tiles (QKV, MLP conv 1), the register-staged loop for 64 x 64 (MLP conv 2, whose
   // two MFMAs per wave and stage leave a DMA loop nothing to hide behind).
   const bool dma =
-      pm == PM_SPLIT3 || (pm == PM_BF16 && (tile == TILE_64x128 || tile == TILE_256x128W8));
+      pm == PM_SPLIT3 || (pm == PM_BF16 && tile == TILE_64x128);
   // A from activation planes (every problem of the launch, or none): the DMA loop's DMA-2 form
   const bool adma = args.p[0].Ap != nullptr;
   const bool yplanes = args.p[0].Yp != nullptr;
@@ -1491,7 +1473,6 @@ int gemm_launch(int epi, int pro, int tile, GemmArgs& args, hipStream_t stream, 
   CASE(EPI_RESID, PRO_NORM_RELU, TILE_64x64, T64x64, PM_BF16, true)
   CASE(EPI_QKV, PRO_PLAIN, TILE_64x128, T64x128, PM_BF16, true)
   CASE(EPI_STATS, PRO_HEADZ, TILE_64x128, T64x128, PM_BF16, true)
-  CASE(EPI_STATS, PRO_HEADZ, TILE_256x128W8, T256x128W8, PM_BF16, true)
   CASE(EPI_RESID, PRO_NORM_RELU, TILE_64x128, T64x128, PM_BF16, true)
   CASE(EPI_ACC, PRO_PLAIN, TILE_64x128, T64x128, PM_BF16, true)
   CASE(EPI_RESID, PRO_NORM_RELU, TILE_32x64W2, T32x64W2, PM_SPLIT3, true)

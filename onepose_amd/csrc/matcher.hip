@@ -1348,8 +1348,8 @@ __global__ __launch_bounds__(256) void mutual_kernel(const unsigned long long* r
 // ------------------------------------------------------------------------------------
 namespace {
 
-// MLP conv 1's finalize counters per sample: column blocks of 32 (tools/experiments/gemm_bal.hip's strips; the
-// 64 x 64 tile uses the first 512 / 64 of them), then that many per stats group
+// MLP conv 1's finalize counters per sample: up to 512 / 32 column blocks (the 64 x 64 tile
+// uses the first 512 / 64 of them), then that many per stats group
 constexpr int kCntPerSide = 512 / 32;
 
 struct Plan {
@@ -1389,27 +1389,16 @@ constexpr int kTileBf16 = TILE_64x128;
 // ms per frame, profiles/r04/sw/); its MLP conv 1 keeps 64 x 64 (64 x 128 gives 320 workgroups
 // at config 2: 0.273 -> 0.313 ms per frame; a DMA stage's time follows the bytes its workgroup
 // moves).
-// The bf16 MLP conv 1 itself runs on the 256 x 128 eight-wave tile (gemm.h TILE_256x128W8: the
-// 64 x 128 tile's partials, tickets, acc0 and bits, with a stage's W rows fetched once per 256
-// rows and A loaded straight into the MFMA registers); its acc0 (object cache) is still written
-// by the 64 x 128 EPI_ACC launch.  (Under evaluation: -DONEPOSE_MLP1_WIDE selects it.)
-#ifdef ONEPOSE_MLP1_WIDE
-constexpr int kTileBf16Mlp1 = TILE_256x128W8;
-#else
+// The bf16 MLP conv 1 runs on the 64 x 128 DMA tile too (a 256 x 128 eight-wave stand-in was
+// built bit-identical and measured slower in the frame: DESIGN.md section 8b, tag r05-lab).
 constexpr int kTileBf16Mlp1 = kTileBf16;
-#endif
 // The split mode's MLP conv 1 runs on the 8-wave 128 x 128 tile (TILE_128x128W8), standing in
 // for its 64 x 64 tiles (the same partials, tickets, acc0 and bits): 160 workgroups at config 2,
 // one per CU, leave the other CUs to the other frame's kernels -- split line 1767 / 1772 ->
 // 1878 / 1882 frames/s, same box (profiles/r05/wsplit/).  The fp32 MLP
 // conv 1 measured slower on it (1699 / 1701 -> 1602 / 1609: its loop is MFMA-bound, so fewer
-// CUs cost time; profiles/r05/wf32/) and keeps 64 x 64.  (-DONEPOSE_MLP1_SPLIT_64: the 64 x 64
-// split tile, for A/B builds.)
-#ifdef ONEPOSE_MLP1_SPLIT_64
-constexpr int kTileSplitMlp1 = kTileMLP1;
-#else
+// CUs cost time; profiles/r05/wf32/) and keeps 64 x 64.
 constexpr int kTileSplitMlp1 = TILE_128x128W8;
-#endif
 int mlp1_tile(int pm) {
   return pm == PM_BF16 ? kTileBf16Mlp1 : pm == PM_SPLIT3 ? kTileSplitMlp1 : kTileMLP1;
 }
@@ -1435,13 +1424,8 @@ int qkv_tile_for(int n3, int B) {
   const int64_t t64 = (int64_t)ceil_div(n3, 64) * 6 * (B > kFusedFoldMaxBatch ? B : 1);
   // (64 x 128 from kQkvWideTiles on through round 5; the 8-wave 128 x 128 stand-in -- 64-row KV
   // chunks, the same bits -- measured +1.1 / +1.4% frames/s at config 2 in profiles/r05/qwide/, and
-  // +0.3% at 300 steps / level at 20 on the confirming run, profiles/r05/qconf/: a marginal gain;
-  // -DONEPOSE_QKV_NARROW: the 64 x 128 tile, for A/B builds)
-#ifdef ONEPOSE_QKV_NARROW
-  return t64 >= kQkvWiderTiles ? TILE_128x128 : t64 >= kQkvWideTiles ? TILE_64x128 : kTileKV;
-#else
+  // +0.3% at 300 steps / level at 20 on the confirming run, profiles/r05/qconf/: a marginal gain)
   return t64 >= kQkvWiderTiles ? TILE_128x128 : t64 >= kQkvWideTiles ? TILE_128x128W8 : kTileKV;
-#endif
 }
 
 bool valid_precision(int p) {

@@ -30,6 +30,12 @@ from . import _lib
 SUPPORTED = {"include_self": True, "additional": False, "with_linear_transform": False}
 
 
+def _version(t):
+    """The tensor's version counter, or None for an inference tensor (torch.inference_mode),
+    which has none -- so an in-place write to it cannot be detected."""
+    return None if torch.is_inference(t) else t._version
+
+
 def _hp(hparams, key, default=None):
     if isinstance(hparams, dict):
         return hparams.get(key, default)
@@ -147,8 +153,11 @@ class GATsSuperGlue(nn.Module):
 
     def packed_weights(self, device):
         tensors = self._weight_tensors()
-        key = (str(device),) + tuple((t.data_ptr(), t._version) for t in tensors)
-        if self._packed is not None and self._packed_key == key:
+        # (a parameter without a version counter -- created under inference_mode -- is packed
+        # again on every call: an in-place update of it would otherwise go unseen)
+        key = (str(device),) + tuple((t.data_ptr(), _version(t)) for t in tensors)
+        if (self._packed is not None and self._packed_key == key
+                and all(k[1] is not None for k in key[1:])):
             return self._packed
         lib = _lib.load()
         host = [t.detach().to("cpu", torch.float32).contiguous() for t in tensors]
@@ -202,7 +211,12 @@ class GATsSuperGlue(nn.Module):
                              f"{tuple(db.shape)}")
         dev = d2.device
         obj = None
-        if self.resident_object and B == 1 and hasattr(_lib.load(), "onepose_match_cached_dt"):
+        # (inference tensors carry no version counter, so an in-place write to the object could
+        # not be detected: they take the uncached forward, the same bits)
+        tracked = not (torch.is_inference(data["descriptors3d_db"]) or
+                       torch.is_inference(data["descriptors2d_db"]))
+        if (self.resident_object and tracked and B == 1
+                and hasattr(_lib.load(), "onepose_match_cached_dt")):
             obj = self._resident(data["descriptors3d_db"], data["descriptors2d_db"], d3, db, n3,
                                  nleaf, half, dev)
         return self._run(d2, s2, d3, s3, db, sl, B, n1, n3, nleaf, dev, obj)
@@ -245,8 +259,12 @@ class GATsSuperGlue(nn.Module):
                                                      n3, nleaf, self.precision, 0,
                                                      cache.data_ptr(), ws.data_ptr(), wsb, s),
                        "object_prepare")
+            # a forward on another stream waits for the prepare (_run)
+            ready = torch.cuda.Event()
+            ready.record(torch.cuda.current_stream(dev))
         del ws   # (stream-ordered: the allocator hands it out only behind the prepare)
-        self._obj = {"key": key, "refs": (t3, tl, d3, db), "pm": pm, "cache": cache}
+        self._obj = {"key": key, "refs": (t3, tl, d3, db), "pm": pm, "cache": cache,
+                     "ready": ready, "stream": torch.cuda.current_stream(dev)}
         return self._obj
 
     def _release_resident(self):
@@ -273,6 +291,13 @@ class GATsSuperGlue(nn.Module):
             ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
             dt = _lib.DT_F16 if d2.dtype == torch.float16 else _lib.DT_F32
             if obj is not None:
+                cur = torch.cuda.current_stream(dev)
+                if cur != obj["stream"]:
+                    # built on another stream: order this forward behind the prepare, and tell
+                    # the allocator the cache is in use here too
+                    cur.wait_event(obj["ready"])
+                    obj["cache"].record_stream(cur)
+                    obj["pm"].record_stream(cur)
                 rc = lib.onepose_match_cached_dt(
                     w.data_ptr(), d2.data_ptr(), dt, s2, obj["cache"].data_ptr(),
                     obj["pm"].data_ptr(), 0, B, n1, n3, nleaf,
@@ -283,9 +308,15 @@ class GATsSuperGlue(nn.Module):
                 _lib.check(rc, "onepose_match_cached")
                 return ({"matches0": m0[0], "matches1": m1[0],
                          "matching_scores0": ms0[0], "matching_scores1": ms1[0]}, conf)
-            # (an older A/B build named by ONEPOSE_LIB has only the fp32 entry point)
-            call = (lib.onepose_match_dt if hasattr(lib, "onepose_match_dt")
-                    else lambda *a: lib.onepose_match_ex(*a[:7], *a[8:]))
+            # (an older A/B build named by ONEPOSE_LIB has only the fp32 entry point, which
+            # would read fp16 descriptors as fp32)
+            if hasattr(lib, "onepose_match_dt"):
+                call = lib.onepose_match_dt
+            elif dt == _lib.DT_F16:
+                raise _lib.OnePoseError("this libonepose_hip build (ABI < 4) has no fp16 "
+                                        "descriptor entry point (onepose_match_dt)")
+            else:
+                call = lambda *a: lib.onepose_match_ex(*a[:7], *a[8:])
             rc = call(
                 w.data_ptr(), d2.data_ptr(), s2, d3.data_ptr(), s3, db.data_ptr(), sl, dt,
                 B, n1, n3, nleaf, float(_hp(self.hparams, "scale_factor")),

@@ -292,6 +292,27 @@ def test_resident_object_forward(precision, half, device):
     t["descriptors2d_db"] = t["descriptors2d_db"].clone()   # a new leaves tensor
     same("new leaves tensor")
     assert (first["matches0"] > -1).sum() > 10
+    # a forward on another stream than the one that prepared the object waits for the prepare
+    res._release_resident()
+    side = torch.cuda.Stream(device)
+    with torch.no_grad():
+        res(t)                                   # prepared on the current stream
+        with torch.cuda.stream(side):
+            p_side, c_side = res(t)              # cached forward on the side stream
+        p_ref, c_ref = unc(t)
+    torch.cuda.synchronize()
+    for k in p_ref:
+        np.testing.assert_array_equal(p_side[k].cpu().numpy(), p_ref[k].cpu().numpy(), err_msg=k)
+    np.testing.assert_array_equal(c_side.cpu().numpy(), c_ref.cpu().numpy())
+    # under torch.inference_mode the inputs carry no version counter: the uncached path, same bits
+    with torch.inference_mode():
+        ti = {k: v.clone() for k, v in t.items()}
+        p_inf, c_inf = res(ti)
+        p_ref, c_ref = unc(ti)
+    torch.cuda.synchronize()
+    for k in p_ref:
+        np.testing.assert_array_equal(p_inf[k].cpu().numpy(), p_ref[k].cpu().numpy(), err_msg=k)
+    np.testing.assert_array_equal(c_inf.cpu().numpy(), c_ref.cpu().numpy())
 
 
 def cached_and_uncached(lib, device, n1, n3, L, B, prec, seed, sd_seed=0, modes=(False, True),
