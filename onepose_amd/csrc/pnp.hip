@@ -970,81 +970,96 @@ struct Shared {
   int ord[4];
   int wave_cnt[4];
   int n_inl;
-  // refit eigensolver (jacobi12_block)
-  double jA[144], jV[144], jc[6], js[6];
-  int jp[6], jq[6], jrot[12];
+  // refit eigensolver (jacobi12_wave)
+  double jA[144], jV[144];
 };
 
 // Eigenvectors of the four smallest eigenvalues of the symmetric 12x12 M^T M (in sh.jA),
 // ascending -> sh.vs (48 doubles), for the EPnP refit.  Cyclic Jacobi in parallel rounds:
 // the circle method pairs the 12 indices into 6 disjoint (p, q) per round, 11 rounds per
-// sweep; a round computes the 6 rotations, then applies them to A's columns and V's columns,
-// then to A's rows.  Workgroup-collective (every thread calls it).  EPnP's result does not
-// depend on the eigenvectors' signs, and any accurate eigensolver gives the oracle's vectors
-// up to sign when the eigenvalues are separated.  (A one-barrier variant -- each thread
-// computing its A' = J^T A J entry from the previous A, six threads the next round's
-// rotations from the entries they need -- measured 2.3x slower: the rotation chain grew.)
-__device__ void jacobi12_block(Shared& sh) {
-  const int t = threadIdx.x;
-  for (int i = t; i < 144; i += kThreads) {
-    const int r = i / 12, c = i - r * 12;
-    sh.jV[i] = r == c ? 1.0 : 0.0;
+// sweep.  One wave runs it (the caller's wave 0), lane I * 6 + J (I, J < 6) owning the 2 x 2
+// block of rows (p_I, q_I) and columns (p_J, q_J) of A and of V in the round: it computes
+// the rotations of pairs I and J from the round's diagonal entries (every lane the same
+// formulas, so the same values), then A's block as J^T (A J) -- the column pass, then the
+// row pass, the arithmetic of the round-4 workgroup version -- and V's block as V J.  A and V
+// stay in LDS in full 12 x 12 layout; within one wave a round needs no workgroup barrier (its
+// reads precede its writes in the wave's LDS order), which is what the workgroup version
+// paid three of per round.  EPnP's result does not depend on the eigenvectors' signs, and
+// any accurate eigensolver gives the oracle's vectors up to sign when the eigenvalues are
+// separated.
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+__device__ __forceinline__ void jacobi_rot(double app, double aqq, double apq, double& c, double& sn) {
+  c = 1.0;
+  sn = 0.0;
+  if (apq != 0.0) {   // t = sgn(theta) / (|theta| + sqrt(theta^2 + 1)), theta = a / b, without
+                       // the division for theta: t = sgn(a) b / (|a| + sqrt(a^2 + b^2))
+    const double a = aqq - app, b = 2.0 * apq;
+    const double tt = (a >= 0.0 ? b : -b) / (fabs(a) + sqrt(a * a + b * b));
+    c = 1.0 / sqrt(tt * tt + 1.0);
+    sn = tt * c;
   }
-  if (t < 12) sh.jrot[t] = 0;
+}
+// pair k of round r (circle method), p < q
+__device__ __forceinline__ void jacobi_pair(int r, int k, int& p, int& q) {
+  const int a = r + k, c = r - k + 11;   // (r + k) % 11, (r - k + 11) % 11
+  p = k == 0 ? r : (a >= 11 ? a - 11 : a);
+  q = k == 0 ? 11 : (c >= 11 ? c - 11 : c);
+  if (p > q) {
+    const int x = p;
+    p = q;
+    q = x;
+  }
+}
+__device__ void jacobi12_wave(Shared& sh) {
+  const int lane = threadIdx.x & 63;
+  for (int i = lane; i < 144; i += 64) sh.jV[i] = (i / 12 == i % 12) ? 1.0 : 0.0;
   double tr = 0.0;   // trace: the scale of "converged" off-diagonals (M^T M is PSD)
   for (int i = 0; i < 12; ++i) tr += fabs(sh.jA[i * 13]);
   const double thr = 1e-22 * tr;
-  __syncthreads();
+  const int I = min(lane / 6, 5), J = lane % 6;   // lanes >= 36 shadow block (5, J): no writes
+  const bool own = lane < 36;
+  double* A = sh.jA;
+  double* V = sh.jV;
+  wave_lds_sync();
   for (int sweep = 0; sweep < 12; ++sweep) {
+    bool big = false;
     for (int round = 0; round < 11; ++round) {
-      if (t < 6) {   // pair t: (round, 11) or ((round + t) % 11, (round - t + 11) % 11)
-        int p = t == 0 ? round : (round + t) % 11;
-        int q = t == 0 ? 11 : (round - t + 11) % 11;
-        if (p > q) {
-          const int x = p;
-          p = q;
-          q = x;
-        }
-        const double apq = sh.jA[p * 12 + q];
-        double c = 1.0, sn = 0.0;
-        if (fabs(apq) > thr) sh.jrot[sweep] = 1;   // not yet converged
-        if (apq != 0.0) {
-          const double theta = (sh.jA[q * 12 + q] - sh.jA[p * 12 + p]) / (2.0 * apq);
-          const double tt = (theta >= 0.0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
-          c = 1.0 / sqrt(tt * tt + 1.0);
-          sn = tt * c;
-        }
-        sh.jp[t] = p;
-        sh.jq[t] = q;
-        sh.jc[t] = c;
-        sh.js[t] = sn;
+      int pI, qI, pJ, qJ;
+      jacobi_pair(round, I, pI, qI);
+      jacobi_pair(round, J, pJ, qJ);
+      // pair J's rotation; pair I's is lane I's pair J (lane I = block (0, I))
+      const double apqJ = A[pJ * 12 + qJ];
+      double cJ, sJ;
+      jacobi_rot(A[pJ * 13], A[qJ * 13], apqJ, cJ, sJ);
+      const double cI = __shfl(cJ, I, 64), sI = __shfl(sJ, I, 64);
+      big |= fabs(apqJ) > thr;   // (every pair is some lane's J)
+      const double app = A[pI * 12 + pJ], apq = A[pI * 12 + qJ];
+      const double aqp = A[qI * 12 + pJ], aqq = A[qI * 12 + qJ];
+      const double vpp = V[pI * 12 + pJ], vpq = V[pI * 12 + qJ];
+      const double vqp = V[qI * 12 + pJ], vqq = V[qI * 12 + qJ];
+      wave_lds_sync();   // every read of the round before any write
+      // A J (columns pJ, qJ), then J^T (A J) (rows pI, qI)
+      const double xpp = cJ * app - sJ * apq, xpq = sJ * app + cJ * apq;
+      const double xqp = cJ * aqp - sJ * aqq, xqq = sJ * aqp + cJ * aqq;
+      if (own) {
+        A[pI * 12 + pJ] = cI * xpp - sI * xqp;
+        A[qI * 12 + pJ] = sI * xpp + cI * xqp;
+        A[pI * 12 + qJ] = cI * xpq - sI * xqq;
+        A[qI * 12 + qJ] = sI * xpq + cI * xqq;
+        V[pI * 12 + pJ] = cJ * vpp - sJ * vpq;
+        V[pI * 12 + qJ] = sJ * vpp + cJ * vpq;
+        V[qI * 12 + pJ] = cJ * vqp - sJ * vqq;
+        V[qI * 12 + qJ] = sJ * vqp + cJ * vqq;
       }
-      __syncthreads();
-      for (int task = t; task < 144; task += kThreads) {   // A J and V J (columns p, q)
-        const int k = task / 24, w = task - k * 24, i = w % 12;
-        double* M = w < 12 ? sh.jA : sh.jV;
-        const int p = sh.jp[k], q = sh.jq[k];
-        const double c = sh.jc[k], sn = sh.js[k];
-        const double aip = M[i * 12 + p], aiq = M[i * 12 + q];
-        M[i * 12 + p] = c * aip - sn * aiq;
-        M[i * 12 + q] = sn * aip + c * aiq;
-      }
-      __syncthreads();
-      for (int task = t; task < 72; task += kThreads) {    // J^T (A J) (rows p, q)
-        const int k = task / 12, j = task - k * 12;
-        const int p = sh.jp[k], q = sh.jq[k];
-        const double c = sh.jc[k], sn = sh.js[k];
-        const double apj = sh.jA[p * 12 + j], aqj = sh.jA[q * 12 + j];
-        sh.jA[p * 12 + j] = c * apj - sn * aqj;
-        sh.jA[q * 12 + j] = sn * apj + c * aqj;
-      }
-      __syncthreads();
+      wave_lds_sync();
     }
-    if (!sh.jrot[sweep]) break;   // a sweep without a rotation: converged (uniform)
+    if (__ballot(big) == 0ull) break;   // a sweep without a rotation: converged
   }
-  const double* A = sh.jA;
-  const double* V = sh.jV;
-  if (t == 0) {   // the four smallest eigenvalues, ascending (ties by index)
+  if (lane == 0) {   // the four smallest eigenvalues, ascending (ties by index)
     int order[12];
     for (int i = 0; i < 12; ++i) order[i] = i;
     for (int i = 0; i < 4; ++i)
@@ -1056,8 +1071,8 @@ __device__ void jacobi12_block(Shared& sh) {
         }
     for (int i = 0; i < 4; ++i) sh.ord[i] = order[i];
   }
-  __syncthreads();
-  if (t < 48) sh.vs[t] = V[(t % 12) * 12 + sh.ord[t / 12]];
+  wave_lds_sync();
+  if (lane < 48) sh.vs[lane] = V[(lane % 12) * 12 + sh.ord[lane / 12]];
 }
 
 // Canonical basis of the 4-dimensional EPnP null space of exactly 4 correspondences (M is
@@ -1129,16 +1144,17 @@ __device__ void null4_basis(const double (&M)[8][12], double (&v)[4][12]) {
   }
 }
 
-// Workgroup-parallel EPnP over the points listed in idx[0..n) (epnp::compute_pose).
+// Workgroup-parallel EPnP over the points p2 / p3 [0, n) (epnp::compute_pose): the kernel's LDS
+// copy of the inliers, in inlier order.
 
-__device__ __forceinline__ void epnp_refit(Shared& sh, const float* p2, const float* p3, const int* idx, int n,
+__device__ __forceinline__ void epnp_refit(Shared& sh, const float* p2, const float* p3, int n,
                            const double* K4, double* R_out, double* t_out) {
   const int t = threadIdx.x;
   const double fu = K4[0], fv = K4[1], uc = K4[2], vc = K4[3];
   // centroid
   double v3[3] = {0, 0, 0};
   for (int i = t; i < n; i += kThreads) {
-    const int j = idx[i];
+    const int j = i;
     v3[0] += (double)p3[3 * j];
     v3[1] += (double)p3[3 * j + 1];
     v3[2] += (double)p3[3 * j + 2];
@@ -1148,7 +1164,7 @@ __device__ __forceinline__ void epnp_refit(Shared& sh, const float* p2, const fl
   // PCA
   double m6[6] = {0, 0, 0, 0, 0, 0};
   for (int i = t; i < n; i += kThreads) {
-    const int j = idx[i];
+    const int j = i;
     const double p0 = (double)p3[3 * j] - c0[0], p1 = (double)p3[3 * j + 1] - c0[1],
                  p2_ = (double)p3[3 * j + 2] - c0[2];
     m6[0] += p0 * p0;
@@ -1193,7 +1209,7 @@ __device__ __forceinline__ void epnp_refit(Shared& sh, const float* p2, const fl
 #pragma unroll
       for (int e = 0; e < 40; ++e) S[e] = 0.0;
       for (int i = lane; i < n; i += 64) {
-        const int j = idx[i];
+        const int j = i;
         double as[4];
         alphas(j, as);
         const double du = uc - (double)p2[2 * j], dv = vc - (double)p2[2 * j + 1];
@@ -1245,7 +1261,7 @@ __device__ __forceinline__ void epnp_refit(Shared& sh, const float* p2, const fl
     }
     __syncthreads();
     // @phase 10
-    jacobi12_block(sh);   // workgroup-collective -> sh.vs
+    if (wave == 0) jacobi12_wave(sh);   // -> sh.vs
     __syncthreads();
     // @phase 11
     if (t < 60) {   // compute_L_6x10, one entry per thread
@@ -1272,7 +1288,7 @@ __device__ __forceinline__ void epnp_refit(Shared& sh, const float* p2, const fl
 #pragma unroll
     for (int i = 0; i < 78; ++i) acc[i] = 0.0;
     for (int i = t; i < n; i += kThreads) {
-      const int j = idx[i];
+      const int j = i;
       double as[4];
       alphas(j, as);
       const double u = (double)p2[2 * j], v = (double)p2[2 * j + 1];
@@ -1298,8 +1314,8 @@ __device__ __forceinline__ void epnp_refit(Shared& sh, const float* p2, const fl
         double M[8][12];
         for (int i = 0; i < 4; ++i) {
           double as[4];
-          alphas(idx[i], as);
-          const double u = (double)p2[2 * idx[i]], v = (double)p2[2 * idx[i] + 1];
+          alphas(i, as);
+          const double u = (double)p2[2 * i], v = (double)p2[2 * i + 1];
           for (int k = 0; k < 4; ++k) {
             M[2 * i][3 * k] = as[k] * fu;
             M[2 * i][3 * k + 1] = 0.0;
@@ -1332,10 +1348,11 @@ __device__ __forceinline__ void epnp_refit(Shared& sh, const float* p2, const fl
       ccs_from_betas(sh.vs, betas, ccs);
       // solve_for_sign looks at the first point's camera-frame depth
       double a[4];
-      alphas(idx[0], a);
+      alphas(0, a);
       const double z0 = a[0] * ccs[0][2] + a[1] * ccs[1][2] + a[2] * ccs[2][2] + a[3] * ccs[3][2];
       sh.wflip[wave] = z0 < 0.0 ? -1.0 : 1.0;
     }
+    // @phase 16
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -1349,7 +1366,7 @@ __device__ __forceinline__ void epnp_refit(Shared& sh, const float* p2, const fl
     };
     double s6[6] = {0, 0, 0, 0, 0, 0};
     for (int i = lane; i < n; i += 64) {
-      const int j = idx[i];
+      const int j = i;
       double pc[3];
       pc_of(j, pc);
       s6[0] += pc[0];
@@ -1364,7 +1381,7 @@ __device__ __forceinline__ void epnp_refit(Shared& sh, const float* p2, const fl
     const double pc0[3] = {s6[0] / n, s6[1] / n, s6[2] / n}, pw0[3] = {s6[3] / n, s6[4] / n, s6[5] / n};
     double abt[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
     for (int i = lane; i < n; i += 64) {
-      const int j = idx[i];
+      const int j = i;
       double pc[3];
       pc_of(j, pc);
       const double pw[3] = {(double)p3[3 * j] - pw0[0], (double)p3[3 * j + 1] - pw0[1],
@@ -1376,13 +1393,15 @@ __device__ __forceinline__ void epnp_refit(Shared& sh, const float* p2, const fl
     }
 #pragma unroll
     for (int k = 0; k < 9; ++k) abt[k] = wave_sum_d(abt[k]);
+    // @phase 17
     double R[9], tt[3];
     finish_R(abt, R);   // every lane (identical inputs): no hand-over needed
+    // @phase 18
 #pragma unroll
     for (int j = 0; j < 3; ++j) tt[j] = pc0[j] - dot3(R + 3 * j, pw0);
     double err = 0.0;
     for (int i = lane; i < n; i += 64) {
-      const int j = idx[i];
+      const int j = i;
       const double pw[3] = {(double)p3[3 * j], (double)p3[3 * j + 1], (double)p3[3 * j + 2]};
       const double Xc = dot3(R, pw) + tt[0], Yc = dot3(R + 3, pw) + tt[1];
       const double iz = 1.0 / (dot3(R + 6, pw) + tt[2]);
@@ -1908,7 +1927,8 @@ void pnp_refit_kernel(
     const int* __restrict__ n_inliers, const int* __restrict__ status,
     const int* __restrict__ idx_ws, const double* __restrict__ pose_gt, int64_t gt_bs,
     double* __restrict__ rerr, double* __restrict__ terr, uint8_t* __restrict__ cmd) {
-  __shared__ Shared sh;
+  extern __shared__ __attribute__((aligned(16))) unsigned char dyn[];
+  Shared& sh = *reinterpret_cast<Shared*>(dyn);
   const int b = blockIdx.x;
   const int t = threadIdx.x;
   double* pose = pose34 + (int64_t)b * 12;
@@ -1925,10 +1945,26 @@ void pnp_refit_kernel(
   const int nin = n_inliers[b];
   const double* K = Kmat + b * K_bs;
   const double K4[4] = {K[0], K[4], K[2], K[5]};
-  const float* p2 = pts2d + (int64_t)b * max_points * 2;
-  const float* p3 = pts3d + (int64_t)b * max_points * 3;
+  // the inliers, compacted into LDS once: every pass of the refit reads them from there (from
+  // global memory each pass's loads sat behind the index load, one round trip after another)
+  float* p2 = reinterpret_cast<float*>(dyn + ((sizeof(Shared) + 15) / 16) * 16);
+  float* p3 = p2 + 2 * max_points;
+  {
+    const float* g2 = pts2d + (int64_t)b * max_points * 2;
+    const float* g3 = pts3d + (int64_t)b * max_points * 3;
+    const int* idx = idx_ws + (int64_t)b * max_points;
+    for (int i = t; i < nin; i += kThreads) {
+      const int j = idx[i];
+      p2[2 * i] = g2[2 * j];
+      p2[2 * i + 1] = g2[2 * j + 1];
+      p3[3 * i] = g3[3 * j];
+      p3[3 * i + 1] = g3[3 * j + 1];
+      p3[3 * i + 2] = g3[3 * j + 2];
+    }
+    __syncthreads();
+  }
   double Rf[9], tf[3], rv[3], Rr[9];
-  epnp_refit(sh, p2, p3, idx_ws + (int64_t)b * max_points, nin, K4, Rf, tf);
+  epnp_refit(sh, p2, p3, nin, K4, Rf, tf);
   // @phase 14
   rodrigues_m2v(Rf, rv);
   rodrigues_v2m(rv, Rr);
@@ -1977,6 +2013,8 @@ int onepose_pnp_ransac(const float* pts2d, const float* pts3d, const int* counts
   if (!attr_set) {
     OP_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(pnp_ransac_kernel),
                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    OP_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(pnp_refit_kernel),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     attr_set = true;
   }
   hipStream_t st = static_cast<hipStream_t>(stream);
@@ -1985,7 +2023,7 @@ int onepose_pnp_ransac(const float* pts2d, const float* pts3d, const int* counts
             counts, max_points, K, K_bstride, scale, reproj_error, max_iters, confidence, pose34,
             inlier_mask, n_inliers, status, static_cast<int*>(workspace), none, nullptr, nullptr,
             nullptr);
-  OP_LAUNCH(K_PNP_REFIT, st, pnp_refit_kernel, dim3(batch), dim3(kThreads), 0, st, pts2d, pts3d,
+  OP_LAUNCH(K_PNP_REFIT, st, pnp_refit_kernel, dim3(batch), dim3(kThreads), lds, st, pts2d, pts3d,
             max_points, K, K_bstride, scale, pose34, n_inliers, status,
             static_cast<const int*>(workspace), nullptr, (int64_t)0, nullptr, nullptr, nullptr);
   return ONEPOSE_OK;
@@ -2021,6 +2059,8 @@ int onepose_pose_stage(const int64_t* matches0, const float* kpts2d, int64_t kpt
   if (!attr_set) {
     OP_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(pnp_ransac_kernel),
                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    OP_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(pnp_refit_kernel),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     attr_set = true;
   }
   hipStream_t st = static_cast<hipStream_t>(stream);
@@ -2029,7 +2069,7 @@ int onepose_pose_stage(const int64_t* matches0, const float* kpts2d, int64_t kpt
             nullptr, max_points, K, K_bstride, scale, reproj_error, max_iters, confidence, pose34,
             inlier_mask, n_inliers, status, static_cast<int*>(workspace), sel, pts2d, pts3d,
             counts);
-  OP_LAUNCH(K_PNP_REFIT, st, pnp_refit_kernel, dim3(batch), dim3(kThreads), 0, st, pts2d, pts3d,
+  OP_LAUNCH(K_PNP_REFIT, st, pnp_refit_kernel, dim3(batch), dim3(kThreads), lds, st, pts2d, pts3d,
             max_points, K, K_bstride, scale, pose34, n_inliers, status,
             static_cast<const int*>(workspace), pose_gt, gt_bstride, R_err_deg, t_err_cm, cmd);
   return ONEPOSE_OK;

@@ -5,8 +5,8 @@
 //
 //   bash tools/probe_src.sh   (generates _gen/pnp.hip with the stamps, then builds)
 //   ./tools/pnp_probe [n] [outlier_frac]
-__device__ unsigned long long g_pph[16];
-__device__ unsigned g_pcnt[16];
+__device__ unsigned long long g_pph[24];
+__device__ unsigned g_pcnt[24];
 #define ONEPOSE_PNP_PHASE(i)                                   \
   if (threadIdx.x == 0 && blockIdx.x == 0) {                   \
     g_pph[(i)] = __builtin_amdgcn_s_memtime();                 \
@@ -89,9 +89,9 @@ int main(int argc, char** argv) {
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
   const int reps = 30;
-  std::vector<std::vector<double>> ph(16);
+  std::vector<std::vector<double>> ph(20);
   std::vector<double> ev;
-  unsigned cnt0[16] = {0}, cnt1[16];
+  unsigned cnt0[24] = {0}, cnt1[24];
   int nin = 0;
   for (int r = 0; r < reps; ++r) {
     CK(hipMemcpyToSymbol(HIP_SYMBOL(g_pcnt), cnt0, sizeof(cnt0)));
@@ -104,11 +104,13 @@ int main(int argc, char** argv) {
     float ms;
     CK(hipEventElapsedTime(&ms, e0, e1));
     ev.push_back(ms * 1e3);
-    unsigned long long st[16];
+    unsigned long long st[24];
     CK(hipMemcpyFromSymbol(st, HIP_SYMBOL(g_pph), sizeof(st)));
     CK(hipMemcpyFromSymbol(cnt1, HIP_SYMBOL(g_pcnt), sizeof(cnt1)));
     for (int i = 1; i < 16; ++i)
       if (cnt1[i] && cnt1[i - 1]) ph[i].push_back((double)(long long)(st[i] - st[i - 1]));
+    for (int i = 16; i < 20; ++i)   // markers inside the refit's approximations: since phase 12
+      if (cnt1[i] && cnt1[12]) ph[i].push_back((double)(long long)(st[i] - st[12]));
     CK(hipMemcpy(&nin, dnin, 4, hipMemcpyDeviceToHost));
   }
   auto med = [](std::vector<double> v) {
@@ -125,5 +127,9 @@ int main(int argc, char** argv) {
                            "refit: L, rho", "refit: 3 approximations", "refit: rest of epnp_refit", ""};
   for (int i = 1; i < 15; ++i)
     if (names[i][0]) printf("  %-40s %8.0f cycles (s_memtime)\n", names[i], med(ph[i]));
+  const char* inner[4] = {"refit approx 1: betas + GN + ccs (lane 0)", "  + centroid / abt sums",
+                          "  + finish_R", ""};
+  for (int i = 16; i < 19; ++i)
+    if (!ph[i].empty()) printf("  %-40s %8.0f cycles since phase 12\n", inner[i - 16], med(ph[i]));
   return 0;
 }
