@@ -29,11 +29,24 @@ struct WgRec {
   unsigned hwid, xcc, pad0, pad1;
 };
 
+// g_stagger (round 6, `stagger` mode): workgroups with hardware id >= g_stagger[0] wait
+// g_stagger[1] shader cycles before their prologue, those >= g_stagger[2] g_stagger[3] cycles
+// (dispatch order: the third workgroup of each CU comes from the last 256 ids) -- do co-resident
+// workgroups whose prologues / epilogues coincide lose the MFMA pipe for them?
+__device__ unsigned long long g_stagger[4];
 template <int EPI, int PRO, class T, int PM, bool WPL, int DMA>
 __global__ __launch_bounds__(T::NT) __attribute__((amdgpu_waves_per_eu(T::WPE)))
 void phase_kernel(GemmArgs args, WgRec* rec) {
   __shared__ StampLds sl;
   StampTick tk{0ull, 0ull};
+  {
+    const unsigned long long d = blockIdx.x >= g_stagger[2] ? g_stagger[3]
+                                 : blockIdx.x >= g_stagger[0] ? g_stagger[1] : 0ull;
+    if (d) {
+      const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+      while (__builtin_amdgcn_s_memtime() - t0 < d) __builtin_amdgcn_s_sleep(8);
+    }
+  }
   const unsigned long long rt0 = __builtin_amdgcn_s_memrealtime();
   const unsigned long long mt0 = __builtin_amdgcn_s_memtime();
   if (threadIdx.x == 0) g_phase[blockIdx.x * 8] = mt0;
@@ -372,6 +385,34 @@ int main(int argc, char** argv) {
   using T64x128 = Tile<64, 128, 1, 4, 32>;
   using T64x128B = Tile<64, 128, 1, 4, 64>;
   for (int r = 0; r < 2; ++r) run<EPI_STATS, PRO_HEADZ, T64x64>("warm", B, 5120, 512, 512, true, 200);
+  if (argc > 1 && !strcmp(argv[1], "stagger")) {   // round 6: staggered workgroup starts
+    // (the event time covers the delays; "span" starts at the first workgroup's post-delay stamp,
+    // so read the event column)
+    auto stag = [&](unsigned long long a, unsigned long long da, unsigned long long b,
+                    unsigned long long db) {
+      unsigned long long v[4] = {a, da, b, db};
+      hipMemcpyToSymbol(HIP_SYMBOL(g_stagger), v, sizeof(v));
+    };
+    for (int m : {5120, 6144}) {
+      printf("--- fp32 mlp1 STATS+HEADZ+fin, M %d: third workgroup per CU delayed ---\n", m);
+      for (int r = 0; r < 2; ++r) {
+        for (unsigned long long d : {0ull, 6000ull, 12000ull, 24000ull, 36000ull}) {
+          stag(512, d, 1u << 30, 0);
+          char nm[64];
+          snprintf(nm, sizeof nm, "ids>=512 +%llu cyc", d);
+          run<EPI_STATS, PRO_HEADZ, T64x64>(nm, B, m, 512, 512, true, it);
+        }
+        for (unsigned long long d : {6000ull, 12000ull, 20000ull}) {
+          stag(256, d, 512, 2 * d);
+          char nm[64];
+          snprintf(nm, sizeof nm, "2nd +%llu, 3rd +%llu", d, 2 * d);
+          run<EPI_STATS, PRO_HEADZ, T64x64>(nm, B, m, 512, 512, true, it);
+        }
+        stag(1u << 30, 0, 1u << 30, 0);
+      }
+    }
+    return 0;
+  }
   if (argc > 1 && !strcmp(argv[1], "mlp2")) {   // round 4: fp32 MLP conv 2 tiles (RESID + NORM)
     using T64x64K2W8 = Tile<64, 64, 2, 8, 64>;
     using T128x32K2W8 = Tile<128, 32, 2, 8, 64>;
