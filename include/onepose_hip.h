@@ -58,8 +58,18 @@ enum { ONEPOSE_DT_F32 = 0, ONEPOSE_DT_F16 = 1 };
 /* Thread-local description of the last error ("" when none). */
 const char* onepose_last_error(void);
 /* ABI version, bumped on any signature change or new entry point (4: the per-precision
- * workspace and object-cache size queries). */
+ * workspace and object-cache size queries; 5: the object cache's device-side header and
+ * onepose_device_errors). */
 int onepose_abi_version(void);
+/* (ABI 5) The library's sticky device-side error bits (ONEPOSE_DEVERR_*), set by kernels that
+ * cannot return a status: *bits receives them, and `clear` != 0 resets them.  Synchronises with
+ * the device (a host query; never call it inside a graph capture). */
+enum {
+  ONEPOSE_DEVERR_STALE_CACHE = 1   /* a cached forward found its object cache's header not the
+                                    * one onepose_object_prepare wrote there (the memory was
+                                    * freed and reused); that forward reported no match */
+};
+int onepose_device_errors(int clear, unsigned* bits);
 
 /* ------------------------------------------------------------------------------------ *
  * GATsSPG matcher  --  replaces GATsSuperGlue.forward
@@ -208,6 +218,13 @@ int onepose_match_prepared(const void* packed_weights,
  * to another cache that is not prepared again); a new onepose_object_prepare at the same
  * address replaces the record. onepose_object_cache_bytes returns 0 for flags that prepare
  * would refuse.
+ * (ABI 5) The record cannot see memory that was freed and handed to something else at the
+ * same address without onepose_object_release.  So the prepare also writes a 64-B header at
+ * the end of the cache (its n3, num_leaf, precision, flags and a generation the record keeps),
+ * and onepose_match_cached's first kernel compares it with the record on the device: a
+ * mismatch makes that forward report no match (matches -1, scores 0) and sets
+ * ONEPOSE_DEVERR_STALE_CACHE (onepose_device_errors) -- without a host synchronisation, so
+ * graph-captured forwards keep the check.
  * ------------------------------------------------------------------------------------ */
 enum {
   ONEPOSE_OBJ_GAT_TABLES = 1    /* build / use the GAT prefix tables (num_leaf <= 8)          */

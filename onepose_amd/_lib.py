@@ -20,7 +20,8 @@ c_void_p, c_char_p = ctypes.c_void_p, ctypes.c_char_p
 
 # onepose_allgather_fn: int (*)(size_t bytes_per_rank, void* stream, void* user)
 ALLGATHER_FN = ctypes.CFUNCTYPE(c_int, c_size_t, c_void_p, c_void_p)
-ABI_VERSION = 4
+ABI_VERSION = 5
+DEVERR_STALE_CACHE = 1   # ONEPOSE_DEVERR_STALE_CACHE
 OBJ_GAT_TABLES = 1   # ONEPOSE_OBJ_GAT_TABLES
 DT_F32, DT_F16 = 0, 1   # ONEPOSE_DT_*
 
@@ -28,6 +29,7 @@ DT_F32, DT_F16 = 0, 1   # ONEPOSE_DT_*
 PROTOTYPES = {
     "onepose_last_error": (c_char_p, []),
     "onepose_abi_version": (c_int, []),
+    "onepose_device_errors": (c_int, [c_int, ctypes.POINTER(ctypes.c_uint)]),
     "onepose_matcher_num_tensors": (c_int, []),
     "onepose_matcher_tensor_name": (c_char_p, [c_int]),
     "onepose_matcher_tensor_numel": (c_int64, [c_int]),
@@ -180,3 +182,12 @@ def stream_ptr(device=None) -> int:
 
 def ptr(t) -> int:
     return 0 if t is None else t.data_ptr()
+
+
+def device_errors(clear: bool = False) -> int:
+    """The library's sticky device-side error bits (DEVERR_*; onepose_device_errors).
+    Synchronises with the device."""
+    lib = load()
+    v = ctypes.c_uint(0)
+    check(lib.onepose_device_errors(1 if clear else 0, ctypes.byref(v)), "device_errors")
+    return int(v.value)

@@ -58,6 +58,29 @@ constexpr int kMlp2WideTiles = 1024;    // fp32 mlp2: 64x64 tiles from this many
 constexpr int kQkvWideTiles = 256;      // fp32 qkv: 64x128 tiles from this many 64-row tiles
 constexpr int kQkvWiderTiles = 4096;    //   of the 3D side; 128x128 from this many (qkv_tile_for)
 
+// Object-cache header (ObjLayout::hdr, written by onepose_object_prepare): what the prepare
+// built and its generation, so a forward can check on the device that the memory it was handed
+// still holds that cache -- a cache freed without onepose_object_release and its address reused
+// passes the host registry's check, not this one.
+constexpr unsigned kCacheMagic = 0x4f504331u;   // "OPC1"
+constexpr int kCacheHdrWords = 8;
+struct CacheHdr {
+  unsigned magic, n3, num_leaf, precision, flags, gen_lo, gen_hi, check;
+};
+static_assert(sizeof(CacheHdr) == kCacheHdrWords * 4, "header words");
+inline CacheHdr cache_hdr(int n3, int num_leaf, int precision, int flags, unsigned long long gen) {
+  CacheHdr h{kCacheMagic, (unsigned)n3, (unsigned)num_leaf, (unsigned)precision, (unsigned)flags,
+             (unsigned)gen, (unsigned)(gen >> 32), 0u};
+  h.check = ~(h.magic ^ h.n3 ^ (h.num_leaf << 8) ^ (h.precision << 16) ^ (h.flags << 24) ^
+              h.gen_lo ^ (h.gen_hi * 2654435761u));
+  return h;
+}
+// the library's sticky device error word (onepose_device_errors)
+__device__ unsigned g_device_errors;
+__global__ void cache_hdr_kernel(unsigned* hdr, CacheHdr h) {
+  if (threadIdx.x < kCacheHdrWords) hdr[threadIdx.x] = (&h.magic)[threadIdx.x];
+}
+
 // ------------------------------------------------------------------------------------
 // errors
 // ------------------------------------------------------------------------------------
@@ -264,9 +287,25 @@ struct TransArgs {
   int npl = 0;      // activation planes per dstp (0: none)
   unsigned long long* zero64 = nullptr;   // the packed column winners (fused conf), zeroed here
   int64_t nzero64 = 0;
+  // object-cache forwards: the cache's header against the one its prepare recorded (a stale
+  // cache -- freed and its memory reused -- sets *err and the sticky device error word, and the
+  // forward's mutual_kernel then reports no match)
+  const unsigned* hdr = nullptr;
+  CacheHdr expect{};
+  unsigned* err = nullptr;
 };
 __global__ __launch_bounds__(256) void transpose_in_kernel(TransArgs args, int batch) {
   __shared__ float tile[64][65];
+  if (blockIdx.x == 0 && threadIdx.x == 0 && args.err != nullptr) {
+    unsigned bad = 0u;
+    if (args.hdr != nullptr) {
+      const unsigned* e = &args.expect.magic;
+#pragma unroll
+      for (int i = 0; i < kCacheHdrWords; ++i) bad |= args.hdr[i] != e[i] ? 1u : 0u;
+    }
+    *args.err = bad;
+    if (bad) atomicOr(&g_device_errors, ONEPOSE_DEVERR_STALE_CACHE);
+  }
   int bid = blockIdx.x;
   const bool second = bid >= args.p[0].tiles * batch;
   const TransProb& P = second ? args.p[1] : args.p[0];
@@ -1316,9 +1355,19 @@ __global__ __launch_bounds__(256) void mutual_kernel(const unsigned long long* r
                                                      const unsigned long long* colbest,
                                                      int batch, int n1, int n3, float thr,
                                                      int64_t* matches0, int64_t* matches1,
-                                                     float* ms0, float* ms1) {
+                                                     float* ms0, float* ms1, const unsigned* err) {
   const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const int64_t nr = (int64_t)batch * n1, nc = (int64_t)batch * n3;
+  if (err != nullptr && *err != 0u) {   // the forward read a stale object cache: no match
+    if (idx < nr) {
+      ms0[idx] = 0.f;
+      matches0[idx] = -1;
+    } else if (idx < nr + nc) {
+      ms1[idx - nr] = 0.f;
+      matches1[idx - nr] = -1;
+    }
+    return;
+  }
   if (idx < nr) {
     const int b = (int)(idx / n1), n = (int)(idx - (int64_t)b * n1);
     const unsigned long long p = rowpart ? row_best(rowpart, ct, idx) : rowbest[idx];
@@ -1369,6 +1418,7 @@ struct Plan {
   unsigned long long *rowbest, *colbest;
   unsigned long long* rowwin;    // [B][n1][ceil(n3 / 256)] conf_kernel's row winners per column tile
   float* leaves_pm;   // point-major copy of the leaves (onepose_match only)
+  unsigned* err;      // this forward's device-side error word (set by its first kernel)
   size_t bytes;
 };
 
@@ -1485,6 +1535,7 @@ Plan make_plan(void* ws, int B, int n1, int n3, int L, bool with_conf, bool plan
   p.rowwin = c.take<unsigned long long>(t2 * (size_t)ceil_div(n3, 256));
   p.colbest = c.take<unsigned long long>(t3);
   p.leaves_pm = c.take<float>(t3 * L * 256);
+  p.err = c.take<unsigned>(1);
   p.bytes = align_up(c.off, 256);
   return p;
 }
@@ -1500,7 +1551,7 @@ using namespace onepose;
 extern "C" {
 
 const char* onepose_last_error(void) { return g_last_error.c_str(); }
-int onepose_abi_version(void) { return 4; }
+int onepose_abi_version(void) { return 5; }
 
 int onepose_profile_begin(uint64_t kind_mask, int capacity) {
   clear_error();
@@ -1909,7 +1960,7 @@ bool obj_tables(int num_leaf, int flags) {
   return (flags & ONEPOSE_OBJ_GAT_TABLES) != 0 && num_leaf <= 8;
 }
 struct ObjLayout {
-  int64_t logits, phiq, acc, ksum, mf, phiqp, slogs, tab, total;
+  int64_t logits, phiq, acc, ksum, mf, phiqp, slogs, tab, hdr, total;
   bool tables;
 };
 ObjLayout obj_layout(int n3, int num_leaf, int flags, bool planes) {
@@ -1925,7 +1976,8 @@ ObjLayout obj_layout(int n3, int num_leaf, int flags, bool planes) {
   L.phiqp = L.mf + kMfFloats;
   L.slogs = L.phiqp + (planes ? (int64_t)kPlanesMax * n3 * 256 / 2 : 0);
   L.tab = L.slogs + (L.tables ? (int64_t)3 * n3 * kLogitStride : 0);
-  L.total = L.tab + (L.tables ? (int64_t)3 * n3 * 2 * num_leaf * 256 : 0);
+  L.hdr = L.tab + (L.tables ? (int64_t)3 * n3 * 2 * num_leaf * 256 : 0);   // CacheHdr (64 B)
+  L.total = L.hdr + 16;
   return L;
 }
 
@@ -2173,7 +2225,8 @@ int match_impl(const void* packed_weights, const void* desc2d, int64_t desc2d_bs
                float match_threshold, int64_t* matches0, int64_t* matches1, float* mscores0,
                float* mscores1, float* conf, const Plan& p, hipStream_t st, int precision,
                const ShardCtx* sh = nullptr, const float* obj_cache = nullptr,
-               int obj_flags = 0, int desc_dt = ONEPOSE_DT_F32) {
+               int obj_flags = 0, int desc_dt = ONEPOSE_DT_F32,
+               const CacheHdr* obj_hdr = nullptr) {
   const bool with_conf = conf != nullptr;
   const int n3g = sh ? sh->n3_total : n3;   // the 3D side's full length (softmax / attention)
   const int pm = attention_pm(precision);   // attention-layer GEMM operand mode
@@ -2210,6 +2263,12 @@ int match_impl(const void* packed_weights, const void* desc2d, int64_t desc2d_bs
     if (conf_stats) {
       ta.zero64 = p.colbest;
       ta.nzero64 = (int64_t)B * n3;
+    }
+    ta.err = p.err;
+    if (obj_cache != nullptr && obj_hdr != nullptr) {
+      ta.hdr = reinterpret_cast<const unsigned*>(
+          obj_cache + obj_layout(n3, num_leaf, obj_flags, npl != 0).hdr);
+      ta.expect = *obj_hdr;
     }
     OP_LAUNCH(K_TRANSPOSE, st, transpose_in_kernel, dim3((ta.p[0].tiles + ta.p[1].tiles) * B),
               dim3(256), 0, st, ta, B);
@@ -2398,7 +2457,7 @@ int match_impl(const void* packed_weights, const void* desc2d, int64_t desc2d_bs
     OP_LAUNCH(K_MUTUAL, st, mutual_kernel, dim3((unsigned)((tot_g + 255) / 256)), dim3(256), 0, st,
                        p.rowbest, rowwin, ceil_div(n3, 256), colbest, B, n1, n3g,
                        match_threshold, matches0, matches1,
-                       mscores0, mscores1);
+                       mscores0, mscores1, p.err);
   }
   return ONEPOSE_OK;
 }
@@ -2677,9 +2736,11 @@ namespace {
 // onepose_match_cached refuses a cache whose record is missing or differs from its arguments.
 struct CacheRecord {
   int n3, num_leaf, precision, flags;
+  unsigned long long gen;   // also in the cache's device header (CacheHdr)
 };
 std::mutex g_cache_mu;
 std::unordered_map<const void*, CacheRecord> g_caches;
+unsigned long long g_cache_gen = 0;
 }  // namespace
 }  // namespace onepose
 
@@ -2721,9 +2782,20 @@ int onepose_object_prepare_dt(const void* packed_weights, const void* desc3d, in
   const int rc = object_prepare_impl(packed_weights, desc3d, desc_dtype, leaves_prepared, n3,
                                      num_leaf, precision, flags, cache, p,
                                      static_cast<hipStream_t>(stream_));
-  if (rc == ONEPOSE_OK) {
+  if (rc != ONEPOSE_OK) return rc;
+  unsigned long long gen;
+  {
     std::lock_guard<std::mutex> lk(g_cache_mu);
-    g_caches[cache] = {n3, num_leaf, precision, flags};
+    gen = ++g_cache_gen;
+  }
+  const CacheHdr h = cache_hdr(n3, num_leaf, precision, flags, gen);
+  hipStream_t st = static_cast<hipStream_t>(stream_);
+  unsigned* hdr = reinterpret_cast<unsigned*>(
+      cache + obj_layout(n3, num_leaf, flags, precision != ONEPOSE_PREC_FP32).hdr);
+  OP_LAUNCH(K_TRANSPOSE, st, cache_hdr_kernel, dim3(1), dim3(64), 0, st, hdr, h);
+  {
+    std::lock_guard<std::mutex> lk(g_cache_mu);
+    g_caches[cache] = {n3, num_leaf, precision, flags, gen};
   }
   return rc;
 }
@@ -2766,6 +2838,7 @@ int onepose_match_cached_dt(const void* packed_weights, const void* desc2d, int 
                             num_leaf, scale_factor, matches0, matches1, mscores0, mscores1,
                             workspace);
   if (rc != ONEPOSE_OK) return rc;
+  CacheHdr hdr;
   {
     std::lock_guard<std::mutex> lk(g_cache_mu);
     const auto it = g_caches.find(object_cache);
@@ -2778,6 +2851,7 @@ int onepose_match_cached_dt(const void* packed_weights, const void* desc2d, int 
                "match_cached: cache prepared for n3=%d num_leaf=%d precision=%d flags=%d, "
                "called with n3=%d num_leaf=%d precision=%d flags=%d",
                c.n3, c.num_leaf, c.precision, c.flags, n3, num_leaf, precision, object_flags);
+    hdr = cache_hdr(c.n3, c.num_leaf, c.precision, c.flags, c.gen);
   }
   const bool planes = precision != ONEPOSE_PREC_FP32;
   const Plan need = make_plan(nullptr, batch, n1, n3, num_leaf, conf != nullptr, planes);
@@ -2790,7 +2864,20 @@ int onepose_match_cached_dt(const void* packed_weights, const void* desc2d, int 
                     prepared_bstride, batch, n1, n3, num_leaf, scale_factor, match_threshold,
                     matches0, matches1, mscores0, mscores1, conf, p,
                     static_cast<hipStream_t>(stream_), precision, nullptr, object_cache,
-                    object_flags, desc_dtype);
+                    object_flags, desc_dtype, &hdr);
+}
+
+int onepose_device_errors(int clear, unsigned* bits) {
+  clear_error();
+  OP_REQUIRE(bits != nullptr, "device_errors: null pointer");
+  unsigned v = 0u;
+  OP_HIP(hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_device_errors), sizeof(v)));
+  if (clear && v != 0u) {
+    const unsigned z = 0u;
+    OP_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_device_errors), &z, sizeof(z)));
+  }
+  *bits = v;
+  return ONEPOSE_OK;
 }
 
 void onepose_shard_range(int n3_total, int world, int rank, int* start, int* count) {

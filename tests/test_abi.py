@@ -30,7 +30,7 @@ def test_library_exports_every_header_symbol():
     missing = [s for s in header_symbols() if not hasattr(lib, s)]
     assert not missing, missing
     assert set(header_symbols()) == set(_lib.PROTOTYPES), "ctypes prototypes out of sync"
-    assert lib.onepose_abi_version() == _lib.ABI_VERSION == 4
+    assert lib.onepose_abi_version() == _lib.ABI_VERSION == 5
 
 
 def test_object_cache_size_follows_its_flags():

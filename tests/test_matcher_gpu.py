@@ -316,9 +316,10 @@ def test_resident_object_forward(precision, half, device):
 
 
 def cached_and_uncached(lib, device, n1, n3, L, B, prec, seed, sd_seed=0, modes=(False, True),
-                        flags=0):
+                        flags=0, between=None):
     """Outputs of onepose_match_prepared_ex (False) / onepose_object_prepare +
-    onepose_match_cached (True, object flags `flags`) on one object shared by the batch."""
+    onepose_match_cached (True, object flags `flags`) on one object shared by the batch.
+    `between(cache)` runs after the prepare, before the forwards."""
     from onepose_amd import _lib
     sd = synthetic.make_state_dict(sd_seed)
     data, _, _ = synthetic.make_matcher_inputs(n1, n3, L, seed=seed, batch=B)
@@ -337,6 +338,8 @@ def cached_and_uncached(lib, device, n1, n3, L, B, prec, seed, sd_seed=0, modes=
     _lib.check(lib.onepose_object_prepare(w.data_ptr(), d3.data_ptr(), pm.data_ptr(), n3, L, prec,
                                           flags, cache.data_ptr(), ws.data_ptr(), wsb, s),
                "prepare")
+    if between is not None:
+        between(cache)
     ws_bytes = lib.onepose_match_workspace_bytes(B, n1, n3, L, 1)
     sf, thr = float(m.hparams["scale_factor"]), float(m.hparams["match_threshold"])
     outs = []
@@ -360,6 +363,29 @@ def cached_and_uncached(lib, device, n1, n3, L, B, prec, seed, sd_seed=0, modes=
         torch.cuda.synchronize()
         outs.append({k: v.cpu().numpy() for k, v in o.items()})
     return outs
+
+
+def test_stale_object_cache_reports_no_match(device):
+    """ABI 5: onepose_object_prepare writes a header (shape, precision, flags, generation) into
+    the cache and onepose_match_cached's first kernel checks it on the device.  A cache whose
+    memory was overwritten after its prepare (freed and reused without onepose_object_release)
+    passes the host registry but not the header: the forward reports no match and sets
+    ONEPOSE_DEVERR_STALE_CACHE, which onepose_device_errors returns and clears."""
+    from onepose_amd import _lib
+    lib = _lib.load()
+    _lib.device_errors(clear=True)
+    ok = cached_and_uncached(lib, device, 200, 777, 8, 1, 0, seed=3, modes=(True,))[0]
+    assert (ok["m0"] > -1).sum() > 10
+    assert _lib.device_errors() == 0
+    bad = cached_and_uncached(lib, device, 200, 777, 8, 1, 0, seed=3, modes=(True,),
+                              between=lambda c: c.zero_())[0]
+    assert (bad["m0"] == -1).all() and (bad["m1"] == -1).all()
+    assert (bad["s0"] == 0).all() and (bad["s1"] == 0).all()
+    assert _lib.device_errors(clear=True) & _lib.DEVERR_STALE_CACHE
+    assert _lib.device_errors() == 0
+    again = cached_and_uncached(lib, device, 200, 777, 8, 1, 0, seed=3, modes=(True,))[0]
+    np.testing.assert_array_equal(again["m0"], ok["m0"])
+    assert _lib.device_errors() == 0
 
 
 @pytest.mark.parametrize("n1,n3,L,B,prec", [(200, 777, 8, 1, 0), (1000, 3001, 8, 1, 0),
