@@ -20,6 +20,7 @@
 
 #include <cstdlib>
 #include <cstring>
+#include <type_traits>
 
 // Pins the pipeline's phase order (the compiler's own schedule measured within +-2%,
 // DESIGN.md §3d).
@@ -1241,21 +1242,32 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
     const int line = t >> 2, qtr = t & 3;
     // quarters of a row (column) of BN (BM) entries: 16 or 32 each
     const int lo_r = qtr * (BN / 4), lo_c = qtr * (BM / 4);
-    auto partial = [&](const float* base, int stride, int count, int lo, int len)
+    // (all LEN staged entries loaded at once -- indices past `count` are still inside the staged
+    // tile -- and kept in registers for the exp pass: the same max and the same left-to-right
+    // sum over i < count as a loop to count, without a dependent LDS round trip per entry, which
+    // made the partials ~60% of the epilogue: 15.8k of its 25.7k cycles, profiles/r03/phase/)
+    auto partial = [&](const float* base, int stride, int count, int lo, auto len_c)
         __attribute__((always_inline)) {
-      const int hi = min(lo + len, count);
+      constexpr int LEN = decltype(len_c)::value;
+      float v[LEN];
+#pragma unroll
+      for (int i = 0; i < LEN; ++i) v[i] = base[(lo + i) * stride];
       float mx = -INFINITY;
-      for (int i = lo; i < hi; ++i) mx = fmaxf(mx, base[i * stride]);
+#pragma unroll
+      for (int i = 0; i < LEN; ++i)
+        if (lo + i < count) mx = fmaxf(mx, v[i]);
       mx = fmaxf(mx, __shfl_xor(mx, 1, 64));
       mx = fmaxf(mx, __shfl_xor(mx, 2, 64));
       float s = 0.f;
-      for (int i = lo; i < hi; ++i) s += expf(base[i * stride] - mx);
+#pragma unroll
+      for (int i = 0; i < LEN; ++i)
+        if (lo + i < count) s += expf(v[i] - mx);
       s += __shfl_xor(s, 1, 64);
       s += __shfl_xor(s, 2, 64);
       return make_float2(mx, s);
     };
     if (line < BM) {   // row `line` over this tile's columns
-      const float2 r = partial(tile + line * TP, 1, cols, lo_r, BN / 4);
+      const float2 r = partial(tile + line * TP, 1, cols, lo_r, std::integral_constant<int, BN / 4>());
       if (qtr == 0 && line < rows) {
         float* o = F(rowstat) + (((int64_t)b * M + m0 + line) * ntiles + nt) * 2;
         o[0] = r.x;
@@ -1263,7 +1275,7 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
       }
     }
     if (line < BN) {   // column `line` over this tile's rows
-      const float2 r = partial(tile + line, TP, rows, lo_c, BM / 4);
+      const float2 r = partial(tile + line, TP, rows, lo_c, std::integral_constant<int, BM / 4>());
       if (qtr == 0 && line < cols) {
         float* o = F(colstat) + (((int64_t)b * mtiles + mt) * N + n0 + line) * 2;
         o[0] = r.x;
