@@ -373,6 +373,18 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
   for (int j = 0; j < FN; ++j)
 #pragma unroll
     for (int i = 0; i < 16; ++i) acc[j][i] = 0.f;
+  // the epilogue's bias of the wave's columns, loaded ahead of the K loop (loaded where the
+  // epilogue starts, it was a global round trip every workgroup waited on there)
+  float bias_pre[FN];
+  {
+    const float* bp = F(bias);
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int gn = n0 + wn * FN * 32 + j * 32 + (lane & 31);
+      bias_pre[j] =
+          (EPI != EPI_SCORE && EPI != EPI_ACC && bp != nullptr && gn < c.N) ? bp[gn] : 0.f;
+    }
+  }
 
   // Main loop, software-pipelined across the per-stage barrier.  Step kt consumes stage kt
   // from registers (fragments read from LDS right after the previous barrier):
@@ -852,7 +864,7 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
       const int col = wn * FN * 32 + j * 32 + (lane & 31);
-      const float bias = biasp != nullptr ? biasp[n0 + col] : 0.f;
+      const float bias = bias_pre[j];   // (n0 + col < N = 768 on every QKV tile)
       // v / vdiv: for a power-of-two source length the product with its reciprocal is the
       // same number (exact scaling), without the division's instruction sequence
       const float vdiv = F(vdiv), vrcp = 1.0f / vdiv;
@@ -959,7 +971,7 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
       const int col = wn * FN * 32 + j * 32 + (lane & 31);
       const int gn = n0 + col;
       const bool col_ok = gn < N;
-      const float bias = (EPI != EPI_SCORE && biasp != nullptr && col_ok) ? biasp[gn] : 0.f;
+      const float bias = bias_pre[j];   // (0 past N, for SCORE, or without a bias)
       float yv[16];
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
