@@ -386,6 +386,22 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
     }
   }
 
+  // RESID with at most two residual float4 per thread (fp32 MLP conv 2's 64 x 32 tile): the
+  // row-store pass's R loads ahead of the K loop too (the same rows and columns it reads there)
+  constexpr int RPER = BM * (BN / 4) / T::NT;
+  constexpr bool kRPre = EPI == EPI_RESID && RPER <= 2 && (BM * (BN / 4)) % T::NT == 0;
+  float4 r_pre[kRPre ? RPER : 1];
+  if constexpr (kRPre) {
+    const float* R = F(R) + b * F(r_bs);
+    const int ldr = F(ldr);
+#pragma unroll
+    for (int p = 0; p < RPER; ++p) {
+      const int idx = t + T::NT * p, r = idx / (BN / 4), cc = (idx % (BN / 4)) * 4;
+      const int gm = min(m0 + r, c.M - 1), gn = min(n0 + cc, c.N - 4);
+      r_pre[p] = *reinterpret_cast<const float4*>(R + (int64_t)gm * ldr + gn);
+    }
+  }
+
   // Main loop, software-pipelined across the per-stage barrier.  Step kt consumes stage kt
   // from registers (fragments read from LDS right after the previous barrier):
   //   issue global loads of stage kt+2 | MFMA kk0 | store stage kt+1 to the other LDS buffer
@@ -1022,7 +1038,10 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
     constexpr int C4 = BN / 4, PER = BM * C4 / T::NT;   // float4 per row, per thread
     static_assert(BM * C4 % T::NT == 0, "row-store pass");
     float4 rv[EPI == EPI_RESID ? PER : 1];
-    if (EPI == EPI_RESID) {   // all residual loads issued before the first store
+    if constexpr (kRPre) {
+#pragma unroll
+      for (int p = 0; p < PER; ++p) rv[p] = r_pre[p];
+    } else if (EPI == EPI_RESID) {   // all residual loads issued before the first store
       const float* R = F(R) + b * F(r_bs);
       const int ldr = F(ldr);
 #pragma unroll
