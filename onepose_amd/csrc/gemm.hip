@@ -389,7 +389,7 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& args, StampTick& tk, S
   // RESID with at most two residual float4 per thread (fp32 MLP conv 2's 64 x 32 tile): the
   // row-store pass's R loads ahead of the K loop too (the same rows and columns it reads there)
   constexpr int RPER = BM * (BN / 4) / T::NT;
-  constexpr bool kRPre = EPI == EPI_RESID && RPER <= 2 && (BM * (BN / 4)) % T::NT == 0;
+  constexpr bool kRPre = EPI == EPI_RESID && RPER <= 4 && (BM * (BN / 4)) % T::NT == 0;
   float4 r_pre[kRPre ? RPER : 1];
   if constexpr (kRPre) {
     const float* R = F(R) + b * F(r_bs);
