@@ -385,6 +385,50 @@ int main(int argc, char** argv) {
   using T64x128 = Tile<64, 128, 1, 4, 32>;
   using T64x128B = Tile<64, 128, 1, 4, 64>;
   for (int r = 0; r < 2; ++r) run<EPI_STATS, PRO_HEADZ, T64x64>("warm", B, 5120, 512, 512, true, 200);
+  if (argc > 1 && !strcmp(argv[1], "placement")) {   // round 6: which CU each hardware block lands on
+    for (int m : {5120, 6144}) {
+      run<EPI_STATS, PRO_HEADZ, T64x64>("placement", B, m, 512, 512, true, 1);
+      const int grid = (m / 64) * 8;
+      std::vector<WgRec> h(grid);
+      hipMemcpy(h.data(), B.rec, grid * sizeof(WgRec), hipMemcpyDeviceToHost);
+      std::map<unsigned, std::vector<int>> percu;
+      for (int i = 0; i < grid; ++i) {
+        const unsigned cu = ((h[i].xcc & 0xf) << 16) | (((h[i].hwid >> 13) & 7) << 8) |
+                            (((h[i].hwid >> 12) & 1) << 4) | ((h[i].hwid >> 8) & 0xf);
+        percu[cu].push_back(i);
+      }
+      // per CU: the within-XCD dispatch indices (block / 8) of its blocks, and the XCD check
+      int xcd_ok = 0, slot_ok = 0, n3 = 0;
+      std::map<int, int> hist;
+      for (auto& kv : percu) {
+        const auto& v = kv.second;
+        bool same_xcd = true;
+        for (int b : v) same_xcd &= (unsigned)(b & 7) == ((kv.first >> 16) & 7);
+        xcd_ok += same_xcd;
+        hist[(int)v.size()]++;
+        // "slot by slot": the CU's k-th block has within-XCD index in [32k, 32k + 32)
+        bool sl = true;
+        std::vector<int> idx;
+        for (int b : v) idx.push_back(b / 8);
+        std::sort(idx.begin(), idx.end());
+        for (size_t k = 0; k < idx.size(); ++k) sl &= idx[k] >= 32 * (int)k && idx[k] < 32 * (int)k + 32;
+        slot_ok += sl;
+        if (v.size() == 3) ++n3;
+      }
+      printf("M %d grid %d: CUs %zu, blocks per CU histogram:", m, grid, percu.size());
+      for (auto& kv : hist) printf(" %d->%d", kv.first, kv.second);
+      printf(" | CUs whose blocks share the block's XCD (b %% 8): %d | CUs filled slot by slot (k-th block index in [32k, 32k+32)): %d\n",
+             xcd_ok, slot_ok);
+      int shown = 0;
+      for (auto& kv : percu) {
+        if (shown++ >= 12) break;
+        printf("  cu %06x:", kv.first);
+        for (int b : kv.second) printf(" %d(x%d,i%d)", b, b & 7, b / 8);
+        printf("\n");
+      }
+    }
+    return 0;
+  }
   if (argc > 1 && !strcmp(argv[1], "stagger")) {   // round 6: staggered workgroup starts
     // (the event time covers the delays; "span" starts at the first workgroup's post-delay stamp,
     // so read the event column)
