@@ -428,12 +428,17 @@ def main():
         return pipe.slots[0]
 
     frame_ids = torch.arange(fs, fe, dtype=torch.float64, device=dev)[:, None]
+    # the bank's global frame indices go to the device here, not inside the timed region: a
+    # pageable host -> device copy there would block the host until the K steps drained and
+    # leave the result rows' launches to start on an idle GPU (~0.2 ms of a 20-step region)
+    bank_gid = (torch.as_tensor(bank["frame_id"], dtype=torch.float64, device=dev)
+                if bank is not None else None)
 
     def result_rows(slot):   # per-frame result row: pose, errors, cm/deg flags, inliers, status,
         # and the frame's index in the global batch (rank 0 checks the gathered order)
         if bank is not None:   # every bank entry's frames (the results of its last run)
             r = pipe.bank_results
-            gid = torch.as_tensor(bank["frame_id"], dtype=torch.float64, device=dev)
+            gid = bank_gid
             return torch.cat([r["pose"].reshape(F * B, 12), r["R_err"].reshape(-1, 1),
                               r["t_err"].reshape(-1, 1), r["cmd"].reshape(-1, 3).double(),
                               r["n_inliers"].reshape(-1, 1).double(),
