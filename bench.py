@@ -302,6 +302,9 @@ def main():
     ap.add_argument("--unfused-pose", action="store_true",
                     help="pose stage as select + RANSAC-EPnP + errors (4 launches) instead of "
                          "onepose_pose_stage (2)")
+    ap.add_argument("--no-staged-inputs", action="store_true",
+                    help="run each step's matcher input stage (transpose_in) at the head of its "
+                         "matcher instead of at the end of the slot's previous pose stage")
     ap.add_argument("--diag-repeats", type=int, default=0,
                     help="diagnostic: after the timed region, time it again this many times "
                          "and report those ms/step too (value always comes from the first)")
@@ -398,7 +401,14 @@ def main():
     if args.no_stamps:   # diagnostic: what device stamping costs the timed region
         stamp_mask = 0
     _lib.check(lib.onepose_profile_begin_device(stamp_mask), "profile_begin_device")
-    stage_graphs = pipe.capture_stages(torch.cuda.graph_pool_handle()) if graphs_on else None
+    # staged inputs (FramePipeline.prime_inputs): each pose stage ends with the input stage of
+    # the step that next uses its slot, so the matcher's launch chain starts at its first layer
+    staged = (overlap and pipe.staged_ok() and not args.no_staged_inputs
+              and not args.diag_no_pose and not args.diag_steps)
+    stage_graphs = (pipe.capture_stages(torch.cuda.graph_pool_handle(), staged=staged)
+                    if graphs_on else None)
+    if staged:
+        pipe.prime_inputs()
     step_graph = pipe.capture(0) if graphs_on and not overlap else None
 
     step_events = []
@@ -418,6 +428,7 @@ def main():
             pipe.run_stream(k, graphs=stage_graphs,
                             marks=marks if record and args.stage_marks else None,
                             match_streams=args.match_streams, pose=not args.diag_no_pose,
+                            staged=staged,
                             pose_streams=args.pose_streams or args.match_streams)
             return pipe.slots[(k - 1) % len(pipe.slots)]
         for _ in range(k):
@@ -608,6 +619,8 @@ def main():
                  "pose stream(s) overlapping the next matchers"
                  if overlap else "serial steps")
         sched += "; stages replayed as HIP graphs" if graphs_on else "; host-launched kernels"
+        sched += ("; each step's matcher input stage run at the end of its slot's previous pose "
+                  "stage" if staged else "")
         sched += ("; object prefix (GAT 0 + 3D half of self-attention 1) prepared once per object"
                   if cached else "; every layer run per frame")
         out = {

@@ -59,7 +59,7 @@ enum { ONEPOSE_DT_F32 = 0, ONEPOSE_DT_F16 = 1 };
 const char* onepose_last_error(void);
 /* ABI version, bumped on any signature change or new entry point (4: the per-precision
  * workspace and object-cache size queries; 5: the object cache's device-side header and
- * onepose_device_errors). */
+ * onepose_device_errors; 6: onepose_match_cached_parts). */
 int onepose_abi_version(void);
 /* (ABI 5) The library's sticky device-side error bits (ONEPOSE_DEVERR_*), set by kernels that
  * cannot return a status: *bits receives them, and `clear` != 0 resets them.  Synchronises with
@@ -267,6 +267,26 @@ int onepose_match_cached_dt(const void* packed_weights,
                             int64_t* matches0, int64_t* matches1,
                             float* mscores0, float* mscores1, float* conf,
                             void* workspace, size_t workspace_bytes, void* stream);
+/* (ABI 6) onepose_match_cached_dt in two parts, for a caller that pipelines frames through
+ * buffer slots (one workspace per slot) and wants the frame's input stage off the matcher's
+ * launch chain.  ONEPOSE_PART_INPUTS is the forward's first kernel alone: desc2d into the
+ * workspace's token-major layout, the workspace's arrival counters zeroed, the object cache's
+ * header checked.  ONEPOSE_PART_MATCH is the rest of the forward, reading what the input part
+ * left in the same workspace.  Both parts with the same arguments, in that order on one stream
+ * or ordered by events, give the bits of one onepose_match_cached_dt call (ONEPOSE_PART_ALL);
+ * nothing else may use the workspace between them.  The input part may therefore run as soon as
+ * the workspace's previous forward has finished, e.g. on the stream of that forward's pose stage. */
+enum { ONEPOSE_PART_INPUTS = 1, ONEPOSE_PART_MATCH = 2, ONEPOSE_PART_ALL = 3 };
+int onepose_match_cached_parts(const void* packed_weights,
+                               const void* desc2d, int desc_dtype, int64_t desc2d_bstride,
+                               const float* object_cache,
+                               const float* leaves_prepared, int64_t prepared_bstride,
+                               int batch, int n1, int n3, int num_leaf,
+                               float scale_factor, float match_threshold, int precision,
+                               int object_flags,
+                               int64_t* matches0, int64_t* matches1,
+                               float* mscores0, float* mscores1, float* conf,
+                               void* workspace, size_t workspace_bytes, int parts, void* stream);
 
 /* ------------------------------------------------------------------------------------ *
  * N3-sharded single frame (SURVEY.md §8e optional / §8f rank 4): one frame's 3D points split

@@ -20,8 +20,9 @@ c_void_p, c_char_p = ctypes.c_void_p, ctypes.c_char_p
 
 # onepose_allgather_fn: int (*)(size_t bytes_per_rank, void* stream, void* user)
 ALLGATHER_FN = ctypes.CFUNCTYPE(c_int, c_size_t, c_void_p, c_void_p)
-ABI_VERSION = 5
+ABI_VERSION = 6
 DEVERR_STALE_CACHE = 1   # ONEPOSE_DEVERR_STALE_CACHE
+PART_INPUTS, PART_MATCH, PART_ALL = 1, 2, 3   # ONEPOSE_PART_* (onepose_match_cached_parts)
 OBJ_GAT_TABLES = 1   # ONEPOSE_OBJ_GAT_TABLES
 DT_F32, DT_F16 = 0, 1   # ONEPOSE_DT_*
 
@@ -49,6 +50,11 @@ PROTOTYPES = {
                                         c_int64, c_int, c_int, c_int, c_int, c_float, c_float,
                                         c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                                         c_void_p, c_void_p, c_size_t, c_void_p]),
+    "onepose_match_cached_parts": (c_int, [c_void_p, c_void_p, c_int, c_int64, c_void_p,
+                                           c_void_p, c_int64, c_int, c_int, c_int, c_int,
+                                           c_float, c_float, c_int, c_int, c_void_p, c_void_p,
+                                           c_void_p, c_void_p, c_void_p, c_void_p, c_size_t,
+                                           c_int, c_void_p]),
     "onepose_match": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64,
                               c_int, c_int, c_int, c_int, c_float, c_float,
                               c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,

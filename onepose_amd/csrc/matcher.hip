@@ -1551,7 +1551,7 @@ using namespace onepose;
 extern "C" {
 
 const char* onepose_last_error(void) { return g_last_error.c_str(); }
-int onepose_abi_version(void) { return 5; }
+int onepose_abi_version(void) { return 6; }
 
 int onepose_profile_begin(uint64_t kind_mask, int capacity) {
   clear_error();
@@ -2226,7 +2226,7 @@ int match_impl(const void* packed_weights, const void* desc2d, int64_t desc2d_bs
                float* mscores1, float* conf, const Plan& p, hipStream_t st, int precision,
                const ShardCtx* sh = nullptr, const float* obj_cache = nullptr,
                int obj_flags = 0, int desc_dt = ONEPOSE_DT_F32,
-               const CacheHdr* obj_hdr = nullptr) {
+               const CacheHdr* obj_hdr = nullptr, int parts = ONEPOSE_PART_ALL) {
   const bool with_conf = conf != nullptr;
   const int n3g = sh ? sh->n3_total : n3;   // the 3D side's full length (softmax / attention)
   const int pm = attention_pm(precision);   // attention-layer GEMM operand mode
@@ -2270,9 +2270,11 @@ int match_impl(const void* packed_weights, const void* desc2d, int64_t desc2d_bs
           obj_cache + obj_layout(n3, num_leaf, obj_flags, npl != 0).hdr);
       ta.expect = *obj_hdr;
     }
-    OP_LAUNCH(K_TRANSPOSE, st, transpose_in_kernel, dim3((ta.p[0].tiles + ta.p[1].tiles) * B),
-              dim3(256), 0, st, ta, B);
+    if (parts & ONEPOSE_PART_INPUTS)
+      OP_LAUNCH(K_TRANSPOSE, st, transpose_in_kernel, dim3((ta.p[0].tiles + ta.p[1].tiles) * B),
+                dim3(256), 0, st, ta, B);
   }
+  if (!(parts & ONEPOSE_PART_MATCH)) return ONEPOSE_OK;
 
   // Current states: side x is read from x?r (batch stride x?bs) and written to p.x?[c? ^ 1];
   // their activation planes (bf16 modes) from x?pr (null: the object cache's state, which only
@@ -2827,7 +2829,25 @@ int onepose_match_cached_dt(const void* packed_weights, const void* desc2d, int 
                             int64_t* matches0, int64_t* matches1, float* mscores0,
                             float* mscores1, float* conf, void* workspace, size_t workspace_bytes,
                             void* stream_) {
+  return onepose_match_cached_parts(packed_weights, desc2d, desc_dtype, desc2d_bstride,
+                                    object_cache, leaves_prepared, prepared_bstride, batch, n1,
+                                    n3, num_leaf, scale_factor, match_threshold, precision,
+                                    object_flags, matches0, matches1, mscores0, mscores1, conf,
+                                    workspace, workspace_bytes, ONEPOSE_PART_ALL, stream_);
+}
+
+int onepose_match_cached_parts(const void* packed_weights, const void* desc2d, int desc_dtype,
+                               int64_t desc2d_bstride, const float* object_cache,
+                               const float* leaves_prepared, int64_t prepared_bstride, int batch,
+                               int n1, int n3, int num_leaf, float scale_factor,
+                               float match_threshold, int precision, int object_flags,
+                               int64_t* matches0, int64_t* matches1, float* mscores0,
+                               float* mscores1, float* conf, void* workspace,
+                               size_t workspace_bytes, int parts, void* stream_) {
   clear_error();
+  OP_REQUIRE(parts == ONEPOSE_PART_INPUTS || parts == ONEPOSE_PART_MATCH ||
+                 parts == ONEPOSE_PART_ALL,
+             "match_cached: parts %d", parts);
   OP_REQUIRE(desc_dtype == ONEPOSE_DT_F32 || desc_dtype == ONEPOSE_DT_F16,
              "match_cached: dtype %d", desc_dtype);
   OP_REQUIRE(valid_precision(precision),
@@ -2864,7 +2884,7 @@ int onepose_match_cached_dt(const void* packed_weights, const void* desc2d, int 
                     prepared_bstride, batch, n1, n3, num_leaf, scale_factor, match_threshold,
                     matches0, matches1, mscores0, mscores1, conf, p,
                     static_cast<hipStream_t>(stream_), precision, nullptr, object_cache,
-                    object_flags, desc_dtype, &hdr);
+                    object_flags, desc_dtype, &hdr, parts);
 }
 
 int onepose_device_errors(int clear, unsigned* bits) {

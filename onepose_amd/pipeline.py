@@ -251,18 +251,26 @@ class FramePipeline:
             self.enqueue_detect(slot)
         self.enqueue_match(slot, frame)
 
-    def enqueue_match(self, slot: int = 0, frame=None):
+    def enqueue_match(self, slot: int = 0, frame=None, parts: int = _lib.PART_ALL):
+        """The matcher on the slot (frame-bank entry `frame` when given).  `parts`
+        (onepose_match_cached_parts): PART_INPUTS is the input stage alone (the frame's
+        descriptors into the slot's workspace, its counters zeroed, the object cache's header
+        checked), PART_MATCH the rest of the forward on what the input stage left there."""
         o = self.slots[slot]
         s = _lib.stream_ptr(self.device)
         desc2d, _ = self._inputs(o, frame)
+        if parts != _lib.PART_ALL and self.object_cache is None:
+            raise ValueError("the matcher's input stage runs apart only with the object cache")
+        if parts == _lib.PART_ALL:
+            self._primed = False   # the slot's staged input (if any) is overwritten
         if self.object_cache is not None:
-            _lib.check(self.lib.onepose_match_cached_dt(
+            _lib.check(self.lib.onepose_match_cached_parts(
                 self.weights.data_ptr(), desc2d.data_ptr(), self.desc_dt, 256 * self.n1,
                 self.object_cache.data_ptr(), self.leaves_pm.data_ptr(), 0,
                 self.B, self.n1, self.n3, self.L, self.scale_factor, self.threshold,
                 self.precision, self.object_flags, o.matches0.data_ptr(), o.matches1.data_ptr(),
                 o.mscores0.data_ptr(), o.mscores1.data_ptr(), _lib.ptr(o._conf),
-                o.ws_match.data_ptr(), o.ws_match_bytes, s), "onepose_match_cached")
+                o.ws_match.data_ptr(), o.ws_match_bytes, parts, s), "onepose_match_cached")
             return
         _lib.check(self.lib.onepose_match_prepared_ex(
             self.weights.data_ptr(), desc2d.data_ptr(), 256 * self.n1,
@@ -332,25 +340,64 @@ class FramePipeline:
             self.enqueue(slot)
         return g
 
-    def capture_stages(self, pool=None):
+    # ---- staged inputs: the matcher's input stage on the pose stream, one step ahead ----
+    # With a frame bank and the object cache, step g runs bank entry g % F in slot g % n.  The
+    # pose stage of step g ends with the input stage of step g + n -- the next step to use the
+    # slot -- so each matcher stage starts at its first layer, and the input kernel (the frame's
+    # descriptors into the slot's workspace, its counters zeroed, the cache header checked) runs
+    # on the pose stream beside the other stream's matcher instead of on the matcher's launch
+    # chain.  Every step still runs one input stage, one matcher and one pose stage; the step
+    # counter carries over between run_stream calls so that the staged inputs are the ones the
+    # next call's first steps need.  prime_inputs() stages the first n steps.
+    _primed = False
+    _next_step = 0
+
+    def staged_ok(self) -> bool:
+        return self.object_cache is not None and self.detector is None and self.bank_size > 0
+
+    def enqueue_inputs(self, slot: int, frame: int):
+        """The matcher's input stage alone for bank entry `frame` into `slot`."""
+        self.enqueue_match(slot, frame, parts=_lib.PART_INPUTS)
+
+    def prime_inputs(self):
+        """Stage the inputs of the next len(slots) steps on the current stream (before the first
+        staged ``run_stream``, and again after anything else used the slots' workspaces)."""
+        if not self.staged_ok():
+            raise ValueError("staged inputs need a frame bank, the object cache and no detector")
+        n, F = len(self.slots), self.bank_size
+        for g in range(self._next_step, self._next_step + n):
+            self.enqueue_inputs(g % n, g % F)
+        self._primed = True
+
+    def capture_stages(self, pool=None, staged: bool = False):
         """Capture, per buffer slot, the front stage ([detector ->] matcher) and the pose stage
         as two HIP graphs (for ``run_stream(graphs=...)``).  With a frame bank, one pair per
-        bank entry j instead (slot j % slots, the entry's inputs and result rows)."""
+        bank entry j instead (slot j % slots, the entry's inputs and result rows).  `staged`:
+        the matcher graph without its input stage, and the pose graph followed by the input
+        stage of entry (j + slots) % F (for ``run_stream(staged=True)``)."""
         out = []
-        F = self.bank_size
-        for j in range(F or len(self.slots)):
-            sl, fr = j % len(self.slots), (j if F else None)
+        F, n = self.bank_size, len(self.slots)
+        if staged and not self.staged_ok():
+            raise ValueError("staged inputs need a frame bank, the object cache and no detector")
+        for j in range(F or n):
+            sl, fr = j % n, (j if F else None)
             gm, gp = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
             with torch.cuda.graph(gm, pool=pool):
-                self.enqueue_front(sl, fr)
+                if staged:
+                    self.enqueue_match(sl, fr, parts=_lib.PART_MATCH)
+                else:
+                    self.enqueue_front(sl, fr)
             with torch.cuda.graph(gp, pool=pool):
                 self.enqueue_pose(sl, frame=fr)
+                if staged:
+                    self.enqueue_inputs(sl, (j + n) % F)
             out.append((gm, gp))
+        self._primed = False   # (the non-staged captures above mark it too)
         return out
 
     def run_stream(self, steps: int, match_stream=None, pose_stream=None, graphs=None,
                    marks=None, match_streams: int = 1, pose: bool = True,
-                   pose_streams: int = 1):
+                   pose_streams: int = 1, staged: bool = False):
         """Enqueue `steps` frames (batches) with matcher(k+1) overlapping pose(k); with
         `graphs` (from ``capture_stages``) each stage is one graph replay.  With
         `match_streams` = m > 1, consecutive frames' matchers run on m streams concurrently
@@ -362,9 +409,22 @@ class FramePipeline:
         together -- the last frames of a batch -- run side by side instead of one after the
         other.  `marks` (a list) receives per step (start, matcher done, pose done) timing
         events.  With a frame bank (``set_frame_bank``), step k runs bank entry k % F; `graphs`
-        then holds one pair per entry (``capture_stages``)."""
+        then holds one pair per entry (``capture_stages``).  `staged` (graphs from
+        ``capture_stages(staged=True)``, after ``prime_inputs``): the steps continue the bank
+        from the previous staged call, and each pose stage stages the inputs of the step that
+        next uses its slot (see ``prime_inputs``)."""
         ms0 = match_stream or torch.cuda.current_stream(self.device)
         F = self.bank_size
+        g0 = 0
+        if staged:
+            if not self.staged_ok():
+                raise ValueError("staged inputs need a frame bank, the object cache and no "
+                                 "detector")
+            if not self._primed:
+                raise RuntimeError("run_stream(staged=True): call prime_inputs() first")
+            if not pose:
+                raise ValueError("staged inputs are staged by the pose stages")
+            g0 = self._next_step
         ps = pose_stream or getattr(self, "_pose_stream", None)
         if ps is None:
             ps = self._pose_stream = torch.cuda.Stream(
@@ -389,7 +449,8 @@ class FramePipeline:
         for s in mss[1:]:
             s.wait_stream(ms0)                    # inputs written on the caller's stream
         for k in range(steps):
-            sl = k % n
+            g = g0 + k                            # the bank step (k unless staged)
+            sl = g % n
             ms = mss[k % len(mss)]
             mk = [torch.cuda.Event(enable_timing=True) for _ in range(3)] if marks is not None \
                 else None
@@ -399,9 +460,11 @@ class FramePipeline:
                 if mk:
                     mk[0].record(ms)
                 if graphs:
-                    graphs[k % len(graphs)][0].replay()
+                    graphs[g % len(graphs)][0].replay()
+                elif staged:
+                    self.enqueue_match(sl, g % F, parts=_lib.PART_MATCH)
                 else:
-                    self.enqueue_front(sl, k % F if F else None)
+                    self.enqueue_front(sl, g % F if F else None)
                 matched[sl].record(ms)
                 if mk:
                     mk[1].record(ms)
@@ -410,9 +473,11 @@ class FramePipeline:
                 ps.wait_event(matched[sl])
                 if pose:   # (False: a diagnostic of the matcher streams alone, bench.py)
                     if graphs:
-                        graphs[k % len(graphs)][1].replay()
+                        graphs[g % len(graphs)][1].replay()
                     else:
-                        self.enqueue_pose(sl, frame=k % F if F else None)
+                        self.enqueue_pose(sl, frame=g % F if F else None)
+                        if staged:
+                            self.enqueue_inputs(sl, (g + n) % F)
                 posed[sl].record(ps)
                 if mk:
                     mk[2].record(ps)
@@ -423,4 +488,6 @@ class FramePipeline:
             ms0.wait_stream(s)
         for s in pss:
             ms0.wait_stream(s)
+        if staged:
+            self._next_step = g0 + steps
         return pss[0]

@@ -18,7 +18,7 @@ float frand() {
 }  // namespace
 
 int main() {
-  if (onepose_abi_version() != 5) return 1;
+  if (onepose_abi_version() != 6) return 1;
   // matcher packer
   {
     const int n = onepose_matcher_num_tensors();

@@ -30,7 +30,7 @@ def test_library_exports_every_header_symbol():
     missing = [s for s in header_symbols() if not hasattr(lib, s)]
     assert not missing, missing
     assert set(header_symbols()) == set(_lib.PROTOTYPES), "ctypes prototypes out of sync"
-    assert lib.onepose_abi_version() == _lib.ABI_VERSION == 5
+    assert lib.onepose_abi_version() == _lib.ABI_VERSION == 6
 
 
 def test_object_cache_size_follows_its_flags():
@@ -235,3 +235,17 @@ def test_unsupported_match_type():
     data, _, _ = synthetic.make_matcher_inputs(16, 8, 2, seed=0)
     with pytest.raises(NotImplementedError):
         m({k: torch.from_numpy(v) for k, v in data.items()})
+
+
+def test_match_cached_parts_rejects_bad_parts():
+    """onepose_match_cached_parts (ABI 6) takes exactly the input part, the match part or both;
+    anything else is refused before any argument is touched (no device needed)."""
+    from onepose_amd import _lib
+    lib = _lib.load()
+    assert (_lib.PART_INPUTS, _lib.PART_MATCH, _lib.PART_ALL) == (1, 2, 3)
+    for parts in (0, 4, -1, 7):
+        rc = lib.onepose_match_cached_parts(None, None, 0, 0, None, None, 0, 1, 8, 8, 8, 1.0, 0.2,
+                                            0, 0, None, None, None, None, None, None, 0, parts,
+                                            None)
+        assert rc != 0
+        assert b"parts" in lib.onepose_last_error()

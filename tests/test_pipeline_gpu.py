@@ -201,6 +201,69 @@ def test_frame_bank_runs_each_entry_like_eager():
 
 
 @pytest.mark.gpu
+def test_frame_bank_staged_inputs_match_eager():
+    """Staged inputs (bench.py's default): the matcher's input stage runs at the end of the
+    slot's previous pose stage (onepose_match_cached_parts), the step counter carries over
+    between run_stream calls.  The two parts give the bits of the one-call forward, and every
+    bank entry's result rows equal an eager run of its frames."""
+    dev = torch.device("cuda", 0)
+    F, n = 6, 3
+    sd = synthetic.make_state_dict(0)
+    data, obj, frames = synthetic.make_matcher_inputs(N1, N3, L, seed=11, batch=F * B)
+    m = matcher.from_state_dict(sd)
+    pipe = FramePipeline(m, data["keypoints3d"][0], data["descriptors3d_db"][0],
+                         data["descriptors2d_db"][0], B, N1, dev, scale=1000.0, slots=n)
+    Ks = np.stack([f.K for f in frames]).reshape(F, B, 3, 3)
+    gts = np.stack([f.pose_gt for f in frames]).reshape(F, B, 3, 4)
+    d2 = data["descriptors2d_query"].reshape(F, B, 256, N1)
+    k2 = data["keypoints2d"].reshape(F, B, N1, 2)
+    ref = []
+    for j in range(F):
+        pipe.set_frames(d2[j], k2[j], Ks[j], gts[j])
+        pipe.enqueue(0)
+        torch.cuda.synchronize()
+        ref.append(_outputs(pipe.slots[0]))
+    pipe.set_frame_bank(d2, k2, Ks, gts)
+    with pytest.raises(RuntimeError, match="prime_inputs"):
+        pipe.run_stream(1, staged=True)
+    # the two parts against the one-call forward, on the library's outputs directly
+    o = pipe.slots[1]
+    keys = ("matches0", "matches1", "mscores0", "mscores1")
+    for j in (0, 4):
+        pipe.enqueue_match(1, j)
+        torch.cuda.synchronize()
+        whole = {k: getattr(o, k).cpu().numpy().copy() for k in keys}
+        for k in keys:
+            getattr(o, k).fill_(7)
+        pipe.enqueue_match(1, j, parts=1)
+        pipe.enqueue_match(1, j, parts=2)
+        torch.cuda.synchronize()
+        for k in keys:
+            np.testing.assert_array_equal(getattr(o, k).cpu().numpy(), whole[k], err_msg=k)
+    graphs = pipe.capture_stages(staged=True)
+    pipe.prime_inputs()
+    pipe.run_stream(7, graphs=graphs, match_streams=2, pose_streams=2, staged=True)
+    pipe.run_stream(5, graphs=graphs, match_streams=2, pose_streams=2, staged=True)
+    torch.cuda.synchronize()
+    assert pipe._next_step == 12
+    r = pipe.bank_results
+    for j in range(F):
+        for k in ("pose", "R_err", "t_err", "cmd", "n_inliers", "status"):
+            np.testing.assert_array_equal(r[k][j].cpu().numpy(), ref[j][k], err_msg=f"{k} {j}")
+    # host-launched staged steps continue the same bank sequence
+    for v in r.values():
+        v.zero_()
+    pipe.run_stream(F, match_streams=2, staged=True)
+    torch.cuda.synchronize()
+    for j in range(F):
+        np.testing.assert_array_equal(r["pose"][j].cpu().numpy(), ref[j]["pose"])
+    # a one-call forward on a slot drops the staged inputs: staged steps need priming again
+    pipe.enqueue_match(0, 0)
+    with pytest.raises(RuntimeError, match="prime_inputs"):
+        pipe.run_stream(1, graphs=graphs, staged=True)
+
+
+@pytest.mark.gpu
 def test_detector_pipeline_from_images():
     """Images -> SuperPoint -> matcher -> selection -> RANSAC-EPnP: the detector stage writes
     exactly what SuperPoint.detect_raw returns, the matcher stage equals the module forward on
