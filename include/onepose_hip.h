@@ -267,16 +267,23 @@ int onepose_match_cached_dt(const void* packed_weights,
                             int64_t* matches0, int64_t* matches1,
                             float* mscores0, float* mscores1, float* conf,
                             void* workspace, size_t workspace_bytes, void* stream);
-/* (ABI 6) onepose_match_cached_dt in two parts, for a caller that pipelines frames through
- * buffer slots (one workspace per slot) and wants the frame's input stage off the matcher's
- * launch chain.  ONEPOSE_PART_INPUTS is the forward's first kernel alone: desc2d into the
- * workspace's token-major layout, the workspace's arrival counters zeroed, the object cache's
- * header checked.  ONEPOSE_PART_MATCH is the rest of the forward, reading what the input part
- * left in the same workspace.  Both parts with the same arguments, in that order on one stream
- * or ordered by events, give the bits of one onepose_match_cached_dt call (ONEPOSE_PART_ALL);
- * nothing else may use the workspace between them.  The input part may therefore run as soon as
- * the workspace's previous forward has finished, e.g. on the stream of that forward's pose stage. */
-enum { ONEPOSE_PART_INPUTS = 1, ONEPOSE_PART_MATCH = 2, ONEPOSE_PART_ALL = 3 };
+/* (ABI 6) onepose_match_cached_dt in stages, for a caller that pipelines frames through
+ * buffer slots (one workspace per slot) and wants the short stages off the matcher's launch
+ * chain.  `parts` is one stage or consecutive stages, OR-ed (1, 2, 4, 3, 6 or 7):
+ *   ONEPOSE_PART_INPUTS   the forward's first kernel: desc2d into the workspace's token-major
+ *                         layout, the workspace's arrival counters zeroed, the object cache's
+ *                         header checked;
+ *   ONEPOSE_PART_LAYERS   the attention layers, the final projection and the score GEMM (S and
+ *                         its softmax partials in the workspace, or S in `conf`);
+ *   ONEPOSE_PART_WINNERS  the dual softmax's winners and the mutual check (matches / scores,
+ *                         and conf when requested).
+ * The stages of one forward, run in order with the same arguments (on one stream or ordered by
+ * events), give the bits of one onepose_match_cached_dt call (ONEPOSE_PART_ALL); nothing else
+ * may use the workspace in between.  So the input stage may run as soon as the workspace's
+ * previous forward has finished -- e.g. on the stream of that forward's pose stage -- and the
+ * winners on the pose stream of their own frame. */
+enum { ONEPOSE_PART_INPUTS = 1, ONEPOSE_PART_LAYERS = 2, ONEPOSE_PART_WINNERS = 4,
+       ONEPOSE_PART_ALL = 7 };
 int onepose_match_cached_parts(const void* packed_weights,
                                const void* desc2d, int desc_dtype, int64_t desc2d_bstride,
                                const float* object_cache,

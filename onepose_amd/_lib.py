@@ -22,7 +22,7 @@ c_void_p, c_char_p = ctypes.c_void_p, ctypes.c_char_p
 ALLGATHER_FN = ctypes.CFUNCTYPE(c_int, c_size_t, c_void_p, c_void_p)
 ABI_VERSION = 6
 DEVERR_STALE_CACHE = 1   # ONEPOSE_DEVERR_STALE_CACHE
-PART_INPUTS, PART_MATCH, PART_ALL = 1, 2, 3   # ONEPOSE_PART_* (onepose_match_cached_parts)
+PART_INPUTS, PART_LAYERS, PART_WINNERS, PART_ALL = 1, 2, 4, 7   # ONEPOSE_PART_* (ABI 6)
 OBJ_GAT_TABLES = 1   # ONEPOSE_OBJ_GAT_TABLES
 DT_F32, DT_F16 = 0, 1   # ONEPOSE_DT_*
 

@@ -2250,6 +2250,69 @@ int match_impl(const void* packed_weights, const void* desc2d, int64_t desc2d_bs
   // (profiles/r05/conf_rpl/, profiles/r05/smx/)
   const int score_mt = ceil_div(n1, pm_out == PM_F32 ? kScoreBM : 64);   // colpart per column
   const bool conf_stats = !sh && score_mt <= kConfColTiles && ceil_div(n3, 64) <= kConfRowTiles;
+  // the dual softmax's winners and the mutual check (ONEPOSE_PART_WINNERS): the score GEMM's
+  // partials and S in the workspace -> matches / scores
+  auto winners = [&]() -> int {
+    int rc;
+    const int ch3 = ceil_div(n3, 64);
+    const int64_t total = (int64_t)B * (n1 + n3);
+    if (!conf_stats)
+      OP_LAUNCH(K_SMX_REDUCE, st, softmax_reduce_kernel, dim3((unsigned)((total + 3) / 4)),
+                dim3(256), 0, st, p.rowpart, ch3, p.colpart, score_mt, B, n1, n3, p.rowmax,
+                p.rowsum, p.colmax, p.colsum, p.rowbest, p.colbest);
+    const int64_t nr = (int64_t)B * n1;
+    if (sh) {   // row softmax over every rank's columns
+      OP_HIP(hipMemcpyAsync(sh->send, p.rowmax, nr * 4, hipMemcpyDeviceToDevice, st));
+      OP_HIP(hipMemcpyAsync(sh->send + nr * 4, p.rowsum, nr * 4, hipMemcpyDeviceToDevice, st));
+      if ((rc = shard_exchange(*sh, nr * 8, st)) != ONEPOSE_OK) return rc;
+      OP_LAUNCH(K_SMX_REDUCE, st, rowstat_merge_kernel, dim3((unsigned)((nr + 255) / 256)),
+                dim3(256), 0, st, reinterpret_cast<const float*>(sh->recv), sh->world, 2 * nr, nr,
+                p.rowmax, p.rowsum);
+    }
+    const int coff = sh ? sh->offset : 0;
+    const dim3 cgrid(ceil_div(n1, 32) * ceil_div(n3, 256), B);
+#define CONF_LAUNCH(V, ST)                                                                   \
+  OP_LAUNCH(K_CONF, st, (conf_kernel<V, ST>), cgrid, dim3(kConfWaves * 64), 0, st, S, n1, n3,  \
+            p.rowmax,                                                                       \
+            p.rowsum, p.colmax, p.colsum, p.rowwin, p.colbest, with_conf ? 1 : 0, coff,     \
+            p.rowpart, ch3, p.colpart, score_mt)
+    if (n3 % 4 == 0) {
+      if (conf_stats) CONF_LAUNCH(true, true);
+      else CONF_LAUNCH(true, false);
+    } else {
+      if (conf_stats) CONF_LAUNCH(false, true);
+      else CONF_LAUNCH(false, false);
+    }
+#undef CONF_LAUNCH
+    const unsigned long long* colbest = p.colbest;
+    const unsigned long long* rowwin = p.rowwin;
+    if (sh) {   // row winners over all columns; every rank's column winners at global columns
+      OP_LAUNCH(K_MUTUAL, st, rowbest_reduce_kernel, dim3((unsigned)((nr + 255) / 256)), dim3(256),
+                0, st, p.rowwin, ceil_div(n3, 256), nr,
+                reinterpret_cast<unsigned long long*>(sh->send));
+      rowwin = nullptr;
+      if ((rc = shard_exchange(*sh, nr * 8, st)) != ONEPOSE_OK) return rc;
+      OP_LAUNCH(K_MUTUAL, st, best_max_kernel, dim3((unsigned)((nr + 255) / 256)), dim3(256), 0, st,
+                reinterpret_cast<const unsigned long long*>(sh->recv), sh->world, nr, nr,
+                p.rowbest);
+      const int64_t nc = (int64_t)B * sh->max_shard;
+      OP_LAUNCH(K_MUTUAL, st, colbest_pack_kernel, dim3((unsigned)((nc + 255) / 256)), dim3(256), 0,
+                st, p.colbest, B, n3, sh->max_shard,
+                reinterpret_cast<unsigned long long*>(sh->send));
+      if ((rc = shard_exchange(*sh, nc * 8, st)) != ONEPOSE_OK) return rc;
+      const int64_t nf = (int64_t)B * n3g;
+      OP_LAUNCH(K_MUTUAL, st, colbest_assemble_kernel, dim3((unsigned)((nf + 255) / 256)),
+                dim3(256), 0, st, reinterpret_cast<const unsigned long long*>(sh->recv), sh->world,
+                nc, B, n3g, sh->max_shard, sh->colbest_full);
+      colbest = sh->colbest_full;
+    }
+    const int64_t tot_g = (int64_t)B * (n1 + n3g);
+    OP_LAUNCH(K_MUTUAL, st, mutual_kernel, dim3((unsigned)((tot_g + 255) / 256)), dim3(256), 0, st,
+                       p.rowbest, rowwin, ceil_div(n3, 256), colbest, B, n1, n3g,
+                       match_threshold, matches0, matches1,
+                       mscores0, mscores1, p.err);
+    return ONEPOSE_OK;
+  };
   {
     TransArgs ta;
     ta.p[0] = {desc2d, desc2d_bstride, n1, ceil_div(n1, 64) * 4, p.x2[0], pl(p.x2p[0])};
@@ -2274,7 +2337,8 @@ int match_impl(const void* packed_weights, const void* desc2d, int64_t desc2d_bs
       OP_LAUNCH(K_TRANSPOSE, st, transpose_in_kernel, dim3((ta.p[0].tiles + ta.p[1].tiles) * B),
                 dim3(256), 0, st, ta, B);
   }
-  if (!(parts & ONEPOSE_PART_MATCH)) return ONEPOSE_OK;
+  if (!(parts & ONEPOSE_PART_LAYERS))
+    return (parts & ONEPOSE_PART_WINNERS) ? winners() : ONEPOSE_OK;
 
   // Current states: side x is read from x?r (batch stride x?bs) and written to p.x?[c? ^ 1];
   // their activation planes (bf16 modes) from x?pr (null: the object cache's state, which only
@@ -2403,65 +2467,7 @@ int match_impl(const void* packed_weights, const void* desc2d, int64_t desc2d_bs
     if ((rc = gemm_launch(EPI_SCORE, PRO_PLAIN, score_tile, a, st, K_SCORE, pm_out)) != ONEPOSE_OK)
       return rc;
   }
-  {
-    const int64_t total = (int64_t)B * (n1 + n3);
-    if (!conf_stats)
-      OP_LAUNCH(K_SMX_REDUCE, st, softmax_reduce_kernel, dim3((unsigned)((total + 3) / 4)),
-                dim3(256), 0, st, p.rowpart, ch3, p.colpart, score_mt, B, n1, n3, p.rowmax,
-                p.rowsum, p.colmax, p.colsum, p.rowbest, p.colbest);
-    const int64_t nr = (int64_t)B * n1;
-    if (sh) {   // row softmax over every rank's columns
-      OP_HIP(hipMemcpyAsync(sh->send, p.rowmax, nr * 4, hipMemcpyDeviceToDevice, st));
-      OP_HIP(hipMemcpyAsync(sh->send + nr * 4, p.rowsum, nr * 4, hipMemcpyDeviceToDevice, st));
-      if ((rc = shard_exchange(*sh, nr * 8, st)) != ONEPOSE_OK) return rc;
-      OP_LAUNCH(K_SMX_REDUCE, st, rowstat_merge_kernel, dim3((unsigned)((nr + 255) / 256)),
-                dim3(256), 0, st, reinterpret_cast<const float*>(sh->recv), sh->world, 2 * nr, nr,
-                p.rowmax, p.rowsum);
-    }
-    const int coff = sh ? sh->offset : 0;
-    const dim3 cgrid(ceil_div(n1, 32) * ceil_div(n3, 256), B);
-#define CONF_LAUNCH(V, ST)                                                                   \
-  OP_LAUNCH(K_CONF, st, (conf_kernel<V, ST>), cgrid, dim3(kConfWaves * 64), 0, st, S, n1, n3,  \
-            p.rowmax,                                                                       \
-            p.rowsum, p.colmax, p.colsum, p.rowwin, p.colbest, with_conf ? 1 : 0, coff,     \
-            p.rowpart, ch3, p.colpart, score_mt)
-    if (n3 % 4 == 0) {
-      if (conf_stats) CONF_LAUNCH(true, true);
-      else CONF_LAUNCH(true, false);
-    } else {
-      if (conf_stats) CONF_LAUNCH(false, true);
-      else CONF_LAUNCH(false, false);
-    }
-#undef CONF_LAUNCH
-    const unsigned long long* colbest = p.colbest;
-    const unsigned long long* rowwin = p.rowwin;
-    if (sh) {   // row winners over all columns; every rank's column winners at global columns
-      OP_LAUNCH(K_MUTUAL, st, rowbest_reduce_kernel, dim3((unsigned)((nr + 255) / 256)), dim3(256),
-                0, st, p.rowwin, ceil_div(n3, 256), nr,
-                reinterpret_cast<unsigned long long*>(sh->send));
-      rowwin = nullptr;
-      if ((rc = shard_exchange(*sh, nr * 8, st)) != ONEPOSE_OK) return rc;
-      OP_LAUNCH(K_MUTUAL, st, best_max_kernel, dim3((unsigned)((nr + 255) / 256)), dim3(256), 0, st,
-                reinterpret_cast<const unsigned long long*>(sh->recv), sh->world, nr, nr,
-                p.rowbest);
-      const int64_t nc = (int64_t)B * sh->max_shard;
-      OP_LAUNCH(K_MUTUAL, st, colbest_pack_kernel, dim3((unsigned)((nc + 255) / 256)), dim3(256), 0,
-                st, p.colbest, B, n3, sh->max_shard,
-                reinterpret_cast<unsigned long long*>(sh->send));
-      if ((rc = shard_exchange(*sh, nc * 8, st)) != ONEPOSE_OK) return rc;
-      const int64_t nf = (int64_t)B * n3g;
-      OP_LAUNCH(K_MUTUAL, st, colbest_assemble_kernel, dim3((unsigned)((nf + 255) / 256)),
-                dim3(256), 0, st, reinterpret_cast<const unsigned long long*>(sh->recv), sh->world,
-                nc, B, n3g, sh->max_shard, sh->colbest_full);
-      colbest = sh->colbest_full;
-    }
-    const int64_t tot_g = (int64_t)B * (n1 + n3g);
-    OP_LAUNCH(K_MUTUAL, st, mutual_kernel, dim3((unsigned)((tot_g + 255) / 256)), dim3(256), 0, st,
-                       p.rowbest, rowwin, ceil_div(n3, 256), colbest, B, n1, n3g,
-                       match_threshold, matches0, matches1,
-                       mscores0, mscores1, p.err);
-  }
-  return ONEPOSE_OK;
+  return (parts & ONEPOSE_PART_WINNERS) ? winners() : ONEPOSE_OK;
 }
 
 // The frame-independent prefix of the 3D side (onepose_object_prepare): transpose, GAT 0
@@ -2845,9 +2851,9 @@ int onepose_match_cached_parts(const void* packed_weights, const void* desc2d, i
                                float* mscores1, float* conf, void* workspace,
                                size_t workspace_bytes, int parts, void* stream_) {
   clear_error();
-  OP_REQUIRE(parts == ONEPOSE_PART_INPUTS || parts == ONEPOSE_PART_MATCH ||
-                 parts == ONEPOSE_PART_ALL,
-             "match_cached: parts %d", parts);
+  // one stage or consecutive stages, in order: 1, 2, 4, 3, 6 or 7
+  OP_REQUIRE(parts >= 1 && parts <= ONEPOSE_PART_ALL && parts != 5, "match_cached: parts %d",
+             parts);
   OP_REQUIRE(desc_dtype == ONEPOSE_DT_F32 || desc_dtype == ONEPOSE_DT_F16,
              "match_cached: dtype %d", desc_dtype);
   OP_REQUIRE(valid_precision(precision),

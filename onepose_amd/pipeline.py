@@ -253,9 +253,10 @@ class FramePipeline:
 
     def enqueue_match(self, slot: int = 0, frame=None, parts: int = _lib.PART_ALL):
         """The matcher on the slot (frame-bank entry `frame` when given).  `parts`
-        (onepose_match_cached_parts): PART_INPUTS is the input stage alone (the frame's
-        descriptors into the slot's workspace, its counters zeroed, the object cache's header
-        checked), PART_MATCH the rest of the forward on what the input stage left there."""
+        (onepose_match_cached_parts): PART_INPUTS the input stage (the frame's descriptors into
+        the slot's workspace, its counters zeroed, the object cache's header checked),
+        PART_LAYERS the attention layers through the score GEMM, PART_WINNERS the dual softmax
+        winners and the mutual check -- each on what the stage before left in the workspace."""
         o = self.slots[slot]
         s = _lib.stream_ptr(self.device)
         desc2d, _ = self._inputs(o, frame)
@@ -340,15 +341,17 @@ class FramePipeline:
             self.enqueue(slot)
         return g
 
-    # ---- staged inputs: the matcher's input stage on the pose stream, one step ahead ----
+    # ---- staged stages: the matcher's short stages on the pose stream ----
     # With a frame bank and the object cache, step g runs bank entry g % F in slot g % n.  The
-    # pose stage of step g ends with the input stage of step g + n -- the next step to use the
-    # slot -- so each matcher stage starts at its first layer, and the input kernel (the frame's
-    # descriptors into the slot's workspace, its counters zeroed, the cache header checked) runs
-    # on the pose stream beside the other stream's matcher instead of on the matcher's launch
-    # chain.  Every step still runs one input stage, one matcher and one pose stage; the step
-    # counter carries over between run_stream calls so that the staged inputs are the ones the
-    # next call's first steps need.  prime_inputs() stages the first n steps.
+    # match stream runs the attention layers through the score GEMM (PART_LAYERS) only; the pose
+    # stream runs the step's winners (dual softmax + mutual check, PART_WINNERS), its pose
+    # stage, and then the input stage of step g + n -- the next step to use the slot.  The
+    # input kernel (the frame's descriptors into the slot's workspace, its counters zeroed, the
+    # cache header checked) and the winners' two kernels thus run beside the other stream's
+    # matcher instead of on this stream's launch chain.  Every step still runs all of its
+    # forward and its pose stage; the step counter carries over between run_stream calls so
+    # that the staged inputs are the ones the next call's first steps need.  prime_inputs()
+    # stages the first n steps.
     _primed = False
     _next_step = 0
 
@@ -373,8 +376,9 @@ class FramePipeline:
         """Capture, per buffer slot, the front stage ([detector ->] matcher) and the pose stage
         as two HIP graphs (for ``run_stream(graphs=...)``).  With a frame bank, one pair per
         bank entry j instead (slot j % slots, the entry's inputs and result rows).  `staged`:
-        the matcher graph without its input stage, and the pose graph followed by the input
-        stage of entry (j + slots) % F (for ``run_stream(staged=True)``)."""
+        the matcher graph is the layers through the score GEMM, the pose graph the winners,
+        the pose stage and the input stage of entry (j + slots) % F (for
+        ``run_stream(staged=True)``)."""
         out = []
         F, n = self.bank_size, len(self.slots)
         if staged and not self.staged_ok():
@@ -384,10 +388,12 @@ class FramePipeline:
             gm, gp = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
             with torch.cuda.graph(gm, pool=pool):
                 if staged:
-                    self.enqueue_match(sl, fr, parts=_lib.PART_MATCH)
+                    self.enqueue_match(sl, fr, parts=_lib.PART_LAYERS)
                 else:
                     self.enqueue_front(sl, fr)
             with torch.cuda.graph(gp, pool=pool):
+                if staged:
+                    self.enqueue_match(sl, fr, parts=_lib.PART_WINNERS)
                 self.enqueue_pose(sl, frame=fr)
                 if staged:
                     self.enqueue_inputs(sl, (j + n) % F)
@@ -411,8 +417,9 @@ class FramePipeline:
         events.  With a frame bank (``set_frame_bank``), step k runs bank entry k % F; `graphs`
         then holds one pair per entry (``capture_stages``).  `staged` (graphs from
         ``capture_stages(staged=True)``, after ``prime_inputs``): the steps continue the bank
-        from the previous staged call, and each pose stage stages the inputs of the step that
-        next uses its slot (see ``prime_inputs``)."""
+        from the previous staged call, the match streams run the layers through the score GEMM,
+        and each pose stream runs the step's winners before its pose stage and the inputs of the
+        step that next uses the slot after it (see ``prime_inputs``)."""
         ms0 = match_stream or torch.cuda.current_stream(self.device)
         F = self.bank_size
         g0 = 0
@@ -462,7 +469,7 @@ class FramePipeline:
                 if graphs:
                     graphs[g % len(graphs)][0].replay()
                 elif staged:
-                    self.enqueue_match(sl, g % F, parts=_lib.PART_MATCH)
+                    self.enqueue_match(sl, g % F, parts=_lib.PART_LAYERS)
                 else:
                     self.enqueue_front(sl, g % F if F else None)
                 matched[sl].record(ms)
@@ -475,6 +482,8 @@ class FramePipeline:
                     if graphs:
                         graphs[g % len(graphs)][1].replay()
                     else:
+                        if staged:
+                            self.enqueue_match(sl, g % F, parts=_lib.PART_WINNERS)
                         self.enqueue_pose(sl, frame=g % F if F else None)
                         if staged:
                             self.enqueue_inputs(sl, (g + n) % F)

@@ -238,12 +238,12 @@ def test_unsupported_match_type():
 
 
 def test_match_cached_parts_rejects_bad_parts():
-    """onepose_match_cached_parts (ABI 6) takes exactly the input part, the match part or both;
-    anything else is refused before any argument is touched (no device needed)."""
+    """onepose_match_cached_parts (ABI 6) takes one stage or consecutive stages (1, 2, 4, 3, 6,
+    7); anything else is refused before any argument is touched (no device needed)."""
     from onepose_amd import _lib
     lib = _lib.load()
-    assert (_lib.PART_INPUTS, _lib.PART_MATCH, _lib.PART_ALL) == (1, 2, 3)
-    for parts in (0, 4, -1, 7):
+    assert (_lib.PART_INPUTS, _lib.PART_LAYERS, _lib.PART_WINNERS, _lib.PART_ALL) == (1, 2, 4, 7)
+    for parts in (0, 5, 8, -1):
         rc = lib.onepose_match_cached_parts(None, None, 0, 0, None, None, 0, 1, 8, 8, 8, 1.0, 0.2,
                                             0, 0, None, None, None, None, None, None, 0, parts,
                                             None)

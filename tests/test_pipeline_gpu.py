@@ -202,10 +202,11 @@ def test_frame_bank_runs_each_entry_like_eager():
 
 @pytest.mark.gpu
 def test_frame_bank_staged_inputs_match_eager():
-    """Staged inputs (bench.py's default): the matcher's input stage runs at the end of the
-    slot's previous pose stage (onepose_match_cached_parts), the step counter carries over
-    between run_stream calls.  The two parts give the bits of the one-call forward, and every
-    bank entry's result rows equal an eager run of its frames."""
+    """Staged stages (bench.py's default): the matcher's input stage runs at the end of the
+    slot's previous pose stage and its winners at the start of its own pose stage
+    (onepose_match_cached_parts), the step counter carries over between run_stream calls.  The
+    stages give the bits of the one-call forward, and every bank entry's result rows equal an
+    eager run of its frames."""
     dev = torch.device("cuda", 0)
     F, n = 6, 3
     sd = synthetic.make_state_dict(0)
@@ -226,20 +227,22 @@ def test_frame_bank_staged_inputs_match_eager():
     pipe.set_frame_bank(d2, k2, Ks, gts)
     with pytest.raises(RuntimeError, match="prime_inputs"):
         pipe.run_stream(1, staged=True)
-    # the two parts against the one-call forward, on the library's outputs directly
+    # the stages against the one-call forward, on the library's outputs directly
     o = pipe.slots[1]
     keys = ("matches0", "matches1", "mscores0", "mscores1")
     for j in (0, 4):
         pipe.enqueue_match(1, j)
         torch.cuda.synchronize()
         whole = {k: getattr(o, k).cpu().numpy().copy() for k in keys}
-        for k in keys:
-            getattr(o, k).fill_(7)
-        pipe.enqueue_match(1, j, parts=1)
-        pipe.enqueue_match(1, j, parts=2)
-        torch.cuda.synchronize()
-        for k in keys:
-            np.testing.assert_array_equal(getattr(o, k).cpu().numpy(), whole[k], err_msg=k)
+        for split in ((1, 2, 4), (3, 4), (1, 6)):
+            for k in keys:
+                getattr(o, k).fill_(7)
+            for parts in split:
+                pipe.enqueue_match(1, j, parts=parts)
+            torch.cuda.synchronize()
+            for k in keys:
+                np.testing.assert_array_equal(getattr(o, k).cpu().numpy(), whole[k],
+                                              err_msg=f"{k} {split}")
     graphs = pipe.capture_stages(staged=True)
     pipe.prime_inputs()
     pipe.run_stream(7, graphs=graphs, match_streams=2, pose_streams=2, staged=True)
