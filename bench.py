@@ -305,6 +305,10 @@ def main():
     ap.add_argument("--no-staged-inputs", action="store_true",
                     help="run each step's matcher input stage (transpose_in) at the head of its "
                          "matcher instead of at the end of the slot's previous pose stage")
+    ap.add_argument("--staged-split", type=int, default=13,
+                    help="staged mode: the forward's first stage on the pose stream "
+                         "(onepose_match_cached_stages: 1 + i = GNN layer i, 13 = final "
+                         "projection, 14 = score GEMM, 15 = dual-softmax winners)")
     ap.add_argument("--diag-repeats", type=int, default=0,
                     help="diagnostic: after the timed region, time it again this many times "
                          "and report those ms/step too (value always comes from the first)")
@@ -405,6 +409,8 @@ def main():
     # the step that next uses its slot, so the matcher's launch chain starts at its first layer
     staged = (overlap and pipe.staged_ok() and not args.no_staged_inputs
               and not args.diag_no_pose and not args.diag_steps)
+    if staged:
+        pipe.staged_split = args.staged_split
     stage_graphs = (pipe.capture_stages(torch.cuda.graph_pool_handle(), staged=staged)
                     if graphs_on else None)
     if staged:
@@ -619,8 +625,13 @@ def main():
                  "pose stream(s) overlapping the next matchers"
                  if overlap else "serial steps")
         sched += "; stages replayed as HIP graphs" if graphs_on else "; host-launched kernels"
-        sched += ("; each step's matcher input stage run at the end of its slot's previous pose "
-                  "stage" if staged else "")
+        tail_name = ({13: "final projection, score GEMM and dual-softmax winners",
+                      14: "score GEMM and dual-softmax winners",
+                      15: "dual-softmax winners"}.get(args.staged_split)
+                     or f"GNN layers {args.staged_split - 1}-11, final projection, score GEMM "
+                        "and dual-softmax winners")
+        sched += (("; each step's matcher input stage run at the end of its slot's previous "
+                   f"pose stage, its {tail_name} at the start of its own") if staged else "")
         sched += ("; object prefix (GAT 0 + 3D half of self-attention 1) prepared once per object"
                   if cached else "; every layer run per frame")
         out = {

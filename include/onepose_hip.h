@@ -59,7 +59,7 @@ enum { ONEPOSE_DT_F32 = 0, ONEPOSE_DT_F16 = 1 };
 const char* onepose_last_error(void);
 /* ABI version, bumped on any signature change or new entry point (4: the per-precision
  * workspace and object-cache size queries; 5: the object cache's device-side header and
- * onepose_device_errors; 6: onepose_match_cached_parts). */
+ * onepose_device_errors; 6: onepose_match_cached_stages). */
 int onepose_abi_version(void);
 /* (ABI 5) The library's sticky device-side error bits (ONEPOSE_DEVERR_*), set by kernels that
  * cannot return a status: *bits receives them, and `clear` != 0 resets them.  Synchronises with
@@ -267,33 +267,39 @@ int onepose_match_cached_dt(const void* packed_weights,
                             int64_t* matches0, int64_t* matches1,
                             float* mscores0, float* mscores1, float* conf,
                             void* workspace, size_t workspace_bytes, void* stream);
-/* (ABI 6) onepose_match_cached_dt in stages, for a caller that pipelines frames through
- * buffer slots (one workspace per slot) and wants the short stages off the matcher's launch
- * chain.  `parts` is one stage or consecutive stages, OR-ed (1, 2, 4, 3, 6 or 7):
- *   ONEPOSE_PART_INPUTS   the forward's first kernel: desc2d into the workspace's token-major
- *                         layout, the workspace's arrival counters zeroed, the object cache's
- *                         header checked;
- *   ONEPOSE_PART_LAYERS   the attention layers, the final projection and the score GEMM (S and
- *                         its softmax partials in the workspace, or S in `conf`);
- *   ONEPOSE_PART_WINNERS  the dual softmax's winners and the mutual check (matches / scores,
- *                         and conf when requested).
- * The stages of one forward, run in order with the same arguments (on one stream or ordered by
- * events), give the bits of one onepose_match_cached_dt call (ONEPOSE_PART_ALL); nothing else
- * may use the workspace in between.  So the input stage may run as soon as the workspace's
- * previous forward has finished -- e.g. on the stream of that forward's pose stage -- and the
- * winners on the pose stream of their own frame. */
-enum { ONEPOSE_PART_INPUTS = 1, ONEPOSE_PART_LAYERS = 2, ONEPOSE_PART_WINNERS = 4,
-       ONEPOSE_PART_ALL = 7 };
-int onepose_match_cached_parts(const void* packed_weights,
-                               const void* desc2d, int desc_dtype, int64_t desc2d_bstride,
-                               const float* object_cache,
-                               const float* leaves_prepared, int64_t prepared_bstride,
-                               int batch, int n1, int n3, int num_leaf,
-                               float scale_factor, float match_threshold, int precision,
-                               int object_flags,
-                               int64_t* matches0, int64_t* matches1,
-                               float* mscores0, float* mscores1, float* conf,
-                               void* workspace, size_t workspace_bytes, int parts, void* stream);
+/* (ABI 6) onepose_match_cached_dt as a range of its stages, for a caller that pipelines frames
+ * through buffer slots (one workspace per slot) and wants stages off the matcher's launch
+ * chain.  The forward's stages, in order:
+ *   ONEPOSE_STAGE_INPUTS        its first kernel: desc2d into the workspace's token-major layout,
+ *                               the workspace's arrival counters zeroed, the object cache's
+ *                               header checked;
+ *   ONEPOSE_STAGE_LAYER0 + i    GNN layer i, i = 0..11 of ['GATs', 'self', 'cross'] x 4
+ *                               (GATs_SuperGlue.py:184-191; the cached object supplies GAT 0 and
+ *                               the 3D half of self-attention 1);
+ *   ONEPOSE_STAGE_FINAL         the final projection (+ L2 normalisation) of both sides;
+ *   ONEPOSE_STAGE_SCORE         the score GEMM (S and its softmax partials in the workspace, or
+ *                               S in `conf`);
+ *   ONEPOSE_STAGE_WINNERS       the dual softmax's winners and the mutual check (matches /
+ *                               scores, and conf when requested).
+ * onepose_match_cached_stages runs stages first_stage..last_stage.  Consecutive ranges of one
+ * forward, run in order with the same arguments (on one stream or ordered by events), give the
+ * bits of one onepose_match_cached_dt call (the range INPUTS..WINNERS); nothing else may use
+ * the workspace in between.  So the input stage may run as soon as the workspace's previous
+ * forward has finished -- e.g. on the stream of that forward's pose stage -- and the last
+ * stages on the pose stream of their own frame. */
+enum { ONEPOSE_STAGE_INPUTS = 0, ONEPOSE_STAGE_LAYER0 = 1, ONEPOSE_STAGE_FINAL = 13,
+       ONEPOSE_STAGE_SCORE = 14, ONEPOSE_STAGE_WINNERS = 15 };
+int onepose_match_cached_stages(const void* packed_weights,
+                                const void* desc2d, int desc_dtype, int64_t desc2d_bstride,
+                                const float* object_cache,
+                                const float* leaves_prepared, int64_t prepared_bstride,
+                                int batch, int n1, int n3, int num_leaf,
+                                float scale_factor, float match_threshold, int precision,
+                                int object_flags,
+                                int64_t* matches0, int64_t* matches1,
+                                float* mscores0, float* mscores1, float* conf,
+                                void* workspace, size_t workspace_bytes, int first_stage,
+                                int last_stage, void* stream);
 
 /* ------------------------------------------------------------------------------------ *
  * N3-sharded single frame (SURVEY.md §8e optional / §8f rank 4): one frame's 3D points split

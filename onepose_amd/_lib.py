@@ -22,7 +22,7 @@ c_void_p, c_char_p = ctypes.c_void_p, ctypes.c_char_p
 ALLGATHER_FN = ctypes.CFUNCTYPE(c_int, c_size_t, c_void_p, c_void_p)
 ABI_VERSION = 6
 DEVERR_STALE_CACHE = 1   # ONEPOSE_DEVERR_STALE_CACHE
-PART_INPUTS, PART_LAYERS, PART_WINNERS, PART_ALL = 1, 2, 4, 7   # ONEPOSE_PART_* (ABI 6)
+STAGE_INPUTS, STAGE_LAYER0, STAGE_FINAL, STAGE_SCORE, STAGE_WINNERS = 0, 1, 13, 14, 15  # ABI 6
 OBJ_GAT_TABLES = 1   # ONEPOSE_OBJ_GAT_TABLES
 DT_F32, DT_F16 = 0, 1   # ONEPOSE_DT_*
 
@@ -50,11 +50,11 @@ PROTOTYPES = {
                                         c_int64, c_int, c_int, c_int, c_int, c_float, c_float,
                                         c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                                         c_void_p, c_void_p, c_size_t, c_void_p]),
-    "onepose_match_cached_parts": (c_int, [c_void_p, c_void_p, c_int, c_int64, c_void_p,
-                                           c_void_p, c_int64, c_int, c_int, c_int, c_int,
-                                           c_float, c_float, c_int, c_int, c_void_p, c_void_p,
-                                           c_void_p, c_void_p, c_void_p, c_void_p, c_size_t,
-                                           c_int, c_void_p]),
+    "onepose_match_cached_stages": (c_int, [c_void_p, c_void_p, c_int, c_int64, c_void_p,
+                                            c_void_p, c_int64, c_int, c_int, c_int, c_int,
+                                            c_float, c_float, c_int, c_int, c_void_p, c_void_p,
+                                            c_void_p, c_void_p, c_void_p, c_void_p, c_size_t,
+                                            c_int, c_int, c_void_p]),
     "onepose_match": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64,
                               c_int, c_int, c_int, c_int, c_float, c_float,
                               c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,

@@ -2226,7 +2226,10 @@ int match_impl(const void* packed_weights, const void* desc2d, int64_t desc2d_bs
                float* mscores1, float* conf, const Plan& p, hipStream_t st, int precision,
                const ShardCtx* sh = nullptr, const float* obj_cache = nullptr,
                int obj_flags = 0, int desc_dt = ONEPOSE_DT_F32,
-               const CacheHdr* obj_hdr = nullptr, int parts = ONEPOSE_PART_ALL) {
+               const CacheHdr* obj_hdr = nullptr, int first_stage = ONEPOSE_STAGE_INPUTS,
+               int last_stage = ONEPOSE_STAGE_WINNERS) {
+  // the stages [first_stage, last_stage] of the forward (onepose_match_cached_stages)
+  auto in_range = [&](int stage) { return stage >= first_stage && stage <= last_stage; };
   const bool with_conf = conf != nullptr;
   const int n3g = sh ? sh->n3_total : n3;   // the 3D side's full length (softmax / attention)
   const int pm = attention_pm(precision);   // attention-layer GEMM operand mode
@@ -2250,7 +2253,7 @@ int match_impl(const void* packed_weights, const void* desc2d, int64_t desc2d_bs
   // (profiles/r05/conf_rpl/, profiles/r05/smx/)
   const int score_mt = ceil_div(n1, pm_out == PM_F32 ? kScoreBM : 64);   // colpart per column
   const bool conf_stats = !sh && score_mt <= kConfColTiles && ceil_div(n3, 64) <= kConfRowTiles;
-  // the dual softmax's winners and the mutual check (ONEPOSE_PART_WINNERS): the score GEMM's
+  // the dual softmax's winners and the mutual check (ONEPOSE_STAGE_WINNERS): the score GEMM's
   // partials and S in the workspace -> matches / scores
   auto winners = [&]() -> int {
     int rc;
@@ -2333,12 +2336,12 @@ int match_impl(const void* packed_weights, const void* desc2d, int64_t desc2d_bs
           obj_cache + obj_layout(n3, num_leaf, obj_flags, npl != 0).hdr);
       ta.expect = *obj_hdr;
     }
-    if (parts & ONEPOSE_PART_INPUTS)
+    if (in_range(ONEPOSE_STAGE_INPUTS))
       OP_LAUNCH(K_TRANSPOSE, st, transpose_in_kernel, dim3((ta.p[0].tiles + ta.p[1].tiles) * B),
                 dim3(256), 0, st, ta, B);
   }
-  if (!(parts & ONEPOSE_PART_LAYERS))
-    return (parts & ONEPOSE_PART_WINNERS) ? winners() : ONEPOSE_OK;
+  if (last_stage < ONEPOSE_STAGE_LAYER0 || first_stage > ONEPOSE_STAGE_SCORE)
+    return in_range(ONEPOSE_STAGE_WINNERS) ? winners() : ONEPOSE_OK;
 
   // Current states: side x is read from x?r (batch stride x?bs) and written to p.x?[c? ^ 1];
   // their activation planes (bf16 modes) from x?pr (null: the object cache's state, which only
@@ -2351,6 +2354,10 @@ int match_impl(const void* packed_weights, const void* desc2d, int64_t desc2d_bs
   const uint16_t* x3pr = obj_cache ? nullptr : pl(p.x3p[0]);
   const int ch2 = ceil_div(n1, 64), ch3 = ceil_div(n3, 64);
   for (int layer = 0; layer < kLayers; ++layer) {
+    if (last_stage < ONEPOSE_STAGE_LAYER0 + layer) return ONEPOSE_OK;
+    // a layer outside the range ran in an earlier call on the same workspace (or runs in a
+    // later one): the loop only tracks which buffers hold the states
+    const bool run_layers = in_range(ONEPOSE_STAGE_LAYER0 + layer);
     const int kind = layer % 3;  // 0 GATs, 1 self, 2 cross
     const bool cached3 = obj_cache && layer < 2;   // the 3D side comes from the cache
     if (kind == 0) {
@@ -2363,7 +2370,8 @@ int match_impl(const void* packed_weights, const void* desc2d, int64_t desc2d_bs
                                 : nullptr;
         const ObjLayout OL = obj_layout(n3, num_leaf, obj_flags, npl != 0);
         uint16_t* yp = pl(p.x3p[c3 ^ 1]);
-        if (slog != nullptr && OL.tables) {
+        if (!run_layers) {
+        } else if (slog != nullptr && OL.tables) {
           OP_LAUNCH(K_GAT, st, gat_tab_kernel, ggrid, dim3(256), 0, st, x3r, gat_weights(wbase, gat),
                     obj_cache + OL.slogs + (int64_t)(gat - 1) * n3 * kLogitStride,
                     obj_cache + OL.tab + (int64_t)(gat - 1) * n3 * 2 * num_leaf * 256,
@@ -2406,8 +2414,9 @@ int match_impl(const void* packed_weights, const void* desc2d, int64_t desc2d_bs
     // sharded frames: one set for the launch
     const LayerTiles tl = !sh && ap <= 2 ? side_tiles(n1, n3, B, pm, kind == 2)
                                          : layer_tiles(qkv_n3, sd, 2, B, pm, sh);
-    int rc;
-    if (cached3) {   // self-attention 1, 2D half (the 3D half is in the object cache)
+    int rc = ONEPOSE_OK;
+    if (!run_layers) {
+    } else if (cached3) {   // self-attention 1, 2D half (the 3D half is in the object cache)
       rc = attention_layer(w, sd, 1, B, p, lcnt, st, pm, sh, tl);
     } else if (obj_cache && layer == 2 && !sh) {
       // cross-attention 1: the 3D side's frame-independent half from the object cache
@@ -2431,8 +2440,9 @@ int match_impl(const void* packed_weights, const void* desc2d, int64_t desc2d_bs
     }
   }
 
+  if (last_stage < ONEPOSE_STAGE_FINAL) return ONEPOSE_OK;
   int rc;
-  {  // final_proj on both sides, then L2 normalise
+  if (in_range(ONEPOSE_STAGE_FINAL)) {  // final_proj on both sides, then L2 normalise
     const float* fw = final_weights(wbase);
     GemmArgs a;
     a.nprob = 2;
@@ -2453,6 +2463,7 @@ int match_impl(const void* packed_weights, const void* desc2d, int64_t desc2d_bs
                 B * n1, p.f3, B * n3);
     }
   }
+  if (!in_range(ONEPOSE_STAGE_SCORE)) return ONEPOSE_OK;   // (a range: no winners either)
   // score tile: 128 x 64 on 8 waves in fp32 (K = 256 is short; fewer operand loads per FLOP
   // than 64 x 64), 64 x 64 in the split mode (its LDS images are three bf16 planes)
   const int score_tile = pm_out == PM_F32 ? kTileScore : TILE_64x64;
@@ -2467,7 +2478,7 @@ int match_impl(const void* packed_weights, const void* desc2d, int64_t desc2d_bs
     if ((rc = gemm_launch(EPI_SCORE, PRO_PLAIN, score_tile, a, st, K_SCORE, pm_out)) != ONEPOSE_OK)
       return rc;
   }
-  return (parts & ONEPOSE_PART_WINNERS) ? winners() : ONEPOSE_OK;
+  return in_range(ONEPOSE_STAGE_WINNERS) ? winners() : ONEPOSE_OK;
 }
 
 // The frame-independent prefix of the 3D side (onepose_object_prepare): transpose, GAT 0
@@ -2835,25 +2846,27 @@ int onepose_match_cached_dt(const void* packed_weights, const void* desc2d, int 
                             int64_t* matches0, int64_t* matches1, float* mscores0,
                             float* mscores1, float* conf, void* workspace, size_t workspace_bytes,
                             void* stream_) {
-  return onepose_match_cached_parts(packed_weights, desc2d, desc_dtype, desc2d_bstride,
+  return onepose_match_cached_stages(packed_weights, desc2d, desc_dtype, desc2d_bstride,
                                     object_cache, leaves_prepared, prepared_bstride, batch, n1,
                                     n3, num_leaf, scale_factor, match_threshold, precision,
                                     object_flags, matches0, matches1, mscores0, mscores1, conf,
-                                    workspace, workspace_bytes, ONEPOSE_PART_ALL, stream_);
+                                    workspace, workspace_bytes, ONEPOSE_STAGE_INPUTS,
+                                    ONEPOSE_STAGE_WINNERS, stream_);
 }
 
-int onepose_match_cached_parts(const void* packed_weights, const void* desc2d, int desc_dtype,
+int onepose_match_cached_stages(const void* packed_weights, const void* desc2d, int desc_dtype,
                                int64_t desc2d_bstride, const float* object_cache,
                                const float* leaves_prepared, int64_t prepared_bstride, int batch,
                                int n1, int n3, int num_leaf, float scale_factor,
                                float match_threshold, int precision, int object_flags,
                                int64_t* matches0, int64_t* matches1, float* mscores0,
                                float* mscores1, float* conf, void* workspace,
-                               size_t workspace_bytes, int parts, void* stream_) {
+                               size_t workspace_bytes, int first_stage, int last_stage,
+                               void* stream_) {
   clear_error();
-  // one stage or consecutive stages, in order: 1, 2, 4, 3, 6 or 7
-  OP_REQUIRE(parts >= 1 && parts <= ONEPOSE_PART_ALL && parts != 5, "match_cached: parts %d",
-             parts);
+  OP_REQUIRE(first_stage >= ONEPOSE_STAGE_INPUTS && first_stage <= last_stage &&
+                 last_stage <= ONEPOSE_STAGE_WINNERS,
+             "match_cached: stages [%d, %d]", first_stage, last_stage);
   OP_REQUIRE(desc_dtype == ONEPOSE_DT_F32 || desc_dtype == ONEPOSE_DT_F16,
              "match_cached: dtype %d", desc_dtype);
   OP_REQUIRE(valid_precision(precision),
@@ -2890,7 +2903,7 @@ int onepose_match_cached_parts(const void* packed_weights, const void* desc2d, i
                     prepared_bstride, batch, n1, n3, num_leaf, scale_factor, match_threshold,
                     matches0, matches1, mscores0, mscores1, conf, p,
                     static_cast<hipStream_t>(stream_), precision, nullptr, object_cache,
-                    object_flags, desc_dtype, &hdr, parts);
+                    object_flags, desc_dtype, &hdr, first_stage, last_stage);
 }
 
 int onepose_device_errors(int clear, unsigned* bits) {

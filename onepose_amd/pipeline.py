@@ -251,27 +251,31 @@ class FramePipeline:
             self.enqueue_detect(slot)
         self.enqueue_match(slot, frame)
 
-    def enqueue_match(self, slot: int = 0, frame=None, parts: int = _lib.PART_ALL):
-        """The matcher on the slot (frame-bank entry `frame` when given).  `parts`
-        (onepose_match_cached_parts): PART_INPUTS the input stage (the frame's descriptors into
-        the slot's workspace, its counters zeroed, the object cache's header checked),
-        PART_LAYERS the attention layers through the score GEMM, PART_WINNERS the dual softmax
-        winners and the mutual check -- each on what the stage before left in the workspace."""
+    def enqueue_match(self, slot: int = 0, frame=None, stages=None):
+        """The matcher on the slot (frame-bank entry `frame` when given).  `stages`
+        (first, last) runs that range of the forward's stages (onepose_match_cached_stages):
+        STAGE_INPUTS (the frame's descriptors into the slot's workspace, its counters zeroed,
+        the object cache's header checked), STAGE_LAYER0 + i (GNN layer i), STAGE_FINAL (final
+        projection), STAGE_SCORE (score GEMM), STAGE_WINNERS (dual softmax winners + mutual
+        check) -- each on what the stages before left in the workspace; None: the whole
+        forward."""
         o = self.slots[slot]
         s = _lib.stream_ptr(self.device)
         desc2d, _ = self._inputs(o, frame)
-        if parts != _lib.PART_ALL and self.object_cache is None:
-            raise ValueError("the matcher's input stage runs apart only with the object cache")
-        if parts == _lib.PART_ALL:
+        if stages is not None and self.object_cache is None:
+            raise ValueError("the matcher runs by stages only with the object cache")
+        if stages is None:
             self._primed = False   # the slot's staged input (if any) is overwritten
+            stages = (_lib.STAGE_INPUTS, _lib.STAGE_WINNERS)
         if self.object_cache is not None:
-            _lib.check(self.lib.onepose_match_cached_parts(
+            _lib.check(self.lib.onepose_match_cached_stages(
                 self.weights.data_ptr(), desc2d.data_ptr(), self.desc_dt, 256 * self.n1,
                 self.object_cache.data_ptr(), self.leaves_pm.data_ptr(), 0,
                 self.B, self.n1, self.n3, self.L, self.scale_factor, self.threshold,
                 self.precision, self.object_flags, o.matches0.data_ptr(), o.matches1.data_ptr(),
                 o.mscores0.data_ptr(), o.mscores1.data_ptr(), _lib.ptr(o._conf),
-                o.ws_match.data_ptr(), o.ws_match_bytes, parts, s), "onepose_match_cached")
+                o.ws_match.data_ptr(), o.ws_match_bytes, stages[0], stages[1], s),
+                "onepose_match_cached")
             return
         _lib.check(self.lib.onepose_match_prepared_ex(
             self.weights.data_ptr(), desc2d.data_ptr(), 256 * self.n1,
@@ -343,24 +347,31 @@ class FramePipeline:
 
     # ---- staged stages: the matcher's short stages on the pose stream ----
     # With a frame bank and the object cache, step g runs bank entry g % F in slot g % n.  The
-    # match stream runs the attention layers through the score GEMM (PART_LAYERS) only; the pose
-    # stream runs the step's winners (dual softmax + mutual check, PART_WINNERS), its pose
-    # stage, and then the input stage of step g + n -- the next step to use the slot.  The
-    # input kernel (the frame's descriptors into the slot's workspace, its counters zeroed, the
-    # cache header checked) and the winners' two kernels thus run beside the other stream's
-    # matcher instead of on this stream's launch chain.  Every step still runs all of its
+    # match stream runs the GNN layers; the pose stream runs the rest of the step's forward from
+    # stage ``staged_split`` (default: the final projection + score GEMM, then the dual-softmax
+    # winners + mutual check), its pose stage, and then the input stage of step g + n -- the
+    # next step to use the slot.  The input kernel (the frame's descriptors into the slot's
+    # workspace, its counters zeroed, the cache header checked) and the forward's tail thus run
+    # beside the other streams' layers instead of on this stream's launch chain.  Every step still runs all of its
     # forward and its pose stage; the step counter carries over between run_stream calls so
     # that the staged inputs are the ones the next call's first steps need.  prime_inputs()
     # stages the first n steps.
     _primed = False
     _next_step = 0
+    staged_split = _lib.STAGE_FINAL   # first stage of the forward on the pose stream
+
+    def _staged_split(self):
+        k = self.staged_split
+        if not _lib.STAGE_LAYER0 < k <= _lib.STAGE_WINNERS:
+            raise ValueError(f"staged_split {k}")
+        return (_lib.STAGE_LAYER0, k - 1), (k, _lib.STAGE_WINNERS)
 
     def staged_ok(self) -> bool:
         return self.object_cache is not None and self.detector is None and self.bank_size > 0
 
     def enqueue_inputs(self, slot: int, frame: int):
         """The matcher's input stage alone for bank entry `frame` into `slot`."""
-        self.enqueue_match(slot, frame, parts=_lib.PART_INPUTS)
+        self.enqueue_match(slot, frame, stages=(_lib.STAGE_INPUTS, _lib.STAGE_INPUTS))
 
     def prime_inputs(self):
         """Stage the inputs of the next len(slots) steps on the current stream (before the first
@@ -376,29 +387,31 @@ class FramePipeline:
         """Capture, per buffer slot, the front stage ([detector ->] matcher) and the pose stage
         as two HIP graphs (for ``run_stream(graphs=...)``).  With a frame bank, one pair per
         bank entry j instead (slot j % slots, the entry's inputs and result rows).  `staged`:
-        the matcher graph is the layers through the score GEMM, the pose graph the winners,
-        the pose stage and the input stage of entry (j + slots) % F (for
+        the matcher graph is the GNN layers before ``staged_split``, the pose graph the rest of
+        the forward, the pose stage and the input stage of entry (j + slots) % F (for
         ``run_stream(staged=True)``)."""
         out = []
         F, n = self.bank_size, len(self.slots)
         if staged and not self.staged_ok():
             raise ValueError("staged inputs need a frame bank, the object cache and no detector")
+        head, tail = self._staged_split()
         for j in range(F or n):
             sl, fr = j % n, (j if F else None)
             gm, gp = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
             with torch.cuda.graph(gm, pool=pool):
                 if staged:
-                    self.enqueue_match(sl, fr, parts=_lib.PART_LAYERS)
+                    self.enqueue_match(sl, fr, stages=head)
                 else:
                     self.enqueue_front(sl, fr)
             with torch.cuda.graph(gp, pool=pool):
                 if staged:
-                    self.enqueue_match(sl, fr, parts=_lib.PART_WINNERS)
+                    self.enqueue_match(sl, fr, stages=tail)
                 self.enqueue_pose(sl, frame=fr)
                 if staged:
                     self.enqueue_inputs(sl, (j + n) % F)
             out.append((gm, gp))
         self._primed = False   # (the non-staged captures above mark it too)
+        self._captured_split = (head, tail) if staged else None
         return out
 
     def run_stream(self, steps: int, match_stream=None, pose_stream=None, graphs=None,
@@ -417,9 +430,10 @@ class FramePipeline:
         events.  With a frame bank (``set_frame_bank``), step k runs bank entry k % F; `graphs`
         then holds one pair per entry (``capture_stages``).  `staged` (graphs from
         ``capture_stages(staged=True)``, after ``prime_inputs``): the steps continue the bank
-        from the previous staged call, the match streams run the layers through the score GEMM,
-        and each pose stream runs the step's winners before its pose stage and the inputs of the
-        step that next uses the slot after it (see ``prime_inputs``)."""
+        from the previous staged call, the match streams run the GNN layers before
+        ``staged_split``, and each pose stream runs the rest of the step's forward before its
+        pose stage and the inputs of the step that next uses the slot after it (see
+        ``prime_inputs``)."""
         ms0 = match_stream or torch.cuda.current_stream(self.device)
         F = self.bank_size
         g0 = 0
@@ -432,6 +446,10 @@ class FramePipeline:
             if not pose:
                 raise ValueError("staged inputs are staged by the pose stages")
             g0 = self._next_step
+            head, tail = self._staged_split()
+            if graphs and getattr(self, "_captured_split", None) != (head, tail):
+                raise ValueError("graphs were not captured with capture_stages(staged=True) "
+                                 "for this staged_split")
         ps = pose_stream or getattr(self, "_pose_stream", None)
         if ps is None:
             ps = self._pose_stream = torch.cuda.Stream(
@@ -469,7 +487,7 @@ class FramePipeline:
                 if graphs:
                     graphs[g % len(graphs)][0].replay()
                 elif staged:
-                    self.enqueue_match(sl, g % F, parts=_lib.PART_LAYERS)
+                    self.enqueue_match(sl, g % F, stages=head)
                 else:
                     self.enqueue_front(sl, g % F if F else None)
                 matched[sl].record(ms)
@@ -483,7 +501,7 @@ class FramePipeline:
                         graphs[g % len(graphs)][1].replay()
                     else:
                         if staged:
-                            self.enqueue_match(sl, g % F, parts=_lib.PART_WINNERS)
+                            self.enqueue_match(sl, g % F, stages=tail)
                         self.enqueue_pose(sl, frame=g % F if F else None)
                         if staged:
                             self.enqueue_inputs(sl, (g + n) % F)

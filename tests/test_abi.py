@@ -237,15 +237,16 @@ def test_unsupported_match_type():
         m({k: torch.from_numpy(v) for k, v in data.items()})
 
 
-def test_match_cached_parts_rejects_bad_parts():
-    """onepose_match_cached_parts (ABI 6) takes one stage or consecutive stages (1, 2, 4, 3, 6,
-    7); anything else is refused before any argument is touched (no device needed)."""
+def test_match_cached_stages_rejects_bad_ranges():
+    """onepose_match_cached_stages (ABI 6) runs a range of the forward's stages; an empty or
+    out-of-order range is refused before any argument is touched (no device needed)."""
     from onepose_amd import _lib
     lib = _lib.load()
-    assert (_lib.PART_INPUTS, _lib.PART_LAYERS, _lib.PART_WINNERS, _lib.PART_ALL) == (1, 2, 4, 7)
-    for parts in (0, 5, 8, -1):
-        rc = lib.onepose_match_cached_parts(None, None, 0, 0, None, None, 0, 1, 8, 8, 8, 1.0, 0.2,
-                                            0, 0, None, None, None, None, None, None, 0, parts,
-                                            None)
+    assert (_lib.STAGE_INPUTS, _lib.STAGE_LAYER0, _lib.STAGE_FINAL, _lib.STAGE_SCORE,
+            _lib.STAGE_WINNERS) == (0, 1, 13, 14, 15)
+    for first, last in ((-1, 15), (0, 16), (5, 4), (15, 14), (16, 16)):
+        rc = lib.onepose_match_cached_stages(None, None, 0, 0, None, None, 0, 1, 8, 8, 8, 1.0,
+                                             0.2, 0, 0, None, None, None, None, None, None, 0,
+                                             first, last, None)
         assert rc != 0
-        assert b"parts" in lib.onepose_last_error()
+        assert b"stages" in lib.onepose_last_error()

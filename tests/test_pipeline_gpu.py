@@ -203,10 +203,10 @@ def test_frame_bank_runs_each_entry_like_eager():
 @pytest.mark.gpu
 def test_frame_bank_staged_inputs_match_eager():
     """Staged stages (bench.py's default): the matcher's input stage runs at the end of the
-    slot's previous pose stage and its winners at the start of its own pose stage
-    (onepose_match_cached_parts), the step counter carries over between run_stream calls.  The
-    stages give the bits of the one-call forward, and every bank entry's result rows equal an
-    eager run of its frames."""
+    slot's previous pose stage and its tail (final projection, score GEMM, winners) at the start
+    of its own pose stage (onepose_match_cached_stages); the step counter carries over between
+    run_stream calls.  Consecutive stage ranges give the bits of the one-call forward, and every
+    bank entry's result rows equal an eager run of its frames."""
     dev = torch.device("cuda", 0)
     F, n = 6, 3
     sd = synthetic.make_state_dict(0)
@@ -234,11 +234,13 @@ def test_frame_bank_staged_inputs_match_eager():
         pipe.enqueue_match(1, j)
         torch.cuda.synchronize()
         whole = {k: getattr(o, k).cpu().numpy().copy() for k in keys}
-        for split in ((1, 2, 4), (3, 4), (1, 6)):
+        for split in ([(0, 0), (1, 12), (13, 13), (14, 14), (15, 15)],
+                      [(0, 5), (6, 12), (13, 15)], [(0, 1), (2, 2), (3, 3), (4, 11), (12, 15)],
+                      [(0, 13), (14, 15)], [(0, 15)]):
             for k in keys:
                 getattr(o, k).fill_(7)
-            for parts in split:
-                pipe.enqueue_match(1, j, parts=parts)
+            for rng in split:
+                pipe.enqueue_match(1, j, stages=rng)
             torch.cuda.synchronize()
             for k in keys:
                 np.testing.assert_array_equal(getattr(o, k).cpu().numpy(), whole[k],
@@ -264,6 +266,20 @@ def test_frame_bank_staged_inputs_match_eager():
     pipe.enqueue_match(0, 0)
     with pytest.raises(RuntimeError, match="prime_inputs"):
         pipe.run_stream(1, graphs=graphs, staged=True)
+    # the last two GNN layers on the pose stream too (bench.py --staged-split 11)
+    pipe.staged_split = 11
+    pipe.prime_inputs()
+    with pytest.raises(ValueError, match="staged_split"):
+        pipe.run_stream(1, graphs=graphs, staged=True)   # graphs of the other split
+    graphs = pipe.capture_stages(staged=True)
+    pipe.prime_inputs()
+    for v in r.values():
+        v.zero_()
+    pipe.run_stream(F + 1, graphs=graphs, match_streams=2, pose_streams=2, staged=True)
+    torch.cuda.synchronize()
+    for j in range(F):
+        for k in ("pose", "R_err", "t_err", "cmd", "n_inliers", "status"):
+            np.testing.assert_array_equal(r[k][j].cpu().numpy(), ref[j][k], err_msg=f"{k} {j}")
 
 
 @pytest.mark.gpu
