@@ -305,10 +305,12 @@ def main():
     ap.add_argument("--no-staged-inputs", action="store_true",
                     help="run each step's matcher input stage (transpose_in) at the head of its "
                          "matcher instead of at the end of the slot's previous pose stage")
-    ap.add_argument("--staged-split", type=int, default=13,
+    ap.add_argument("--staged-split", type=int, default=0,
                     help="staged mode: the forward's first stage on the pose stream "
                          "(onepose_match_cached_stages: 1 + i = GNN layer i, 13 = final "
-                         "projection, 14 = score GEMM, 15 = dual-softmax winners)")
+                         "projection, 14 = score GEMM, 15 = dual-softmax winners; 0 = the "
+                         "measured best for the precision: 13 for fp32 / fp32_split, 15 for "
+                         "bf16, profiles/r06/staged3, profiles/r06/prec)")
     ap.add_argument("--diag-repeats", type=int, default=0,
                     help="diagnostic: after the timed region, time it again this many times "
                          "and report those ms/step too (value always comes from the first)")
@@ -409,6 +411,11 @@ def main():
     # the step that next uses its slot, so the matcher's launch chain starts at its first layer
     staged = (overlap and pipe.staged_ok() and not args.no_staged_inputs
               and not args.diag_no_pose and not args.diag_steps)
+    if not args.staged_split:
+        # the pose streams' share of the forward that measured best on one box: with bf16
+        # attention the layers take 0.33 ms per frame instead of 0.54, so a longer pose-stream
+        # chain delays the slot's next matcher and only the winners move there
+        args.staged_split = 15 if args.precision == "bf16" else 13
     if staged:
         pipe.staged_split = args.staged_split
     stage_graphs = (pipe.capture_stages(torch.cuda.graph_pool_handle(), staged=staged)
