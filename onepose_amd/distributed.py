@@ -23,9 +23,12 @@ def env():
 
 def init(backend: str = "nccl", device=None):
     """Join the process group when WORLD_SIZE > 1 (MASTER_ADDR/PORT from the environment).
-    Returns True when a group is active."""
+    Returns True when a group is active.  ONEPOSE_FORCE_PG=1 (diagnostic, under
+    torch.distributed.run) joins it at WORLD_SIZE 1 too, so that a one-GPU box runs the N > 1
+    bench path with its RCCL communicator and streams."""
     world, _, _ = env()
-    if world <= 1:
+    if world <= 1 and not (os.environ.get("ONEPOSE_FORCE_PG") == "1"
+                           and "MASTER_ADDR" in os.environ):
         return False
     if not dist.is_initialized():
         kw = {"device_id": device} if (backend == "nccl" and device is not None) else {}

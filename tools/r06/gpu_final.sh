@@ -64,7 +64,9 @@ timeout -s KILL 240 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ
 python3 tools/pmc_summary.py --sq $O/sq_c5/raw > $O/sq_c5/sq_summary.json || exit $?
 echo "c5 counters ok"
 # the N > 1 code path (sharding, gather, global frame order) on real HIP results: 2 ranks, gloo
-ONEPOSE_REHEARSE_ONE_GPU=1 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 \
+# (two processes on one GPU: eight hardware queues each, or their streams share queues --
+# profiles/r06/hwq/; the driver's multi-GPU run is one process per GPU)
+GPU_MAX_HW_QUEUES=8 ONEPOSE_REHEARSE_ONE_GPU=1 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 \
   --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 20 \
   --warmup 5 --no-cpu-baseline > $O/rehearse_n2.json 2> $O/rehearse_n2.err || exit $?
 tail -1 $O/rehearse_n2.json
