@@ -441,6 +441,8 @@ class FramePipeline:
         ms0 = match_stream or torch.cuda.current_stream(self.device)
         F = self.bank_size
         g0 = 0
+        if not staged:
+            self._primed = False   # whole forwards (graphs or not) overwrite the staged inputs
         if staged:
             if not self.staged_ok():
                 raise ValueError("staged inputs need a frame bank, the object cache and no "

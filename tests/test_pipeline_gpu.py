@@ -262,8 +262,13 @@ def test_frame_bank_staged_inputs_match_eager():
     torch.cuda.synchronize()
     for j in range(F):
         np.testing.assert_array_equal(r["pose"][j].cpu().numpy(), ref[j]["pose"])
-    # a one-call forward on a slot drops the staged inputs: staged steps need priming again
+    # a one-call forward on a slot (or an unstaged run) drops the staged inputs: staged steps
+    # need priming again
     pipe.enqueue_match(0, 0)
+    with pytest.raises(RuntimeError, match="prime_inputs"):
+        pipe.run_stream(1, graphs=graphs, staged=True)
+    pipe.prime_inputs()
+    pipe.run_stream(1, match_streams=2)
     with pytest.raises(RuntimeError, match="prime_inputs"):
         pipe.run_stream(1, graphs=graphs, staged=True)
     # the last two GNN layers on the pose stream too (bench.py --staged-split 11)
