@@ -288,6 +288,56 @@ def test_frame_bank_staged_inputs_match_eager():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("precision,desc,split", [("bf16", "fp16", 15), ("fp32_split", "fp32", 13),
+                                                   ("bf16", "fp32", 13)])
+def test_staged_stages_other_precisions(precision, desc, split):
+    """The bench's staged schedules of the other lines (bf16 attention with only the winners on
+    the pose stream, config 5's fp16 descriptors; the split mode from the final projection): the
+    stage ranges give the one-call bits and every bank entry equals an eager run."""
+    from onepose_amd import synthetic as S
+    dev = torch.device("cuda", 0)
+    F, n = 3, 3
+    sd = S.make_state_dict(0)
+    data, obj, frames = S.make_matcher_inputs(N1, N3, L, seed=13, batch=F * B)
+    m = matcher.from_state_dict(sd, dict(S.DEFAULT_HPARAMS, attention_precision=precision))
+    pipe = FramePipeline(m, data["keypoints3d"][0], data["descriptors3d_db"][0],
+                         data["descriptors2d_db"][0], B, N1, dev, scale=1000.0, slots=n,
+                         desc_dtype=desc)
+    Ks = np.stack([f.K for f in frames]).reshape(F, B, 3, 3)
+    gts = np.stack([f.pose_gt for f in frames]).reshape(F, B, 3, 4)
+    d2 = data["descriptors2d_query"].reshape(F, B, 256, N1)
+    k2 = data["keypoints2d"].reshape(F, B, N1, 2)
+    ref = []
+    for j in range(F):
+        pipe.set_frames(d2[j], k2[j], Ks[j], gts[j])
+        pipe.enqueue(0)
+        torch.cuda.synchronize()
+        ref.append(_outputs(pipe.slots[0]))
+    pipe.set_frame_bank(d2, k2, Ks, gts)
+    o = pipe.slots[1]
+    keys = ("matches0", "matches1", "mscores0", "mscores1")
+    pipe.enqueue_match(1, 2)
+    torch.cuda.synchronize()
+    whole = {k: getattr(o, k).cpu().numpy().copy() for k in keys}
+    for k in keys:
+        getattr(o, k).fill_(7)
+    for rng in [(0, 0), (1, split - 1), (split, 15)]:
+        pipe.enqueue_match(1, 2, stages=rng)
+    torch.cuda.synchronize()
+    for k in keys:
+        np.testing.assert_array_equal(getattr(o, k).cpu().numpy(), whole[k], err_msg=k)
+    pipe.staged_split = split
+    graphs = pipe.capture_stages(staged=True)
+    pipe.prime_inputs()
+    pipe.run_stream(2 * F + 1, graphs=graphs, match_streams=2, pose_streams=2, staged=True)
+    torch.cuda.synchronize()
+    r = pipe.bank_results
+    for j in range(F):
+        for k in ("pose", "R_err", "t_err", "cmd", "n_inliers", "status"):
+            np.testing.assert_array_equal(r[k][j].cpu().numpy(), ref[j][k], err_msg=f"{k} {j}")
+
+
+@pytest.mark.gpu
 def test_detector_pipeline_from_images():
     """Images -> SuperPoint -> matcher -> selection -> RANSAC-EPnP: the detector stage writes
     exactly what SuperPoint.detect_raw returns, the matcher stage equals the module forward on
