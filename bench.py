@@ -537,7 +537,10 @@ def main():
                     "pose_mean": round(float(np.mean(pt)), 4),
                     "pose_max": round(float(np.max(pt)), 4),
                     "stream_gap_mean": round(float(np.mean(sgap)), 4) if sgap else None,
-                    "stream_gap_max": round(float(np.max(sgap)), 4) if sgap else None}
+                    "stream_gap_max": round(float(np.max(sgap)), 4) if sgap else None,
+                    # per step, from the region's start: matcher start, matcher done, pose done
+                    "per_step_ms": [[round(ev_begin.elapsed_time(e), 3) for e in m]
+                                    for m in marks]}
     diag = []
     if step_events:
         diag.append([round(a.elapsed_time(b), 3) for a, b in zip(step_events, step_events[1:])])
