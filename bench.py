@@ -311,6 +311,12 @@ def main():
                          "projection, 14 = score GEMM, 15 = dual-softmax winners; 0 = the "
                          "measured best for the precision: 13 for fp32 / fp32_split, 15 for "
                          "bf16, profiles/r06/staged3, profiles/r06/prec)")
+    ap.add_argument("--staged-head", type=int, default=0,
+                    help="staged mode: the forward's first stage on the match streams; the "
+                         "stages before it run with the input stage at the end of the slot's "
+                         "previous pose stage (1 = the input stage alone, 3 = with "
+                         "self-attention 1's 2D half; 0 = the measured best: 1 for bf16 "
+                         "attention at up to 1024 x 4096, else 3, profiles/r06/head)")
     ap.add_argument("--diag-repeats", type=int, default=0,
                     help="diagnostic: after the timed region, time it again this many times "
                          "and report those ms/step too (value always comes from the first)")
@@ -416,8 +422,14 @@ def main():
         # attention the layers take 0.33 ms per frame instead of 0.54, so a longer pose-stream
         # chain delays the slot's next matcher and only the winners move there
         args.staged_split = 15 if args.precision == "bf16" else 13
+    if not args.staged_head:
+        # self-attention 1's 2D half (a few small launches) ahead on the pose stream: +1-2% at
+        # fp32 / split, +4% at config 5, but -11% for bf16 attention at config 2, whose 0.33 ms
+        # layers leave the pose streams no room
+        args.staged_head = 1 if args.precision == "bf16" and n1 * n3 <= 1024 * 4096 else 3
     if staged:
         pipe.staged_split = args.staged_split
+        pipe.staged_head = args.staged_head
     stage_graphs = (pipe.capture_stages(torch.cuda.graph_pool_handle(), staged=staged)
                     if graphs_on else None)
     if staged:
@@ -640,7 +652,10 @@ def main():
                       15: "dual-softmax winners"}.get(args.staged_split)
                      or f"GNN layers {args.staged_split - 1}-11, final projection, score GEMM "
                         "and dual-softmax winners")
-        sched += (("; each step's matcher input stage run at the end of its slot's previous "
+        head_name = ("input stage" if args.staged_head <= 1 else
+                     "input stage and self-attention 1's 2D half" if args.staged_head == 3 else
+                     f"input stage and GNN layers 0-{args.staged_head - 2}")
+        sched += ((f"; each step's matcher {head_name} run at the end of its slot's previous "
                    f"pose stage, its {tail_name} at the start of its own") if staged else "")
         sched += ("; object prefix (GAT 0 + 3D half of self-attention 1) prepared once per object"
                   if cached else "; every layer run per frame")

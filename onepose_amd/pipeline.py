@@ -364,18 +364,23 @@ class FramePipeline:
     _next_step = 0
     staged_split = _lib.STAGE_FINAL   # first stage of the forward on the pose stream
 
+    # first stage of the forward on the match streams: the stages before it run ahead, with the
+    # input stage, at the end of the slot's previous pose stage (LAYER0: the input stage alone)
+    staged_head = _lib.STAGE_LAYER0
+
     def _staged_split(self):
-        k = self.staged_split
-        if not _lib.STAGE_LAYER0 < k <= _lib.STAGE_WINNERS:
-            raise ValueError(f"staged_split {k}")
-        return (_lib.STAGE_LAYER0, k - 1), (k, _lib.STAGE_WINNERS)
+        k, h = self.staged_split, self.staged_head
+        if not _lib.STAGE_LAYER0 <= h < k <= _lib.STAGE_WINNERS:
+            raise ValueError(f"staged_head {h} / staged_split {k}")
+        return (h, k - 1), (k, _lib.STAGE_WINNERS)
 
     def staged_ok(self) -> bool:
         return self.object_cache is not None and self.detector is None and self.bank_size > 0
 
     def enqueue_inputs(self, slot: int, frame: int):
-        """The matcher's input stage alone for bank entry `frame` into `slot`."""
-        self.enqueue_match(slot, frame, stages=(_lib.STAGE_INPUTS, _lib.STAGE_INPUTS))
+        """The matcher's input stage for bank entry `frame` into `slot` (and the stages before
+        ``staged_head``)."""
+        self.enqueue_match(slot, frame, stages=(_lib.STAGE_INPUTS, self.staged_head - 1))
 
     def prime_inputs(self):
         """Stage the inputs of the next len(slots) steps on the current stream (before the first

@@ -285,12 +285,26 @@ def test_frame_bank_staged_inputs_match_eager():
     for j in range(F):
         for k in ("pose", "R_err", "t_err", "cmd", "n_inliers", "status"):
             np.testing.assert_array_equal(r[k][j].cpu().numpy(), ref[j][k], err_msg=f"{k} {j}")
+    # self-attention 1 run ahead with the input stage (bench.py --staged-head 3)
+    pipe.staged_split, pipe.staged_head = 13, 3
+    graphs = pipe.capture_stages(staged=True)
+    pipe.prime_inputs()
+    for v in r.values():
+        v.zero_()
+    pipe.run_stream(F + 2, graphs=graphs, match_streams=2, pose_streams=2, staged=True)
+    pipe.run_stream(F - 1, match_streams=2, staged=True)   # host-launched, continuing
+    torch.cuda.synchronize()
+    for j in range(F):
+        for k in ("pose", "R_err", "t_err", "cmd", "n_inliers", "status"):
+            np.testing.assert_array_equal(r[k][j].cpu().numpy(), ref[j][k], err_msg=f"{k} {j}")
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("precision,desc,split", [("bf16", "fp16", 15), ("fp32_split", "fp32", 13),
-                                                   ("bf16", "fp32", 13)])
-def test_staged_stages_other_precisions(precision, desc, split):
+@pytest.mark.parametrize("precision,desc,split,head", [("bf16", "fp16", 15, 3),
+                                                        ("bf16", "fp16", 15, 1),
+                                                        ("fp32_split", "fp32", 13, 3),
+                                                        ("bf16", "fp32", 13, 1)])
+def test_staged_stages_other_precisions(precision, desc, split, head):
     """The bench's staged schedules of the other lines (bf16 attention with only the winners on
     the pose stream, config 5's fp16 descriptors; the split mode from the final projection): the
     stage ranges give the one-call bits and every bank entry equals an eager run."""
@@ -326,7 +340,7 @@ def test_staged_stages_other_precisions(precision, desc, split):
     torch.cuda.synchronize()
     for k in keys:
         np.testing.assert_array_equal(getattr(o, k).cpu().numpy(), whole[k], err_msg=k)
-    pipe.staged_split = split
+    pipe.staged_split, pipe.staged_head = split, head
     graphs = pipe.capture_stages(staged=True)
     pipe.prime_inputs()
     pipe.run_stream(2 * F + 1, graphs=graphs, match_streams=2, pose_streams=2, staged=True)
