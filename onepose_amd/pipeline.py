@@ -349,17 +349,16 @@ class FramePipeline:
             self.enqueue(slot)
         return g
 
-    # ---- staged stages: the matcher's short stages on the pose stream ----
+    # ---- staged stages: the forward's short stages on the pose streams ----
     # With a frame bank and the object cache, step g runs bank entry g % F in slot g % n.  The
-    # match stream runs the GNN layers; the pose stream runs the rest of the step's forward from
-    # stage ``staged_split`` (default: the final projection + score GEMM, then the dual-softmax
-    # winners + mutual check), its pose stage, and then the input stage of step g + n -- the
-    # next step to use the slot.  The input kernel (the frame's descriptors into the slot's
-    # workspace, its counters zeroed, the cache header checked) and the forward's tail thus run
-    # beside the other streams' layers instead of on this stream's launch chain.  Every step still runs all of its
-    # forward and its pose stage; the step counter carries over between run_stream calls so
-    # that the staged inputs are the ones the next call's first steps need.  prime_inputs()
-    # stages the first n steps.
+    # match stream runs the GNN layers from ``staged_head`` up to ``staged_split``; the pose
+    # stream runs the rest of the step's forward (default: the final projection, the score GEMM,
+    # the dual-softmax winners + mutual check), its pose stage, and then the input stage -- with
+    # the stages before ``staged_head`` -- of step g + n, the next step to use the slot.  These
+    # short stages thus run beside the other streams' layers instead of on this stream's launch
+    # chain.  Every step still runs all of its forward and its pose stage; the step counter
+    # carries over between run_stream calls so that the staged inputs are the ones the next
+    # call's first steps need.  prime_inputs() stages the first n steps.
     _primed = False
     _next_step = 0
     staged_split = _lib.STAGE_FINAL   # first stage of the forward on the pose stream
