@@ -2352,7 +2352,6 @@ int match_impl(const void* packed_weights, const void* desc2d, int64_t desc2d_bs
   int64_t x3bs = obj_cache ? 0 : (int64_t)n3 * 256;
   const uint16_t* x2pr = pl(p.x2p[0]);
   const uint16_t* x3pr = obj_cache ? nullptr : pl(p.x3p[0]);
-  const int ch2 = ceil_div(n1, 64), ch3 = ceil_div(n3, 64);
   for (int layer = 0; layer < kLayers; ++layer) {
     if (last_stage < ONEPOSE_STAGE_LAYER0 + layer) return ONEPOSE_OK;
     // a layer outside the range ran in an earlier call on the same workspace (or runs in a
