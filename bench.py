@@ -681,6 +681,10 @@ def main():
                        # frame buffer slots of the pipeline (a pipeline setting: rounds 1-4 ran 3,
                        # the 64-frame bank since round 5 gives 4 with two match streams)
                        "slots": nslots, "frame_bank": F,
+                       # the staged schedule's stage split (onepose_match_cached_stages): the
+                       # match streams run stages [head, split), the pose streams the rest
+                       "staged": ({"head": args.staged_head, "split": args.staged_split}
+                                  if staged else None),
                        "parallelism": f"frame-dp{world} (one object; global batch of "
                                       f"{n_global} frames sharded contiguously over ranks)"},
             "pose": pose_summary,
