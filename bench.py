@@ -426,7 +426,10 @@ def main():
         # self-attention 1's 2D half (a few small launches) ahead on the pose stream: +1-2% at
         # fp32 / split, +4% at config 5, but -11% for bf16 attention at config 2, whose 0.33 ms
         # layers leave the pose streams no room
-        args.staged_head = 1 if args.precision == "bf16" and n1 * n3 <= 1024 * 4096 else 3
+        # (--e2e: the detector is staged with the inputs, and self-attention 1 ahead as well
+        # loses, profiles/r06/e2e_staged)
+        args.staged_head = (1 if args.e2e or (args.precision == "bf16" and n1 * n3 <= 1024 * 4096)
+                            else 3)
     if staged:
         pipe.staged_split = args.staged_split
         pipe.staged_head = args.staged_head

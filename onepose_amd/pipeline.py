@@ -374,21 +374,27 @@ class FramePipeline:
         return (h, k - 1), (k, _lib.STAGE_WINNERS)
 
     def staged_ok(self) -> bool:
-        return self.object_cache is not None and self.detector is None and self.bank_size > 0
+        """Staged runs need the object cache and inputs known ahead: a frame bank, or the
+        detector's per-slot images (each step re-detects its slot's image)."""
+        return self.object_cache is not None and (self.detector is not None
+                                                  or self.bank_size > 0)
 
-    def enqueue_inputs(self, slot: int, frame: int):
-        """The matcher's input stage for bank entry `frame` into `slot` (and the stages before
-        ``staged_head``)."""
+    def enqueue_inputs(self, slot: int, frame):
+        """The matcher's input stage for bank entry `frame` (None: the slot's detector
+        outputs, after running the detector on the slot's image) into `slot`, with the stages
+        before ``staged_head``."""
+        if self.detector is not None:
+            self.enqueue_detect(slot)
         self.enqueue_match(slot, frame, stages=(_lib.STAGE_INPUTS, self.staged_head - 1))
 
     def prime_inputs(self):
         """Stage the inputs of the next len(slots) steps on the current stream (before the first
         staged ``run_stream``, and again after anything else used the slots' workspaces)."""
         if not self.staged_ok():
-            raise ValueError("staged inputs need a frame bank, the object cache and no detector")
+            raise ValueError("staged inputs need the object cache and a frame bank or a detector")
         n, F = len(self.slots), self.bank_size
         for g in range(self._next_step, self._next_step + n):
-            self.enqueue_inputs(g % n, g % F)
+            self.enqueue_inputs(g % n, g % F if F else None)
         self._primed = True
 
     def capture_stages(self, pool=None, staged: bool = False):
@@ -401,7 +407,7 @@ class FramePipeline:
         out = []
         F, n = self.bank_size, len(self.slots)
         if staged and not self.staged_ok():
-            raise ValueError("staged inputs need a frame bank, the object cache and no detector")
+            raise ValueError("staged inputs need the object cache and a frame bank or a detector")
         head, tail = self._staged_split()
         for j in range(F or n):
             sl, fr = j % n, (j if F else None)
@@ -416,7 +422,7 @@ class FramePipeline:
                     self.enqueue_match(sl, fr, stages=tail)
                 self.enqueue_pose(sl, frame=fr)
                 if staged:
-                    self.enqueue_inputs(sl, (j + n) % F)
+                    self.enqueue_inputs(sl, (j + n) % F if F else None)
             out.append((gm, gp))
         self._primed = False   # (the non-staged captures above mark it too)
         self._captured_split = (head, tail) if staged else None
@@ -449,7 +455,7 @@ class FramePipeline:
             self._primed = False   # whole forwards (graphs or not) overwrite the staged inputs
         if staged:
             if not self.staged_ok():
-                raise ValueError("staged inputs need a frame bank, the object cache and no "
+                raise ValueError("staged inputs need the object cache and a frame bank or a "
                                  "detector")
             if not self._primed:
                 raise RuntimeError("run_stream(staged=True): call prime_inputs() first")
@@ -497,7 +503,7 @@ class FramePipeline:
                 if graphs:
                     graphs[g % len(graphs)][0].replay()
                 elif staged:
-                    self.enqueue_match(sl, g % F, stages=head)
+                    self.enqueue_match(sl, g % F if F else None, stages=head)
                 else:
                     self.enqueue_front(sl, g % F if F else None)
                 matched[sl].record(ms)
@@ -511,10 +517,10 @@ class FramePipeline:
                         graphs[g % len(graphs)][1].replay()
                     else:
                         if staged:
-                            self.enqueue_match(sl, g % F, stages=tail)
+                            self.enqueue_match(sl, g % F if F else None, stages=tail)
                         self.enqueue_pose(sl, frame=g % F if F else None)
                         if staged:
-                            self.enqueue_inputs(sl, (g + n) % F)
+                            self.enqueue_inputs(sl, (g + n) % F if F else None)
                 posed[sl].record(ps)
                 if mk:
                     mk[2].record(ps)

@@ -394,6 +394,20 @@ def test_detector_pipeline_from_images():
     torch.cuda.synchronize()
     for s in pipe.slots:
         _assert_same(ref, _outputs(s))
+    # staged: each slot's detector + input stage (+ self-attention 1) at the end of the slot's
+    # previous pose stage, the tail on the frame's own pose stream (bench.py --e2e)
+    for head in (1, 3):
+        pipe.staged_split, pipe.staged_head = 13, head
+        graphs = pipe.capture_stages(staged=True)
+        pipe.prime_inputs()
+        for s in pipe.slots:
+            for k in ("pose", "matches0", "n_inliers"):
+                getattr(s, k).zero_()
+        pipe.run_stream(7, graphs=graphs, match_streams=2, pose_streams=2, staged=True)
+        pipe.run_stream(2, match_streams=2, pose_streams=2, staged=True)   # host-launched
+        torch.cuda.synchronize()
+        for s in pipe.slots:
+            _assert_same(ref, _outputs(s))
 
 
 @pytest.mark.gpu
