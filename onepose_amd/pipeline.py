@@ -21,9 +21,10 @@ Streaming (``run_stream``): the pose stage of frame k needs one CU (one workgrou
 frame) while the matcher of frame k+1 needs the whole chip, so the two run on separate HIP
 streams with two buffer slots; events order matcher(k) -> pose(k) and pose(k) -> the
 matcher that next overwrites slot k % 2.  Every frame still runs every kernel.  Staged
-(``run_stream(staged=True)``, bench.py's default with a frame bank): the match streams run only
-the GNN layers; the pose stream of frame k runs its final projection, score GEMM and dual-softmax
-winners, its pose stage and then the input stage of the frame that next uses the slot
+(``run_stream(staged=True)``, bench.py's default with a frame bank or a detector): the match
+streams run only the GNN layers; the pose stream of frame k runs its final projection, score
+GEMM and dual-softmax winners, its pose stage and then the input stage ([detector ->]
+transpose [-> self-attention 1]) of the frame that next uses the slot
 (``onepose_match_cached_stages``; see ``prime_inputs``).
 
 With a ``detector`` (``onepose_amd.superpoint.SuperPoint``) the pipeline starts from images
