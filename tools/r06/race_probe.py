@@ -145,11 +145,127 @@ def variants(n=int(os.environ.get("RACE_N", "30"))):
     print("fp32_split side-stream mismatches of", n, ":", counts, flush=True)
 
 
+def stress(n=int(os.environ.get("RACE_N", "40")), prec=os.environ.get("RACE_PREC", "fp32_split")):
+    """Uncached forwards on the default stream while several cached (or uncached) forwards run
+    on a side stream; every default-stream result against the sequential reference."""
+    dev = torch.device("cuda", 0)
+    sd = synthetic.make_state_dict(3)
+    hp = {**synthetic.DEFAULT_HPARAMS, "attention_precision": prec}
+    res = matcher.from_state_dict(sd, hp).to(dev)
+    unc = matcher.from_state_dict(sd, hp).to(dev)
+    unc.resident_object = False
+    unc2 = matcher.from_state_dict(sd, hp).to(dev)
+    unc2.resident_object = False
+    data, _, _ = synthetic.make_matcher_inputs(300, 1000, 8, seed=9)
+    t = {k: torch.from_numpy(v).to(dev) for k, v in data.items()}
+    side = torch.cuda.Stream(dev)
+    with torch.no_grad():
+        ref, cref = unc(t)
+        res(t)
+        torch.cuda.synchronize()
+        ref = {k: v.cpu().numpy() for k, v in ref.items()}
+        cref = cref.cpu().numpy()
+        counts = {"unc || 4 cached": 0, "unc || 4 uncached": 0, "cached || 4 uncached": 0}
+        for _ in range(n):
+            for key, bg, fg in (("unc || 4 cached", res, unc), ("unc || 4 uncached", unc2, unc),
+                                ("cached || 4 uncached", unc2, res)):
+                side.wait_stream(torch.cuda.current_stream(dev))
+                with torch.cuda.stream(side):
+                    for _ in range(4):
+                        bg(t)
+                outs = [fg(t) for _ in range(3)]
+                torch.cuda.synchronize()
+                for p, c in outs:
+                    if (any((p[k].cpu().numpy() != ref[k]).any() for k in ref)
+                            or (c.cpu().numpy() != cref).any()):
+                        counts[key] += 1
+    print(prec, "mismatching default-stream forwards of", 3 * n, ":", counts, flush=True)
+
+
+def stress_prepare(n=int(os.environ.get("RACE_N", "30")),
+                   prec=os.environ.get("RACE_PREC", "fp32_split")):
+    """The object prepare (GAT 0, self-attention 1's and cross-attention 1's 3D halves -- the
+    work only an uncached forward repeats) on the default stream while uncached forwards run on
+    a side stream; each cache against one prepared alone, by layout region (floats)."""
+    from onepose_amd import _lib
+    dev = torch.device("cuda", 0)
+    lib = _lib.load()
+    sd = synthetic.make_state_dict(3)
+    hp = {**synthetic.DEFAULT_HPARAMS, "attention_precision": prec}
+    m = matcher.from_state_dict(sd, hp).to(dev)
+    unc = matcher.from_state_dict(sd, hp).to(dev)
+    unc.resident_object = False
+    data, _, _ = synthetic.make_matcher_inputs(300, 1000, 8, seed=9)
+    t = {k: torch.from_numpy(v).to(dev) for k, v in data.items()}
+    d3, _ = m._operand(t["descriptors3d_db"])
+    db, _ = m._operand(t["descriptors2d_db"])
+    n3, L = d3.shape[2], db.shape[2] // d3.shape[2]
+    w = m.packed_weights(dev)
+    pm = torch.empty(n3 * L * 256, device=dev)
+    _lib.check(lib.onepose_prepare_leaves_dt(db.data_ptr(), _lib.DT_F32, 0, 1, n3, L,
+                                             pm.data_ptr(), _lib.stream_ptr(dev)), "leaves")
+    nb = _lib.object_cache_bytes(lib, n3, L, 0, m.precision)
+    wsb = lib.onepose_object_prepare_workspace_bytes(n3, L)
+
+    def prepare():
+        cache = torch.zeros(nb // 4, dtype=torch.float32, device=dev)
+        ws = torch.zeros(wsb, dtype=torch.uint8, device=dev)
+        _lib.check(lib.onepose_object_prepare_dt(w.data_ptr(), d3.data_ptr(), _lib.DT_F32,
+                                                 pm.data_ptr(), n3, L, m.precision, 0,
+                                                 cache.data_ptr(), ws.data_ptr(), wsb,
+                                                 _lib.stream_ptr(dev)), "prepare")
+        lib.onepose_object_release(cache.data_ptr())
+        return cache
+
+    ref = prepare()
+    torch.cuda.synchronize()
+    ref = ref.view(torch.int32).cpu().numpy()
+    # region starts in floats (matcher.hip obj_layout, flags 0)
+    kl = 16
+    regions = {"state": 0, "logits": n3 * 256}
+    regions["phiq"] = regions["logits"] + 3 * n3 * kl
+    regions["acc"] = regions["phiq"] + n3 * 256
+    regions["ksum"] = regions["acc"] + ((n3 + 63) // 64) * 64 * 512
+    regions["mf+"] = regions["ksum"] + 256
+    names = list(regions)
+    hdr = nb // 4 - 16   # the header (64 B, its generation differs per prepare) excluded
+    bad = {}
+    side = torch.cuda.Stream(dev)
+    alone = {}
+    for _ in range(n):   # control: prepares alone
+        c = prepare()
+        torch.cuda.synchronize()
+        k = int((c.view(torch.int32).cpu().numpy()[:hdr] != ref[:hdr]).sum())
+        alone[k] = alone.get(k, 0) + 1
+    print(prec, "lone prepares: differing element counts -> runs", alone, flush=True)
+    with torch.no_grad():
+        for _ in range(n):
+            side.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(side):
+                for _ in range(4):
+                    unc(t)
+            c = prepare()
+            torch.cuda.synchronize()
+            diff = np.nonzero(c.view(torch.int32).cpu().numpy()[:hdr] != ref[:hdr])[0]
+            for i in diff:
+                r = max((k for k in names if regions[k] <= i), key=lambda k: regions[k])
+                bad[r] = bad.get(r, 0) + 1
+            if len(diff):
+                bad["runs"] = bad.get("runs", 0) + 1
+                bad.setdefault("per run", []).append(int(len(diff)))
+    print(prec, "prepares under concurrency differing from the lone prepare, elements by region,",
+          "of", n, "runs:", bad or "none", flush=True)
+
+
 if __name__ == "__main__":
     if sys.argv[1:] == ["test"]:
         repeat_test()
     elif sys.argv[1:] == ["variants"]:
         variants()
+    elif sys.argv[1:] == ["stress"]:
+        stress()
+    elif sys.argv[1:] == ["prepare"]:
+        stress_prepare()
     else:
         for prec in sys.argv[1:] or ["fp32", "fp32_split", "bf16"]:
             run(prec)
