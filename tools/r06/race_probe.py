@@ -257,6 +257,43 @@ def stress_prepare(n=int(os.environ.get("RACE_N", "30")),
           "of", n, "runs:", bad or "none", flush=True)
 
 
+def stress_foreign(n=int(os.environ.get("RACE_N", "40")),
+                   prec=os.environ.get("RACE_PREC", "fp32_split")):
+    """Uncached forwards on the default stream while the side stream runs PyTorch's own kernels
+    (fp32 GEMMs and a large copy) instead of matcher forwards."""
+    dev = torch.device("cuda", 0)
+    sd = synthetic.make_state_dict(3)
+    hp = {**synthetic.DEFAULT_HPARAMS, "attention_precision": prec}
+    unc = matcher.from_state_dict(sd, hp).to(dev)
+    unc.resident_object = False
+    data, _, _ = synthetic.make_matcher_inputs(300, 1000, 8, seed=9)
+    t = {k: torch.from_numpy(v).to(dev) for k, v in data.items()}
+    a = torch.randn(2048, 2048, device=dev)
+    big = torch.empty(64 << 20, device=dev)
+    side = torch.cuda.Stream(dev)
+    with torch.no_grad():
+        ref, cref = unc(t)
+        torch.cuda.synchronize()
+        ref = {k: v.cpu().numpy() for k, v in ref.items()}
+        cref = cref.cpu().numpy()
+        bad = 0
+        for _ in range(n):
+            side.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(side):
+                for _ in range(4):
+                    a2 = a @ a
+                    big.copy_(big.flip(0))
+            outs = [unc(t) for _ in range(3)]
+            torch.cuda.synchronize()
+            for p, c in outs:
+                if (any((p[k].cpu().numpy() != ref[k]).any() for k in ref)
+                        or (c.cpu().numpy() != cref).any()):
+                    bad += 1
+        del a2
+    print(prec, "uncached forwards beside PyTorch kernels differing from the lone forward:",
+          bad, "of", 3 * n, flush=True)
+
+
 if __name__ == "__main__":
     if sys.argv[1:] == ["test"]:
         repeat_test()
@@ -266,6 +303,8 @@ if __name__ == "__main__":
         stress()
     elif sys.argv[1:] == ["prepare"]:
         stress_prepare()
+    elif sys.argv[1:] == ["foreign"]:
+        stress_foreign()
     else:
         for prec in sys.argv[1:] or ["fp32", "fp32_split", "bf16"]:
             run(prec)
