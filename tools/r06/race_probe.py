@@ -294,6 +294,42 @@ def stress_foreign(n=int(os.environ.get("RACE_N", "40")),
           bad, "of", 3 * n, flush=True)
 
 
+def stress_bg(n=int(os.environ.get("RACE_N", "40")), prec=os.environ.get("RACE_PREC", "fp32_split"),
+              bg_prec=os.environ.get("RACE_BG_PREC", "fp32")):
+    """Uncached `prec` forwards on the default stream while cached forwards of another precision
+    (`bg_prec`: different GEMM loops) run on the side stream."""
+    dev = torch.device("cuda", 0)
+    sd = synthetic.make_state_dict(3)
+    unc = matcher.from_state_dict(sd, {**synthetic.DEFAULT_HPARAMS,
+                                       "attention_precision": prec}).to(dev)
+    unc.resident_object = False
+    bg = matcher.from_state_dict(sd, {**synthetic.DEFAULT_HPARAMS,
+                                      "attention_precision": bg_prec}).to(dev)
+    data, _, _ = synthetic.make_matcher_inputs(300, 1000, 8, seed=9)
+    t = {k: torch.from_numpy(v).to(dev) for k, v in data.items()}
+    side = torch.cuda.Stream(dev)
+    with torch.no_grad():
+        ref, cref = unc(t)
+        bg(t)
+        torch.cuda.synchronize()
+        ref = {k: v.cpu().numpy() for k, v in ref.items()}
+        cref = cref.cpu().numpy()
+        bad = 0
+        for _ in range(n):
+            side.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(side):
+                for _ in range(4):
+                    bg(t)
+            outs = [unc(t) for _ in range(3)]
+            torch.cuda.synchronize()
+            for p, c in outs:
+                if (any((p[k].cpu().numpy() != ref[k]).any() for k in ref)
+                        or (c.cpu().numpy() != cref).any()):
+                    bad += 1
+    print(prec, "uncached forwards beside cached", bg_prec, "forwards differing:", bad, "of",
+          3 * n, flush=True)
+
+
 if __name__ == "__main__":
     if sys.argv[1:] == ["test"]:
         repeat_test()
@@ -305,6 +341,8 @@ if __name__ == "__main__":
         stress_prepare()
     elif sys.argv[1:] == ["foreign"]:
         stress_foreign()
+    elif sys.argv[1:] == ["bg"]:
+        stress_bg()
     else:
         for prec in sys.argv[1:] or ["fp32", "fp32_split", "bf16"]:
             run(prec)
