@@ -330,6 +330,68 @@ def stress_bg(n=int(os.environ.get("RACE_N", "40")), prec=os.environ.get("RACE_P
           3 * n, flush=True)
 
 
+def stress_stages(n=int(os.environ.get("RACE_N", "40")), prec=os.environ.get("RACE_PREC", "fp32_split")):
+    """Uncached `prec` forwards on the default stream while the side stream re-runs one stage
+    range of a cached split forward (onepose_match_cached_stages on a workspace a whole forward
+    filled first): GNN layers only, or the tail only."""
+    from onepose_amd import _lib
+    dev = torch.device("cuda", 0)
+    lib = _lib.load()
+    sd = synthetic.make_state_dict(3)
+    hp = {**synthetic.DEFAULT_HPARAMS, "attention_precision": prec}
+    unc = matcher.from_state_dict(sd, hp).to(dev)
+    unc.resident_object = False
+    bgm = matcher.from_state_dict(sd, hp).to(dev)
+    data, _, _ = synthetic.make_matcher_inputs(300, 1000, 8, seed=9)
+    t = {k: torch.from_numpy(v).to(dev) for k, v in data.items()}
+    side = torch.cuda.Stream(dev)
+    with torch.no_grad():
+        ref, cref = unc(t)
+        bgm(t)   # builds the object cache
+        torch.cuda.synchronize()
+        ref = {k: v.cpu().numpy() for k, v in ref.items()}
+        cref = cref.cpu().numpy()
+        obj = bgm._obj
+        d2, s2 = bgm._operand(t["descriptors2d_query"])
+        B, n1, n3, L = 1, 300, 1000, 8
+        w = bgm.packed_weights(dev)
+        m0 = torch.empty(B, n1, dtype=torch.int64, device=dev)
+        m1 = torch.empty(B, n3, dtype=torch.int64, device=dev)
+        ms0, ms1 = torch.empty(B, n1, device=dev), torch.empty(B, n3, device=dev)
+        conf = torch.empty(B, n1, n3, device=dev)
+        wsb = _lib.workspace_bytes(lib, B, n1, n3, L, True, bgm.precision)
+        with torch.cuda.stream(side):
+            ws = torch.zeros(wsb, dtype=torch.uint8, device=dev)
+        sc, th = float(hp["scale_factor"]), float(hp["match_threshold"])
+
+        def stages(first, last):
+            _lib.check(lib.onepose_match_cached_stages(
+                w.data_ptr(), d2.data_ptr(), _lib.DT_F32, s2, obj["cache"].data_ptr(),
+                obj["pm"].data_ptr(), 0, B, n1, n3, L, sc, th, bgm.precision, 0, m0.data_ptr(),
+                m1.data_ptr(), ms0.data_ptr(), ms1.data_ptr(), conf.data_ptr(), ws.data_ptr(), wsb,
+                first, last, side.cuda_stream), "stages")
+
+        side.wait_stream(torch.cuda.current_stream(dev))
+        stages(_lib.STAGE_INPUTS, _lib.STAGE_WINNERS)
+        torch.cuda.synchronize()
+        for name, (a, b) in (("layers", (_lib.STAGE_LAYER0, _lib.STAGE_FINAL - 1)),
+                             ("tail", (_lib.STAGE_FINAL, _lib.STAGE_WINNERS)),
+                             ("whole", (_lib.STAGE_INPUTS, _lib.STAGE_WINNERS))):
+            bad = 0
+            for _ in range(n):
+                side.wait_stream(torch.cuda.current_stream(dev))
+                for _ in range(4):
+                    stages(a, b)
+                outs = [unc(t) for _ in range(3)]
+                torch.cuda.synchronize()
+                for p, c in outs:
+                    if (any((p[k].cpu().numpy() != ref[k]).any() for k in ref)
+                            or (c.cpu().numpy() != cref).any()):
+                        bad += 1
+            print(prec, "uncached forwards beside cached-forward stages", name, "differing:",
+                  bad, "of", 3 * n, flush=True)
+
+
 if __name__ == "__main__":
     if sys.argv[1:] == ["test"]:
         repeat_test()
@@ -343,6 +405,8 @@ if __name__ == "__main__":
         stress_foreign()
     elif sys.argv[1:] == ["bg"]:
         stress_bg()
+    elif sys.argv[1:] == ["stages"]:
+        stress_stages()
     else:
         for prec in sys.argv[1:] or ["fp32", "fp32_split", "bf16"]:
             run(prec)
